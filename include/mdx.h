@@ -1,0 +1,104 @@
+/*
+ * mdx.h -- C ABI of the MI355X-native moseq2-detectron-extract hot path.
+ *
+ * Every entry point takes plain device pointers + sizes and an optional HIP
+ * stream (mdx_stream_t == hipStream_t, NULL = default stream).  The caller owns
+ * every input/output buffer (PyTorch-ROCm allocates them); the library only
+ * allocates workspace it owns through a handle.  All work is enqueued on the
+ * given stream; no entry point synchronises the host unless its comment says
+ * so.  Return value: 0 on success, a negative MDX_E* code on failure, with a
+ * thread-local message in mdx_last_error().
+ *
+ * Each function cites the reference interface it replaces
+ * (M/ = moseq2_detectron_extract/ in tischfieldlab/moseq2-detectron-extract).
+ */
+#ifndef MDX_H_
+#define MDX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *mdx_stream_t; /* hipStream_t */
+
+enum {
+    MDX_OK = 0,
+    MDX_EINVAL = -1,   /* bad argument / shape */
+    MDX_EHIP = -2,     /* HIP runtime error */
+    MDX_ENOMEM = -3,   /* workspace allocation failed */
+    MDX_ELIMIT = -4    /* input exceeds a compiled-in limit */
+};
+
+/* Thread-local text of the last error ("" when none). */
+const char *mdx_last_error(void);
+/* Library version string, e.g. "mdx 0.1.0 gfx950". */
+const char *mdx_version(void);
+
+/* ---------------------------------------------------------------------
+ * Frame ops (M/proc/proc.py)
+ * ------------------------------------------------------------------- */
+
+/* prep_raw_frames(frames, bground_im, roi, vmin, vmax, 'uint8',
+ *                 fix_invalid_pixels) -- numpy part.  M/proc/proc.py:129-172,
+ * find_invalid_pixels :175-186, apply_roi/get_bbox M/proc/roi.py:215-254.
+ * raw      int16 [n][H][W]
+ * bg       float64 [H][W] or NULL (no background subtraction)
+ * roi      uint8 [H][W] 0/1 or NULL (no masking); [y0,y1)x[x0,x1) is the
+ *          crop (get_bbox max is exclusive, reference quirk)
+ * flags    bit0: vmin given, bit1: vmax given
+ * out      uint8 [n][y1-y0][x1-x0]
+ * invalid  uint8 [n][y1-y0][x1-x0] or NULL: (raw==0)*roi, cropped */
+int mdx_prep_frames(const int16_t *raw, int64_t n, int H, int W, const double *bg,
+                    const uint8_t *roi, int y0, int y1, int x0, int x1, int flags,
+                    double vmin, double vmax, uint8_t *out, uint8_t *invalid,
+                    mdx_stream_t stream);
+
+/* fill_invalid_pixels -> cv2.inpaint(frame, invalid, 3, cv2.INPAINT_NS) per
+ * frame, in place on `frames`.  M/proc/proc.py:189-210.  workspace: device
+ * buffer of at least mdx_inpaint_workspace_bytes(n, H, W) bytes. */
+int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W);
+int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W,
+                   int radius, void *workspace, mdx_stream_t stream);
+
+/* scale_raw_frames(frames, vmin, vmax, 'uint8') as a 256-entry LUT built on
+ * the host in float64 (M/proc/proc.py:214-234).  int_vmin != 0 reproduces
+ * numpy's uint8 - int wraparound.  Host-only, no device work. */
+int mdx_build_scale_lut(double vmin, double vmax, int int_vmin, uint8_t lut[256]);
+/* out[i] = lut[in[i]] for count bytes (device pointers; lut is host). */
+int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t lut[256], uint8_t *out,
+                     mdx_stream_t stream);
+
+/* clean_frames(frames, prefilter_space=(median_k,), strel_tail=strel,
+ * iters_tail=iters) -- M/proc/proc.py:480-515: per frame medianBlur(median_k)
+ * (0 = skip; only 3 supported) then morphologyEx(MORPH_OPEN, strel, iters).
+ * strel: host uint8 [kh][kw] (each row one contiguous run, kh,kw <= 15).
+ * src and out must not alias. */
+int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k,
+                     const uint8_t *strel, int kh, int kw, int iters, uint8_t *out,
+                     mdx_stream_t stream);
+
+/* get_frame_features(frames, frame_threshold=thr, mask=mask, use_cc=*) +
+ * im_moment_features -- M/proc/proc.py:237-302, :518-549.  Largest contour
+ * (findContours RETR_TREE + contourArea argmax) and its polygon moments.
+ * mask may be NULL.  Outputs (float64, NaN when no contour):
+ * centroid [n][2] (x, y), orientation [n] (rad), axis_length [n][2],
+ * area [n] (contourArea of the chosen contour; may be NULL). */
+int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W,
+                      double thr, double *centroid, double *orientation, double *axis_length,
+                      double *area, mdx_stream_t stream);
+
+/* crop_and_rotate_frame(frame, center, angle, crop_size=(cw, ch)) for every
+ * frame of src0 (and of src1 when not NULL, same centers/angles) --
+ * M/proc/proc.py:305-340, called twice per frame at
+ * M/pipeline/process_features_step.py:186-198.
+ * center float64 [n][2] (x, y), angle_deg float64 [n]; out uint8 [n][ch][cw]. */
+int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, int W,
+                    const double *center, const double *angle_deg, int cw, int ch,
+                    uint8_t *out0, uint8_t *out1, mdx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDX_H_ */

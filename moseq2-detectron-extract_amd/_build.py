@@ -1,0 +1,84 @@
+"""Build the in-tree HIP library ``libmdx.so`` for gfx950.
+
+``python -m`` is not needed: ``__graft_entry__.build()`` and the package loader
+call :func:`build`.  Objects go to ``csrc/build/``; the shared library lands
+next to this file so it travels with the repository snapshot to the GPU box
+(git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(CSRC, "build")
+LIB = os.path.join(HERE, "libmdx.so")
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: cannot build the mdx HIP library")
+
+
+def _flags():
+    return ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
+            "-munsafe-fp-atomics", f"-I{os.path.dirname(HERE)}"]
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _deps_newer(target: str, srcs) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(os.path.dirname(HERE), "include", "*.h"))
+    return any(os.path.getmtime(s) > t for s in list(srcs) + hdrs)
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    cc = hipcc()
+    srcs = sources()
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if force or _deps_newer(o, [s]):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        cmd = [cc, *_flags(), "-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+        return o
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            list(ex.map(comp, todo))
+    if force or todo or _deps_newer(LIB, objs):
+        cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link of libmdx.so failed:\n{r.stderr[-6000:]}")
+    return LIB
+
+
+if __name__ == "__main__":
+    import sys
+    print(build(force="-f" in sys.argv, verbose=True))

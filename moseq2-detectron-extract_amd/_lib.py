@@ -1,0 +1,65 @@
+"""ctypes binding of the in-tree HIP library ``libmdx.so`` (C ABI: include/mdx.h).
+
+There is no CPU fallback: if the library is missing or the device is not a
+GPU, every op raises :class:`MdxError`.  ``torch`` is imported before the
+library is opened so that ``libmdx.so``'s ``libamdhip64.so.7`` dependency binds
+to the HIP runtime PyTorch already loaded (one runtime, shared streams).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmdx.so")
+_LIB = None
+
+
+class MdxError(RuntimeError):
+    pass
+
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F64 = ctypes.c_double
+
+# name -> (restype, argtypes); mirrors include/mdx.h
+SIGNATURES = {
+    "mdx_last_error": (ctypes.c_char_p, []),
+    "mdx_version": (ctypes.c_char_p, []),
+    "mdx_prep_frames": (I32, [P, I64, I32, I32, P, P, I32, I32, I32, I32, I32, F64, F64, P, P, P]),
+    "mdx_inpaint_workspace_bytes": (I64, [I64, I32, I32]),
+    "mdx_inpaint_ns": (I32, [P, P, I64, I32, I32, I32, P, P]),
+    "mdx_build_scale_lut": (I32, [F64, F64, I32, P]),
+    "mdx_scale_frames": (I32, [P, I64, P, P, P]),
+    "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P]),
+    "mdx_frame_moments": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P]),
+    "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P]),
+}
+
+
+def lib():
+    """Open (once) and return the library; raises MdxError if unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (binds libamdhip64.so.7 first)
+    if not os.path.exists(LIB_PATH):
+        raise MdxError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                       "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def call(name: str, *args) -> int:
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if isinstance(rc, int) and rc < 0 and SIGNATURES[name][0] is I32:
+        raise MdxError(f"{name} failed ({rc}): {L.mdx_last_error().decode()}")
+    return rc

@@ -1,0 +1,46 @@
+// Shared helpers of the mdx HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/mdx.h"
+
+namespace mdx {
+
+void set_error(const char *fmt, ...);
+inline hipStream_t as_stream(mdx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch-error check after every kernel launch (asynchronous errors surface
+// at the next synchronising call made by the caller).
+#define MDX_CHECK_LAUNCH(name)                                                       \
+    do {                                                                             \
+        hipError_t e_ = hipGetLastError();                                           \
+        if (e_ != hipSuccess) {                                                      \
+            ::mdx::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));  \
+            return MDX_EHIP;                                                         \
+        }                                                                            \
+    } while (0)
+
+#define MDX_REQUIRE(cond, ...)                  \
+    do {                                        \
+        if (!(cond)) {                          \
+            ::mdx::set_error(__VA_ARGS__);      \
+            return MDX_EINVAL;                  \
+        }                                       \
+    } while (0)
+
+#define MDX_HIP(call)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            ::mdx::set_error("%s: %s", #call, hipGetErrorString(e_));                 \
+            return MDX_EHIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace mdx

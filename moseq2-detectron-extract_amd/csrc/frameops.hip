@@ -1,0 +1,595 @@
+// Frame-op kernels of the extraction hot path (gfx950).
+//
+//   k_prep        prep_raw_frames numpy part      M/proc/proc.py:129-186, M/proc/roi.py:215-254
+//   k_scale       scale_raw_frames (256-entry LUT) M/proc/proc.py:214-234
+//   k_clean       clean_frames: medianBlur(3) + morphologyEx(OPEN, strel, iters),
+//                 all passes fused per LDS tile    M/proc/proc.py:480-515
+//   k_moments     get_frame_features + im_moment_features
+//                 (largest contour, polygon moments) M/proc/proc.py:237-302,518-549
+//   k_crop        crop_and_rotate_frame (warpAffine INTER_LINEAR fixed point)
+//                                                  M/proc/proc.py:305-340
+//
+// All double/float arithmetic that the reference performs in a fixed order is
+// written in that order with FMA contraction disabled, so results are
+// bit-identical to the oracle (oracle/frameops.c).
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace mdx {
+
+// ---------------------------------------------------------------------------
+// prep
+// ---------------------------------------------------------------------------
+constexpr int PREP_FRAMES_PER_BLOCK = 8;
+
+__global__ __launch_bounds__(256) void k_prep(const int16_t *__restrict__ raw, int64_t n, int H, int W,
+                                              const double *__restrict__ bg, const uint8_t *__restrict__ roi,
+                                              int y0, int x0, int oh, int ow, int flags, double vmin,
+                                              double vmax, uint8_t *__restrict__ out, uint8_t *__restrict__ inv) {
+    const int64_t npix = (int64_t)oh * ow;
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    const int y = (int)(p / ow), x = (int)(p - (int64_t)y * ow);
+    const int64_t si = (int64_t)(y + y0) * W + x + x0;
+    const double b = bg ? bg[si] : 0.0;
+    const uint8_t r8 = roi ? roi[si] : (uint8_t)1;
+    const int64_t f0 = (int64_t)blockIdx.y * PREP_FRAMES_PER_BLOCK;
+    const int64_t f1 = f0 + PREP_FRAMES_PER_BLOCK < n ? f0 + PREP_FRAMES_PER_BLOCK : n;
+    const int64_t fstride = (int64_t)H * W;
+    for (int64_t f = f0; f < f1; ++f) {
+        const int16_t r = raw[f * fstride + si];
+        double v = bg ? b - (double)r : (double)r;       // bground_im - frames (float64)
+        if (roi) v = v * (double)r8;                      // frames * roi
+        if ((flags & 1) && v < vmin) v = 0.0;             // frames[frames < vmin] = 0
+        if ((flags & 2) && v > vmax) v = vmax;            // frames[frames > vmax] = vmax
+        out[f * npix + p] = (uint8_t)(int32_t)v;          // astype(uint8) (truncation)
+        if (inv) inv[f * npix + p] = (uint8_t)((r == 0) * r8);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scale LUT
+// ---------------------------------------------------------------------------
+struct Lut256 {
+    uint8_t v[256];
+};
+
+__global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ in, int64_t count, Lut256 lut,
+                                               uint8_t *__restrict__ out) {
+    __shared__ uint8_t s_lut[256];
+    s_lut[threadIdx.x] = lut.v[threadIdx.x];
+    __syncthreads();
+    const int64_t nvec = count / 16;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+        uint4 v = reinterpret_cast<const uint4 *>(in)[i];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) o |= (uint32_t)s_lut[(w[k] >> (8 * b)) & 255] << (8 * b);
+            w[k] = o;
+        }
+        reinterpret_cast<uint4 *>(out)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = nvec * 16 + threadIdx.x; i < count; i += 256) out[i] = s_lut[in[i]];
+}
+
+// ---------------------------------------------------------------------------
+// clean_frames: median3 (replicate border) -> erode^iters -> dilate^iters,
+// fused per output tile.  Pixels outside the image hold the neutral element of
+// the next pass (255 before an erosion, 0 before a dilation), which is exactly
+// OpenCV's morphologyDefaultBorderValue behaviour applied per pass.
+// ---------------------------------------------------------------------------
+constexpr int CT_W = 64, CT_H = 32, CT_THREADS = 256, MAX_KH = 15;
+
+struct StrelSpans {
+    int kh, ay, ax, rad;
+    int8_t j1[MAX_KH], j2[MAX_KH];  // row ky: ones in [j1, j2)
+};
+
+__device__ __forceinline__ uint8_t med3x3(const uint8_t *b, int stride, int ly, int lx) {
+    // exact median of 9 values (sorting network on the 3x3 window)
+    int v[9];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) v[dy * 3 + dx] = b[(ly + dy - 1) * stride + lx + dx - 1];
+#define MDX_S(a, c)            \
+    {                          \
+        int lo = min(v[a], v[c]); \
+        int hi = max(v[a], v[c]); \
+        v[a] = lo;             \
+        v[c] = hi;             \
+    }
+    MDX_S(1, 2); MDX_S(4, 5); MDX_S(7, 8); MDX_S(0, 1); MDX_S(3, 4); MDX_S(6, 7);
+    MDX_S(1, 2); MDX_S(4, 5); MDX_S(7, 8); MDX_S(0, 3); MDX_S(5, 8); MDX_S(4, 7);
+    MDX_S(3, 6); MDX_S(1, 4); MDX_S(2, 5); MDX_S(4, 7); MDX_S(4, 2); MDX_S(6, 4);
+    MDX_S(4, 2);
+#undef MDX_S
+    return (uint8_t)v[4];
+}
+
+__global__ __launch_bounds__(CT_THREADS) void k_clean(const uint8_t *__restrict__ src, int H, int W,
+                                                      int median, StrelSpans st, int iters,
+                                                      uint8_t *__restrict__ out, int tiles_x, int halo) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int TW = CT_W + 2 * halo, TH = CT_H + 2 * halo;
+    uint8_t *A = smem, *B = smem + TW * TH;
+    const int64_t frame = blockIdx.y;
+    const int tx0 = (blockIdx.x % tiles_x) * CT_W - halo;  // global x of local 0
+    const int ty0 = (blockIdx.x / tiles_x) * CT_H - halo;
+    const uint8_t *s = src + frame * (int64_t)H * W;
+
+    // load (replicate border for the median; neutral 255 if no median)
+    for (int i = threadIdx.x; i < TW * TH; i += CT_THREADS) {
+        const int ly = i / TW, lx = i - ly * TW;
+        int gy = ty0 + ly, gx = tx0 + lx;
+        const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+        gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
+        uint8_t v = s[(int64_t)gy * W + gx];
+        if (!median && !inside) v = 255;
+        A[i] = v;
+    }
+    __syncthreads();
+    int rem = halo;  // valid margin of the current buffer
+    if (median) {
+        rem -= 1;
+        const int lo = halo - rem;
+        const int w = TW - 2 * lo, h = TH - 2 * lo;
+        for (int i = threadIdx.x; i < w * h; i += CT_THREADS) {
+            const int ly = lo + i / w, lx = lo + i % w;
+            const int gy = ty0 + ly, gx = tx0 + lx;
+            const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            B[ly * TW + lx] = inside ? med3x3(A, TW, ly, lx) : (uint8_t)255;
+        }
+        __syncthreads();
+        uint8_t *t = A; A = B; B = t;
+    }
+    for (int pass = 0; pass < 2 * iters; ++pass) {
+        const bool dil = pass >= iters;
+        // the value outside the image after this pass is the neutral element of
+        // the NEXT pass: 255 for erosions, 0 for dilations
+        const uint8_t outside_next = (pass + 1 >= iters) ? (uint8_t)0 : (uint8_t)255;
+        rem -= st.rad;
+        const int lo = halo - rem;
+        const int w = TW - 2 * lo, h = TH - 2 * lo;
+        for (int i = threadIdx.x; i < w * h; i += CT_THREADS) {
+            const int ly = lo + i / w, lx = lo + i % w;
+            const int gy = ty0 + ly, gx = tx0 + lx;
+            const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            uint8_t r;
+            if (!inside) {
+                r = outside_next;
+            } else {
+                int acc = dil ? 0 : 255;
+                for (int ky = 0; ky < st.kh; ++ky) {
+                    const uint8_t *row = A + (ly + ky - st.ay) * TW + lx - st.ax;
+                    for (int kx = st.j1[ky]; kx < st.j2[ky]; ++kx) {
+                        const int v = row[kx];
+                        acc = dil ? max(acc, v) : min(acc, v);
+                    }
+                }
+                r = (uint8_t)acc;
+            }
+            B[ly * TW + lx] = r;
+        }
+        __syncthreads();
+        uint8_t *t = A; A = B; B = t;
+    }
+    uint8_t *o = out + frame * (int64_t)H * W;
+    for (int i = threadIdx.x; i < CT_W * CT_H; i += CT_THREADS) {
+        const int ly = i / CT_W, lx = i - ly * CT_W;
+        const int gy = ty0 + halo + ly, gx = tx0 + halo + lx;
+        if (gy < H && gx < W) o[(int64_t)gy * W + gx] = A[(ly + halo) * TW + lx + halo];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// moments: one workgroup per frame.
+// The blob mask (frame > thr) & mask is bit-packed into LDS with a 1-pixel
+// zero frame (findContours pads the image with zeros).  Every pixel that can
+// start the outer border of its 8-connected blob (fg, with W, NW, N, NE all
+// background; the raster-first pixel of every blob qualifies) is traced with
+// the Suzuki85 outer-border follower, accumulating the Green's-theorem sums of
+// cv::contourMoments in int64 (exact, so trace order does not matter).  The
+// largest |a00| wins (contourArea argmax; ties -> raster-first start, which is
+// the reference's first blob in scan order).  Traces started inside a hole
+// produce hole borders whose area never exceeds their blob's outer border.
+// ---------------------------------------------------------------------------
+constexpr int MOM_THREADS = 256;
+
+struct Green {
+    long long a00, a10, a01, a20, a11, a02;
+};
+
+__device__ __forceinline__ void green_edge(Green &g, long long xi_1, long long yi_1, long long xi, long long yi) {
+    const long long xi2 = xi * xi, yi2 = yi * yi;
+    const long long dxy = xi_1 * yi - xi * yi_1;
+    const long long xii_1 = xi_1 + xi, yii_1 = yi_1 + yi;
+    g.a00 += dxy;
+    g.a10 += dxy * xii_1;
+    g.a01 += dxy * yii_1;
+    g.a20 += dxy * (xi_1 * xii_1 + xi2);
+    g.a11 += dxy * (xi_1 * (yii_1 + yi_1) + xi * (yii_1 + yi));
+    g.a02 += dxy * (yi_1 * yii_1 + yi2);
+}
+
+__constant__ int c_dx[8] = {1, 1, 0, -1, -1, -1, 0, 1};
+__constant__ int c_dy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+
+__device__ __forceinline__ int getbit(const uint32_t *bits, int pww, int px, int py) {
+    return (bits[py * pww + (px >> 5)] >> (px & 31)) & 1;
+}
+
+__device__ Green trace_outer(const uint32_t *bits, int pww, int x0, int y0, long long max_steps) {
+    Green g = {0, 0, 0, 0, 0, 0};
+    int s = 4;
+    const int s_end = 4;
+    int x1 = 0, y1 = 0;
+    do {
+        s = (s - 1) & 7;
+        x1 = x0 + c_dx[s];
+        y1 = y0 + c_dy[s];
+    } while (!getbit(bits, pww, x1, y1) && s != s_end);
+    if (s == s_end) return g;
+    int x3 = x0, y3 = y0;
+    long long px = x0 - 1, py = y0 - 1;
+    const long long sx = px, sy = py;
+    bool first = true;
+    for (long long step = 0; step < max_steps; ++step) {
+        int x4 = 0, y4 = 0;
+        for (int c = 0; c < 8; ++c) {
+            s = (s + 1) & 7;
+            x4 = x3 + c_dx[s];
+            y4 = y3 + c_dy[s];
+            if (getbit(bits, pww, x4, y4)) break;
+        }
+        if (!first) {
+            green_edge(g, px, py, x3 - 1, y3 - 1);
+            px = x3 - 1;
+            py = y3 - 1;
+        }
+        first = false;
+        if (x4 == x0 && y4 == y0 && x3 == x1 && y3 == y1) break;
+        x3 = x4;
+        y3 = y4;
+        s = (s + 4) & 7;
+    }
+    green_edge(g, px, py, sx, sy);
+    return g;
+}
+
+__device__ void moments_to_features(const Green &g, double *cen, double *ori, double *ax) {
+    double m00 = 0, m10 = 0, m01 = 0, m20 = 0, m11 = 0, m02 = 0;
+    const double a00 = (double)g.a00;
+    if (fabs(a00) > FLT_EPSILON) {
+        double db1_2, db1_6, db1_12, db1_24;
+        if (a00 > 0) {
+            db1_2 = 0.5; db1_6 = 0.16666666666666666666666666666667;
+            db1_12 = 0.083333333333333333333333333333333; db1_24 = 0.041666666666666666666666666666667;
+        } else {
+            db1_2 = -0.5; db1_6 = -0.16666666666666666666666666666667;
+            db1_12 = -0.083333333333333333333333333333333; db1_24 = -0.041666666666666666666666666666667;
+        }
+        m00 = a00 * db1_2;
+        m10 = (double)g.a10 * db1_6;
+        m01 = (double)g.a01 * db1_6;
+        m20 = (double)g.a20 * db1_12;
+        m11 = (double)g.a11 * db1_24;
+        m02 = (double)g.a02 * db1_12;
+    }
+    double mcx = 0, mcy = 0;
+    if (fabs(m00) > DBL_EPSILON) {
+        const double inv_m00 = 1. / m00;
+        mcx = m10 * inv_m00;
+        mcy = m01 * inv_m00;
+    }
+    const double mu20 = m20 - m10 * mcx;
+    const double mu11 = m11 - m10 * mcy;
+    const double mu02 = m02 - m01 * mcy;
+    if (m00 == 0) {
+        cen[0] = cen[1] = ori[0] = ax[0] = ax[1] = __builtin_nan("");
+        return;
+    }
+    const double num = 2 * mu11;
+    const double den = mu20 - mu02;
+    const double common = sqrt(4 * (mu11 * mu11) + den * den);
+    ori[0] = -.5 * atan2(num, den);
+    cen[0] = m10 / m00;
+    cen[1] = m01 / m00;
+    const double k = 2 * sqrt(2.0);
+    ax[0] = k * sqrt((mu20 + mu02 + common) / m00);
+    ax[1] = k * sqrt((mu20 + mu02 - common) / m00);
+}
+
+__global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restrict__ frames,
+                                                         const uint8_t *__restrict__ mask, int H, int W,
+                                                         double thr, double *__restrict__ cen,
+                                                         double *__restrict__ ori, double *__restrict__ axl,
+                                                         double *__restrict__ area, int pww) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
+    __shared__ unsigned long long s_best;
+    __shared__ Green s_g;
+    const int64_t f = blockIdx.x;
+    const uint8_t *fr = frames + f * (int64_t)H * W;
+    const uint8_t *mk = mask ? mask + f * (int64_t)H * W : nullptr;
+    const int PH = H + 2, PW = W + 2;
+    const int nwords = PH * pww;
+    if (threadIdx.x == 0) s_best = 0ull;
+    for (int w = threadIdx.x; w < nwords; w += MOM_THREADS) {
+        const int py = w / pww, wx = w - py * pww;
+        uint32_t word = 0;
+        if (py >= 1 && py <= H) {
+            const int64_t rowoff = (int64_t)(py - 1) * W;
+            for (int b = 0; b < 32; ++b) {
+                const int x = wx * 32 + b - 1;
+                if (x >= 0 && x < W) {
+                    const bool on = (double)fr[rowoff + x] > thr && (!mk || mk[rowoff + x]);
+                    word |= (uint32_t)on << b;
+                }
+            }
+        }
+        bits[w] = word;
+    }
+    __syncthreads();
+    unsigned long long best = 0ull;
+    Green bg = {0, 0, 0, 0, 0, 0};
+    const long long max_steps = 8ll * PH * PW + 16;
+    for (int w = threadIdx.x; w < nwords; w += MOM_THREADS) {
+        const uint32_t word = bits[w];
+        if (!word) continue;
+        const int py = w / pww, wx = w - py * pww;
+        const uint32_t prev = wx > 0 ? bits[w - 1] : 0u;
+        const uint32_t up = bits[w - pww];  // py >= 1 for any set bit
+        const uint32_t upprev = wx > 0 ? bits[w - pww - 1] : 0u;
+        const uint32_t upnext = wx + 1 < pww ? bits[w - pww + 1] : 0u;
+        const uint32_t L = (word << 1) | (prev >> 31);
+        const uint32_t UL = (up << 1) | (upprev >> 31);
+        const uint32_t UR = (up >> 1) | (upnext << 31);
+        uint32_t cand = word & ~L & ~up & ~UL & ~UR;
+        while (cand) {
+            const int b = __builtin_ctz(cand);
+            cand &= cand - 1;
+            const int px = wx * 32 + b;
+            const Green g = trace_outer(bits, pww, px, py, max_steps);
+            const unsigned long long a = (unsigned long long)(g.a00 < 0 ? -g.a00 : g.a00);
+            const unsigned long long start = (unsigned long long)py * PW + px;
+            const unsigned long long key = (a << 32) | (0xFFFFFFFFull - start);
+            if (key > best) {
+                best = key;
+                bg = g;
+            }
+        }
+    }
+    atomicMax(&s_best, best);
+    __syncthreads();
+    if (best != 0ull && best == s_best) s_g = bg;  // keys are unique (start index)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double c[2], o, a[2];
+        if (s_best == 0ull) {
+            c[0] = c[1] = o = a[0] = a[1] = __builtin_nan("");
+            if (area) area[f] = __builtin_nan("");
+        } else {
+            moments_to_features(s_g, c, &o, a);
+            if (area) area[f] = fabs((double)s_g.a00 * 0.5);
+        }
+        cen[2 * f] = c[0];
+        cen[2 * f + 1] = c[1];
+        ori[f] = o;
+        axl[2 * f] = a[0];
+        axl[2 * f + 1] = a[1];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// crop_and_rotate_frame: one workgroup per frame, both sources share the map.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, const uint8_t *__restrict__ src1,
+                                              int H, int W, const double *__restrict__ center,
+                                              const double *__restrict__ angle, int cw, int ch,
+                                              uint8_t *__restrict__ out0, uint8_t *__restrict__ out1) {
+    const int64_t f = blockIdx.x;
+    const double cxc = center[2 * f], cyc = center[2 * f + 1], ang_deg = angle[f];
+    uint8_t *o0 = out0 + f * (int64_t)cw * ch;
+    uint8_t *o1 = out1 ? out1 + f * (int64_t)cw * ch : nullptr;
+    bool zero = isnan(ang_deg) || isnan(cxc) || isnan(cyc) || cxc < 0 || cyc < 0;
+    int xmin = 0, ymin = 0, pw = 0, ph = 0;
+    double M[6] = {0, 0, 0, 0, 0, 0};
+    if (!zero) {
+        xmin = (int)(cxc - cw / 2) + cw;
+        const int xmax = (int)(cxc + cw / 2) + cw;
+        ymin = (int)(cyc - ch / 2) + ch;
+        const int ymax = (int)(cyc + ch / 2) + ch;
+        const int PWd = W + 2 * cw, PHd = H + 2 * ch;
+        const int sx0 = xmin < 0 ? 0 : (xmin > PWd ? PWd : xmin);
+        const int sx1 = xmax < 0 ? 0 : (xmax > PWd ? PWd : xmax);
+        const int sy0 = ymin < 0 ? 0 : (ymin > PHd ? PHd : ymin);
+        const int sy1 = ymax < 0 ? 0 : (ymax > PHd ? PHd : ymax);
+        xmin = sx0;
+        ymin = sy0;
+        pw = sx1 - sx0;
+        ph = sy1 - sy0;
+        if (pw <= 0 || ph <= 0) zero = true;
+        const double CV_PI_ = 3.1415926535897932384626433832795;
+        const double ang = ang_deg * (CV_PI_ / 180);
+        const double alpha = cos(ang) * 1.0, beta = sin(ang) * 1.0;
+        const double ccx = (double)(float)(cw / 2), ccy = (double)(float)(ch / 2);
+        M[0] = alpha; M[1] = beta; M[2] = (1 - alpha) * ccx - beta * ccy;
+        M[3] = -beta; M[4] = alpha; M[5] = beta * ccx + (1 - alpha) * ccy;
+        double D = M[0] * M[4] - M[1] * M[3];
+        D = D != 0 ? 1. / D : 0;
+        const double A11 = M[4] * D, A22 = M[0] * D;
+        M[0] = A11; M[1] *= -D;
+        M[3] *= -D; M[4] = A22;
+        const double b1 = -M[0] * M[2] - M[1] * M[5];
+        const double b2 = -M[3] * M[2] - M[4] * M[5];
+        M[2] = b1; M[5] = b2;
+    }
+    const int AB_BITS = 10, AB_SCALE = 1 << AB_BITS, INTER_BITS = 5, TAB = 1 << INTER_BITS;
+    const int round_delta = AB_SCALE / TAB / 2;
+    const uint8_t *s0 = src0 + f * (int64_t)H * W;
+    const uint8_t *s1 = src1 ? src1 + f * (int64_t)H * W : nullptr;
+    for (int i = threadIdx.x; i < cw * ch; i += 256) {
+        if (zero) {
+            o0[i] = 0;
+            if (o1) o1[i] = 0;
+            continue;
+        }
+        const int y = i / cw, x = i - y * cw;
+        const int X0 = __double2int_rn((M[1] * y + M[2]) * AB_SCALE) + round_delta;
+        const int Y0 = __double2int_rn((M[4] * y + M[5]) * AB_SCALE) + round_delta;
+        const int adelta = __double2int_rn(M[0] * x * AB_SCALE);
+        const int bdelta = __double2int_rn(M[3] * x * AB_SCALE);
+        const int X = (X0 + adelta) >> (AB_BITS - INTER_BITS);
+        const int Y = (Y0 + bdelta) >> (AB_BITS - INTER_BITS);
+        const int sx = X >> INTER_BITS, sy = Y >> INTER_BITS;
+        const int tx = X & (TAB - 1), ty = Y & (TAB - 1);
+        const int w[4] = {(32 - ty) * (32 - tx) * 32, (32 - ty) * tx * 32, ty * (32 - tx) * 32, ty * tx * 32};
+        int acc0 = 0, acc1 = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int qx = sx + (t & 1), qy = sy + (t >> 1);
+            if (qx >= 0 && qx < pw && qy >= 0 && qy < ph) {
+                const int fx = xmin + qx - cw, fy = ymin + qy - ch;
+                if (fx >= 0 && fx < W && fy >= 0 && fy < H) {
+                    acc0 += s0[(int64_t)fy * W + fx] * w[t];
+                    if (s1) acc1 += s1[(int64_t)fy * W + fx] * w[t];
+                }
+            }
+        }
+        acc0 = (acc0 + (1 << 14)) >> 15;
+        o0[i] = (uint8_t)(acc0 < 0 ? 0 : (acc0 > 255 ? 255 : acc0));
+        if (o1) {
+            acc1 = (acc1 + (1 << 14)) >> 15;
+            o1[i] = (uint8_t)(acc1 < 0 ? 0 : (acc1 > 255 ? 255 : acc1));
+        }
+    }
+}
+
+}  // namespace mdx
+
+using namespace mdx;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int mdx_prep_frames(const int16_t *raw, int64_t n, int H, int W, const double *bg, const uint8_t *roi,
+                               int y0, int y1, int x0, int x1, int flags, double vmin, double vmax, uint8_t *out,
+                               uint8_t *invalid, mdx_stream_t stream) {
+    MDX_REQUIRE(raw && out, "mdx_prep_frames: null raw/out");
+    MDX_REQUIRE(n >= 0 && H > 0 && W > 0, "mdx_prep_frames: bad shape n=%lld H=%d W=%d", (long long)n, H, W);
+    MDX_REQUIRE(0 <= y0 && y0 <= y1 && y1 <= H && 0 <= x0 && x0 <= x1 && x1 <= W,
+                "mdx_prep_frames: bad crop [%d,%d)x[%d,%d) for %dx%d", y0, y1, x0, x1, H, W);
+    const int oh = y1 - y0, ow = x1 - x0;
+    if (n == 0 || oh == 0 || ow == 0) return MDX_OK;
+    dim3 grid((unsigned)ceil_div((int64_t)oh * ow, 256), (unsigned)ceil_div(n, PREP_FRAMES_PER_BLOCK));
+    hipLaunchKernelGGL(k_prep, grid, dim3(256), 0, as_stream(stream), raw, n, H, W, bg, roi, y0, x0, oh, ow, flags,
+                       vmin, vmax, out, invalid);
+    MDX_CHECK_LAUNCH("mdx_prep_frames");
+    return MDX_OK;
+}
+
+extern "C" int mdx_build_scale_lut(double vmin, double vmax, int int_vmin, uint8_t lut[256]) {
+    MDX_REQUIRE(lut != nullptr, "mdx_build_scale_lut: null lut");
+    const double k = (255.0 - 0.0) / (vmax - vmin);
+    for (int v = 0; v < 256; ++v) {
+        const double d = int_vmin ? (double)(uint8_t)(v - (int)vmin) : (double)v - vmin;
+        const double r = d * k + 0.0;
+        lut[v] = (uint8_t)(int32_t)r;
+    }
+    return MDX_OK;
+}
+
+extern "C" int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t lut[256], uint8_t *out,
+                                mdx_stream_t stream) {
+    MDX_REQUIRE(in && out && lut, "mdx_scale_frames: null pointer");
+    if (count <= 0) return MDX_OK;
+    MDX_REQUIRE(((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0, "mdx_scale_frames: buffers must be 16-B aligned");
+    Lut256 L;
+    memcpy(L.v, lut, 256);
+    const int64_t nvec = count / 16;
+    int blocks = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(nvec, 256), 1), 2048);
+    hipLaunchKernelGGL(k_scale, dim3(blocks), dim3(256), 0, as_stream(stream), in, count, L, out);
+    MDX_CHECK_LAUNCH("mdx_scale_frames");
+    return MDX_OK;
+}
+
+extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k, const uint8_t *strel,
+                                int kh, int kw, int iters, uint8_t *out, mdx_stream_t stream) {
+    MDX_REQUIRE(src && out && src != out, "mdx_clean_frames: null or aliased buffers");
+    MDX_REQUIRE(median_k == 0 || median_k == 3, "mdx_clean_frames: median_k must be 0 or 3 (got %d)", median_k);
+    MDX_REQUIRE(iters >= 0, "mdx_clean_frames: iters < 0");
+    StrelSpans st{};
+    st.kh = 0;
+    if (iters > 0) {
+        MDX_REQUIRE(strel && kh > 0 && kw > 0 && kh <= MAX_KH && kw <= MAX_KH, "mdx_clean_frames: strel %dx%d", kh, kw);
+        st.kh = kh;
+        st.ay = kh / 2;
+        st.ax = kw / 2;
+        int rad = std::max(st.ay, kh - 1 - st.ay);
+        for (int r = 0; r < kh; ++r) {
+            int j1 = -1, j2 = -1;
+            for (int c = 0; c < kw; ++c) {
+                if (strel[r * kw + c]) {
+                    if (j1 < 0) j1 = c;
+                    MDX_REQUIRE(j2 < 0, "mdx_clean_frames: strel row %d is not one contiguous run", r);
+                    if (c + 1 == kw || !strel[r * kw + c + 1]) j2 = c + 1;
+                }
+            }
+            if (j1 < 0) j1 = j2 = 0;
+            st.j1[r] = (int8_t)j1;
+            st.j2[r] = (int8_t)j2;
+            if (j2 > j1) rad = std::max(rad, std::max(st.ax - j1, j2 - 1 - st.ax));
+        }
+        st.rad = rad;
+    }
+    if (n == 0) return MDX_OK;
+    const int halo = (median_k ? 1 : 0) + 2 * iters * st.rad;
+    MDX_REQUIRE(halo <= 96, "mdx_clean_frames: halo %d too large", halo);
+    const int tiles_x = (int)ceil_div(W, CT_W), tiles_y = (int)ceil_div(H, CT_H);
+    const size_t lds = 2 * (size_t)(CT_W + 2 * halo) * (CT_H + 2 * halo);
+    MDX_REQUIRE(lds <= 160 * 1024, "mdx_clean_frames: LDS %zu too large", lds);
+    MDX_REQUIRE(n <= 65535, "mdx_clean_frames: n > 65535 per call");
+    hipLaunchKernelGGL(k_clean, dim3(tiles_x * tiles_y, (unsigned)n), dim3(CT_THREADS), lds, as_stream(stream), src, H,
+                       W, median_k ? 1 : 0, st, iters, out, tiles_x, halo);
+    MDX_CHECK_LAUNCH("mdx_clean_frames");
+    return MDX_OK;
+}
+
+extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W, double thr,
+                                 double *centroid, double *orientation, double *axis_length, double *area,
+                                 mdx_stream_t stream) {
+    MDX_REQUIRE(frames && centroid && orientation && axis_length, "mdx_frame_moments: null pointer");
+    MDX_REQUIRE(H > 0 && W > 0, "mdx_frame_moments: bad shape");
+    if (n == 0) return MDX_OK;
+    const int pww = (int)ceil_div(W + 2, 32);
+    const size_t lds = (size_t)(H + 2) * pww * 4;
+    MDX_REQUIRE(lds <= 120 * 1024, "mdx_frame_moments: frame %dx%d too large for LDS", H, W);
+    MDX_REQUIRE(n <= 0x7fffffff, "mdx_frame_moments: n too large");
+    hipLaunchKernelGGL(k_moments, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask, H, W,
+                       thr, centroid, orientation, axis_length, area, pww);
+    MDX_CHECK_LAUNCH("mdx_frame_moments");
+    return MDX_OK;
+}
+
+extern "C" int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, int W,
+                               const double *center, const double *angle_deg, int cw, int ch, uint8_t *out0,
+                               uint8_t *out1, mdx_stream_t stream) {
+    MDX_REQUIRE(src0 && out0 && center && angle_deg, "mdx_crop_rotate: null pointer");
+    MDX_REQUIRE(!src1 == !out1, "mdx_crop_rotate: src1/out1 must both be set or both NULL");
+    MDX_REQUIRE(cw > 0 && ch > 0 && H > 0 && W > 0, "mdx_crop_rotate: bad shape");
+    if (n == 0) return MDX_OK;
+    hipLaunchKernelGGL(k_crop, dim3((unsigned)n), dim3(256), 0, as_stream(stream), src0, src1, H, W, center,
+                       angle_deg, cw, ch, out0, out1);
+    MDX_CHECK_LAUNCH("mdx_crop_rotate");
+    return MDX_OK;
+}

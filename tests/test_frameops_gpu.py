@@ -1,0 +1,135 @@
+"""GPU parity of the frame-op kernels against the CPU oracle (bit-exact for
+the integer/byte ops and the fixed-order float64 moment arithmetic)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def session(mdx):
+    from moseq2_detectron_extract_amd import synth
+    return synth.SyntheticSession(24, seed=3)
+
+
+@pytest.fixture(scope="module")
+def raw(session):
+    return session.frames(0, 24)
+
+
+def test_prep_matches_golden(mdx, golden):
+    from moseq2_detectron_extract_amd import proc
+    tags = sorted({k[len("prep_out_"):] for k in golden if k.startswith("prep_out_")})
+    for tag in tags:
+        vmin = float(golden[f"prep_vmin_{tag}"]); vmax = float(golden[f"prep_vmax_{tag}"])
+        out = proc.prep_raw_frames(golden[f"prep_raw_{tag}"], golden[f"prep_bg_{tag}"], golden[f"prep_roi_{tag}"],
+                                   None if np.isnan(vmin) else vmin, None if np.isnan(vmax) else vmax,
+                                   fix_invalid_pixels=False)
+        np.testing.assert_array_equal(out, golden[f"prep_out_{tag}"], err_msg=tag)
+
+
+def test_scale_matches_golden(mdx, golden):
+    from moseq2_detectron_extract_amd import proc
+    for k in range(5):
+        vmin, vmax = golden[f"scale_vmin_{k}"].item(), golden[f"scale_vmax_{k}"].item()
+        x = np.ascontiguousarray(golden[f"scale_in_{k}"])
+        np.testing.assert_array_equal(proc.scale_raw_frames(x, vmin, vmax), golden[f"scale_out_{k}"])
+
+
+def test_prep_full_size_and_invalid(mdx, session, raw):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    prep = proc.FramePrep(session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+    out, inv = prep(raw, return_invalid=True)
+    ref, rinv = O.prep_raw_frames(raw, session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+    assert out.shape == (24, 423, 511)
+    np.testing.assert_array_equal(out, ref)
+    np.testing.assert_array_equal(inv, rinv)
+
+
+@pytest.mark.parametrize("roi_kind", ["full", "arena"])
+def test_prep_with_inpaint(mdx, roi_kind):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc, synth
+    s = synth.SyntheticSession(6, seed=11, roi=roi_kind)
+    raw = s.frames(0, 6)
+    raw[2, 100:104, 200:203] = 0  # a larger hole to exercise the FMM order
+    raw[3, 0, :40] = 0            # invalid pixels on the frame edge (OpenCV skip quirk)
+    out = proc.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
+    ref, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100, fix_invalid_pixels=True)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_clean_frames(mdx, session, raw):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    prepped, _ = O.prep_raw_frames(raw[:6], session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+    for iters in (0, 1, 3):
+        got = proc.clean_frames(prepped, iters_tail=iters)
+        want = O.clean_frames(prepped, iters_tail=iters)
+        np.testing.assert_array_equal(got, want, err_msg=f"iters={iters}")
+    # no median, rect strel
+    got = proc.clean_frames(prepped, prefilter_space=None, strel_tail=np.ones((5, 5), np.uint8), iters_tail=2)
+    want = O.morph(prepped, "open", np.ones((5, 5), np.uint8), 2)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_clean_random_edges(mdx):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 256, size=(3, 71, 133), dtype=np.uint8)
+    np.testing.assert_array_equal(proc.clean_frames(x, iters_tail=2), O.clean_frames(x, iters_tail=2))
+
+
+def test_frame_features(mdx, session, raw):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    prepped, _ = O.prep_raw_frames(raw, session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+    cl = O.clean_frames(prepped, iters_tail=3)
+    rng = np.random.default_rng(0)
+    mask = (rng.random(cl.shape) < 0.97).astype(np.uint8)  # punch holes: many blobs / hole borders
+    for m in (None, mask):
+        got, _ = proc.get_frame_features(cl, frame_threshold=3, mask=m if m is not None else np.array([]))
+        want = O.get_frame_features(cl, 3, mask=m)
+        np.testing.assert_array_equal(got["centroid"], want["centroid"])
+        np.testing.assert_array_equal(got["axis_length"], want["axis_length"])
+        # atan2 may differ by an ulp between ocml and glibc
+        np.testing.assert_allclose(got["orientation"], want["orientation"], rtol=0, atol=4e-16 * 8)
+
+
+def test_frame_features_shapes(mdx):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    rng = np.random.default_rng(9)
+    f = np.zeros((5, 60, 90), np.uint8)
+    f[1, 10:20, 5:35] = 10                # rectangle
+    f[2] = (rng.random((60, 90)) < 0.45) * 9  # noise: many blobs, holes
+    f[3, 0:60, 0:90] = 50                 # full frame (touches the border)
+    f[3, 20:30, 40:50] = 0                # with a hole
+    f[4, 30, 40] = 7                      # single pixel -> NaN
+    got = proc.frame_moments(f, None, 3.0)
+    want = O.get_frame_features(f, 3)
+    for k in ("centroid", "axis_length", "area"):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), want[k], err_msg=k)
+    np.testing.assert_allclose(got["orientation"].cpu().numpy(), want["orientation"], atol=1e-14)
+    assert np.isnan(want["centroid"][0]).all() and np.isnan(want["centroid"][4]).all()
+
+
+def test_crop_and_rotate(mdx, session, raw):
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    prepped, _ = O.prep_raw_frames(raw, session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+    n = prepped.shape[0]
+    rng = np.random.default_rng(2)
+    centers = np.column_stack([rng.uniform(-5, 520, n), rng.uniform(-5, 430, n)])
+    centers[0] = [np.nan, 10]; centers[1] = [30.5, 12.25]; centers[2] = [600, 500]
+    angles = rng.uniform(0, 360, n); angles[3] = np.nan; angles[4] = 0.0; angles[5] = 90.0
+    masks = (prepped > 10).astype(np.uint8)
+    got, gotm = proc.crop_and_rotate_frames(prepped, centers, angles, frames2=masks)
+    want = O.crop_and_rotate_frames(prepped, centers, angles)
+    wantm = O.crop_and_rotate_frames(masks, centers, angles)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gotm, wantm)
+    one = proc.crop_and_rotate_frame(prepped[7], centers[7], angles[7])
+    np.testing.assert_array_equal(one, want[7])
