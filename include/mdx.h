@@ -98,6 +98,82 @@ int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, 
                     const double *center, const double *angle_deg, int cw, int ch,
                     uint8_t *out0, uint8_t *out1, mdx_stream_t stream);
 
+
+/* ---------------------------------------------------------------------
+ * Mask/Keypoint R-CNN forward (Predictor.__call__, M/model/predict.py:53-102,
+ * Detectron2 GeneralizedRCNN built by M/model/config.py:21-94).  Tensors are
+ * NHWC; dtype codes: 0 = float32, 1 = float16 (fp32 accumulation).
+ * ------------------------------------------------------------------- */
+
+/* Implicit-GEMM convolution / linear layer on MFMA:
+ * out = act(conv(x, w) + bias (+ residual)).  x (N,H,W,Cin); w packed
+ * [Cout][KH][KW][Cin] (FrozenBN folded); bias float32 [Cout] or NULL;
+ * residual like out or NULL; relu 0/1.  out_mode 0: (N,OH,OW,Cout);
+ * out_mode 1: ConvTranspose2d(k=2,s=2) pixel shuffle of a 1x1 GEMM with
+ * Cout = 4*Co -> (N,2H,2W,Co).  Cin must be a multiple of 8 (fp16) / 4 (fp32). */
+int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
+               int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
+               int in_dtype, int out_dtype, void *out, mdx_stream_t stream);
+
+/* scale_raw_frames LUT + replicate 1->C channels + (x - mean[c]) / std[c] + zero
+ * pad to (Hp, Wp) with Cp (>= C) channels.  frames uint8 (B,h,w). */
+int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], const float *mean,
+                   const float *std_, int C, int Cp, int Hp, int Wp, int dtype, void *out,
+                   mdx_stream_t stream);
+
+/* max_pool2d(k, s, p), NHWC. */
+int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
+                  mdx_stream_t stream);
+
+/* GroupNorm(G, C, eps) with affine; fuse 1: out = gn + up2(up), 2: (gn + up2(up)) / 2
+ * (FPN top-down, nearest x2).  stats: float workspace [N*G*2]. */
+int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, const float *gamma,
+                  const float *beta, const void *up, int fuse, int dtype, void *out, float *stats,
+                  mdx_stream_t stream);
+
+/* RPN find_top_rpn_proposals: per level head tensor float32 (B,H_l,W_l,A*5)
+ * = [objectness(A), deltas(A*4)]; cell_anchors float32 [L][A][4].
+ * out_boxes (B,post_topk,4), out_scores (B,post_topk) (logits, -inf pad),
+ * out_count (B).  workspace >= mdx_rpn_workspace_bytes(B, L, pre_topk). */
+int64_t mdx_rpn_workspace_bytes(int B, int L, int pre_topk);
+int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
+                      int L, int B, int A, const float *cell_anchors, float offset, int img_h, int img_w,
+                      int pre_topk, int post_topk, float nms_thresh, float min_size, float clampv,
+                      float *out_boxes, float *out_scores, int *out_count, void *workspace,
+                      mdx_stream_t stream);
+
+/* ROIPooler(ROIAlignV2): rois float32 (R,4) XYXY, R = B*per_image, rows with
+ * index >= counts[b] produce zeros.  out (R,P,P,C). */
+int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
+                  int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
+                  int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
+                  void *out, mdx_stream_t stream);
+
+/* fast_rcnn_inference_single_image + detector_postprocess for 1 class:
+ * pred float32 (B*R, ld_pred) = [cls0, bg, dx, dy, dw, dh].  Outputs
+ * (B,D,4), (B,D), int64 (B,D), ndet (B). */
+int mdx_box_postprocess(const float *pred, int ld_pred, const float *proposals, const int *counts, int B,
+                        int R, int D, float score_thresh, float nms_thresh, int img_h, int img_w,
+                        const float *reg_weights, float clampv, float *det_boxes, float *det_scores,
+                        int64_t *det_classes, int *ndet, mdx_stream_t stream);
+
+/* mask_rcnn_inference sigmoid + paste_masks_in_image (grid_sample) >= thresh:
+ * logits float32 (B*D, M, M) -> out uint8 (B, D, img_h, img_w). */
+int mdx_paste_masks(const float *logits, const float *boxes, const int *counts, int B, int D, int M,
+                    int img_h, int img_w, float thresh, uint8_t *out, mdx_stream_t stream);
+
+/* keypoint head score_lowres ConvTranspose2d(k=4, s=2, p=1): x (R,Hi,Wi,Cin),
+ * w float32 [Cin][Co][4][4] -> out float32 (R, Co, 2Hi, 2Wi). */
+int mdx_keypoint_deconv(const void *x, int R, int Hi, int Wi, int Cin, const float *w, const float *bias,
+                        int Co, int dtype, float *out, mdx_stream_t stream);
+
+/* F.interpolate(scale_factor=2, bilinear, align_corners=False), float32 NCHW. */
+int mdx_upsample_bilinear2x(const float *x, int NC, int H, int W, float *out, mdx_stream_t stream);
+
+/* heatmaps_to_keypoints: maps float32 (B*D, K, M, M) -> (B*D, K, 3) [x, y, score]. */
+int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
+                              int K, int M, float *out, mdx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

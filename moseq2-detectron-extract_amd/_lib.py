@@ -23,6 +23,7 @@ P = ctypes.c_void_p
 I64 = ctypes.c_int64
 I32 = ctypes.c_int
 F64 = ctypes.c_double
+F32 = ctypes.c_float
 
 # name -> (restype, argtypes); mirrors include/mdx.h
 SIGNATURES = {
@@ -36,6 +37,19 @@ SIGNATURES = {
     "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P]),
     "mdx_frame_moments": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P]),
     "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P]),
+    "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
+    "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),
+    "mdx_maxpool2d": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "mdx_groupnorm": (I32, [P, I32, I32, I32, I32, I32, F32, P, P, P, I32, I32, P, P, P]),
+    "mdx_rpn_workspace_bytes": (I64, [I32, I32, I32]),
+    "mdx_rpn_proposals": (I32, [P, P, P, P, I32, I32, I32, P, F32, I32, I32, I32, I32, F32, F32, F32,
+                                P, P, P, P, P]),
+    "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
+    "mdx_box_postprocess": (I32, [P, I32, P, P, I32, I32, I32, F32, F32, I32, I32, P, F32, P, P, P, P, P]),
+    "mdx_paste_masks": (I32, [P, P, P, I32, I32, I32, I32, I32, F32, P, P]),
+    "mdx_keypoint_deconv": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, P, P]),
+    "mdx_upsample_bilinear2x": (I32, [P, I32, I32, I32, P, P]),
+    "mdx_heatmaps_to_keypoints": (I32, [P, P, P, I32, I32, I32, I32, P, P]),
 }
 
 

@@ -1,0 +1,276 @@
+// Implicit-GEMM convolution / linear layer on MFMA (gfx950).
+//
+// Every convolution and FC layer of the Mask/Keypoint R-CNN forward (ResNet
+// stem + bottlenecks, FPN lateral/output, RPN head, box FCs, mask and keypoint
+// head convs, the 2x2/s2 mask deconv) is one launch of this kernel.
+//
+//   out[m][n] = act( sum_k A[m][k] * B[n][k] + bias[n] (+ res[m][n]) )
+//   m = (b, oy, ox) output pixel (NHWC rows), n = output channel,
+//   k = (ky, kx, ci), A gathered on the fly from the NHWC input (zero padding),
+//   B = weights packed [Cout][KH][KW][Cin] (Cin fastest, BN folded).
+//
+// Tiles: 128(M) x 128(N) per 256-thread workgroup, 4 waves as 2x2, each wave
+// 64x64 = 4x4 MFMA tiles of 16x16.  K staged through LDS in 128-byte rows
+// (BK = 64 halves or 32 floats), double-buffered, register-staged global loads
+// of 16 B per lane issued one K-step ahead.
+//   fp16:  v_mfma_f32_16x16x32_f16  (fp32 accumulate)
+//   fp32:  v_mfma_f32_16x16x4_f32   (exact fp32 products, fp32 accumulate)
+// Output modes: NHWC, or the ConvTranspose(k=2,s=2) pixel shuffle (N = 4*Co).
+// Blocks are remapped XCD-contiguously so the tiles that share an input row
+// panel run on one XCD's L2.
+#include "common.h"
+
+namespace mdx {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float float4v __attribute__((ext_vector_type(4)));
+
+template <typename T>
+struct Prec;
+template <>
+struct Prec<_Float16> {
+    static constexpr int BK = 64, VEC = 8;
+};
+template <>
+struct Prec<float> {
+    static constexpr int BK = 32, VEC = 4;
+};
+
+constexpr int BM = 128, BN = 128, CONV_THREADS = 256;
+constexpr int ROWB = 128;          // bytes of K per LDS row
+constexpr int PITCH = ROWB + 16;   // padded row pitch (bytes)
+constexpr int TILE_BYTES = BM * PITCH;
+
+struct ConvArgs {
+    const void *x;
+    const void *w;
+    const float *bias;  // [N] or null
+    const void *res;    // [M][N] (same dtype as out) or null
+    void *out;
+    int H, W, Cin, Cout, KH, KW, stride, pad, OH, OW;
+    int M, K;
+    int relu;
+    int out_mode;  // 0: NHWC, 1: deconv2x2 pixel shuffle
+    int tiles_n, tiles_total;
+};
+
+template <typename TO>
+__device__ __forceinline__ void store_out(TO *p, float v) { *p = (TO)v; }
+
+template <typename T, typename TO>
+__global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
+    constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *As = smem;                       // [2][BM][PITCH]
+    char *Bs = smem + 2 * TILE_BYTES;      // [2][BN][PITCH]
+
+    // XCD-contiguous remap of the linear block id (bijective)
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // ---- per-thread load descriptors: rows tid/8 + 32*i, 16-byte chunk tid%8
+    const int kc = tid & 7;
+    const int lrow = tid >> 3;
+    int a_iy0[4], a_ix0[4];
+    long long a_base[4];
+    bool a_ok[4];
+    const int ohw = a.OH * a.OW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int gm = m0 + lrow + 32 * i;
+        a_ok[i] = gm < a.M;
+        const int gmc = a_ok[i] ? gm : 0;
+        const int b = gmc / ohw, rem = gmc - b * ohw;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_iy0[i] = oy * a.stride - a.pad;
+        a_ix0[i] = ox * a.stride - a.pad;
+        a_base[i] = (long long)b * a.H * a.W * a.Cin;
+    }
+    // k decomposition of this thread's chunk, advanced by BK per K-step
+    int kci = (kc * VEC) % a.Cin;
+    int kr = (kc * VEC) / a.Cin;
+    int kkx = kr % a.KW, kky = kr / a.KW;
+    int kglob = kc * VEC;
+
+    const T *X = reinterpret_cast<const T *>(a.x);
+    const T *Wt = reinterpret_cast<const T *>(a.w);
+    uint4 ra[4], rb[4];
+
+    auto load_global = [&]() {
+        const bool kok = kglob < a.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                v = *reinterpret_cast<const uint4 *>(X + a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci);
+            ra[i] = v;
+            const int gn = n0 + lrow + 32 * i;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (kok && gn < a.Cout) u = *reinterpret_cast<const uint4 *>(Wt + (long long)gn * a.K + kglob);
+            rb[i] = u;
+        }
+    };
+    auto advance_k = [&]() {
+        kglob += BK;
+        kci += BK;
+        while (kci >= a.Cin) {
+            kci -= a.Cin;
+            if (++kkx == a.KW) {
+                kkx = 0;
+                ++kky;
+            }
+        }
+    };
+    auto store_lds = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int off = buf * TILE_BYTES + (lrow + 32 * i) * PITCH + kc * 16;
+            *reinterpret_cast<uint4 *>(As + off) = ra[i];
+            *reinterpret_cast<uint4 *>(Bs + off) = rb[i];
+        }
+    };
+
+    float4v acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (a.K + BK - 1) / BK;
+    load_global();
+    advance_k();
+    store_lds(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            load_global();
+            advance_k();
+        }
+        const char *Ab = As + cur * TILE_BYTES + (wm * 64 + (lane & 15)) * PITCH;
+        const char *Bb = Bs + cur * TILE_BYTES + (wn * 64 + (lane & 15)) * PITCH;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int koff = s * 64 + (lane >> 4) * 16;
+            if constexpr (sizeof(T) == 2) {
+                half8 af[4], bf[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * PITCH + koff);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * PITCH + koff);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            } else {
+                float4v af[4], bf[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+            }
+        }
+        if (more) store_lds(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: bias, residual, ReLU, store (C/D: col = lane&15, row = 4*(lane>>4)+r)
+    TO *O = reinterpret_cast<TO *>(a.out);
+    const TO *RS = reinterpret_cast<const TO *>(a.res);
+    const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int gn = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (gn >= a.Cout) continue;
+        const float bv = a.bias ? a.bias[gn] : 0.f;
+        int q = 0, co = gn;
+        if (a.out_mode == 1) {
+            q = gn / Co;
+            co = gn - q * Co;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gm = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                if (gm >= a.M) continue;
+                float v = acc[i][j][r] + bv;
+                long long oi;
+                if (a.out_mode == 0) {
+                    oi = (long long)gm * a.Cout + gn;
+                } else {
+                    const int b = gm / ohw, rem = gm - b * ohw;
+                    const int y = rem / a.OW, xx = rem - y * a.OW;
+                    oi = (((long long)b * (2 * a.OH) + 2 * y + (q >> 1)) * (2 * a.OW) + 2 * xx + (q & 1)) * Co + co;
+                }
+                if (RS) v += (float)RS[oi];
+                if (a.relu) v = v > 0.f ? v : 0.f;
+                store_out<TO>(O + oi, v);
+            }
+        }
+    }
+}
+
+}  // namespace mdx
+
+using namespace mdx;
+
+// dtype codes: 0 = fp32, 1 = fp16
+extern "C" int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
+                          int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
+                          int in_dtype, int out_dtype, void *out, mdx_stream_t stream) {
+    MDX_REQUIRE(x && w && out, "mdx_conv2d: null pointer");
+    MDX_REQUIRE(in_dtype == 0 || in_dtype == 1, "mdx_conv2d: in_dtype must be 0 (f32) or 1 (f16)");
+    MDX_REQUIRE(out_dtype == 0 || out_dtype == 1, "mdx_conv2d: out_dtype must be 0 (f32) or 1 (f16)");
+    const int VEC = in_dtype == 1 ? 8 : 4;
+    MDX_REQUIRE(Cin % VEC == 0, "mdx_conv2d: Cin=%d must be a multiple of %d (pad channels)", Cin, VEC);
+    MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+                "mdx_conv2d: bad shape");
+    MDX_REQUIRE(out_mode == 0 || (out_mode == 1 && KH == 1 && KW == 1 && stride == 1 && pad == 0 && Cout % 4 == 0),
+                "mdx_conv2d: out_mode 1 (deconv2x2) needs a 1x1/s1 GEMM with Cout = 4*Co");
+    const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+    MDX_REQUIRE(OH > 0 && OW > 0, "mdx_conv2d: empty output");
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.res = residual; a.out = out;
+    a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.OH = OH; a.OW = OW;
+    const long long M = (long long)N * OH * OW;
+    MDX_REQUIRE(M < (1ll << 31), "mdx_conv2d: M too large");
+    a.M = (int)M;
+    a.K = KH * KW * Cin;
+    a.relu = relu;
+    a.out_mode = out_mode;
+    const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, BN);
+    a.tiles_n = tiles_n;
+    a.tiles_total = tiles_m * tiles_n;
+    const size_t lds = 4 * (size_t)TILE_BYTES;
+    hipStream_t s = as_stream(stream);
+    if (in_dtype == 1 && out_dtype == 1)
+        hipLaunchKernelGGL((k_conv<_Float16, _Float16>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+    else if (in_dtype == 1 && out_dtype == 0)
+        hipLaunchKernelGGL((k_conv<_Float16, float>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+    else if (in_dtype == 0 && out_dtype == 0)
+        hipLaunchKernelGGL((k_conv<float, float>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_conv<float, _Float16>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+    MDX_CHECK_LAUNCH("mdx_conv2d");
+    return MDX_OK;
+}

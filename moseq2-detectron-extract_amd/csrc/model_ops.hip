@@ -1,0 +1,1041 @@
+// Non-GEMM kernels of the Mask/Keypoint R-CNN forward (gfx950).
+//
+//   k_preprocess     scale LUT + (x - mean)/std + zero pad to /32, NHWC
+//                    (Predictor.__call__ M/model/predict.py:53-102 +
+//                     GeneralizedRCNN.preprocess_image; scale_raw_frames fused)
+//   k_maxpool        stem max_pool2d(3,2,1) and LastLevelMaxPool (k1,s2)
+//   k_gn_stats/apply GroupNorm(32) of the FPN convs, fused with the top-down
+//                    nearest x2 upsample + add (+ /2 for FUSE_TYPE avg)
+//   k_rpn_topk       per (image, level): radix-select top-k objectness,
+//                    bitonic sort, anchor decode (Box2BoxTransform), clip,
+//                    nonempty                        (find_top_rpn_proposals)
+//   k_nms_mask/scan  greedy NMS on score-sorted boxes: IoU bitmask + one-wave
+//                    serial sweep                     (torchvision nms)
+//   k_rpn_merge      batched_nms merge of levels, top post_nms_topk
+//   k_roi_align      ROIPooler + ROIAlignV2 (level assignment, adaptive grid)
+//   k_box_post       softmax, decode (10,10,5,5), clip, score filter, NMS,
+//                    top-k, detector_postprocess nonempty
+//   k_paste          mask sigmoid + paste_masks_in_image (grid_sample) >= 0.5
+//   k_kp_deconv      ConvTranspose2d(k4, s2, p1) of the keypoint head
+//   k_upsample2x     F.interpolate(x2, bilinear, align_corners=False)
+//   k_heatmap_kp     heatmaps_to_keypoints (bicubic resize, argmax, score)
+// Float arithmetic follows the reference's operation order with FMA
+// contraction disabled.
+#include <cfloat>
+#include <cmath>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace mdx {
+
+constexpr int MAX_LEVELS = 8;
+
+template <typename T>
+__device__ __forceinline__ float ld(const T *p) {
+    return (float)*p;
+}
+template <typename T>
+__device__ __forceinline__ void st(T *p, float v) {
+    *p = (T)v;
+}
+
+// ---------------------------------------------------------------------------
+// preprocess
+// ---------------------------------------------------------------------------
+struct PrepArgs {
+    uint8_t lut[256];
+    float mean[4], stdv[4];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_preprocess(const uint8_t *__restrict__ fr, int B, int h, int w, int C, int Cp,
+                                                    int Hp, int Wp, PrepArgs pa, T *__restrict__ out) {
+    const long long total = (long long)B * Hp * Wp;
+    for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+        const int b = (int)(p / ((long long)Hp * Wp));
+        const int rem = (int)(p - (long long)b * Hp * Wp);
+        const int y = rem / Wp, x = rem - y * Wp;
+        T *o = out + p * Cp;
+        if (y < h && x < w) {
+            const float v = (float)pa.lut[fr[((long long)b * h + y) * w + x]];
+            for (int c = 0; c < Cp; ++c) o[c] = c < C ? (T)((v - pa.mean[c]) / pa.stdv[c]) : (T)0.f;
+        } else {
+            for (int c = 0; c < Cp; ++c) o[c] = (T)0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// maxpool NHWC
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_maxpool(const T *__restrict__ x, int N, int H, int W, int C, int k, int s,
+                                                 int p, int OH, int OW, T *__restrict__ out) {
+    const long long total = (long long)N * OH * OW * C;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        long long r = i / C;
+        const int ox = (int)(r % OW);
+        r /= OW;
+        const int oy = (int)(r % OH);
+        const int n = (int)(r / OH);
+        float m = -INFINITY;
+        for (int ky = 0; ky < k; ++ky) {
+            const int iy = oy * s - p + ky;
+            if (iy < 0 || iy >= H) continue;
+            for (int kx = 0; kx < k; ++kx) {
+                const int ix = ox * s - p + kx;
+                if (ix < 0 || ix >= W) continue;
+                const float v = ld(x + (((long long)n * H + iy) * W + ix) * C + c);
+                m = v > m ? v : m;
+            }
+        }
+        st(out + i, m);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GroupNorm
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum(float v, float *red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float s = 0.f;
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    return s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int HW, int C, int G, float eps,
+                                                  float *__restrict__ stats) {
+    __shared__ float red[8];
+    const int bg = blockIdx.x;
+    const int b = bg / G, g = bg - b * G;
+    const int cpg = C / G;
+    const long long base = (long long)b * HW * C + (long long)g * cpg;
+    const long long cnt = (long long)HW * cpg;
+    float s = 0.f;
+    for (long long i = threadIdx.x; i < cnt; i += 256) {
+        const long long px = i / cpg, c = i - px * cpg;
+        s += ld(x + base + px * C + c);
+    }
+    const float mean = block_sum(s, red) / (float)cnt;
+    float s2 = 0.f;
+    for (long long i = threadIdx.x; i < cnt; i += 256) {
+        const long long px = i / cpg, c = i - px * cpg;
+        const float d = ld(x + base + px * C + c) - mean;
+        s2 += d * d;
+    }
+    const float var = block_sum(s2, red) / (float)cnt;
+    if (threadIdx.x == 0) {
+        stats[2 * bg] = mean;
+        stats[2 * bg + 1] = 1.0f / sqrtf(var + eps);
+    }
+}
+
+// y = (x - mean) * rstd * gamma + beta; optionally fused: y = (y + up(prev)) * scale
+template <typename T>
+__global__ __launch_bounds__(256) void k_gn_apply(const T *__restrict__ x, int N, int H, int W, int C, int G,
+                                                  const float *__restrict__ stats, const float *__restrict__ gamma,
+                                                  const float *__restrict__ beta, const T *__restrict__ up, int fuse,
+                                                  T *__restrict__ out) {
+    const long long total = (long long)N * H * W * C;
+    const int cpg = C / G;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const long long pix = i / C;
+        const int n = (int)(pix / ((long long)H * W));
+        const int g = c / cpg;
+        const float mean = stats[2 * (n * G + g)], rstd = stats[2 * (n * G + g) + 1];
+        float y = (ld(x + i) - mean) * rstd * gamma[c] + beta[c];
+        if (fuse) {
+            const int rem = (int)(pix - (long long)n * H * W);
+            const int yy = rem / W, xx = rem - yy * W;
+            const int UH = H / 2, UW = W / 2;
+            const float u = ld(up + (((long long)n * UH + (yy >> 1)) * UW + (xx >> 1)) * C + c);
+            y = y + u;
+            if (fuse == 2) y = y / 2.0f;
+        }
+        st(out + i, y);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// box helpers (Box2BoxTransform.apply_deltas, Boxes.clip / nonempty)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void apply_delta(const float *box, float dxr, float dyr, float dwr, float dhr,
+                                            const float *wts, float clampv, float *o) {
+    const float widths = box[2] - box[0];
+    const float heights = box[3] - box[1];
+    const float ctr_x = box[0] + 0.5f * widths;
+    const float ctr_y = box[1] + 0.5f * heights;
+    const float dx = dxr / wts[0], dy = dyr / wts[1];
+    float dw = dwr / wts[2], dh = dhr / wts[3];
+    dw = dw > clampv ? clampv : dw;
+    dh = dh > clampv ? clampv : dh;
+    const float pcx = dx * widths + ctr_x;
+    const float pcy = dy * heights + ctr_y;
+    const float pw = expf(dw) * widths;
+    const float ph = expf(dh) * heights;
+    o[0] = pcx - 0.5f * pw;
+    o[1] = pcy - 0.5f * ph;
+    o[2] = pcx + 0.5f * pw;
+    o[3] = pcy + 0.5f * ph;
+}
+
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ unsigned fkey(float v) {
+    const unsigned u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// bitonic sort of n (power of two, <= blockDim*k) (key, val) pairs in LDS,
+// descending by key then ascending by val
+__device__ void bitonic_desc(unsigned *key, unsigned *val, int n) {
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < n / 2; i += blockDim.x) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = ((lo & size) == 0);  // segment direction
+                const unsigned ka = key[lo], kb = key[hi], va = val[lo], vb = val[hi];
+                // "a before b" in final (descending key, ascending val) order
+                const bool a_first = ka > kb || (ka == kb && va < vb);
+                const bool swap = up ? !a_first : a_first;
+                if (swap) {
+                    key[lo] = kb; key[hi] = ka;
+                    val[lo] = vb; val[hi] = va;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// RPN: top-k + decode per (image, level)
+// ---------------------------------------------------------------------------
+struct RpnLevels {
+    const float *head[MAX_LEVELS];  // (B, H, W, A*5) f32: [obj(A), deltas(A*4)]
+    int H[MAX_LEVELS], W[MAX_LEVELS], stride[MAX_LEVELS];
+    float cell[MAX_LEVELS][4][4];  // up to 4 aspect ratios
+    int L, A, B, pre_topk;
+    float offset, img_h, img_w, min_size, clampv;
+};
+
+constexpr int TOPK_THREADS = 1024, TOPK_MAX = 1024;
+
+__global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *__restrict__ ws_boxes,
+                                                           float *__restrict__ ws_scores, int *__restrict__ ws_valid,
+                                                           int *__restrict__ ws_k) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_key[TOPK_MAX], s_val[TOPK_MAX];
+    __shared__ unsigned s_prefix, s_kk, s_cnt_gt, s_cnt_eq;
+    const int seg = blockIdx.x;  // b * L + l
+    const int b = seg / rl.L, l = seg - b * rl.L;
+    const int A = rl.A, CH = A * 5;
+    const int HW = rl.H[l] * rl.W[l];
+    const int n = HW * A;
+    const int k = n < rl.pre_topk ? n : rl.pre_topk;
+    const float *hd = rl.head[l] + (long long)b * HW * CH;
+    auto keyat = [&](int i) {
+        const int pix = i / A, a = i - pix * A;
+        return fkey(hd[(long long)pix * CH + a]);
+    };
+    // radix select of the k-th largest key
+    unsigned prefix = 0, mask = 0, kk = (unsigned)k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = threadIdx.x; i < 256; i += TOPK_THREADS) hist[i] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
+            const unsigned key = keyat(i);
+            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned above = 0;
+            int d = 255;
+            for (; d > 0; --d) {
+                if (above + hist[d] >= kk) break;
+                above += hist[d];
+            }
+            s_prefix = prefix | ((unsigned)d << shift);
+            s_kk = kk - above;
+        }
+        __syncthreads();
+        prefix = s_prefix;
+        kk = s_kk;
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    const unsigned T = prefix;  // k-th largest key; take kk of the ties (lowest indices)
+    if (threadIdx.x == 0) {
+        s_cnt_gt = 0;
+        s_cnt_eq = 0;
+    }
+    for (int i = threadIdx.x; i < TOPK_MAX; i += TOPK_THREADS) {
+        s_key[i] = 0;
+        s_val[i] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const unsigned n_gt = (unsigned)k - kk;
+    // keys > T (any order, sorted later); keys == T in index order (ordered scan)
+    for (int base = 0; base < n; base += TOPK_THREADS) {
+        const int i = base + threadIdx.x;
+        unsigned key = 0;
+        bool gt = false, eq = false;
+        if (i < n) {
+            key = keyat(i);
+            gt = key > T;
+            eq = key == T;
+        }
+        if (gt) {
+            const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
+            s_key[pos] = key;
+            s_val[pos] = (unsigned)i;
+        }
+        // ordered compaction of ties: prefix count within the chunk
+        const unsigned long long bal = __ballot(eq);
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        __shared__ unsigned wcnt[TOPK_THREADS / 64];
+        if (lane == 0) wcnt[wid] = (unsigned)__popcll(bal);
+        __syncthreads();
+        if (eq) {
+            unsigned before = s_cnt_eq;
+            for (int w2 = 0; w2 < wid; ++w2) before += wcnt[w2];
+            before += (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+            if (before < kk) {
+                s_key[n_gt + before] = key;
+                s_val[n_gt + before] = (unsigned)i;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned tot = 0;
+            for (int w2 = 0; w2 < TOPK_THREADS / 64; ++w2) tot += wcnt[w2];
+            s_cnt_eq += tot;
+        }
+        __syncthreads();
+    }
+    bitonic_desc(s_key, s_val, TOPK_MAX);
+    // decode the k sorted entries
+    const int st = rl.stride[l];
+    float *ob = ws_boxes + (long long)seg * rl.pre_topk * 4;
+    float *os = ws_scores + (long long)seg * rl.pre_topk;
+    int *ov = ws_valid + (long long)seg * rl.pre_topk;
+    const float wts[4] = {1.f, 1.f, 1.f, 1.f};
+    for (int r = threadIdx.x; r < k; r += TOPK_THREADS) {
+        const int i = (int)s_val[r];
+        const int pix = i / A, a = i - pix * A;
+        const int y = pix / rl.W[l], x = pix - y * rl.W[l];
+        const float sx = rl.offset * (float)st + (float)(x * st);
+        const float sy = rl.offset * (float)st + (float)(y * st);
+        const float anc[4] = {sx + rl.cell[l][a][0], sy + rl.cell[l][a][1], sx + rl.cell[l][a][2],
+                              sy + rl.cell[l][a][3]};
+        const float *dl = hd + (long long)pix * CH + A + a * 4;
+        float bx[4];
+        apply_delta(anc, dl[0], dl[1], dl[2], dl[3], wts, rl.clampv, bx);
+        const float score = hd[(long long)pix * CH + a];
+        bool fin = isfinite(bx[0]) && isfinite(bx[1]) && isfinite(bx[2]) && isfinite(bx[3]) && isfinite(score);
+        bx[0] = clampf(bx[0], 0.f, rl.img_w);
+        bx[1] = clampf(bx[1], 0.f, rl.img_h);
+        bx[2] = clampf(bx[2], 0.f, rl.img_w);
+        bx[3] = clampf(bx[3], 0.f, rl.img_h);
+        const bool ne = (bx[2] - bx[0]) > rl.min_size && (bx[3] - bx[1]) > rl.min_size;
+        ob[4 * r + 0] = bx[0];
+        ob[4 * r + 1] = bx[1];
+        ob[4 * r + 2] = bx[2];
+        ob[4 * r + 3] = bx[3];
+        os[r] = score;
+        ov[r] = (fin && ne) ? 1 : 0;
+    }
+    if (threadIdx.x == 0) ws_k[seg] = k;
+}
+
+// ---------------------------------------------------------------------------
+// NMS over score-sorted segments
+// ---------------------------------------------------------------------------
+// mask[seg][i][w]: bit j%64 of word w set when IoU(i, j) > thresh, j > i
+__global__ __launch_bounds__(256) void k_nms_mask(const float *__restrict__ boxes, const int *__restrict__ kseg,
+                                                  int cap, int words, float thresh,
+                                                  unsigned long long *__restrict__ mask) {
+    const int seg = blockIdx.y;
+    const int k = kseg[seg];
+    const float *bx = boxes + (long long)seg * cap * 4;
+    unsigned long long *mk = mask + (long long)seg * cap * words;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < k * words; t += gridDim.x * 256) {
+        const int i = t / words, w = t - i * words;
+        const float ix1 = bx[4 * i], iy1 = bx[4 * i + 1], ix2 = bx[4 * i + 2], iy2 = bx[4 * i + 3];
+        const float iarea = (ix2 - ix1) * (iy2 - iy1);
+        unsigned long long bits = 0ull;
+        const int j0 = w * 64;
+        for (int jj = 0; jj < 64; ++jj) {
+            const int j = j0 + jj;
+            if (j <= i || j >= k) continue;
+            const float jx1 = bx[4 * j], jy1 = bx[4 * j + 1], jx2 = bx[4 * j + 2], jy2 = bx[4 * j + 3];
+            const float xx1 = fmaxf(ix1, jx1), yy1 = fmaxf(iy1, jy1);
+            const float xx2 = fminf(ix2, jx2), yy2 = fminf(iy2, jy2);
+            const float w_ = fmaxf(0.f, xx2 - xx1), h_ = fmaxf(0.f, yy2 - yy1);
+            const float inter = w_ * h_;
+            const float jarea = (jx2 - jx1) * (jy2 - jy1);
+            const float ovr = inter / (iarea + jarea - inter);
+            if (ovr > thresh) bits |= 1ull << jj;
+        }
+        mk[(long long)i * words + w] = bits;
+    }
+}
+
+// one wave per segment: greedy sweep in score order; invalid boxes never keep
+// nor suppress (Detectron2 removes them before NMS)
+__global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, const int *__restrict__ kseg, int cap,
+                                                 int words, const unsigned long long *__restrict__ mask,
+                                                 int *__restrict__ keep) {
+    const int seg = blockIdx.x, lane = threadIdx.x;
+    const int k = kseg[seg];
+    const int *vl = valid + (long long)seg * cap;
+    const unsigned long long *mk = mask + (long long)seg * cap * words;
+    int *kp = keep + (long long)seg * cap;
+    unsigned long long removed = 0ull;  // lane w < words holds word w
+    for (int i = 0; i < k; ++i) {
+        const unsigned long long rw = __shfl(removed, i >> 6);
+        const bool sup = (rw >> (i & 63)) & 1ull;
+        const bool ok = !sup && vl[i];
+        if (lane == 0) kp[i] = ok ? 1 : 0;
+        if (ok && lane < words) removed |= mk[(long long)i * words + lane];
+    }
+    for (int i = k + lane; i < cap; i += 64) kp[i] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// merge levels: batched_nms result sorted by score, first post_topk
+// ---------------------------------------------------------------------------
+constexpr int MERGE_MAX = 8192;
+
+__global__ __launch_bounds__(1024) void k_rpn_merge(const float *__restrict__ ws_boxes,
+                                                    const float *__restrict__ ws_scores,
+                                                    const int *__restrict__ keep, const int *__restrict__ kseg,
+                                                    int L, int cap, int post_topk, float *__restrict__ out_boxes,
+                                                    float *__restrict__ out_scores, int *__restrict__ out_count) {
+    extern __shared__ unsigned sm[];
+    unsigned *key = sm, *val = sm + MERGE_MAX;
+    __shared__ unsigned s_n;
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0) s_n = 0;
+    for (int i = threadIdx.x; i < MERGE_MAX; i += blockDim.x) {
+        key[i] = 0;
+        val[i] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (int l = 0; l < L; ++l) {
+        const int seg = b * L + l;
+        const int k = kseg[seg];
+        for (int r = threadIdx.x; r < k; r += blockDim.x) {
+            if (keep[(long long)seg * cap + r]) {
+                const unsigned pos = atomicAdd(&s_n, 1u);
+                key[pos] = fkey(ws_scores[(long long)seg * cap + r]);
+                val[pos] = (unsigned)(l * cap + r);  // level-major tie order
+            }
+        }
+    }
+    __syncthreads();
+    const int n = (int)s_n;
+    int sz = 1;
+    while (sz < n) sz <<= 1;
+    bitonic_desc(key, val, sz < 2 ? 2 : sz);
+    const int m = n < post_topk ? n : post_topk;
+    for (int r = threadIdx.x; r < post_topk; r += blockDim.x) {
+        float *ob = out_boxes + ((long long)b * post_topk + r) * 4;
+        if (r < m) {
+            const unsigned v = val[r];
+            const int l = (int)(v / cap), rr = (int)(v - (unsigned)l * cap);
+            const long long src = (long long)(b * L + l) * cap + rr;
+            ob[0] = ws_boxes[src * 4];
+            ob[1] = ws_boxes[src * 4 + 1];
+            ob[2] = ws_boxes[src * 4 + 2];
+            ob[3] = ws_boxes[src * 4 + 3];
+            out_scores[(long long)b * post_topk + r] = ws_scores[src];
+        } else {
+            ob[0] = ob[1] = ob[2] = ob[3] = 0.f;
+            out_scores[(long long)b * post_topk + r] = -INFINITY;
+        }
+    }
+    if (threadIdx.x == 0) out_count[b] = m;
+}
+
+// ---------------------------------------------------------------------------
+// ROIAlign (ROIPooler, ROIAlignV2)
+// ---------------------------------------------------------------------------
+struct RoiLevels {
+    const void *feat[MAX_LEVELS];
+    int H[MAX_LEVELS], W[MAX_LEVELS];
+    float scale[MAX_LEVELS];
+    int L, min_level, C, P, sampling, aligned, per_image;
+    float canonical_size, canonical_level;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
+                                                   const int *__restrict__ counts, T *__restrict__ out) {
+    const int r = blockIdx.x;
+    const int b = r / rl.per_image, ri = r - b * rl.per_image;
+    const int C = rl.C, P = rl.P;
+    T *o = out + (long long)r * P * P * C;
+    if (ri >= counts[b]) {
+        for (int i = threadIdx.x; i < P * P * C; i += 256) o[i] = (T)0.f;
+        return;
+    }
+    const float x1 = rois[4 * r], y1 = rois[4 * r + 1], x2 = rois[4 * r + 2], y2 = rois[4 * r + 3];
+    // level assignment (assign_boxes_to_levels)
+    const float area = (x2 - x1) * (y2 - y1);
+    const float bs = sqrtf(area);
+    float lv = floorf(rl.canonical_level + log2f(bs / rl.canonical_size + 1e-8f));
+    const float maxl = (float)(rl.min_level + rl.L - 1);
+    lv = lv < (float)rl.min_level ? (float)rl.min_level : (lv > maxl ? maxl : lv);
+    const int li = (int)lv - rl.min_level;
+    const T *f = reinterpret_cast<const T *>(rl.feat[li]) + (long long)b * rl.H[li] * rl.W[li] * C;
+    const int H = rl.H[li], W = rl.W[li];
+    const float sc = rl.scale[li];
+    const float off = rl.aligned ? 0.5f : 0.f;
+    const float rsw = x1 * sc - off, rsh = y1 * sc - off;
+    const float rew = x2 * sc - off, reh = y2 * sc - off;
+    float rw = rew - rsw, rh = reh - rsh;
+    if (!rl.aligned) {
+        rw = fmaxf(rw, 1.f);
+        rh = fmaxf(rh, 1.f);
+    }
+    const float bh = rh / (float)P, bw = rw / (float)P;
+    const int gh = rl.sampling > 0 ? rl.sampling : (int)ceilf(rh / (float)P);
+    const int gw = rl.sampling > 0 ? rl.sampling : (int)ceilf(rw / (float)P);
+    const float count = (float)max(gh * gw, 1);
+    for (int t = threadIdx.x; t < P * P * C; t += 256) {
+        const int c = t % C;
+        const int bin = t / C;
+        const int ph = bin / P, pw = bin - ph * P;
+        float acc = 0.f;
+        for (int iy = 0; iy < gh; ++iy) {
+            float y = rsh + (float)ph * bh + ((float)iy + .5f) * bh / (float)gh;
+            for (int ix = 0; ix < gw; ++ix) {
+                float x = rsw + (float)pw * bw + ((float)ix + .5f) * bw / (float)gw;
+                if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) continue;
+                float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
+                int yl = (int)yy, xl = (int)xx, yh, xh;
+                if (yl >= H - 1) {
+                    yh = yl = H - 1;
+                    yy = (float)yl;
+                } else
+                    yh = yl + 1;
+                if (xl >= W - 1) {
+                    xh = xl = W - 1;
+                    xx = (float)xl;
+                } else
+                    xh = xl + 1;
+                const float ly = yy - (float)yl, lx = xx - (float)xl;
+                const float hy = 1.f - ly, hx = 1.f - lx;
+                const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+                const float v1 = ld(f + ((long long)yl * W + xl) * C + c);
+                const float v2 = ld(f + ((long long)yl * W + xh) * C + c);
+                const float v3 = ld(f + ((long long)yh * W + xl) * C + c);
+                const float v4 = ld(f + ((long long)yh * W + xh) * C + c);
+                acc += w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+            }
+        }
+        st(o + t, acc / count);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// box head post-process (fast_rcnn_inference_single_image + detector_postprocess)
+// ---------------------------------------------------------------------------
+struct BoxPostArgs {
+    int R, ld_pred;  // rows per image, row stride of pred (f32 columns)
+    int D;           // detections per image
+    float score_thresh, nms_thresh, img_h, img_w, clampv;
+    float wts[4];
+};
+
+__global__ __launch_bounds__(1024) void k_box_post(BoxPostArgs ba, const float *__restrict__ pred,
+                                                   const float *__restrict__ props, const int *__restrict__ counts,
+                                                   float *__restrict__ det_boxes, float *__restrict__ det_scores,
+                                                   long long *__restrict__ det_classes, int *__restrict__ ndet) {
+    __shared__ unsigned key[1024], val[1024];
+    __shared__ float bxs[1024][4];
+    __shared__ float scs[1024];
+    const int b = blockIdx.x;
+    const int R = ba.R;
+    for (int i = threadIdx.x; i < 1024; i += 1024) {
+        key[i] = 0;
+        val[i] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const int n = counts[b];
+    for (int r = threadIdx.x; r < R && r < 1024; r += 1024) {
+        if (r >= n) continue;
+        const float *p = pred + ((long long)b * R + r) * ba.ld_pred;
+        // softmax over (cls0, bg)
+        const float l0 = p[0], l1 = p[1];
+        const float mx = fmaxf(l0, l1);
+        const float e0 = expf(l0 - mx), e1 = expf(l1 - mx);
+        const float sum = e0 + e1;
+        const float s0 = e0 / sum;
+        float bx[4];
+        apply_delta(props + ((long long)b * R + r) * 4, p[2], p[3], p[4], p[5], ba.wts, ba.clampv, bx);
+        const bool fin = isfinite(bx[0]) && isfinite(bx[1]) && isfinite(bx[2]) && isfinite(bx[3]) && isfinite(s0) &&
+                         isfinite(e1 / sum);
+        bx[0] = clampf(bx[0], 0.f, ba.img_w);
+        bx[1] = clampf(bx[1], 0.f, ba.img_h);
+        bx[2] = clampf(bx[2], 0.f, ba.img_w);
+        bx[3] = clampf(bx[3], 0.f, ba.img_h);
+        bxs[r][0] = bx[0]; bxs[r][1] = bx[1]; bxs[r][2] = bx[2]; bxs[r][3] = bx[3];
+        scs[r] = s0;
+        if (fin && s0 > ba.score_thresh) {
+            key[r] = fkey(s0);
+            val[r] = (unsigned)r;
+        }
+    }
+    bitonic_desc(key, val, 1024);
+    if (threadIdx.x == 0) {
+        int kept[16];
+        int nk = 0;
+        for (int i = 0; i < 1024 && nk < ba.D; ++i) {
+            if (val[i] == 0xFFFFFFFFu) break;
+            const int r = (int)val[i];
+            const float ix1 = bxs[r][0], iy1 = bxs[r][1], ix2 = bxs[r][2], iy2 = bxs[r][3];
+            bool sup = false;
+            for (int q = 0; q < nk && !sup; ++q) {
+                const int j = kept[q];
+                // torchvision: suppress j (later) by kept i (earlier): IoU with the kept box
+                const float kx1 = bxs[j][0], ky1 = bxs[j][1], kx2 = bxs[j][2], ky2 = bxs[j][3];
+                const float karea = (kx2 - kx1) * (ky2 - ky1);
+                const float xx1 = fmaxf(kx1, ix1), yy1 = fmaxf(ky1, iy1);
+                const float xx2 = fminf(kx2, ix2), yy2 = fminf(ky2, iy2);
+                const float w_ = fmaxf(0.f, xx2 - xx1), h_ = fmaxf(0.f, yy2 - yy1);
+                const float inter = w_ * h_;
+                const float iarea = (ix2 - ix1) * (iy2 - iy1);
+                const float ovr = inter / (karea + iarea - inter);
+                sup = ovr > ba.nms_thresh;
+            }
+            if (!sup) kept[nk++] = r;
+        }
+        // detector_postprocess: clip (no-op, already clipped) + nonempty
+        int m = 0;
+        for (int q = 0; q < nk; ++q) {
+            const int r = kept[q];
+            if (!((bxs[r][2] - bxs[r][0]) > 0.f && (bxs[r][3] - bxs[r][1]) > 0.f)) continue;
+            float *ob = det_boxes + ((long long)b * ba.D + m) * 4;
+            ob[0] = bxs[r][0]; ob[1] = bxs[r][1]; ob[2] = bxs[r][2]; ob[3] = bxs[r][3];
+            det_scores[(long long)b * ba.D + m] = scs[r];
+            det_classes[(long long)b * ba.D + m] = 0;
+            ++m;
+        }
+        for (int q = m; q < ba.D; ++q) {
+            float *ob = det_boxes + ((long long)b * ba.D + q) * 4;
+            ob[0] = ob[1] = ob[2] = ob[3] = 0.f;
+            det_scores[(long long)b * ba.D + q] = 0.f;
+            det_classes[(long long)b * ba.D + q] = 0;
+        }
+        ndet[b] = m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// mask paste: sigmoid(logits) -> grid_sample(bilinear, zeros, align_corners=False) >= thr
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_paste(const float *__restrict__ logits, const float *__restrict__ boxes,
+                                               const int *__restrict__ counts, int D, int M, int img_h, int img_w,
+                                               float thr, uint8_t *__restrict__ out) {
+    __shared__ float prob[64 * 64];
+    const int r = blockIdx.y;
+    const int b = r / D, d = r - b * D;
+    uint8_t *o = out + (long long)r * img_h * img_w;
+    const int rows_per_block = 8;
+    const int y0 = blockIdx.x * rows_per_block;
+    if (d >= counts[b]) {
+        for (int i = threadIdx.x; i < rows_per_block * img_w; i += 256) {
+            const int y = y0 + i / img_w, x = i % img_w;
+            if (y < img_h) o[(long long)y * img_w + x] = 0;
+        }
+        return;
+    }
+    for (int i = threadIdx.x; i < M * M; i += 256) {
+        const float v = logits[(long long)r * M * M + i];
+        prob[i] = 1.0f / (1.0f + expf(-v));
+    }
+    __syncthreads();
+    const float bx0 = boxes[4 * r], by0 = boxes[4 * r + 1], bx1 = boxes[4 * r + 2], by1 = boxes[4 * r + 3];
+    for (int i = threadIdx.x; i < rows_per_block * img_w; i += 256) {
+        const int y = y0 + i / img_w, x = i % img_w;
+        if (y >= img_h) continue;
+        const float gy = ((float)y + 0.5f - by0) / (by1 - by0) * 2.f - 1.f;
+        const float gx = ((float)x + 0.5f - bx0) / (bx1 - bx0) * 2.f - 1.f;
+        // ATen GridSamplerKernel (vectorised CPU path, align_corners=False):
+        // unnormalize = (g + 1) * (size / 2) - 0.5; weights from floor distances
+        const float ix = (gx + 1.f) * ((float)M / 2.f) - 0.5f;
+        const float iy = (gy + 1.f) * ((float)M / 2.f) - 0.5f;
+        const float fx = floorf(ix), fy = floorf(iy);
+        const int xw = (int)fx, yn = (int)fy;
+        const float w_ = ix - fx, e_ = 1.f - w_;
+        const float n_ = iy - fy, s_ = 1.f - n_;
+        const float nw = s_ * e_, ne = s_ * w_, sw = n_ * e_, se = n_ * w_;
+        auto at = [&](int yy, int xx) -> float {
+            return (yy >= 0 && yy < M && xx >= 0 && xx < M) ? prob[yy * M + xx] : 0.f;
+        };
+        const float v = ((at(yn, xw) * nw + at(yn, xw + 1) * ne) + at(yn + 1, xw) * sw) + at(yn + 1, xw + 1) * se;
+        o[(long long)y * img_w + x] = v >= thr ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// keypoint head tail
+// ---------------------------------------------------------------------------
+// ConvTranspose2d(Cin -> Co, k=4, s=2, p=1): x (R, Hi, Wi, Cin) T, w f32 [Cin][Co][4][4]
+// -> out f32 (R, Co, 2Hi, 2Wi)
+template <typename T>
+__global__ __launch_bounds__(256) void k_kp_deconv(const T *__restrict__ x, const float *__restrict__ w,
+                                                   const float *__restrict__ bias, int Hi, int Wi, int Cin, int Co,
+                                                   float *__restrict__ out) {
+    const int r = blockIdx.x;
+    const int OH = 2 * Hi, OW = 2 * Wi;
+    const T *xi = x + (long long)r * Hi * Wi * Cin;
+    for (int t = threadIdx.x; t < Co * OH * OW; t += 256) {
+        const int co = t / (OH * OW), rem = t - co * OH * OW;
+        const int oy = rem / OW, ox = rem - oy * OW;
+        float acc = bias ? bias[co] : 0.f;
+        for (int ky = 0; ky < 4; ++ky) {
+            const int ty = oy + 1 - ky;  // oy = iy*2 - 1 + ky
+            if (ty < 0 || (ty & 1)) continue;
+            const int iy = ty >> 1;
+            if (iy >= Hi) continue;
+            for (int kx = 0; kx < 4; ++kx) {
+                const int tx = ox + 1 - kx;
+                if (tx < 0 || (tx & 1)) continue;
+                const int ix = tx >> 1;
+                if (ix >= Wi) continue;
+                const T *xp = xi + ((long long)iy * Wi + ix) * Cin;
+                const float *wp = w + (long long)co * 16 + ky * 4 + kx;
+                for (int ci = 0; ci < Cin; ++ci) acc += ld(xp + ci) * wp[(long long)ci * Co * 16];
+            }
+        }
+        out[((long long)r * Co + co) * OH * OW + oy * OW + ox] = acc;
+    }
+}
+
+// F.interpolate(scale_factor=2, mode='bilinear', align_corners=False), NCHW f32
+__global__ __launch_bounds__(256) void k_upsample2x(const float *__restrict__ x, int NC, int H, int W,
+                                                    float *__restrict__ out) {
+    const int OH = 2 * H, OW = 2 * W;
+    const long long total = (long long)NC * OH * OW;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int ox = (int)(i % OW);
+        const int oy = (int)((i / OW) % OH);
+        const long long nc = i / ((long long)OH * OW);
+        const float rh = 0.5f, rw = 0.5f;  // 1 / scale_factor
+        float sy = ((float)oy + 0.5f) * rh - 0.5f;
+        sy = sy < 0.f ? 0.f : sy;
+        float sx = ((float)ox + 0.5f) * rw - 0.5f;
+        sx = sx < 0.f ? 0.f : sx;
+        const int y0 = (int)sy, x0 = (int)sx;
+        const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+        const float l1y = sy - (float)y0, l0y = 1.f - l1y;
+        const float l1x = sx - (float)x0, l0x = 1.f - l1x;
+        const float *p = x + nc * H * W;
+        out[i] = l0y * (l0x * p[y0 * W + x0] + l1x * p[y0 * W + x1]) +
+                 l1y * (l0x * p[y1 * W + x0] + l1x * p[y1 * W + x1]);
+    }
+}
+
+__device__ __forceinline__ float cubic1(float x, float A) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; }
+__device__ __forceinline__ float cubic2(float x, float A) {
+    return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A;
+}
+
+// heatmaps_to_keypoints: one block per (roi, keypoint)
+__global__ __launch_bounds__(256) void k_heatmap_kp(const float *__restrict__ maps, const float *__restrict__ boxes,
+                                                    const int *__restrict__ counts, int D, int K, int M,
+                                                    float *__restrict__ out) {
+    __shared__ float red_v[256];
+    __shared__ int red_i[256];
+    __shared__ float red_s[256];
+    const int r = blockIdx.x / K, kpt = blockIdx.x - r * K;
+    const int b = r / D, d = r - b * D;
+    float *o = out + ((long long)r * K + kpt) * 3;
+    if (d >= counts[b]) {
+        if (threadIdx.x == 0) o[0] = o[1] = o[2] = 0.f;
+        return;
+    }
+    const float *mp = maps + ((long long)r * K + kpt) * M * M;
+    const float x0 = boxes[4 * r], y0 = boxes[4 * r + 1], x1 = boxes[4 * r + 2], y1 = boxes[4 * r + 3];
+    float wdt = x1 - x0, hgt = y1 - y0;
+    wdt = wdt < 1.f ? 1.f : wdt;
+    hgt = hgt < 1.f ? 1.f : hgt;
+    const float wc = ceilf(wdt), hc = ceilf(hgt);
+    const int OW = (int)wc, OH = (int)hc;
+    const float sw = (float)M / (float)OW, sh = (float)M / (float)OH;  // area_pixel_compute_scale
+    const float A = -0.75f;
+    float best = -INFINITY;
+    int besti = 0x7fffffff;
+    for (int t = threadIdx.x; t < OH * OW; t += 256) {
+        const int oy = t / OW, ox = t - oy * OW;
+        const float ry = sh * ((float)oy + 0.5f) - 0.5f;
+        const float rx = sw * ((float)ox + 0.5f) - 0.5f;
+        const float fy = floorf(ry), fx = floorf(rx);
+        const int iy = (int)fy, ix = (int)fx;
+        const float ty = ry - fy, tx = rx - fx;
+        const float cx[4] = {cubic2(tx + 1.f, A), cubic1(tx, A), cubic1(1.f - tx, A), cubic2(2.f - tx, A)};
+        const float cy[4] = {cubic2(ty + 1.f, A), cubic1(ty, A), cubic1(1.f - ty, A), cubic2(2.f - ty, A)};
+        float rows[4];
+        for (int i = 0; i < 4; ++i) {
+            int yy = iy - 1 + i;
+            yy = yy < 0 ? 0 : (yy > M - 1 ? M - 1 : yy);
+            float acc = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                int xx = ix - 1 + j;
+                xx = xx < 0 ? 0 : (xx > M - 1 ? M - 1 : xx);
+                acc = acc + mp[yy * M + xx] * cx[j];
+            }
+            rows[i] = acc;
+        }
+        const float v = ((rows[0] * cy[0] + rows[1] * cy[1]) + rows[2] * cy[2]) + rows[3] * cy[3];
+        if (v > best || (v == best && t < besti)) {
+            best = v;
+            besti = t;
+        }
+    }
+    red_v[threadIdx.x] = best;
+    red_i[threadIdx.x] = besti;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            const float ov = red_v[threadIdx.x + s];
+            const int oi = red_i[threadIdx.x + s];
+            if (ov > red_v[threadIdx.x] || (ov == red_v[threadIdx.x] && oi < red_i[threadIdx.x])) {
+                red_v[threadIdx.x] = ov;
+                red_i[threadIdx.x] = oi;
+            }
+        }
+        __syncthreads();
+    }
+    const float mx = red_v[0];
+    const int pos = red_i[0];
+    float s = 0.f;
+    for (int t = threadIdx.x; t < M * M; t += 256) s += expf(mp[t] - mx);
+    red_s[threadIdx.x] = s;
+    __syncthreads();
+    for (int q = 128; q > 0; q >>= 1) {
+        if (threadIdx.x < q) red_s[threadIdx.x] += red_s[threadIdx.x + q];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int xi = pos % OW, yi = pos / OW;
+        const float wcor = wdt / wc, hcor = hgt / hc;
+        o[0] = ((float)xi + 0.5f) * wcor + x0;
+        o[1] = ((float)yi + 0.5f) * hcor + y0;
+        o[2] = 1.0f / red_s[0];  // exp(max - max) / sum(exp(maps - max))
+    }
+}
+
+}  // namespace mdx
+
+using namespace mdx;
+
+static int grid_for(long long total) {
+    long long g = (total + 255) / 256;
+    return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+extern "C" int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], const float *mean,
+                              const float *stdv, int C, int Cp, int Hp, int Wp, int dtype, void *out,
+                              mdx_stream_t stream) {
+    MDX_REQUIRE(frames && lut && mean && stdv && out, "mdx_preprocess: null pointer");
+    MDX_REQUIRE(C >= 1 && C <= 4 && Cp >= C && Cp <= 8 && Hp >= h && Wp >= w, "mdx_preprocess: bad shape");
+    PrepArgs pa;
+    for (int i = 0; i < 256; ++i) pa.lut[i] = lut[i];
+    for (int c = 0; c < 4; ++c) {
+        pa.mean[c] = c < C ? mean[c] : 0.f;
+        pa.stdv[c] = c < C ? stdv[c] : 1.f;
+    }
+    const long long total = (long long)B * Hp * Wp;
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_preprocess<_Float16>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames, B,
+                           h, w, C, Cp, Hp, Wp, pa, (_Float16 *)out);
+    else
+        hipLaunchKernelGGL(k_preprocess<float>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames, B, h,
+                           w, C, Cp, Hp, Wp, pa, (float *)out);
+    MDX_CHECK_LAUNCH("mdx_preprocess");
+    return MDX_OK;
+}
+
+extern "C" int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
+                             mdx_stream_t stream) {
+    MDX_REQUIRE(x && out && k > 0 && s > 0 && p >= 0, "mdx_maxpool2d: bad args");
+    const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+    const long long total = (long long)N * OH * OW * C;
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_maxpool<_Float16>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                           (const _Float16 *)x, N, H, W, C, k, s, p, OH, OW, (_Float16 *)out);
+    else
+        hipLaunchKernelGGL(k_maxpool<float>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), (const float *)x,
+                           N, H, W, C, k, s, p, OH, OW, (float *)out);
+    MDX_CHECK_LAUNCH("mdx_maxpool2d");
+    return MDX_OK;
+}
+
+extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, const float *gamma,
+                             const float *beta, const void *up, int fuse, int dtype, void *out, float *stats,
+                             mdx_stream_t stream) {
+    MDX_REQUIRE(x && out && gamma && beta && stats && G > 0 && C % G == 0, "mdx_groupnorm: bad args");
+    MDX_REQUIRE(!fuse || (up && H % 2 == 0 && W % 2 == 0), "mdx_groupnorm: fuse needs up and even H, W");
+    hipStream_t s = as_stream(stream);
+    const long long total = (long long)N * H * W * C;
+    if (dtype == 1) {
+        hipLaunchKernelGGL(k_gn_stats<_Float16>, dim3(N * G), dim3(256), 0, s, (const _Float16 *)x, H * W, C, G, eps,
+                           stats);
+        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total)), dim3(256), 0, s, (const _Float16 *)x, N, H, W,
+                           C, G, stats, gamma, beta, (const _Float16 *)up, fuse, (_Float16 *)out);
+    } else {
+        hipLaunchKernelGGL(k_gn_stats<float>, dim3(N * G), dim3(256), 0, s, (const float *)x, H * W, C, G, eps, stats);
+        hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total)), dim3(256), 0, s, (const float *)x, N, H, W, C, G,
+                           stats, gamma, beta, (const float *)up, fuse, (float *)out);
+    }
+    MDX_CHECK_LAUNCH("mdx_groupnorm");
+    return MDX_OK;
+}
+
+extern "C" int64_t mdx_rpn_workspace_bytes(int B, int L, int pre_topk) {
+    const long long segs = (long long)B * L;
+    const long long words = (pre_topk + 63) / 64;
+    return segs * pre_topk * (16 + 4 + 4 + 4) + segs * 4 + segs * pre_topk * words * 8 + 256;
+}
+
+extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
+                                 int L, int B, int A, const float *cell_anchors, float offset, int img_h, int img_w,
+                                 int pre_topk, int post_topk, float nms_thresh, float min_size, float clampv,
+                                 float *out_boxes, float *out_scores, int *out_count, void *workspace,
+                                 mdx_stream_t stream) {
+    MDX_REQUIRE(head && lvl_h && lvl_w && strides && cell_anchors && out_boxes && out_scores && out_count && workspace,
+                "mdx_rpn_proposals: null pointer");
+    MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && A >= 1 && A <= 4, "mdx_rpn_proposals: L or A out of range");
+    MDX_REQUIRE(pre_topk >= 1 && pre_topk <= TOPK_MAX, "mdx_rpn_proposals: pre_topk must be in [1, %d]", TOPK_MAX);
+    MDX_REQUIRE(post_topk >= 1 && L * pre_topk <= MERGE_MAX, "mdx_rpn_proposals: too many candidates to merge");
+    RpnLevels rl{};
+    for (int l = 0; l < L; ++l) {
+        rl.head[l] = head[l];
+        rl.H[l] = lvl_h[l];
+        rl.W[l] = lvl_w[l];
+        rl.stride[l] = strides[l];
+        for (int a = 0; a < A; ++a)
+            for (int c = 0; c < 4; ++c) rl.cell[l][a][c] = cell_anchors[(l * A + a) * 4 + c];
+    }
+    rl.L = L; rl.A = A; rl.B = B; rl.pre_topk = pre_topk;
+    rl.offset = offset; rl.img_h = (float)img_h; rl.img_w = (float)img_w; rl.min_size = min_size; rl.clampv = clampv;
+    const long long segs = (long long)B * L;
+    const int words = (pre_topk + 63) / 64;
+    char *ws = (char *)workspace;
+    float *wb = (float *)ws; ws += segs * pre_topk * 16;
+    float *wsc = (float *)ws; ws += segs * pre_topk * 4;
+    int *wv = (int *)ws; ws += segs * pre_topk * 4;
+    int *wkeep = (int *)ws; ws += segs * pre_topk * 4;
+    int *wk = (int *)ws; ws += segs * 4;
+    ws = (char *)(((uintptr_t)ws + 15) & ~(uintptr_t)15);
+    unsigned long long *wmask = (unsigned long long *)ws;
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_rpn_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
+    hipLaunchKernelGGL(k_nms_mask, dim3((pre_topk * words + 255) / 256, (unsigned)segs), dim3(256), 0, s, wb, wk,
+                       pre_topk, words, nms_thresh, wmask);
+    hipLaunchKernelGGL(k_nms_scan, dim3((unsigned)segs), dim3(64), 0, s, wv, wk, pre_topk, words, wmask, wkeep);
+    hipLaunchKernelGGL(k_rpn_merge, dim3(B), dim3(1024), 2 * MERGE_MAX * sizeof(unsigned), s, wb, wsc, wkeep, wk, L,
+                       pre_topk, post_topk, out_boxes, out_scores, out_count);
+    MDX_CHECK_LAUNCH("mdx_rpn_proposals");
+    return MDX_OK;
+}
+
+extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
+                             int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
+                             int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
+                             void *out, mdx_stream_t stream) {
+    MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
+    MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
+    if (R == 0) return MDX_OK;
+    RoiLevels rl{};
+    for (int l = 0; l < L; ++l) {
+        rl.feat[l] = feats[l];
+        rl.H[l] = fh[l];
+        rl.W[l] = fw[l];
+        rl.scale[l] = scales[l];
+    }
+    rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
+    rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                           (_Float16 *)out);
+    else
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                           (float *)out);
+    MDX_CHECK_LAUNCH("mdx_roi_align");
+    return MDX_OK;
+}
+
+extern "C" int mdx_box_postprocess(const float *pred, int ld_pred, const float *proposals, const int *counts, int B,
+                                   int R, int D, float score_thresh, float nms_thresh, int img_h, int img_w,
+                                   const float *reg_weights, float clampv, float *det_boxes, float *det_scores,
+                                   int64_t *det_classes, int *ndet, mdx_stream_t stream) {
+    MDX_REQUIRE(pred && proposals && counts && det_boxes && det_scores && det_classes && ndet && reg_weights,
+                "mdx_box_postprocess: null pointer");
+    MDX_REQUIRE(R >= 1 && R <= 1024 && D >= 1 && D <= 16 && ld_pred >= 6, "mdx_box_postprocess: R<=1024, D<=16");
+    BoxPostArgs ba{};
+    ba.R = R; ba.ld_pred = ld_pred; ba.D = D; ba.score_thresh = score_thresh; ba.nms_thresh = nms_thresh;
+    ba.img_h = (float)img_h; ba.img_w = (float)img_w; ba.clampv = clampv;
+    for (int i = 0; i < 4; ++i) ba.wts[i] = reg_weights[i];
+    hipLaunchKernelGGL(k_box_post, dim3(B), dim3(1024), 0, as_stream(stream), ba, pred, proposals, counts, det_boxes,
+                       det_scores, (long long *)det_classes, ndet);
+    MDX_CHECK_LAUNCH("mdx_box_postprocess");
+    return MDX_OK;
+}
+
+extern "C" int mdx_paste_masks(const float *logits, const float *boxes, const int *counts, int B, int D, int M,
+                               int img_h, int img_w, float thresh, uint8_t *out, mdx_stream_t stream) {
+    MDX_REQUIRE(logits && boxes && counts && out && M <= 64, "mdx_paste_masks: bad args");
+    dim3 grid((img_h + 7) / 8, B * D);
+    hipLaunchKernelGGL(k_paste, grid, dim3(256), 0, as_stream(stream), logits, boxes, counts, D, M, img_h, img_w,
+                       thresh, out);
+    MDX_CHECK_LAUNCH("mdx_paste_masks");
+    return MDX_OK;
+}
+
+extern "C" int mdx_keypoint_deconv(const void *x, int R, int Hi, int Wi, int Cin, const float *w, const float *bias,
+                                   int Co, int dtype, float *out, mdx_stream_t stream) {
+    MDX_REQUIRE(x && w && out, "mdx_keypoint_deconv: null pointer");
+    if (R == 0) return MDX_OK;
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_kp_deconv<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), (const _Float16 *)x, w,
+                           bias, Hi, Wi, Cin, Co, out);
+    else
+        hipLaunchKernelGGL(k_kp_deconv<float>, dim3(R), dim3(256), 0, as_stream(stream), (const float *)x, w, bias, Hi,
+                           Wi, Cin, Co, out);
+    MDX_CHECK_LAUNCH("mdx_keypoint_deconv");
+    return MDX_OK;
+}
+
+extern "C" int mdx_upsample_bilinear2x(const float *x, int NC, int H, int W, float *out, mdx_stream_t stream) {
+    MDX_REQUIRE(x && out, "mdx_upsample_bilinear2x: null pointer");
+    const long long total = (long long)NC * 4 * H * W;
+    hipLaunchKernelGGL(k_upsample2x, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, NC, H, W, out);
+    MDX_CHECK_LAUNCH("mdx_upsample_bilinear2x");
+    return MDX_OK;
+}
+
+extern "C" int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
+                                         int K, int M, float *out, mdx_stream_t stream) {
+    MDX_REQUIRE(maps && boxes && counts && out, "mdx_heatmaps_to_keypoints: null pointer");
+    hipLaunchKernelGGL(k_heatmap_kp, dim3(B * D * K), dim3(256), 0, as_stream(stream), maps, boxes, counts, D, K, M,
+                       out);
+    MDX_CHECK_LAUNCH("mdx_heatmaps_to_keypoints");
+    return MDX_OK;
+}

@@ -1,0 +1,339 @@
+"""GPU parity of the Mask/Keypoint R-CNN kernels and forward against the
+PyTorch-CPU oracle (oracle/model_ref.py).
+
+Floating-point tolerances (written per test):
+* fp32 conv (exact-f32 MFMA):  |err| <= 2e-5 * sum|a*b| scale  (rel. 1e-4 of max)
+* fp16 conv (fp16 operands, fp32 accumulate): rel. 2e-3 of max (output rounding)
+* post-processing kernels on identical inputs: bit-identical integer decisions
+  (top-k, NMS keeps, argmax) up to 1-ulp transcendental differences.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt(mdx):
+    from moseq2_detectron_extract_amd.model import runtime
+    return runtime
+
+
+def _conv_ref(x, w, b, stride, pad, res=None, relu=False):
+    y = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), None if b is None else b.double(), stride, pad)
+    y = y.permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + res.double()
+    return torch.relu(y) if relu else y
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, k, stride, pad, residual, relu
+    (2, 13, 17, 64, 96, 3, 1, 1, False, True),
+    (1, 20, 22, 8, 64, 7, 2, 3, False, True),
+    (3, 9, 9, 128, 130, 1, 2, 0, False, False),
+    (300, 1, 1, 1232, 72, 1, 1, 0, False, True),
+    (2, 14, 16, 256, 256, 3, 2, 1, True, True),
+    (1, 33, 31, 64, 256, 1, 1, 0, True, True),
+]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d(mdx, dtype, case):
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    N, H, W, Cin, Cout, k, s, p, use_res, relu = case
+    if dtype == "fp32" and Cin % 4:
+        pytest.skip()
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    tdt = torch.float16 if dtype == "fp16" else torch.float32
+    x = torch.randn(N, H, W, Cin, generator=g).to(tdt)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(tdt)
+    b = torch.randn(Cout, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = torch.randn(N, OH, OW, Cout, generator=g).to(tdt) if use_res else None
+    want = _conv_ref(x.float(), w.float(), b, s, p, None if res is None else res.float(), relu)
+    xd = x.cuda()
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
+    out = torch.empty(N, OH, OW, Cout, dtype=tdt, device="cuda")
+    rd = res.cuda() if res is not None else None
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    dc = 1 if dtype == "fp16" else 0
+    call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
+         P(out), None)
+    got = out.cpu().double()
+    scale = want.abs().max().item() + 1e-6
+    tol = 2e-3 if dtype == "fp16" else 1e-4
+    err = (got - want).abs().max().item() / scale
+    assert err < tol, f"max rel err {err:.2e}"
+
+
+def test_conv_mfma_layout_identity(mdx):
+    """A = I (as a 1x1 conv over an identity input) with an asymmetric B catches a
+    transposed C write."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    for dt, tdt, dc in (("fp16", torch.float16, 1), ("fp32", torch.float32, 0)):
+        M = 128
+        x = torch.eye(M, dtype=tdt).view(M, 1, 1, M)
+        wt = (torch.arange(96 * M, dtype=torch.float32).view(96, M) % 7 - 3).to(tdt)  # asymmetric
+        out = torch.empty(M, 1, 1, 96, dtype=tdt, device="cuda")
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        xd, wd = x.cuda(), wt.cuda()
+        call("mdx_conv2d", P(xd), M, 1, 1, M, P(wd), None, 96, 1, 1, 1, 0, None, 0, 0, dc, dc, P(out), None)
+        torch.testing.assert_close(out.cpu().view(M, 96).float(), wt.t().float(), rtol=0, atol=0)
+
+
+def test_deconv2x2_pixel_shuffle(mdx, rt):
+    from moseq2_detectron_extract_amd.model.runtime import Conv
+    import ctypes
+    from moseq2_detectron_extract_amd._lib import call
+    g = torch.Generator().manual_seed(3)
+    N, H, W, Cin, Co = 2, 5, 6, 64, 24
+    x = torch.randn(N, H, W, Cin, generator=g)
+    wt = torch.randn(Cin, Co, 2, 2, generator=g) / 8
+    b = torch.randn(Co, generator=g)
+    want = F.conv_transpose2d(x.permute(0, 3, 1, 2).double(), wt.double(), b.double(), stride=2).permute(0, 2, 3, 1)
+    wp = wt.permute(2, 3, 1, 0).reshape(4 * Co, Cin).contiguous().cuda()
+    out = torch.empty(N, 2 * H, 2 * W, Co, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    xd = x.cuda()
+    call("mdx_conv2d", P(xd), N, H, W, Cin, P(wp), P(b.repeat(4).cuda()), 4 * Co, 1, 1, 1, 0, None, 0, 1, 0, 0,
+         P(out), None)
+    torch.testing.assert_close(out.cpu().double(), want, rtol=1e-5, atol=1e-5)
+
+
+def _model(cfg, seed=0, dtype="fp32"):
+    from moseq2_detectron_extract_amd.model import MaskRCNN, synthetic_state_dict
+    sd = synthetic_state_dict(cfg, seed)
+    return sd, MaskRCNN(cfg, sd, dtype=dtype)
+
+
+@pytest.fixture(scope="module")
+def small_case(mdx):
+    from moseq2_detectron_extract_amd.model import ModelConfig
+    cfg = ModelConfig(score_thresh_test=0.0)
+    sd, m = _model(cfg)
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, size=(2, 100, 130, 1), dtype=np.uint8)
+    return cfg, sd, m, imgs
+
+
+def test_backbone_fpn_fp32(small_case):
+    from oracle import model_ref as R
+    cfg, sd, m, imgs = small_case
+    out = m.forward(torch.from_numpy(imgs[..., 0]).cuda(), intermediates=True)
+    _, inter = R.forward(sd, cfg, imgs)
+    gi = out["intermediates"]
+    torch.testing.assert_close(gi["input"].cpu()[..., :3].permute(0, 3, 1, 2), inter["input"], rtol=0, atol=0)
+    for k in ("res2", "res3", "res4", "res5", "p2", "p3", "p4", "p5", "p6"):
+        got = gi[k].cpu().permute(0, 3, 1, 2).double()
+        want = inter[k].double()
+        err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+        assert err < 2e-4, f"{k}: rel err {err:.2e}"
+
+
+def test_rpn_proposals_from_identical_heads(mdx):
+    """Same head tensors into the GPU and the oracle proposal selection."""
+    import ctypes
+    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd.model import ModelConfig
+    from oracle import model_ref as R
+    cfg = ModelConfig()
+    B, A = 2, 3
+    sizes = [(112, 128), (56, 64), (28, 32), (14, 16), (7, 8)]
+    g = torch.Generator().manual_seed(1)
+    heads, logits, deltas, anchors = [], [], [], []
+    for i, (H, W) in enumerate(sizes):
+        hd = torch.cat([torch.randn(B, H, W, A, generator=g) * 2, torch.randn(B, H, W, 4 * A, generator=g) * 0.3], -1)
+        heads.append(hd.contiguous().cuda())
+        logits.append(hd[..., :A].reshape(B, -1))
+        deltas.append(hd[..., A:].reshape(B, H * W * A, 4))
+        anchors.append(R.anchors_for(cfg, i, H, W))
+    want = R.find_top_rpn_proposals(logits, deltas, anchors, cfg, (423, 511))
+    from moseq2_detectron_extract_amd.model.runtime import MaskRCNN  # noqa: F401
+    import math
+    cells = []
+    for size in cfg.anchor_sizes:
+        for ar in cfg.aspect_ratios:
+            w_ = math.sqrt(float(size) ** 2 / ar); h_ = ar * w_
+            cells.append([-w_ / 2, -h_ / 2, w_ / 2, h_ / 2])
+    cells = np.array(cells, np.float32)
+    post = cfg.rpn_post_nms_topk_test
+    boxes = torch.empty(B, post, 4, device="cuda"); scores = torch.empty(B, post, device="cuda")
+    cnt = torch.empty(B, dtype=torch.int32, device="cuda")
+    ws = torch.empty(call("mdx_rpn_workspace_bytes", B, 5, 1000), dtype=torch.uint8, device="cuda")
+    ptrs = (ctypes.c_void_p * 5)(*[h.data_ptr() for h in heads])
+    ia = lambda v: (ctypes.c_int * len(v))(*v)  # noqa: E731
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]), 5,
+         B, A, cells.ctypes.data_as(ctypes.c_void_p), 0.0, 423, 511, 1000, post, 0.7, 0.0, cfg.bbox_reg_clamp,
+         P(boxes), P(scores), P(cnt), P(ws), None)
+    for b in range(B):
+        wb, wsc = want[b]
+        n = int(cnt[b])
+        assert n == len(wb)
+        gsc = scores[b, :n].cpu()
+        torch.testing.assert_close(gsc, wsc, rtol=0, atol=0)  # logits are copied, order must match
+        torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
+
+
+def test_roi_align_matches_oracle(mdx, rt):
+    import ctypes
+    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd.model import ModelConfig
+    from oracle import model_ref as R
+    cfg = ModelConfig()
+    g = torch.Generator().manual_seed(5)
+    B, C = 2, 16
+    sizes = {2: (28, 32), 3: (14, 16), 4: (7, 8), 5: (4, 4)}
+    feats = {f"p{l}": torch.randn(B, C, *s, generator=g) for l, s in sizes.items()}
+    per = 40
+    xy = torch.rand(B, per, 2, generator=g) * torch.tensor([120.0, 100.0])
+    wh = torch.rand(B, per, 2, generator=g) ** 2 * 110 + 0.5
+    boxes = torch.cat([xy, xy + wh], -1)
+    counts = torch.tensor([per, per - 7], dtype=torch.int32)
+    want = R.pooler(feats, [boxes[0], boxes[1, :per - 7]], 7, cfg)
+    fl = [feats[f"p{l}"].permute(0, 2, 3, 1).contiguous().cuda() for l in (2, 3, 4, 5)]
+    out = torch.empty(B * per, 7, 7, C, device="cuda")
+    ptrs = (ctypes.c_void_p * 4)(*[f.data_ptr() for f in fl])
+    ia = lambda v: (ctypes.c_int * 4)(*v)  # noqa: E731
+    sc = (ctypes.c_float * 4)(*[0.25, 0.125, 0.0625, 0.03125])
+    bd, cd = boxes.contiguous().cuda(), counts.cuda()
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4, 2, C,
+         P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, 0, P(out), None)
+    got = out.cpu().permute(0, 3, 1, 2)
+    got = torch.cat([got[:per], got[per:2 * per - 7]])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+    assert out[2 * per - 7:].abs().max().item() == 0  # padded rows are zero
+
+
+def test_box_postprocess_matches_oracle(mdx):
+    import ctypes
+    from moseq2_detectron_extract_amd._lib import call
+    from oracle import model_ref as R
+    g = torch.Generator().manual_seed(9)
+    B, Rr, D = 3, 1000, 4
+    xy = torch.rand(B, Rr, 2, generator=g) * torch.tensor([450.0, 380.0])
+    props = torch.cat([xy, xy + torch.rand(B, Rr, 2, generator=g) * 90 + 2], -1)
+    pred = torch.cat([torch.randn(B, Rr, 2, generator=g) * 2, torch.randn(B, Rr, 4, generator=g) * 0.5], -1)
+    counts = torch.tensor([1000, 517, 3], dtype=torch.int32)
+    for thr in (0.0, 0.5):
+        db = torch.empty(B, D, 4, device="cuda"); ds = torch.empty(B, D, device="cuda")
+        dc = torch.empty(B, D, dtype=torch.int64, device="cuda"); nd = torch.empty(B, dtype=torch.int32, device="cuda")
+        rw = np.array([10, 10, 5, 5], np.float32)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        pd, ppd, cd = pred.contiguous().cuda(), props.contiguous().cuda(), counts.cuda()
+        import math
+        call("mdx_box_postprocess", P(pd), 6, P(ppd), P(cd), B, Rr, D, thr, 0.5, 423, 511,
+             rw.ctypes.data_as(ctypes.c_void_p), math.log(1000 / 16), P(db), P(ds), P(dc), P(nd), None)
+        for b in range(B):
+            n = int(counts[b])
+            scores = F.softmax(pred[b, :n, :2], -1)
+            boxes = R.apply_deltas(pred[b, :n, 2:], props[b, :n], (10, 10, 5, 5), math.log(1000 / 16))
+            wb, wsc, _ = R.fast_rcnn_inference_single(boxes, scores, (423, 511), thr, 0.5, D)
+            ne = ((wb[:, 2] - wb[:, 0]) > 0) & ((wb[:, 3] - wb[:, 1]) > 0)
+            wb, wsc = wb[ne], wsc[ne]
+            assert int(nd[b]) == len(wb)
+            torch.testing.assert_close(db[b, :len(wb)].cpu(), wb, rtol=1e-5, atol=1e-4)
+            torch.testing.assert_close(ds[b, :len(wb)].cpu(), wsc, rtol=1e-5, atol=1e-6)
+
+
+def test_paste_and_keypoint_tail(mdx):
+    import ctypes
+    from moseq2_detectron_extract_amd._lib import call
+    from oracle import model_ref as R
+    g = torch.Generator().manual_seed(4)
+    B, D, M, h, w = 2, 4, 28, 123, 157
+    logits = torch.randn(B * D, M, M, generator=g) * 3
+    xy = torch.rand(B * D, 2, generator=g) * torch.tensor([100.0, 80.0])
+    boxes = torch.cat([xy, xy + torch.rand(B * D, 2, generator=g) * 60 + 1.5], -1)
+    counts = torch.tensor([4, 2], dtype=torch.int32)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    out = torch.empty(B, D, h, w, dtype=torch.uint8, device="cuda")
+    ld, bd, cd = logits.contiguous().cuda(), boxes.contiguous().cuda(), counts.cuda()
+    call("mdx_paste_masks", P(ld), P(bd), P(cd), B, D, M, h, w, 0.5, P(out), None)
+    want = R.paste_masks(logits.sigmoid(), boxes, h, w, 0.5)
+    got = out.cpu().view(B * D, h, w).bool()
+    valid = [0, 1, 2, 3, 4, 5]
+    mism = (got[valid] != want[valid]).sum().item()
+    assert mism <= 2, f"{mism} mismatched mask pixels"
+    assert not got[6:].any()
+    # keypoint head tail: deconv + bilinear x2 + heatmaps_to_keypoints
+    K, Cin = 8, 64
+    x = torch.randn(B * D, 7, 7, Cin, generator=g)
+    wt = torch.randn(Cin, K, 4, 4, generator=g) * 0.05
+    bb = torch.randn(K, generator=g) * 0.1
+    low = torch.empty(B * D, K, 14, 14, device="cuda")
+    xd, wd, bdd = x.cuda(), wt.cuda(), bb.cuda()
+    call("mdx_keypoint_deconv", P(xd), B * D, 7, 7, Cin, P(wd), P(bdd), K, 0, P(low), None)
+    wl = F.conv_transpose2d(x.permute(0, 3, 1, 2), wt, bb, stride=2, padding=1)
+    torch.testing.assert_close(low.cpu(), wl, rtol=1e-4, atol=1e-4)
+    hm = torch.empty(B * D, K, 28, 28, device="cuda")
+    call("mdx_upsample_bilinear2x", P(low), B * D * K, 14, 14, P(hm), None)
+    wh = F.interpolate(wl, scale_factor=2, mode="bilinear", align_corners=False)
+    torch.testing.assert_close(hm.cpu(), wh, rtol=1e-4, atol=1e-4)
+    kp = torch.empty(B, D, K, 3, device="cuda")
+    hmw = wh.contiguous().cuda()
+    call("mdx_heatmaps_to_keypoints", P(hmw), P(bd), P(cd), B, D, K, 28, P(kp), None)
+    wk = R.heatmaps_to_keypoints(wh, boxes)[:, :, [0, 1, 3]]
+    gk = kp.cpu().view(B * D, K, 3)
+    close = (gk[valid, :, :2] - wk[valid, :, :2]).abs().max(-1).values < 1e-3
+    assert close.float().mean() > 0.95  # argmax of near-equal bicubic values may differ
+    torch.testing.assert_close(gk[valid, :, 2][close], wk[valid, :, 2][close], rtol=1e-4, atol=1e-6)
+
+
+def test_forward_fp32_end_to_end(small_case):
+    from oracle import model_ref as R
+    cfg, sd, m, imgs = small_case
+    out = m.forward(torch.from_numpy(imgs[..., 0]).cuda())
+    want, _ = R.forward(sd, cfg, imgs)
+    for b in range(len(imgs)):
+        n = int(out["ndet"][b])
+        wb = want[b]["pred_boxes"]
+        assert n == len(wb)
+        torch.testing.assert_close(out["boxes"][b, :n].cpu(), wb, rtol=1e-3, atol=5e-2)
+        torch.testing.assert_close(out["scores"][b, :n].cpu(), want[b]["scores"], rtol=1e-3, atol=1e-4)
+        gm = out["masks"][b, :n].cpu().bool()
+        wm = want[b]["pred_masks"]
+        inter = (gm & wm).sum().item(); union = (gm | wm).sum().item()
+        assert union == 0 or inter / union > 0.97
+        gk = out["keypoints"][b, :n].cpu()
+        wk = want[b]["pred_keypoints"]
+        assert ((gk[..., :2] - wk[..., :2]).abs().max(-1).values < 1.0).float().mean() > 0.9
+
+
+def test_forward_fp16_close_to_fp32(small_case):
+    from moseq2_detectron_extract_amd.model import MaskRCNN
+    cfg, sd, m32, imgs = small_case
+    m16 = MaskRCNN(cfg, sd, dtype="fp16")
+    x = torch.from_numpy(imgs[..., 0]).cuda()
+    a = m32.forward(x, intermediates=True)["intermediates"]
+    b = m16.forward(x, intermediates=True)["intermediates"]
+    for k in ("res5", "p2", "p5"):
+        ga, gb = a[k].float(), b[k].float()
+        err = ((ga - gb).norm() / ga.norm()).item()
+        assert err < 3e-2, f"{k}: fp16 relative L2 error {err:.2e}"
+
+
+def test_predictor_instances(mdx):
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    p = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, size=(3, 96, 128, 1), dtype=np.uint8)
+    res = p(img)
+    assert len(res) == 3
+    ins = res[0]["instances"].to("cpu")
+    assert ins.image_size == (96, 128)
+    n = len(ins)
+    assert 1 <= n <= 4
+    assert ins.pred_masks.shape == (n, 96, 128) and ins.pred_masks.dtype == torch.bool
+    assert ins.pred_keypoints.shape == (n, 8, 3)
+    assert ins.pred_keypoint_heatmaps.shape == (n, 8, 28, 28)
+    assert ins.pred_boxes.tensor.shape == (n, 4) and ins.pred_classes.dtype == torch.int64
+    single = p(img[0])
+    assert isinstance(single, dict) and "instances" in single
