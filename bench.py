@@ -1,0 +1,215 @@
+"""Throughput of the extraction hot path on MI355X.
+
+metric : extracted frames/sec, 512x424 depth video, batch = 32 (BASELINE.json)
+step   : one pass of the hot path over one batch of 32 synthetic raw int16
+         512x424 frames already resident in HBM:
+         prep_raw_frames (bg subtract, ROI, clamp, NS inpaint) -> scale (fused)
+         -> R50-FPN Mask/Keypoint R-CNN forward (fp16 MFMA, SCORE_THRESH_TEST=0
+         so every frame carries exactly 4 detections) -> mask-IoU NMS +
+         instance-0 selection -> clean_frames (median3 + 3x open ellipse9)
+         -> moments -> angle -> crop_and_rotate (depth + mask).
+value  : frames processed by all ranks / max-over-ranks wall time.
+scaling: weak (every rank processes its own 32-frame batches; frames shard
+         with no data-path collective; N>1 gathers each step's 80x80 crops to
+         rank 0 over RCCL, the reference's result hand-off to the writer).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]
+        (N>1 via torch.distributed.run, one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--depth", type=int, default=50, choices=[50, 101])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-sample-frames", type=int, default=2)
+    return ap.parse_args()
+
+
+def conv_roofline(extractor, raw, steps=3):
+    """Time every conv launch of a step with HIP events on the launch stream;
+    returns (algorithmic conv FLOP per step, conv seconds per step, launches)."""
+    import torch
+    from moseq2_detectron_extract_amd.model import runtime as RT
+    model = extractor.predictor.model
+    rec = []
+    orig = RT.MaskRCNN.conv
+
+    def timed(self, x, N, H, W, c, relu, out=None, residual=None, out_f32=False, out_mode=0):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        r = orig(self, x, N, H, W, c, relu, out, residual, out_f32, out_mode)
+        e1.record(s)
+        OH, OW = r[1], r[2]
+        cin_alg = 3 if c is self.stem else c.cin
+        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * c.k * c.k * cin_alg))
+        return r
+
+    RT.MaskRCNN.conv = timed
+    try:
+        for _ in range(steps):
+            extractor.step_device(raw)
+        torch.cuda.synchronize()
+    finally:
+        RT.MaskRCNN.conv = orig
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in rec)
+    fl = sum(f for _, _, f in rec)
+    return fl / steps, ms / 1e3 / steps, len(rec) // steps
+
+
+def cpu_baseline(nframes: int, dtype_cfg):
+    """Oracle (CPU restatement) timed on the host cores: prep+inpaint (C),
+    PyTorch-CPU fp32 model forward, clean/moments/crop (C)."""
+    import numpy as np
+    import torch
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import synthetic_state_dict
+    from oracle import frameops as O
+    from oracle import model_ref as R
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    s = synth.SyntheticSession(nframes, seed=123)
+    raw = s.frames(0, nframes)
+    sd = synthetic_state_dict(dtype_cfg, 0)
+    t0 = time.perf_counter()
+    prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
+    scaled = O.scale_raw_frames(prepped, 0, 100)
+    res, _ = R.forward(sd, dtype_cfg, scaled[..., None], keep_intermediates=False)
+    d2 = np.stack([r["pred_masks"][0].numpy().astype(np.uint8) if len(r["pred_masks"]) else
+                   np.zeros(prepped.shape[1:], np.uint8) for r in res])
+    cl = O.clean_frames(prepped, iters_tail=3)
+    f = O.get_frame_features(cl, 3, mask=d2)
+    ang = np.mod(-np.rad2deg(f["orientation"]), 360)
+    O.crop_and_rotate_frames(prepped, f["centroid"], ang)
+    O.crop_and_rotate_frames(d2, f["centroid"], ang)
+    dt = time.perf_counter() - t0
+    return {"value": nframes / dt, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{nframes} synthetic 512x424 frames through the CPU oracle (C frame ops + PyTorch-CPU fp32 "
+                      f"R50-FPN Mask/Keypoint R-CNN, SCORE_THRESH_TEST=0), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.model.runtime import flops_per_image
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+
+    B = args.batch
+    cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
+    pred = Predictor.from_config(cfg, dtype=args.dtype, seed=0)
+    sess = synth.SyntheticSession(2 * B, seed=1000 + rank)
+    raw_all = torch.from_numpy(sess.frames(0, 2 * B)).cuda()
+    ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B))
+
+    gather_bufs = None
+    if world > 1:
+        gather_bufs = [torch.empty((B, 2, 80, 80), dtype=torch.uint8, device="cuda") for _ in range(world)]
+
+    def step(i):
+        raw = raw_all[(i % 2) * B:(i % 2) * B + B]
+        r = ex.step_device(raw)
+        if world > 1:
+            payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
+            dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
+        return r
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    frames = world * args.steps * B
+    value = frames / dt
+
+    roof = None
+    if not args.no_roofline:
+        fl, sec, nl = conv_roofline(ex, raw_all[:B])
+        peak = 2500.0 if args.dtype == "fp16" else 157.3
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "conv_pmc_summary.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as fh:
+                    traffic = json.load(fh).get("hbm_bytes_per_step")
+            except Exception:
+                traffic = None
+        ach = fl / sec / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": traffic,
+                "kernel": f"k_conv<{args.dtype}> implicit-GEMM, {nl} launches/step, {fl / 1e12:.3f} TFLOP/step "
+                          f"in {sec * 1e3:.2f} ms (HIP events on the launch stream)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args.cpu_sample_frames, ModelConfig(depth=args.depth, score_thresh_test=0.0))
+        except Exception as e:  # the baseline must never sink the bench line
+            cpu = {"value": None, "error": repr(e)[:200]}
+
+    if rank == 0:
+        line = {
+            "metric": "extracted frames/sec, 512x424 depth video batch=32",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+            "config": {"workload": f"full extract hot path (prep+inpaint, scale, R{args.depth}-FPN Mask/Keypoint "
+                                   f"R-CNN {args.dtype}, mask NMS, clean, moments, crop), 512x424 int16 frames",
+                       "global_batch": B * world, "per_gpu_batch": B, "frame": [424, 512],
+                       "model_gflop_per_frame": round(flops_per_image(cfg) / 1e9, 2),
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

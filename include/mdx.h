@@ -170,6 +170,16 @@ int mdx_keypoint_deconv(const void *x, int R, int Hi, int Wi, int Cin, const flo
 /* F.interpolate(scale_factor=2, bilinear, align_corners=False), float32 NCHW. */
 int mdx_upsample_bilinear2x(const float *x, int NC, int H, int W, float *out, mdx_stream_t stream);
 
+/* ProcessFeaturesStep.__nms_mask_instances (mask-IoU NMS, reference quirks
+ * kept; M/pipeline/process_features_step.py:63-113) + instance-0 selection of
+ * mask_and_keypoints_from_model_output (M/proc/proc.py:657-685).
+ * masks uint8 (B,D,h,w), scores (B,D), ndet (B), kpts float32 (B,D,K,3) ->
+ * keep_idx int32 (B,D) (-1 padded, pick order), nkeep (B), sel_mask uint8
+ * (B,h,w), sel_kpts float64 (B,K,3) (NaN when no instance). */
+int mdx_mask_nms_select(const uint8_t *masks, const float *scores, const int *ndet, const float *kpts,
+                        int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx, int *nkeep,
+                        uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream);
+
 /* heatmaps_to_keypoints: maps float32 (B*D, K, M, M) -> (B*D, K, 3) [x, y, score]. */
 int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
                               int K, int M, float *out, mdx_stream_t stream);

@@ -1,0 +1,126 @@
+// Instance selection after inference (gfx950):
+//   ProcessFeaturesStep.__nms_mask_instances   M/pipeline/process_features_step.py:63-113
+//   mask_and_keypoints_from_model_output (instance 0)  M/proc/proc.py:657-685
+//
+// One workgroup per frame.  Areas and pairwise intersections of the <= D
+// pasted masks are popcount reductions over the frame; the reference's
+// sequential pick loop (including its quirk: every row index with ANY later
+// IoU > thr is deleted, plus `last`) then runs on one lane.  The selected
+// instance 0's mask and keypoints are written out for the frame-feature stage.
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace mdx {
+
+constexpr int SEL_MAXD = 8;
+
+__global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restrict__ masks,
+                                                         const float *__restrict__ scores,
+                                                         const int *__restrict__ ndet,
+                                                         const float *__restrict__ kpts, int D, int K, long long hw,
+                                                         float thr, int *__restrict__ keep_idx,
+                                                         int *__restrict__ nkeep, uint8_t *__restrict__ sel_mask,
+                                                         double *__restrict__ sel_kpts) {
+    __shared__ unsigned long long s_cnt[SEL_MAXD * SEL_MAXD];
+    __shared__ int s_sel;
+    const int b = blockIdx.x;
+    const int n = ndet[b];
+    const uint8_t *mb = masks + (long long)b * D * hw;
+    for (int i = threadIdx.x; i < SEL_MAXD * SEL_MAXD; i += 256) s_cnt[i] = 0;
+    __syncthreads();
+    if (n > 1) {
+        // cnt[i][j] (j >= i): |m_i & m_j| ; cnt[i][i] = area_i (planes need not be aligned)
+        unsigned long long loc[SEL_MAXD * (SEL_MAXD + 1) / 2];
+        for (int q = 0; q < SEL_MAXD * (SEL_MAXD + 1) / 2; ++q) loc[q] = 0;
+        for (long long p = threadIdx.x; p < hw; p += 256) {
+            unsigned m[SEL_MAXD];
+            for (int i = 0; i < n; ++i) m[i] = mb[(long long)i * hw + p] != 0;
+            int q = 0;
+            for (int i = 0; i < n; ++i)
+                for (int j = i; j < n; ++j, ++q) loc[q] += m[i] & m[j];
+        }
+        int q = 0;
+        for (int i = 0; i < n; ++i)
+            for (int j = i; j < n; ++j, ++q) atomicAdd(&s_cnt[i * SEL_MAXD + j], loc[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int pick[SEL_MAXD];
+        int np = 0;
+        if (n <= 1) {
+            for (int i = 0; i < n; ++i) pick[np++] = i;
+        } else {
+            // drop instances with an empty mask
+            int cand[SEL_MAXD];
+            int nc = 0;
+            for (int i = 0; i < n; ++i)
+                if (s_cnt[i * SEL_MAXD + i] > 0) cand[nc++] = i;
+            // idxs = argsort(scores) ascending (stable for these sizes)
+            int idxs[SEL_MAXD];
+            for (int i = 0; i < nc; ++i) idxs[i] = cand[i];
+            for (int i = 1; i < nc; ++i) {
+                const int v = idxs[i];
+                int j = i - 1;
+                while (j >= 0 && scores[b * D + idxs[j]] > scores[b * D + v]) {
+                    idxs[j + 1] = idxs[j];
+                    --j;
+                }
+                idxs[j + 1] = v;
+            }
+            int len = nc;
+            while (len > 0) {
+                const int last = len - 1;
+                pick[np++] = idxs[last];
+                bool del[SEL_MAXD];
+                for (int r = 0; r < len; ++r) del[r] = (r == last);
+                for (int r = 0; r < len; ++r) {
+                    for (int c = r + 1; c < len; ++c) {
+                        const int a = idxs[r], bb = idxs[c];
+                        const int lo = a < bb ? a : bb, hi = a < bb ? bb : a;
+                        const long long inter = (long long)s_cnt[lo * SEL_MAXD + hi];
+                        const long long uni = (long long)s_cnt[a * SEL_MAXD + a] + (long long)s_cnt[bb * SEL_MAXD + bb] -
+                                              inter;
+                        const float iou = (float)inter / (float)uni;
+                        if (iou > thr) del[r] = true;
+                    }
+                }
+                int nl = 0;
+                for (int r = 0; r < len; ++r)
+                    if (!del[r]) idxs[nl++] = idxs[r];
+                len = nl;
+            }
+        }
+        for (int i = 0; i < D; ++i) keep_idx[b * D + i] = i < np ? pick[i] : -1;
+        nkeep[b] = np;
+        s_sel = np > 0 ? pick[0] : -1;
+        const double nan = __builtin_nan("");
+        for (int k = 0; k < K; ++k)
+            for (int c = 0; c < 3; ++c)
+                sel_kpts[((long long)b * K + k) * 3 + c] =
+                    np > 0 ? (double)kpts[(((long long)b * D + pick[0]) * K + k) * 3 + c] : nan;
+    }
+    __syncthreads();
+    const int s = s_sel;
+    uint8_t *o = sel_mask + (long long)b * hw;
+    const uint8_t *src = s >= 0 ? mb + (long long)s * hw : nullptr;
+    for (long long p = threadIdx.x; p < hw; p += 256) o[p] = src ? src[p] : (uint8_t)0;
+}
+
+}  // namespace mdx
+
+using namespace mdx;
+
+extern "C" int mdx_mask_nms_select(const uint8_t *masks, const float *scores, const int *ndet, const float *kpts,
+                                   int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx, int *nkeep,
+                                   uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream) {
+    MDX_REQUIRE(masks && scores && ndet && kpts && keep_idx && nkeep && sel_mask && sel_kpts,
+                "mdx_mask_nms_select: null pointer");
+    MDX_REQUIRE(D >= 1 && D <= SEL_MAXD, "mdx_mask_nms_select: D must be in [1, %d]", SEL_MAXD);
+    const long long hw = (long long)h * w;
+    if (B == 0) return MDX_OK;
+    hipLaunchKernelGGL(k_mask_nms_select, dim3(B), dim3(256), 0, as_stream(stream), masks, scores, ndet, kpts, D, K, hw,
+                       iou_thresh, keep_idx, nkeep, sel_mask, sel_kpts);
+    MDX_CHECK_LAUNCH("mdx_mask_nms_select");
+    return MDX_OK;
+}

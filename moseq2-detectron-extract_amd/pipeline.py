@@ -1,0 +1,116 @@
+"""Device-resident extraction hot path for one GPU.
+
+Replaces the chain ProduceFramesStep -> InferenceStep -> ProcessFeaturesStep
+(M/pipeline/produce_frames_step.py:19-48, M/pipeline/inference_step.py:57-72,
+M/pipeline/process_features_step.py:56-199) for one chunk of raw frames:
+
+  prep_raw_frames (+NS inpaint)  -> scale_raw_frames (fused into the model's
+  preprocess) -> Mask/Keypoint R-CNN forward (batch_size frames per launch
+  sequence) -> mask-IoU NMS + instance-0 selection -> clean_frames ->
+  get_frame_features (moments) -> [host: angle finalisation] ->
+  crop_and_rotate_frame (depth and mask)
+
+Everything between the int16 raw chunk and the 80x80 crops stays in HBM; the
+only host traffic is the per-frame feature vector needed by the sequential
+angle logic (A19, host-side in the reference too) and the results handed to
+the writer.  The data-dict keys match the reference's steps so the writer and
+h5 schema drop in unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import proc
+from ._lib import call
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@dataclass
+class ExtractConfig:
+    """The extract CLI options on the hot path (M/cli.py:333-418 defaults)."""
+    min_height: float = 0
+    max_height: float = 100
+    chunk_size: int = 1000
+    chunk_overlap: int = 0
+    batch_size: int = 32
+    crop_size: Tuple[int, int] = (80, 80)
+    frame_threshold: float = 3
+    iters_tail: int = 3
+    mask_iou_threshold: float = 0.5
+    fix_invalid_pixels: bool = True
+
+
+def mask_nms_select(out: dict, iou_thresh: float = 0.5):
+    """GPU mask-IoU NMS + instance-0 selection over a forward's outputs.
+    Returns (d2_mask uint8 (B,h,w), keypoints float64 (B,K,3), nkeep int32 (B,),
+    keep_idx int32 (B,D))."""
+    masks = out["masks"]
+    B, D, h, w = masks.shape
+    K = out["keypoints"].shape[2]
+    dev = masks.device
+    keep_idx = torch.empty((B, D), dtype=torch.int32, device=dev)
+    nkeep = torch.empty((B,), dtype=torch.int32, device=dev)
+    sel = torch.empty((B, h, w), dtype=torch.uint8, device=dev)
+    kp = torch.empty((B, K, 3), dtype=torch.float64, device=dev)
+    call("mdx_mask_nms_select", _p(masks), _p(out["scores"]), _p(out["ndet"]), _p(out["keypoints"]), B, D, K, h, w,
+         float(iou_thresh), _p(keep_idx), _p(nkeep), _p(sel), _p(kp), _stream())
+    return sel, kp, nkeep, keep_idx
+
+
+class GPUExtractor:
+    """Chunk processor of the hot path on the current GPU."""
+
+    def __init__(self, bground_im, roi, predictor, config: ExtractConfig = ExtractConfig()):
+        self.cfg = config
+        self.prep = proc.FramePrep(bground_im, roi, config.min_height, config.max_height, config.fix_invalid_pixels)
+        self.lut = proc.scale_lut(config.min_height, config.max_height)
+        self.predictor = predictor
+        self.strel = proc.ELLIPSE9
+
+    def infer(self, prepped: torch.Tensor):
+        """Model forward over a prepped chunk in batch_size slices
+        (InferenceStep.process); returns concatenated device outputs."""
+        outs = []
+        n = prepped.shape[0]
+        bs = min(self.cfg.batch_size, n)
+        for i in range(0, n, bs):
+            o = self.predictor.run(prepped[i:i + bs], self.lut)
+            sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
+            o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+            outs.append(o)
+        keys = ("boxes", "scores", "classes", "ndet", "keypoints", "d2_mask", "sel_keypoints", "nkeep", "keep_idx")
+        return {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
+
+    def features(self, prepped: torch.Tensor, d2_mask: torch.Tensor):
+        """clean_frames(iters_tail=3) + get_frame_features(mask=d2, thr=3)."""
+        cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
+        feats = proc.frame_moments(cleaned, d2_mask, float(self.cfg.frame_threshold))
+        return cleaned, feats
+
+    def crop(self, prepped, d2_mask, centroid, angle_deg):
+        return proc.crop_and_rotate_frames(prepped, centroid, angle_deg, self.cfg.crop_size, frames2=d2_mask)
+
+    def step_device(self, raw: torch.Tensor):
+        """One pass over a batch with the angle computed on the device
+        (clamp_angles_deg(-rad2deg(orientation)), the non-tracking path
+        before flip correction).  Used by bench.py; returns the crops."""
+        prepped = self.prep(raw)
+        inf = self.infer(prepped)
+        cleaned, feats = self.features(prepped, inf["d2_mask"])
+        ang = -torch.rad2deg(feats["orientation"])
+        ang = torch.where(ang < 0, 360 + ang, ang) % 360
+        depth, mask = self.crop(prepped, inf["d2_mask"], feats["centroid"], ang)
+        return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
+                "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}

@@ -337,3 +337,51 @@ def test_predictor_instances(mdx):
     assert ins.pred_boxes.tensor.shape == (n, 4) and ins.pred_classes.dtype == torch.int64
     single = p(img[0])
     assert isinstance(single, dict) and "instances" in single
+
+
+def test_mask_nms_select(mdx):
+    from moseq2_detectron_extract_amd.pipeline import mask_nms_select
+    from oracle import features_ref as FR
+    rng = np.random.default_rng(8)
+    B, D, K, h, w = 6, 4, 8, 37, 53
+    masks = np.zeros((B, D, h, w), np.uint8)
+    for b in range(B):
+        for d in range(D):
+            y0, x0 = rng.integers(0, 25), rng.integers(0, 35)
+            masks[b, d, y0:y0 + rng.integers(3, 14), x0:x0 + rng.integers(3, 20)] = 1
+    masks[1, 2] = masks[1, 0]           # duplicate -> suppressed
+    masks[2, 1] = 0                     # empty mask dropped
+    masks[3, :, 5:30, 5:40] = 1         # all overlap
+    scores = rng.random((B, D)).astype(np.float32)
+    ndet = np.array([4, 4, 4, 4, 1, 0], np.int32)
+    kpts = rng.random((B, D, K, 3)).astype(np.float32)
+    out = {"masks": torch.from_numpy(masks).cuda(), "scores": torch.from_numpy(scores).cuda(),
+           "ndet": torch.from_numpy(ndet).cuda(), "keypoints": torch.from_numpy(kpts).cuda()}
+    sel, kp, nkeep, keep = mask_nms_select(out, 0.5)
+    for b in range(B):
+        n = ndet[b]
+        want = FR.nms_mask_instances(masks[b, :n].astype(bool), scores[b, :n])
+        got = keep[b, :int(nkeep[b])].cpu().tolist()
+        assert got == want, (b, got, want)
+        if want:
+            np.testing.assert_array_equal(sel[b].cpu().numpy(), masks[b, want[0]])
+            np.testing.assert_array_equal(kp[b].cpu().numpy(), kpts[b, want[0]].astype(np.float64))
+        else:
+            assert not sel[b].any() and torch.isnan(kp[b]).all()
+
+
+def test_gpu_extractor_step(mdx):
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    from oracle import frameops as O
+    s = synth.SyntheticSession(4, seed=2)
+    raw = s.frames(0, 4)
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
+    r = ex.step_device(torch.from_numpy(raw).cuda())
+    assert r["depth_frames"].shape == (4, 80, 80) and r["mask_frames"].shape == (4, 80, 80)
+    # the crops equal the oracle crop of the same prepped frames at the same centre/angle
+    prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
+    c = r["centroid"].cpu().numpy(); a = r["angle"].cpu().numpy()
+    np.testing.assert_array_equal(r["depth_frames"].cpu().numpy(), O.crop_and_rotate_frames(prepped, c, a))
