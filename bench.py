@@ -86,6 +86,9 @@ def cpu_baseline(nframes: int, dtype_cfg):
     from oracle import frameops as O
     from oracle import model_ref as R
     cores = len(os.sched_getaffinity(0))
+    # the GPU box exposes the whole machine's cores but grants this job a share
+    # (OMP_NUM_THREADS); oversubscribing 256 threads is far slower
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     torch.set_num_threads(cores)
     s = synth.SyntheticSession(nframes, seed=123)
     raw = s.frames(0, nframes)
