@@ -39,10 +39,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
+    ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     return ap.parse_args()
 
 
-def conv_roofline(extractor, raw, steps=3):
+def conv_roofline(extractor, raw, steps=3, dump=None):
     """Time every conv launch of a step with HIP events on the launch stream;
     returns (algorithmic conv FLOP per step, conv seconds per step, launches)."""
     import torch
@@ -59,7 +60,8 @@ def conv_roofline(extractor, raw, steps=3):
         e1.record(s)
         OH, OW = r[1], r[2]
         cin_alg = 3 if c is self.stem else c.cin
-        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * c.k * c.k * cin_alg))
+        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * c.k * c.k * cin_alg,
+                    (N * OH * OW, c.cout, c.k * c.k * c.cin, c.k, c.stride, out_mode, residual is not None)))
         return r
 
     RT.MaskRCNN.conv = timed
@@ -69,8 +71,15 @@ def conv_roofline(extractor, raw, steps=3):
         torch.cuda.synchronize()
     finally:
         RT.MaskRCNN.conv = orig
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in rec)
-    fl = sum(f for _, _, f in rec)
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in rec)
+    fl = sum(f for _, _, f, _ in rec)
+    if dump:
+        per = len(rec) // steps
+        rows = [{"M": sh[0], "N": sh[1], "K": sh[2], "k": sh[3], "stride": sh[4], "mode": sh[5], "res": sh[6],
+                 "us": e0.elapsed_time(e1) * 1e3, "tflops": f / (e0.elapsed_time(e1) * 1e-3) / 1e12}
+                for e0, e1, f, sh in rec[-per:]]
+        with open(dump, "w") as fh:
+            json.dump(rows, fh, indent=0)
     return fl / steps, ms / 1e3 / steps, len(rec) // steps
 
 
@@ -173,7 +182,7 @@ def main():
 
     roof = None
     if not args.no_roofline:
-        fl, sec, nl = conv_roofline(ex, raw_all[:B])
+        fl, sec, nl = conv_roofline(ex, raw_all[:B], dump=args.dump_convs)
         peak = 2500.0 if args.dtype == "fp16" else 157.3
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "conv_pmc_summary.json")

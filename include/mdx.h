@@ -158,14 +158,18 @@ int mdx_box_postprocess(const float *pred, int ld_pred, const float *proposals, 
                         int64_t *det_classes, int *ndet, mdx_stream_t stream);
 
 /* mask_rcnn_inference sigmoid + paste_masks_in_image (grid_sample) >= thresh:
- * logits float32 (B*D, M, M) -> out uint8 (B, D, img_h, img_w). */
+ * logits float32 (B*D, M, M) -> out uint8, plane r = b*D + d at
+ * out + r*plane_stride (img_h x img_w, row-major; plane_stride >= img_h*img_w,
+ * a multiple of 16 keeps every plane 16-B aligned). */
 int mdx_paste_masks(const float *logits, const float *boxes, const int *counts, int B, int D, int M,
-                    int img_h, int img_w, float thresh, uint8_t *out, mdx_stream_t stream);
+                    int img_h, int img_w, int64_t plane_stride, float thresh, uint8_t *out,
+                    mdx_stream_t stream);
 
-/* keypoint head score_lowres ConvTranspose2d(k=4, s=2, p=1): x (R,Hi,Wi,Cin),
- * w float32 [Cin][Co][4][4] -> out float32 (R, Co, 2Hi, 2Wi). */
-int mdx_keypoint_deconv(const void *x, int R, int Hi, int Wi, int Cin, const float *w, const float *bias,
-                        int Co, int dtype, float *out, mdx_stream_t stream);
+/* keypoint head score_lowres ConvTranspose2d(k=4, s=2, p=1) second half:
+ * y float32 (R*Hi*Wi, Co*16) = mdx_conv2d(x, W[co*16+ky*4+kx][ci]) ->
+ * out float32 (R, Co, 2Hi, 2Wi) (col2im + bias). */
+int mdx_deconv_col2im(const float *y, const float *bias, int R, int Hi, int Wi, int Co, float *out,
+                      mdx_stream_t stream);
 
 /* F.interpolate(scale_factor=2, bilinear, align_corners=False), float32 NCHW. */
 int mdx_upsample_bilinear2x(const float *x, int NC, int H, int W, float *out, mdx_stream_t stream);
@@ -173,12 +177,13 @@ int mdx_upsample_bilinear2x(const float *x, int NC, int H, int W, float *out, md
 /* ProcessFeaturesStep.__nms_mask_instances (mask-IoU NMS, reference quirks
  * kept; M/pipeline/process_features_step.py:63-113) + instance-0 selection of
  * mask_and_keypoints_from_model_output (M/proc/proc.py:657-685).
- * masks uint8 (B,D,h,w), scores (B,D), ndet (B), kpts float32 (B,D,K,3) ->
+ * masks uint8 planes of plane_stride bytes (B*D planes of h*w), scores (B,D),
+ * ndet (B), kpts float32 (B,D,K,3) ->
  * keep_idx int32 (B,D) (-1 padded, pick order), nkeep (B), sel_mask uint8
  * (B,h,w), sel_kpts float64 (B,K,3) (NaN when no instance). */
-int mdx_mask_nms_select(const uint8_t *masks, const float *scores, const int *ndet, const float *kpts,
-                        int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx, int *nkeep,
-                        uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream);
+int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, const float *scores, const int *ndet,
+                        const float *kpts, int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx,
+                        int *nkeep, uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream);
 
 /* heatmaps_to_keypoints: maps float32 (B*D, K, M, M) -> (B*D, K, 3) [x, y, score]. */
 int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,

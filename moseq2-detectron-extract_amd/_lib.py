@@ -46,11 +46,11 @@ SIGNATURES = {
                                 P, P, P, P, P]),
     "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "mdx_box_postprocess": (I32, [P, I32, P, P, I32, I32, I32, F32, F32, I32, I32, P, F32, P, P, P, P, P]),
-    "mdx_paste_masks": (I32, [P, P, P, I32, I32, I32, I32, I32, F32, P, P]),
-    "mdx_keypoint_deconv": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, P, P]),
+    "mdx_paste_masks": (I32, [P, P, P, I32, I32, I32, I32, I32, I64, F32, P, P]),
+    "mdx_deconv_col2im": (I32, [P, P, I32, I32, I32, I32, P, P]),
     "mdx_upsample_bilinear2x": (I32, [P, I32, I32, I32, P, P]),
     "mdx_heatmaps_to_keypoints": (I32, [P, P, P, I32, I32, I32, I32, P, P]),
-    "mdx_mask_nms_select": (I32, [P, P, P, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P]),
+    "mdx_mask_nms_select": (I32, [P, I64, P, P, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P]),
 }
 
 

@@ -2,17 +2,23 @@
 // (M/proc/proc.py:189-210; OpenCV imgproc/inpaint.cpp icvNSInpaintFMM as
 // restated in oracle/frameops.c orc_inpaint_ns_one).
 //
-// One wavefront per frame.  The fast-marching order is inherently serial per
-// frame, so the frame axis carries the parallelism (a 1000-frame chunk keeps
-// ~1000 waves in flight); inside a frame the 64 lanes evaluate the (2r+1)^2
-// window taps of one pixel in parallel and lane 0 folds them in the
-// reference's k-major/l-minor order (float adds are not reassociated).
+// Parallel decomposition that is EXACT w.r.t. the serial fast-marching order:
+// computing an unknown pixel reads state only within Chebyshev distance
+// `range + 1` of it (window taps +-range, gradients +-1, FMM neighbours +-1),
+// and writes only the pixel itself.  Unknown pixels are therefore grouped into
+// clusters (connected under Chebyshev distance <= range + 1); two clusters
+// never read each other's changing state.  OpenCV's priority list pops by
+// (T, insertion order); restricted to one cluster that order is the order a
+// cluster-local list produces (its initial narrow band is pushed in raster
+// order with T = 0, every later push has T >= 0.5), so each cluster can be
+// marched independently -- one lane per cluster -- and the result is
+// bit-identical to the serial algorithm.
 //
-// Priority queue: OpenCV's sorted list pops by (T, insertion order).  The
-// initial narrow band is pushed in raster order with T = 0 and every later
-// push has T >= 0.5, so the band drains first, in raster order: it is kept as
-// a FIFO array; later pushes go to a binary min-heap on (T, seq) in LDS (or in
-// global workspace when a frame has more unknown pixels than LDS holds).
+//   k_inp_setup   (one workgroup per frame): flags/T image, raster-ordered
+//                 unknown-pixel list, narrow band, cluster labels (min-label
+//                 propagation + pointer jumping), cluster member lists.
+//   k_inp_march   (one lane per cluster): local FIFO(band) + heap(T, seq) FMM
+//                 with the NS weights, pixel values written in place.
 #include <cmath>
 
 #include "common.h"
@@ -21,8 +27,33 @@
 
 namespace mdx {
 
-constexpr int INP_KNOWN = 0, INP_BAND = 1, INP_INSIDE = 2;
-constexpr int INP_LDS_HEAP = 3072;  // entries (12 B each)
+// code image: >= 0 unknown (index into the unknown list); -1 KNOWN; -2 BAND
+constexpr int C_KNOWN = -1, C_BAND = -2;
+constexpr int INP_SETUP_THREADS = 256, INP_MARCH_BLOCKS = 16;
+
+struct InpLayout {
+    long long np;  // padded pixels
+    // offsets (in int32 units) of the per-frame arrays
+    long long o_code, o_t, o_ins, o_lab, o_cnt, o_start, o_fill, o_ord, o_scr, o_hdr, total;
+};
+
+static inline InpLayout inp_layout(int H, int W) {
+    InpLayout L;
+    L.np = (long long)(H + 2) * (W + 2);
+    long long o = 0;
+    L.o_hdr = o; o += 16;
+    L.o_code = o; o += L.np;
+    L.o_t = o; o += L.np;
+    L.o_ins = o; o += L.np;
+    L.o_lab = o; o += L.np;
+    L.o_cnt = o; o += L.np;
+    L.o_start = o; o += L.np + 1;
+    L.o_fill = o; o += L.np;
+    L.o_ord = o; o += L.np;
+    L.o_scr = o; o += 7 * L.np;
+    L.total = (o + 3) / 4 * 4;
+    return L;
+}
 
 struct HEnt {
     float T;
@@ -61,19 +92,20 @@ __device__ HEnt heap_pop(HEnt *h, int &n) {
     return top;
 }
 
-__device__ __forceinline__ float fm_solve(int i1, int j1, int i2, int j2, const uint8_t *f, const float *t, int PW) {
+__device__ __forceinline__ float fm_solve(int i1, int j1, int i2, int j2, const int *code, const float *t, int PW) {
     double sol;
     const double a11 = t[i1 * PW + j1], a22 = t[i2 * PW + j2];
     const double m12 = a11 < a22 ? a11 : a22;
-    if (f[i1 * PW + j1] != INP_INSIDE) {
-        if (f[i2 * PW + j2] != INP_INSIDE) {
+    const bool in1 = code[i1 * PW + j1] >= 0, in2 = code[i2 * PW + j2] >= 0;
+    if (!in1) {
+        if (!in2) {
             if (fabs(a11 - a22) >= 1.0)
                 sol = 1 + m12;
             else
                 sol = (a11 + a22 + sqrt((double)(2 - (a11 - a22) * (a11 - a22)))) * 0.5;
         } else
             sol = 1 + a11;
-    } else if (f[i2 * PW + j2] != INP_INSIDE)
+    } else if (!in2)
         sol = 1 + a22;
     else
         sol = 1 + m12;
@@ -85,168 +117,289 @@ __device__ __forceinline__ float min4f(float a, float b, float c, float d) {
     return x < y ? x : y;
 }
 
-static inline int64_t inp_frame_bytes(int H, int W) {
-    const int64_t np = (int64_t)(H + 2) * (W + 2);
-    const int64_t fb = (np + 15) / 16 * 16;
-    return fb + 4 * np + (int64_t)sizeof(HEnt) * np + 16;
+__device__ __forceinline__ int block_scan_excl(int v, int *sh, int &total) {
+    // exclusive prefix sum over a 256-thread block (sh: >= 256 ints)
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < INP_SETUP_THREADS; o <<= 1) {
+        const int a = tid >= o ? sh[tid - o] : 0;
+        __syncthreads();
+        sh[tid] += a;
+        __syncthreads();
+    }
+    const int incl = sh[tid];
+    total = sh[INP_SETUP_THREADS - 1];
+    __syncthreads();
+    return incl - v;
 }
 
-__global__ __launch_bounds__(64) void k_inpaint(uint8_t *__restrict__ frames, const uint8_t *__restrict__ invalid,
-                                                int H, int W, int range, uint8_t *__restrict__ ws,
-                                                int64_t ws_per_frame) {
-    __shared__ HEnt s_heap[INP_LDS_HEAP];
-    __shared__ int s_cnt[2];
-    __shared__ float s_w[64], s_wv[64];
-    const int lane = threadIdx.x;
-    const int64_t fidx = blockIdx.x;
-    uint8_t *out = frames + fidx * (int64_t)H * W;
-    const uint8_t *msk = invalid + fidx * (int64_t)H * W;
+__global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *__restrict__ invalid, int H, int W,
+                                                                 int range, int *__restrict__ ws, InpLayout L) {
+    __shared__ int sh[INP_SETUP_THREADS];
+    __shared__ int s_flag;
+    const int tid = threadIdx.x;
+    const long long f = blockIdx.x;
+    const uint8_t *msk = invalid + f * (long long)H * W;
+    int *base = ws + f * L.total;
+    int *hdr = base + L.o_hdr;
+    int *code = base + L.o_code;
+    float *t = reinterpret_cast<float *>(base + L.o_t);
+    int *ins = base + L.o_ins, *lab = base + L.o_lab, *cnt = base + L.o_cnt, *start = base + L.o_start;
+    int *fill = base + L.o_fill, *ord = base + L.o_ord;
     const int PH = H + 2, PW = W + 2;
-    const int64_t np = (int64_t)PH * PW;
-    uint8_t *base = ws + fidx * ws_per_frame;
-    uint8_t *f = base;
-    float *t = reinterpret_cast<float *>(base + (np + 15) / 16 * 16);
-    HEnt *fifo = reinterpret_cast<HEnt *>(t + np);  // band FIFO, then global heap storage
-
-    // any unknown pixel at all?  (inpaint is a no-op otherwise)
     int any = 0;
-    for (int64_t i = lane; i < (int64_t)H * W; i += 64) any |= msk[i] != 0;
-    if (!__any(any)) return;
-
-    for (int64_t i = lane; i < np; i += 64) {
-        const int y = (int)(i / PW), x = (int)(i - (int64_t)y * PW);
-        const bool in = y >= 1 && y <= H && x >= 1 && x <= W && msk[(int64_t)(y - 1) * W + x - 1] != 0;
-        f[i] = in ? INP_INSIDE : INP_KNOWN;
+    for (long long i = tid; i < (long long)H * W; i += INP_SETUP_THREADS) any |= msk[i] != 0;
+    if (tid == 0) s_flag = 0;
+    __syncthreads();
+    if (any) atomicOr(&s_flag, 1);
+    __syncthreads();
+    if (!s_flag) {
+        if (tid == 0) hdr[0] = hdr[1] = 0;
+        return;
+    }
+    for (long long i = tid; i < L.np; i += INP_SETUP_THREADS) {
+        code[i] = C_KNOWN;
         t[i] = 1.0e6f;
     }
     __syncthreads();
-    // narrow band = dilate(mask, cross) - mask on the interior, raster order
-    int nband = 0, ninside = 0;
-    for (int64_t i0 = 0; i0 < np; i0 += 64) {
-        const int64_t i = i0 + lane;
-        bool band = false;
-        if (i < np) {
-            const int y = (int)(i / PW), x = (int)(i - (int64_t)y * PW);
-            if (y >= 1 && y < PH - 1 && x >= 1 && x < PW - 1) {
-                if (f[i] == INP_INSIDE) {
-                    ++ninside;
-                } else {
-                    band = f[i - 1] == INP_INSIDE || f[i + 1] == INP_INSIDE || f[i - PW] == INP_INSIDE ||
-                           f[i + PW] == INP_INSIDE;
-                }
-            }
+    // unknown pixels in raster order (interior of the padded frame)
+    int nin = 0;
+    for (long long i0 = 0; i0 < L.np; i0 += INP_SETUP_THREADS) {
+        const long long i = i0 + tid;
+        int in = 0;
+        if (i < L.np) {
+            const int y = (int)(i / PW), x = (int)(i - (long long)y * PW);
+            in = (y >= 1 && y <= H && x >= 1 && x <= W && msk[(long long)(y - 1) * W + x - 1] != 0) ? 1 : 0;
         }
-        const unsigned long long bal = __ballot(band);
-        if (band) {
-            const int pos = nband + __popcll(bal & ((1ull << lane) - 1ull));
-            fifo[pos] = HEnt{0.0f, pos, (int)i};
+        int tot;
+        const int pos = nin + block_scan_excl(in, sh, tot);
+        if (in) {
+            ins[pos] = (int)i;
+            code[i] = pos;
+            lab[pos] = pos;
         }
-        nband += __popcll(bal);
+        nin += tot;
     }
-    // ninside is per-lane: reduce
-    for (int o = 32; o > 0; o >>= 1) ninside += __shfl_xor(ninside, o);
     __syncthreads();
-    for (int k = lane; k < nband; k += 64) {
-        const int i = fifo[k].idx;
-        f[i] = INP_BAND;
-        t[i] = 0.0f;
-    }
-    const bool lds_heap = ninside <= INP_LDS_HEAP;
-    HEnt *heap = lds_heap ? s_heap : fifo + nband;
-    int heap_n = 0, head = 0, seq = nband;
-    __syncthreads();
-
-    const int wsz = 2 * range + 1;
-    for (;;) {
-        // pop: FIFO (T = 0) first, then the heap
-        int idx = -1;
-        if (lane == 0) {
-            if (head < nband)
-                idx = fifo[head++].idx;
-            else if (heap_n > 0)
-                idx = heap_pop(heap, heap_n).idx;
-        }
-        idx = __shfl(idx, 0);
-        if (idx < 0) break;
-        const int ii = idx / PW, jj = idx - ii * PW;
-        if (lane == 0) f[idx] = INP_KNOWN;
-        __syncthreads();
+    // narrow band: interior 4-neighbours of unknown pixels that are not unknown
+    for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
+        const int i = ins[k];
+        const int nb[4] = {i - PW, i - 1, i + PW, i + 1};
         for (int q = 0; q < 4; ++q) {
-            int i, j;
-            if (q == 0) { i = ii - 1; j = jj; }
-            else if (q == 1) { i = ii; j = jj - 1; }
-            else if (q == 2) { i = ii + 1; j = jj; }
-            else { i = ii; j = jj + 1; }
-            if (i <= 1 || j <= 1 || i > PH - 1 || j > PW - 1) continue;
-            if (f[i * PW + j] != INP_INSIDE) continue;
-            const float dist = min4f(fm_solve(i - 1, j, i, j - 1, f, t, PW), fm_solve(i + 1, j, i, j - 1, f, t, PW),
-                                     fm_solve(i - 1, j, i, j + 1, f, t, PW), fm_solve(i + 1, j, i, j + 1, f, t, PW));
-            // window taps, one per lane (range <= 3)
-            float w = 0.0f, wv = 0.0f;
-            bool valid = false;
-            if (lane < wsz * wsz) {
-                const int k = i - range + lane / wsz, l = j - range + lane % wsz;
-                const int km = k - 1 + (k == 1), kp = k - 1 - (k == PH - 2);
-                const int lm = l - 1 + (l == 1), lp = l - 1 - (l == PW - 2);
-                if (k > 0 && l > 0 && k < PH - 1 && l < PW - 1 && f[k * PW + l] != INP_INSIDE &&
-                    (l - j) * (l - j) + (k - i) * (k - i) <= range * range) {
-                    valid = true;
-                    const float ry = (float)(k - i), rx = (float)(l - j);
-                    const float lr = rx * rx + ry * ry;
-                    const float dst = (float)(1. / (lr * sqrt((double)lr)));
-                    const bool up_ok = f[(k - 1) * PW + l] != INP_INSIDE, dn_ok = f[(k + 1) * PW + l] != INP_INSIDE;
-                    const bool lf_ok = f[k * PW + l - 1] != INP_INSIDE, rt_ok = f[k * PW + l + 1] != INP_INSIDE;
-                    float gx, gy;
-                    if (dn_ok) {
-                        if (up_ok)
-                            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm]) +
-                                         abs(out[kp * W + lm] - out[(km - 1) * W + lm]));
-                        else
-                            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm])) * 2.0f;
-                    } else {
-                        if (up_ok)
-                            gx = (float)(abs(out[kp * W + lm] - out[(km - 1) * W + lm])) * 2.0f;
-                        else
-                            gx = 0;
+            const int p = nb[q];
+            const int y = p / PW, x = p - y * PW;
+            if (y >= 1 && y < PH - 1 && x >= 1 && x < PW - 1 && code[p] < 0) {
+                code[p] = C_BAND;
+                t[p] = 0.0f;
+            }
+        }
+    }
+    __syncthreads();
+    // clusters: min-label propagation over Chebyshev distance <= range + 1
+    const int R = range + 1;
+    for (int iter = 0; iter < 1 << 20; ++iter) {
+        if (tid == 0) s_flag = 0;
+        __syncthreads();
+        int changed = 0;
+        for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
+            const int i = ins[k];
+            const int y = i / PW, x = i - y * PW;
+            int m = lab[k];
+            for (int dy = -R; dy <= R; ++dy) {
+                const int yy = y + dy;
+                if (yy < 1 || yy > H) continue;
+                for (int dx = -R; dx <= R; ++dx) {
+                    const int xx = x + dx;
+                    if (xx < 1 || xx > W) continue;
+                    const int c = code[yy * PW + xx];
+                    if (c >= 0) {
+                        const int l = lab[c];
+                        m = l < m ? l : m;
                     }
-                    if (rt_ok) {
-                        if (lf_ok)
-                            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm]) +
-                                          abs(out[km * W + lm] - out[km * W + lm - 1]));
-                        else
-                            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm])) * 2.0f;
-                    } else {
-                        if (lf_ok)
-                            gy = -(float)(abs(out[km * W + lm] - out[km * W + lm - 1])) * 2.0f;
-                        else
-                            gy = 0;
-                    }
-                    const float dot = rx * gx + ry * gy;
-                    const float lg = gx * gx + gy * gy;
-                    float dir = fabsf(dot / sqrtf(lr * lg));
-                    if (!(dir > 0.01f)) dir = 0.000001f;
-                    w = dst * dir;
-                    wv = w * (float)out[km * W + lm];
                 }
             }
-            s_w[lane] = valid ? w : 0.0f;
-            s_wv[lane] = valid ? wv : -1.0f;  // -1 marks a skipped tap
-            __syncthreads();
-            if (lane == 0) {
+            m = lab[m] < m ? lab[m] : m;  // pointer jump
+            if (m < lab[k]) {
+                atomicMin(&lab[k], m);
+                changed = 1;
+            }
+        }
+        if (changed) atomicOr(&s_flag, 1);
+        __syncthreads();
+        if (!s_flag) break;
+    }
+    // cluster ids for roots (lab[k] == k) in raster order, member counts, starts
+    int ncl = 0;
+    for (int k0 = 0; k0 < nin; k0 += INP_SETUP_THREADS) {
+        const int k = k0 + tid;
+        const int root = (k < nin && lab[k] == k) ? 1 : 0;
+        int tot;
+        const int pos = ncl + block_scan_excl(root, sh, tot);
+        if (root) {
+            fill[k] = pos;  // temporarily: root index -> cluster id
+            cnt[pos] = 0;
+        }
+        ncl += tot;
+    }
+    __syncthreads();
+    for (int k = tid; k < nin; k += INP_SETUP_THREADS) atomicAdd(&cnt[fill[lab[k]]], 1);
+    __syncthreads();
+    int run = 0;
+    for (int c0 = 0; c0 < ncl; c0 += INP_SETUP_THREADS) {
+        const int c = c0 + tid;
+        const int v = c < ncl ? cnt[c] : 0;
+        int tot;
+        const int pos = run + block_scan_excl(v, sh, tot);
+        if (c < ncl) start[c] = pos;
+        run += tot;
+    }
+    if (tid == 0) start[ncl] = nin;
+    __syncthreads();
+    // members: cluster id per member, then atomic slot (sorted per cluster later)
+    for (int k = tid; k < nin; k += INP_SETUP_THREADS) lab[k] = fill[lab[k]];
+    __syncthreads();
+    for (int c = tid; c < ncl; c += INP_SETUP_THREADS) cnt[c] = 0;
+    __syncthreads();
+    for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
+        const int c = lab[k];
+        const int slot = atomicAdd(&cnt[c], 1);
+        ord[start[c] + slot] = k;
+    }
+    if (tid == 0) {
+        hdr[0] = nin;
+        hdr[1] = ncl;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_inp_march(uint8_t *__restrict__ frames, int H, int W, int range,
+                                                   int *__restrict__ ws, InpLayout L) {
+    const long long f = blockIdx.y;
+    int *base = ws + f * L.total;
+    const int ncl = base[L.o_hdr + 1];
+    int *code = base + L.o_code;
+    float *t = reinterpret_cast<float *>(base + L.o_t);
+    const int *ins = base + L.o_ins;
+    const int *start = base + L.o_start;
+    int *ord = base + L.o_ord;
+    int *scr = base + L.o_scr;
+    uint8_t *out = frames + f * (long long)H * W;
+    const int PH = H + 2, PW = W + 2;
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < ncl; c += gridDim.x * 256) {
+        const int s0 = start[c], m = start[c + 1] - s0;
+        int *mem = ord + s0;
+        // members in raster order (unknown-list index order == raster order)
+        for (int a = 1; a < m; ++a) {
+            const int v = mem[a];
+            int b = a - 1;
+            while (b >= 0 && mem[b] > v) {
+                mem[b + 1] = mem[b];
+                --b;
+            }
+            mem[b + 1] = v;
+        }
+        // this cluster's narrow band, raster order, unique
+        int *band = scr + 7LL * s0;
+        HEnt *heap = reinterpret_cast<HEnt *>(band + 4LL * m);
+        int nb = 0;
+        for (int a = 0; a < m; ++a) {
+            const int i = ins[mem[a]];
+            const int cand[4] = {i - PW, i - 1, i + 1, i + PW};
+            for (int q = 0; q < 4; ++q) {
+                const int p = cand[q];
+                if (code[p] != C_BAND) continue;
+                // insert sorted, skip duplicates
+                int b = nb - 1;
+                bool dup = false;
+                while (b >= 0 && band[b] >= p) {
+                    if (band[b] == p) {
+                        dup = true;
+                        break;
+                    }
+                    --b;
+                }
+                if (dup) continue;
+                for (int z = nb; z > b + 1; --z) band[z] = band[z - 1];
+                band[b + 1] = p;
+                ++nb;
+            }
+        }
+        int head = 0, hn = 0, seq = nb;
+        for (;;) {
+            int idx;
+            if (head < nb)
+                idx = band[head++];
+            else if (hn > 0)
+                idx = heap_pop(heap, hn).idx;
+            else
+                break;
+            const int ii = idx / PW, jj = idx - ii * PW;
+            code[idx] = C_KNOWN;
+            for (int q = 0; q < 4; ++q) {
+                int i, j;
+                if (q == 0) { i = ii - 1; j = jj; }
+                else if (q == 1) { i = ii; j = jj - 1; }
+                else if (q == 2) { i = ii + 1; j = jj; }
+                else { i = ii; j = jj + 1; }
+                if (i <= 1 || j <= 1 || i > PH - 1 || j > PW - 1) continue;
+                if (code[i * PW + j] < 0) continue;
+                const float dist =
+                    min4f(fm_solve(i - 1, j, i, j - 1, code, t, PW), fm_solve(i + 1, j, i, j - 1, code, t, PW),
+                          fm_solve(i - 1, j, i, j + 1, code, t, PW), fm_solve(i + 1, j, i, j + 1, code, t, PW));
                 float Ia = 0.0f, s = 1.0e-20f;
-                for (int L = 0; L < wsz * wsz; ++L) {
-                    if (s_wv[L] < 0.0f) continue;
-                    Ia += s_wv[L];
-                    s += s_w[L];
+                for (int k = i - range; k <= i + range; ++k) {
+                    const int km = k - 1 + (k == 1), kp = k - 1 - (k == PH - 2);
+                    for (int l = j - range; l <= j + range; ++l) {
+                        const int lm = l - 1 + (l == 1), lp = l - 1 - (l == PW - 2);
+                        if (!(k > 0 && l > 0 && k < PH - 1 && l < PW - 1)) continue;
+                        if (code[k * PW + l] >= 0) continue;
+                        if ((l - j) * (l - j) + (k - i) * (k - i) > range * range) continue;
+                        const float ry = (float)(k - i), rx = (float)(l - j);
+                        const float lr = rx * rx + ry * ry;
+                        const float dst = (float)(1. / (lr * sqrt((double)lr)));
+                        const bool up_ok = code[(k - 1) * PW + l] < 0, dn_ok = code[(k + 1) * PW + l] < 0;
+                        const bool lf_ok = code[k * PW + l - 1] < 0, rt_ok = code[k * PW + l + 1] < 0;
+                        float gx, gy;
+                        if (dn_ok) {
+                            if (up_ok)
+                                gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm]) +
+                                             abs(out[kp * W + lm] - out[(km - 1) * W + lm]));
+                            else
+                                gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm])) * 2.0f;
+                        } else {
+                            if (up_ok)
+                                gx = (float)(abs(out[kp * W + lm] - out[(km - 1) * W + lm])) * 2.0f;
+                            else
+                                gx = 0;
+                        }
+                        if (rt_ok) {
+                            if (lf_ok)
+                                gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm]) +
+                                              abs(out[km * W + lm] - out[km * W + lm - 1]));
+                            else
+                                gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm])) * 2.0f;
+                        } else {
+                            if (lf_ok)
+                                gy = -(float)(abs(out[km * W + lm] - out[km * W + lm - 1])) * 2.0f;
+                            else
+                                gy = 0;
+                        }
+                        const float dot = rx * gx + ry * gy;
+                        const float lg = gx * gx + gy * gy;
+                        float dir = fabsf(dot / sqrtf(lr * lg));
+                        if (!(dir > 0.01f)) dir = 0.000001f;
+                        const float w = dst * dir;
+                        Ia += w * (float)out[km * W + lm];
+                        s += w;
+                    }
                 }
                 const double v = (double)Ia / s;
                 const int r = __double2int_rn(v);
                 out[(i - 1) * W + (j - 1)] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
                 t[i * PW + j] = dist;
-                f[i * PW + j] = INP_BAND;
-                heap_push(heap, heap_n, HEnt{dist, seq++, i * PW + j});
+                code[i * PW + j] = C_BAND;
+                heap_push(heap, hn, HEnt{dist, seq++, i * PW + j});
             }
-            __syncthreads();
         }
     }
 }
@@ -257,20 +410,24 @@ using namespace mdx;
 
 extern "C" int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W) {
     if (n <= 0 || H <= 0 || W <= 0) return 0;
-    return n * inp_frame_bytes(H, W);
+    return n * inp_layout(H, W).total * 4;
 }
 
 extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
                               void *workspace, mdx_stream_t stream) {
     MDX_REQUIRE(frames && invalid, "mdx_inpaint_ns: null frames/invalid");
-    MDX_REQUIRE(radius >= 0 && radius <= 3, "mdx_inpaint_ns: radius must be in [0, 3] (got %d)", radius);
+    MDX_REQUIRE(radius >= 0 && radius <= 7, "mdx_inpaint_ns: radius must be in [0, 7] (got %d)", radius);
     MDX_REQUIRE(H > 0 && W > 0, "mdx_inpaint_ns: bad shape");
     if (n == 0) return MDX_OK;
     MDX_REQUIRE(workspace != nullptr, "mdx_inpaint_ns: null workspace");
-    MDX_REQUIRE((int64_t)(H + 2) * (W + 2) < (1ll << 31), "mdx_inpaint_ns: frame too large");
-    MDX_REQUIRE(n <= 0x7fffffff, "mdx_inpaint_ns: n too large");
-    hipLaunchKernelGGL(k_inpaint, dim3((unsigned)n), dim3(64), 0, as_stream(stream), frames, invalid, H, W, radius,
-                       (uint8_t *)workspace, inp_frame_bytes(H, W));
+    MDX_REQUIRE((int64_t)(H + 2) * (W + 2) < (1ll << 30), "mdx_inpaint_ns: frame too large");
+    MDX_REQUIRE(n <= 65535, "mdx_inpaint_ns: at most 65535 frames per call");
+    const InpLayout L = inp_layout(H, W);
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_inp_setup, dim3((unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W, radius,
+                       (int *)workspace, L);
+    hipLaunchKernelGGL(k_inp_march, dim3(INP_MARCH_BLOCKS, (unsigned)n), dim3(256), 0, s, frames, H, W, radius,
+                       (int *)workspace, L);
     MDX_CHECK_LAUNCH("mdx_inpaint_ns");
     return MDX_OK;
 }

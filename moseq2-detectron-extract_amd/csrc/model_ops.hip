@@ -41,6 +41,32 @@ __device__ __forceinline__ void st(T *p, float v) {
     *p = (T)v;
 }
 
+template <typename T>
+__device__ __forceinline__ void ld8(const T *p, float *v) {
+    if constexpr (sizeof(T) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+        const T *e = reinterpret_cast<const T *>(&u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (float)e[i];
+    } else {
+        const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T *p, const float *v) {
+    if constexpr (sizeof(T) == 2) {
+        uint4 u;
+        T *e = reinterpret_cast<T *>(&u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = (T)v[i];
+        *reinterpret_cast<uint4 *>(p) = u;
+    } else {
+        *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4 *>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // preprocess
 // ---------------------------------------------------------------------------
@@ -73,26 +99,31 @@ __global__ __launch_bounds__(256) void k_preprocess(const uint8_t *__restrict__ 
 template <typename T>
 __global__ __launch_bounds__(256) void k_maxpool(const T *__restrict__ x, int N, int H, int W, int C, int k, int s,
                                                  int p, int OH, int OW, T *__restrict__ out) {
-    const long long total = (long long)N * OH * OW * C;
+    const int CV = C / 8;
+    const long long total = (long long)N * OH * OW * CV;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-        const int c = (int)(i % C);
-        long long r = i / C;
+        const int c0 = (int)(i % CV) * 8;
+        long long r = i / CV;
         const int ox = (int)(r % OW);
         r /= OW;
         const int oy = (int)(r % OH);
         const int n = (int)(r / OH);
-        float m = -INFINITY;
+        float m[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
         for (int ky = 0; ky < k; ++ky) {
             const int iy = oy * s - p + ky;
             if (iy < 0 || iy >= H) continue;
             for (int kx = 0; kx < k; ++kx) {
                 const int ix = ox * s - p + kx;
                 if (ix < 0 || ix >= W) continue;
-                const float v = ld(x + (((long long)n * H + iy) * W + ix) * C + c);
-                m = v > m ? v : m;
+                float v[8];
+                ld8(x + (((long long)n * H + iy) * W + ix) * C + c0, v);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) m[q] = v[q] > m[q] ? v[q] : m[q];
             }
         }
-        st(out + i, m);
+        st8(out + (((long long)n * OH + oy) * OW + ox) * C + c0, m);
     }
 }
 
@@ -111,6 +142,8 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     return s;
 }
 
+// stats of one (image, group); the group's channels are read 8 at a time
+// when C/G is a multiple of 8 (the FPN's 256/32)
 template <typename T>
 __global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int HW, int C, int G, float eps,
                                                   float *__restrict__ stats) {
@@ -120,17 +153,42 @@ __global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int H
     const int cpg = C / G;
     const long long base = (long long)b * HW * C + (long long)g * cpg;
     const long long cnt = (long long)HW * cpg;
+    const bool vec = (cpg % 8) == 0;
+    const int nv = cpg / 8;
     float s = 0.f;
-    for (long long i = threadIdx.x; i < cnt; i += 256) {
-        const long long px = i / cpg, c = i - px * cpg;
-        s += ld(x + base + px * C + c);
+    if (vec) {
+        for (long long i = threadIdx.x; i < (long long)HW * nv; i += 256) {
+            const long long px = i / nv, cv = i - px * nv;
+            float v[8];
+            ld8(x + base + px * C + cv * 8, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += v[k];
+        }
+    } else {
+        for (long long i = threadIdx.x; i < cnt; i += 256) {
+            const long long px = i / cpg, c = i - px * cpg;
+            s += ld(x + base + px * C + c);
+        }
     }
     const float mean = block_sum(s, red) / (float)cnt;
     float s2 = 0.f;
-    for (long long i = threadIdx.x; i < cnt; i += 256) {
-        const long long px = i / cpg, c = i - px * cpg;
-        const float d = ld(x + base + px * C + c) - mean;
-        s2 += d * d;
+    if (vec) {
+        for (long long i = threadIdx.x; i < (long long)HW * nv; i += 256) {
+            const long long px = i / nv, cv = i - px * nv;
+            float v[8];
+            ld8(x + base + px * C + cv * 8, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float d = v[k] - mean;
+                s2 += d * d;
+            }
+        }
+    } else {
+        for (long long i = threadIdx.x; i < cnt; i += 256) {
+            const long long px = i / cpg, c = i - px * cpg;
+            const float d = ld(x + base + px * C + c) - mean;
+            s2 += d * d;
+        }
     }
     const float var = block_sum(s2, red) / (float)cnt;
     if (threadIdx.x == 0) {
@@ -139,30 +197,40 @@ __global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int H
     }
 }
 
-// y = (x - mean) * rstd * gamma + beta; optionally fused: y = (y + up(prev)) * scale
+// y = (x - mean) * rstd * gamma + beta; optionally fused: y = (y + up(prev)) [/ 2]
+// 8 consecutive channels per lane (C % 8 == 0 and C/G % 8 == 0 required)
 template <typename T>
 __global__ __launch_bounds__(256) void k_gn_apply(const T *__restrict__ x, int N, int H, int W, int C, int G,
                                                   const float *__restrict__ stats, const float *__restrict__ gamma,
                                                   const float *__restrict__ beta, const T *__restrict__ up, int fuse,
                                                   T *__restrict__ out) {
-    const long long total = (long long)N * H * W * C;
+    const long long total = (long long)N * H * W * (C / 8);
     const int cpg = C / G;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-        const int c = (int)(i % C);
-        const long long pix = i / C;
+        const int c0 = (int)(i % (C / 8)) * 8;
+        const long long pix = i / (C / 8);
         const int n = (int)(pix / ((long long)H * W));
-        const int g = c / cpg;
+        const int g = c0 / cpg;
         const float mean = stats[2 * (n * G + g)], rstd = stats[2 * (n * G + g) + 1];
-        float y = (ld(x + i) - mean) * rstd * gamma[c] + beta[c];
+        float v[8];
+        ld8(x + pix * C + c0, v);
+        float u[8];
         if (fuse) {
             const int rem = (int)(pix - (long long)n * H * W);
             const int yy = rem / W, xx = rem - yy * W;
             const int UH = H / 2, UW = W / 2;
-            const float u = ld(up + (((long long)n * UH + (yy >> 1)) * UW + (xx >> 1)) * C + c);
-            y = y + u;
-            if (fuse == 2) y = y / 2.0f;
+            ld8(up + (((long long)n * UH + (yy >> 1)) * UW + (xx >> 1)) * C + c0, u);
         }
-        st(out + i, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float y = (v[k] - mean) * rstd * gamma[c0 + k] + beta[c0 + k];
+            if (fuse) {
+                y = y + u[k];
+                if (fuse == 2) y = y / 2.0f;
+            }
+            v[k] = y;
+        }
+        st8(out + pix * C + c0, v);
     }
 }
 
@@ -482,14 +550,45 @@ struct RoiLevels {
 };
 
 template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+    static constexpr int N = 4;
+};
+template <>
+struct Vec16<_Float16> {
+    static constexpr int N = 8;
+};
+
+template <typename T>
+__device__ __forceinline__ void ld16(const T *p, float *v) {
+    const uint4 u = *reinterpret_cast<const uint4 *>(p);
+    const T *e = reinterpret_cast<const T *>(&u);
+#pragma unroll
+    for (int i = 0; i < Vec16<T>::N; ++i) v[i] = (float)e[i];
+}
+template <typename T>
+__device__ __forceinline__ void st16(T *p, const float *v) {
+    uint4 u;
+    T *e = reinterpret_cast<T *>(&u);
+#pragma unroll
+    for (int i = 0; i < Vec16<T>::N; ++i) e[i] = (T)v[i];
+    *reinterpret_cast<uint4 *>(p) = u;
+}
+
+// one block per ROI; one lane per (bin, 16-byte channel group)
+template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
                                                    const int *__restrict__ counts, T *__restrict__ out) {
+    constexpr int V = Vec16<T>::N;
     const int r = blockIdx.x;
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
+    const int CG = C / V;
     T *o = out + (long long)r * P * P * C;
     if (ri >= counts[b]) {
-        for (int i = threadIdx.x; i < P * P * C; i += 256) o[i] = (T)0.f;
+        const float z[V] = {};
+        for (int i = threadIdx.x; i < P * P * CG; i += 256) st16(o + (long long)i * V, z);
         return;
     }
     const float x1 = rois[4 * r], y1 = rois[4 * r + 1], x2 = rois[4 * r + 2], y2 = rois[4 * r + 3];
@@ -515,15 +614,18 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     const int gh = rl.sampling > 0 ? rl.sampling : (int)ceilf(rh / (float)P);
     const int gw = rl.sampling > 0 ? rl.sampling : (int)ceilf(rw / (float)P);
     const float count = (float)max(gh * gw, 1);
-    for (int t = threadIdx.x; t < P * P * C; t += 256) {
-        const int c = t % C;
-        const int bin = t / C;
+    for (int t = threadIdx.x; t < P * P * CG; t += 256) {
+        const int cg = t % CG;
+        const int bin = t / CG;
         const int ph = bin / P, pw = bin - ph * P;
-        float acc = 0.f;
+        const int c0 = cg * V;
+        float acc[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] = 0.f;
         for (int iy = 0; iy < gh; ++iy) {
-            float y = rsh + (float)ph * bh + ((float)iy + .5f) * bh / (float)gh;
+            const float y = rsh + (float)ph * bh + ((float)iy + .5f) * bh / (float)gh;
             for (int ix = 0; ix < gw; ++ix) {
-                float x = rsw + (float)pw * bw + ((float)ix + .5f) * bw / (float)gw;
+                const float x = rsw + (float)pw * bw + ((float)ix + .5f) * bw / (float)gw;
                 if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) continue;
                 float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
                 int yl = (int)yy, xl = (int)xx, yh, xh;
@@ -540,14 +642,18 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
                 const float ly = yy - (float)yl, lx = xx - (float)xl;
                 const float hy = 1.f - ly, hx = 1.f - lx;
                 const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
-                const float v1 = ld(f + ((long long)yl * W + xl) * C + c);
-                const float v2 = ld(f + ((long long)yl * W + xh) * C + c);
-                const float v3 = ld(f + ((long long)yh * W + xl) * C + c);
-                const float v4 = ld(f + ((long long)yh * W + xh) * C + c);
-                acc += w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+                float v1[V], v2[V], v3[V], v4[V];
+                ld16(f + ((long long)yl * W + xl) * C + c0, v1);
+                ld16(f + ((long long)yl * W + xh) * C + c0, v2);
+                ld16(f + ((long long)yh * W + xl) * C + c0, v3);
+                ld16(f + ((long long)yh * W + xh) * C + c0, v4);
+#pragma unroll
+                for (int i = 0; i < V; ++i) acc[i] += w1 * v1[i] + w2 * v2[i] + w3 * v3[i] + w4 * v4[i];
             }
         }
-        st(o + t, acc / count);
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] = acc[i] / count;
+        st16(o + (long long)bin * C + c0, acc);
     }
 }
 
@@ -650,11 +756,11 @@ __global__ __launch_bounds__(1024) void k_box_post(BoxPostArgs ba, const float *
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_paste(const float *__restrict__ logits, const float *__restrict__ boxes,
                                                const int *__restrict__ counts, int D, int M, int img_h, int img_w,
-                                               float thr, uint8_t *__restrict__ out) {
+                                               long long plane, float thr, uint8_t *__restrict__ out) {
     __shared__ float prob[64 * 64];
     const int r = blockIdx.y;
     const int b = r / D, d = r - b * D;
-    uint8_t *o = out + (long long)r * img_h * img_w;
+    uint8_t *o = out + (long long)r * plane;
     const int rows_per_block = 8;
     const int y0 = blockIdx.x * rows_per_block;
     if (d >= counts[b]) {
@@ -695,21 +801,21 @@ __global__ __launch_bounds__(256) void k_paste(const float *__restrict__ logits,
 // ---------------------------------------------------------------------------
 // keypoint head tail
 // ---------------------------------------------------------------------------
-// ConvTranspose2d(Cin -> Co, k=4, s=2, p=1): x (R, Hi, Wi, Cin) T, w f32 [Cin][Co][4][4]
-// -> out f32 (R, Co, 2Hi, 2Wi)
-template <typename T>
-__global__ __launch_bounds__(256) void k_kp_deconv(const T *__restrict__ x, const float *__restrict__ w,
-                                                   const float *__restrict__ bias, int Hi, int Wi, int Cin, int Co,
-                                                   float *__restrict__ out) {
-    const int r = blockIdx.x;
+// ConvTranspose2d(Cin -> Co, k=4, s=2, p=1) as GEMM + col2im:
+// y (R*Hi*Wi, Co*16) f32 = x @ W[ci][co*16 + ky*4 + kx] (k_conv), then
+// out[r][co][oy][ox] = bias[co] + sum_{ky,kx: oy = 2*iy - 1 + ky, ox = 2*ix - 1 + kx} y[r,iy,ix][co,ky,kx]
+__global__ __launch_bounds__(256) void k_deconv_col2im(const float *__restrict__ y, const float *__restrict__ bias,
+                                                       int R, int Hi, int Wi, int Co, float *__restrict__ out) {
     const int OH = 2 * Hi, OW = 2 * Wi;
-    const T *xi = x + (long long)r * Hi * Wi * Cin;
-    for (int t = threadIdx.x; t < Co * OH * OW; t += 256) {
-        const int co = t / (OH * OW), rem = t - co * OH * OW;
-        const int oy = rem / OW, ox = rem - oy * OW;
+    const long long total = (long long)R * Co * OH * OW;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int ox = (int)(i % OW);
+        const int oy = (int)((i / OW) % OH);
+        const int co = (int)((i / ((long long)OH * OW)) % Co);
+        const int r = (int)(i / ((long long)OH * OW * Co));
         float acc = bias ? bias[co] : 0.f;
         for (int ky = 0; ky < 4; ++ky) {
-            const int ty = oy + 1 - ky;  // oy = iy*2 - 1 + ky
+            const int ty = oy + 1 - ky;
             if (ty < 0 || (ty & 1)) continue;
             const int iy = ty >> 1;
             if (iy >= Hi) continue;
@@ -718,12 +824,10 @@ __global__ __launch_bounds__(256) void k_kp_deconv(const T *__restrict__ x, cons
                 if (tx < 0 || (tx & 1)) continue;
                 const int ix = tx >> 1;
                 if (ix >= Wi) continue;
-                const T *xp = xi + ((long long)iy * Wi + ix) * Cin;
-                const float *wp = w + (long long)co * 16 + ky * 4 + kx;
-                for (int ci = 0; ci < Cin; ++ci) acc += ld(xp + ci) * wp[(long long)ci * Co * 16];
+                acc += y[(((long long)r * Hi + iy) * Wi + ix) * (Co * 16) + co * 16 + ky * 4 + kx];
             }
         }
-        out[((long long)r * Co + co) * OH * OW + oy * OW + ox] = acc;
+        out[i] = acc;
     }
 }
 
@@ -874,9 +978,9 @@ extern "C" int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const 
 
 extern "C" int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
                              mdx_stream_t stream) {
-    MDX_REQUIRE(x && out && k > 0 && s > 0 && p >= 0, "mdx_maxpool2d: bad args");
+    MDX_REQUIRE(x && out && k > 0 && s > 0 && p >= 0 && C % 8 == 0, "mdx_maxpool2d: bad args (C % 8 == 0)");
     const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
-    const long long total = (long long)N * OH * OW * C;
+    const long long total = (long long)N * OH * OW * (C / 8);
     if (dtype == 1)
         hipLaunchKernelGGL(k_maxpool<_Float16>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
                            (const _Float16 *)x, N, H, W, C, k, s, p, OH, OW, (_Float16 *)out);
@@ -892,16 +996,17 @@ extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, f
                              mdx_stream_t stream) {
     MDX_REQUIRE(x && out && gamma && beta && stats && G > 0 && C % G == 0, "mdx_groupnorm: bad args");
     MDX_REQUIRE(!fuse || (up && H % 2 == 0 && W % 2 == 0), "mdx_groupnorm: fuse needs up and even H, W");
+    MDX_REQUIRE(C % 8 == 0 && (C / G) % 8 == 0, "mdx_groupnorm: C and C/G must be multiples of 8");
     hipStream_t s = as_stream(stream);
     const long long total = (long long)N * H * W * C;
     if (dtype == 1) {
         hipLaunchKernelGGL(k_gn_stats<_Float16>, dim3(N * G), dim3(256), 0, s, (const _Float16 *)x, H * W, C, G, eps,
                            stats);
-        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total)), dim3(256), 0, s, (const _Float16 *)x, N, H, W,
+        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const _Float16 *)x, N, H, W,
                            C, G, stats, gamma, beta, (const _Float16 *)up, fuse, (_Float16 *)out);
     } else {
         hipLaunchKernelGGL(k_gn_stats<float>, dim3(N * G), dim3(256), 0, s, (const float *)x, H * W, C, G, eps, stats);
-        hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total)), dim3(256), 0, s, (const float *)x, N, H, W, C, G,
+        hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const float *)x, N, H, W, C, G,
                            stats, gamma, beta, (const float *)up, fuse, (float *)out);
     }
     MDX_CHECK_LAUNCH("mdx_groupnorm");
@@ -962,6 +1067,7 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
                              void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
+    MDX_REQUIRE(C % (dtype == 1 ? 8 : 4) == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
     if (R == 0) return MDX_OK;
     RoiLevels rl{};
     for (int l = 0; l < L; ++l) {
@@ -1000,26 +1106,25 @@ extern "C" int mdx_box_postprocess(const float *pred, int ld_pred, const float *
 }
 
 extern "C" int mdx_paste_masks(const float *logits, const float *boxes, const int *counts, int B, int D, int M,
-                               int img_h, int img_w, float thresh, uint8_t *out, mdx_stream_t stream) {
+                               int img_h, int img_w, int64_t plane_stride, float thresh, uint8_t *out,
+                               mdx_stream_t stream) {
     MDX_REQUIRE(logits && boxes && counts && out && M <= 64, "mdx_paste_masks: bad args");
+    MDX_REQUIRE(plane_stride >= (int64_t)img_h * img_w, "mdx_paste_masks: plane_stride < img_h*img_w");
     dim3 grid((img_h + 7) / 8, B * D);
     hipLaunchKernelGGL(k_paste, grid, dim3(256), 0, as_stream(stream), logits, boxes, counts, D, M, img_h, img_w,
-                       thresh, out);
+                       (long long)plane_stride, thresh, out);
     MDX_CHECK_LAUNCH("mdx_paste_masks");
     return MDX_OK;
 }
 
-extern "C" int mdx_keypoint_deconv(const void *x, int R, int Hi, int Wi, int Cin, const float *w, const float *bias,
-                                   int Co, int dtype, float *out, mdx_stream_t stream) {
-    MDX_REQUIRE(x && w && out, "mdx_keypoint_deconv: null pointer");
+extern "C" int mdx_deconv_col2im(const float *y, const float *bias, int R, int Hi, int Wi, int Co, float *out,
+                                 mdx_stream_t stream) {
+    MDX_REQUIRE(y && out, "mdx_deconv_col2im: null pointer");
     if (R == 0) return MDX_OK;
-    if (dtype == 1)
-        hipLaunchKernelGGL(k_kp_deconv<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), (const _Float16 *)x, w,
-                           bias, Hi, Wi, Cin, Co, out);
-    else
-        hipLaunchKernelGGL(k_kp_deconv<float>, dim3(R), dim3(256), 0, as_stream(stream), (const float *)x, w, bias, Hi,
-                           Wi, Cin, Co, out);
-    MDX_CHECK_LAUNCH("mdx_keypoint_deconv");
+    const long long total = (long long)R * Co * 4 * Hi * Wi;
+    hipLaunchKernelGGL(k_deconv_col2im, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), y, bias, R, Hi, Wi,
+                       Co, out);
+    MDX_CHECK_LAUNCH("mdx_deconv_col2im");
     return MDX_OK;
 }
 

@@ -19,23 +19,34 @@ __global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restri
                                                          const float *__restrict__ scores,
                                                          const int *__restrict__ ndet,
                                                          const float *__restrict__ kpts, int D, int K, long long hw,
-                                                         float thr, int *__restrict__ keep_idx,
+                                                         long long plane, float thr, int *__restrict__ keep_idx,
                                                          int *__restrict__ nkeep, uint8_t *__restrict__ sel_mask,
                                                          double *__restrict__ sel_kpts) {
     __shared__ unsigned long long s_cnt[SEL_MAXD * SEL_MAXD];
     __shared__ int s_sel;
     const int b = blockIdx.x;
     const int n = ndet[b];
-    const uint8_t *mb = masks + (long long)b * D * hw;
+    const uint8_t *mb = masks + (long long)b * D * plane;
     for (int i = threadIdx.x; i < SEL_MAXD * SEL_MAXD; i += 256) s_cnt[i] = 0;
     __syncthreads();
     if (n > 1) {
-        // cnt[i][j] (j >= i): |m_i & m_j| ; cnt[i][i] = area_i (planes need not be aligned)
+        // cnt[i][j] (j >= i): |m_i & m_j| ; cnt[i][i] = area_i.  Mask bytes are
+        // 0/1, so the popcount of the AND of 16-byte words counts pixels.
         unsigned long long loc[SEL_MAXD * (SEL_MAXD + 1) / 2];
         for (int q = 0; q < SEL_MAXD * (SEL_MAXD + 1) / 2; ++q) loc[q] = 0;
-        for (long long p = threadIdx.x; p < hw; p += 256) {
+        const long long nv = (plane % 16 == 0) ? hw / 16 : 0;
+        for (long long v = threadIdx.x; v < nv; v += 256) {
+            uint4 w[SEL_MAXD];
+            for (int i = 0; i < n; ++i) w[i] = reinterpret_cast<const uint4 *>(mb + (long long)i * plane)[v];
+            int q = 0;
+            for (int i = 0; i < n; ++i)
+                for (int j = i; j < n; ++j, ++q)
+                    loc[q] += __popc(w[i].x & w[j].x) + __popc(w[i].y & w[j].y) + __popc(w[i].z & w[j].z) +
+                              __popc(w[i].w & w[j].w);
+        }
+        for (long long p = nv * 16 + threadIdx.x; p < hw; p += 256) {
             unsigned m[SEL_MAXD];
-            for (int i = 0; i < n; ++i) m[i] = mb[(long long)i * hw + p] != 0;
+            for (int i = 0; i < n; ++i) m[i] = mb[(long long)i * plane + p] != 0;
             int q = 0;
             for (int i = 0; i < n; ++i)
                 for (int j = i; j < n; ++j, ++q) loc[q] += m[i] & m[j];
@@ -103,7 +114,7 @@ __global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restri
     __syncthreads();
     const int s = s_sel;
     uint8_t *o = sel_mask + (long long)b * hw;
-    const uint8_t *src = s >= 0 ? mb + (long long)s * hw : nullptr;
+    const uint8_t *src = s >= 0 ? mb + (long long)s * plane : nullptr;
     for (long long p = threadIdx.x; p < hw; p += 256) o[p] = src ? src[p] : (uint8_t)0;
 }
 
@@ -111,16 +122,19 @@ __global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restri
 
 using namespace mdx;
 
-extern "C" int mdx_mask_nms_select(const uint8_t *masks, const float *scores, const int *ndet, const float *kpts,
-                                   int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx, int *nkeep,
-                                   uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream) {
+extern "C" int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, const float *scores,
+                                   const int *ndet, const float *kpts, int B, int D, int K, int h, int w,
+                                   float iou_thresh, int *keep_idx, int *nkeep, uint8_t *sel_mask, double *sel_kpts,
+                                   mdx_stream_t stream) {
     MDX_REQUIRE(masks && scores && ndet && kpts && keep_idx && nkeep && sel_mask && sel_kpts,
                 "mdx_mask_nms_select: null pointer");
     MDX_REQUIRE(D >= 1 && D <= SEL_MAXD, "mdx_mask_nms_select: D must be in [1, %d]", SEL_MAXD);
     const long long hw = (long long)h * w;
+    MDX_REQUIRE(plane_stride >= hw, "mdx_mask_nms_select: plane_stride < h*w");
+    MDX_REQUIRE(plane_stride % 16 != 0 || ((uintptr_t)masks % 16) == 0, "mdx_mask_nms_select: unaligned masks");
     if (B == 0) return MDX_OK;
     hipLaunchKernelGGL(k_mask_nms_select, dim3(B), dim3(256), 0, as_stream(stream), masks, scores, ndet, kpts, D, K, hw,
-                       iou_thresh, keep_idx, nkeep, sel_mask, sel_kpts);
+                       (long long)plane_stride, iou_thresh, keep_idx, nkeep, sel_mask, sel_kpts);
     MDX_CHECK_LAUNCH("mdx_mask_nms_select");
     return MDX_OK;
 }

@@ -155,7 +155,11 @@ class MaskRCNN:
             self.kp_convs = [self._conv(sd[f"roi_heads.keypoint_head.conv_fcn{i + 1}.weight"],
                                         sd[f"roi_heads.keypoint_head.conv_fcn{i + 1}.bias"], 1, 1)
                              for i in range(len(cfg.keypoint_conv_dims))]
-            self.kp_deconv_w = self._dev(sd["roi_heads.keypoint_head.score_lowres.weight"], torch.float32)
+            kw_ = sd["roi_heads.keypoint_head.score_lowres.weight"]  # (Cin, K, 4, 4)
+            cin, kk = kw_.shape[0], kw_.shape[1]
+            # ConvTranspose2d(k4,s2,p1) = GEMM to (K*16) columns + col2im
+            self.kp_deconv = Conv(self._dev(kw_.permute(1, 2, 3, 0).reshape(kk * 16, cin)), None, cin, kk * 16, 1, 1,
+                                  0)
             self.kp_deconv_b = self._dev(sd["roi_heads.keypoint_head.score_lowres.bias"], torch.float32)
         self.pixel_mean = np.ascontiguousarray(np.asarray(sd["pixel_mean"].reshape(-1), np.float32))
         self.pixel_std = np.ascontiguousarray(np.asarray(sd["pixel_std"].reshape(-1), np.float32))
@@ -328,10 +332,12 @@ class MaskRCNN:
                 t, _, _ = self.conv(t, R2, M, M, c, relu=True)
             t, _, _ = self.conv(t, R2, M, M, self.mask_deconv, relu=True, out_mode=1)
             logits, _, _ = self.conv(t, R2, 2 * M, 2 * M, self.mask_pred, relu=False, out_f32=True)
-            masks = torch.empty((B, D, h, w), dtype=torch.uint8, device=self.device)
-            call("mdx_paste_masks", _p(logits), _p(det_boxes), _p(ndet), B, D, 2 * M, h, w,
-                 float(cfg.mask_threshold), _p(masks), _stream())
-            out["masks"] = masks
+            plane = (h * w + 15) // 16 * 16  # 16-B aligned planes for the selection kernel
+            mbuf = torch.empty((B, D, plane), dtype=torch.uint8, device=self.device)
+            call("mdx_paste_masks", _p(logits), _p(det_boxes), _p(ndet), B, D, 2 * M, h, w, plane,
+                 float(cfg.mask_threshold), _p(mbuf), _stream())
+            out["masks"] = torch.as_strided(mbuf, (B, D, h, w), (D * plane, plane, w, 1))
+            out["mask_planes"] = (mbuf, plane)
             if intermediates:
                 inter["mask_logits"] = logits
         if cfg.keypoint_on:
@@ -340,9 +346,9 @@ class MaskRCNN:
             for c in self.kp_convs:
                 t, _, _ = self.conv(t, R2, Pk, Pk, c, relu=True)
             K = cfg.num_keypoints
+            y, _, _ = self.conv(t, R2, Pk, Pk, self.kp_deconv, relu=False, out_f32=True)
             low = torch.empty((R2, K, 2 * Pk, 2 * Pk), dtype=torch.float32, device=self.device)
-            call("mdx_keypoint_deconv", _p(t), R2, Pk, Pk, self.kp_convs[-1].cout, _p(self.kp_deconv_w),
-                 _p(self.kp_deconv_b), K, self.dcode, _p(low), _stream())
+            call("mdx_deconv_col2im", _p(y), _p(self.kp_deconv_b), R2, Pk, Pk, K, _p(low), _stream())
             hm = torch.empty((R2, K, 4 * Pk, 4 * Pk), dtype=torch.float32, device=self.device)
             call("mdx_upsample_bilinear2x", _p(low), R2 * K, 2 * Pk, 2 * Pk, _p(hm), _stream())
             kps = torch.empty((B, D, K, 3), dtype=torch.float32, device=self.device)
@@ -391,5 +397,5 @@ def flops_per_image(cfg: ModelConfig, h: int = 423, w: int = 511, proposals: int
     for dim in cfg.keypoint_conv_dims:
         mac += dets * Pk * Pk * dim * cin * 9
         cin = dim
-    mac += dets * (2 * Pk) ** 2 * cfg.num_keypoints * cin * 4
+    mac += dets * Pk * Pk * cfg.num_keypoints * 16 * cin  # ConvTranspose2d(4, s2) as a GEMM
     return 2.0 * mac

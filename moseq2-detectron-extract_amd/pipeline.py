@@ -58,13 +58,16 @@ def mask_nms_select(out: dict, iou_thresh: float = 0.5):
     keep_idx int32 (B,D))."""
     masks = out["masks"]
     B, D, h, w = masks.shape
+    mbuf, plane = out.get("mask_planes", (None, None))
+    if mbuf is None:
+        mbuf, plane = masks.contiguous(), h * w
     K = out["keypoints"].shape[2]
     dev = masks.device
     keep_idx = torch.empty((B, D), dtype=torch.int32, device=dev)
     nkeep = torch.empty((B,), dtype=torch.int32, device=dev)
     sel = torch.empty((B, h, w), dtype=torch.uint8, device=dev)
     kp = torch.empty((B, K, 3), dtype=torch.float64, device=dev)
-    call("mdx_mask_nms_select", _p(masks), _p(out["scores"]), _p(out["ndet"]), _p(out["keypoints"]), B, D, K, h, w,
+    call("mdx_mask_nms_select", _p(mbuf), int(plane), _p(out["scores"]), _p(out["ndet"]), _p(out["keypoints"]), B, D, K, h, w,
          float(iou_thresh), _p(keep_idx), _p(nkeep), _p(sel), _p(kp), _stream())
     return sel, kp, nkeep, keep_idx
 

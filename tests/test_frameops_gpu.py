@@ -133,3 +133,18 @@ def test_crop_and_rotate(mdx, session, raw):
     np.testing.assert_array_equal(gotm, wantm)
     one = proc.crop_and_rotate_frame(prepped[7], centers[7], angles[7])
     np.testing.assert_array_equal(one, want[7])
+
+
+@pytest.mark.parametrize("p,seed", [(0.03, 1), (0.2, 2)])
+def test_inpaint_dense_holes(mdx, p, seed):
+    """Dense invalid pixels make large hole clusters (one lane marches a big
+    cluster); results must equal the serial oracle bit for bit."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    rng = np.random.default_rng(seed)
+    f = rng.integers(0, 100, size=(2, 90, 120), dtype=np.uint8)
+    m = (rng.random(f.shape) < p).astype(np.uint8)
+    m[1, 30:60, 40:90] = 1  # a big blob
+    got = proc.fill_invalid_pixels(f.copy(), m)
+    want = O.inpaint_ns(f, m)
+    np.testing.assert_array_equal(got, want)

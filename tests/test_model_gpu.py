@@ -256,7 +256,7 @@ def test_paste_and_keypoint_tail(mdx):
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     out = torch.empty(B, D, h, w, dtype=torch.uint8, device="cuda")
     ld, bd, cd = logits.contiguous().cuda(), boxes.contiguous().cuda(), counts.cuda()
-    call("mdx_paste_masks", P(ld), P(bd), P(cd), B, D, M, h, w, 0.5, P(out), None)
+    call("mdx_paste_masks", P(ld), P(bd), P(cd), B, D, M, h, w, h * w, 0.5, P(out), None)
     want = R.paste_masks(logits.sigmoid(), boxes, h, w, 0.5)
     got = out.cpu().view(B * D, h, w).bool()
     valid = [0, 1, 2, 3, 4, 5]
@@ -269,8 +269,11 @@ def test_paste_and_keypoint_tail(mdx):
     wt = torch.randn(Cin, K, 4, 4, generator=g) * 0.05
     bb = torch.randn(K, generator=g) * 0.1
     low = torch.empty(B * D, K, 14, 14, device="cuda")
-    xd, wd, bdd = x.cuda(), wt.cuda(), bb.cuda()
-    call("mdx_keypoint_deconv", P(xd), B * D, 7, 7, Cin, P(wd), P(bdd), K, 0, P(low), None)
+    xd, bdd = x.cuda(), bb.cuda()
+    wg = wt.permute(1, 2, 3, 0).reshape(K * 16, Cin).contiguous().cuda()
+    y = torch.empty(B * D, 7, 7, K * 16, device="cuda")
+    call("mdx_conv2d", P(xd), B * D, 7, 7, Cin, P(wg), None, K * 16, 1, 1, 1, 0, None, 0, 0, 0, 0, P(y), None)
+    call("mdx_deconv_col2im", P(y), P(bdd), B * D, 7, 7, K, P(low), None)
     wl = F.conv_transpose2d(x.permute(0, 3, 1, 2), wt, bb, stride=2, padding=1)
     torch.testing.assert_close(low.cpu(), wl, rtol=1e-4, atol=1e-4)
     hm = torch.empty(B * D, K, 28, 28, device="cuda")
