@@ -57,12 +57,43 @@ struct ConvArgs {
 template <typename TO>
 __device__ __forceinline__ void store_out(TO *p, float v) { *p = (TO)v; }
 
-template <typename T, typename TO>
+template <typename TO>
+__device__ __forceinline__ void load8(const TO *p, float *v) {
+    if constexpr (sizeof(TO) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+        const TO *e = reinterpret_cast<const TO *>(&u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (float)e[i];
+    } else {
+        const float4 x = *reinterpret_cast<const float4 *>(p), y = *reinterpret_cast<const float4 *>(p + 4);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    }
+}
+template <typename TO>
+__device__ __forceinline__ void store8(TO *p, const float *v) {
+    if constexpr (sizeof(TO) == 2) {
+        uint4 u;
+        TO *e = reinterpret_cast<TO *>(&u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = (TO)v[i];
+        *reinterpret_cast<uint4 *>(p) = u;
+    } else {
+        *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4 *>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
+// BN_: N tile (128 or 64).  4 waves as 2x2; wave tile (BM/2) x (BN_/2) =
+// TI x TJ MFMA tiles of 16x16.
+template <typename T, typename TO, int BN_>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
+    constexpr int TI = BM / 32, TJ = BN_ / 32;
+    constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
+    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;  // 16-B chunks of B per thread
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *As = smem;                       // [2][BM][PITCH]
-    char *Bs = smem + 2 * TILE_BYTES;      // [2][BN][PITCH]
+    char *As = smem;                   // [2][BM][PITCH]
+    char *Bs = smem + 2 * A_TILE;      // [2][BN_][PITCH]
 
     // XCD-contiguous remap of the linear block id (bijective)
     int tile;
@@ -72,7 +103,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
     }
     const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = tm * BM, n0 = tn * BN_;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
 
@@ -94,7 +125,6 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         a_ix0[i] = ox * a.stride - a.pad;
         a_base[i] = (long long)b * a.H * a.W * a.Cin;
     }
-    // k decomposition of this thread's chunk, advanced by BK per K-step
     int kci = (kc * VEC) % a.Cin;
     int kr = (kc * VEC) / a.Cin;
     int kkx = kr % a.KW, kky = kr / a.KW;
@@ -102,7 +132,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
 
     const T *X = reinterpret_cast<const T *>(a.x);
     const T *Wt = reinterpret_cast<const T *>(a.w);
-    uint4 ra[4], rb[4];
+    uint4 ra[4], rb[BLOADS];
 
     auto load_global = [&]() {
         const bool kok = kglob < a.K;
@@ -113,6 +143,9 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             if (kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
                 v = *reinterpret_cast<const uint4 *>(X + a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci);
             ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i) {
             const int gn = n0 + lrow + 32 * i;
             uint4 u = make_uint4(0, 0, 0, 0);
             if (kok && gn < a.Cout) u = *reinterpret_cast<const uint4 *>(Wt + (long long)gn * a.K + kglob);
@@ -132,18 +165,18 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     };
     auto store_lds = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int off = buf * TILE_BYTES + (lrow + 32 * i) * PITCH + kc * 16;
-            *reinterpret_cast<uint4 *>(As + off) = ra[i];
-            *reinterpret_cast<uint4 *>(Bs + off) = rb[i];
-        }
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4 *>(As + buf * A_TILE + (lrow + 32 * i) * PITCH + kc * 16) = ra[i];
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i)
+            *reinterpret_cast<uint4 *>(Bs + buf * B_TILE + (lrow + 32 * i) * PITCH + kc * 16) = rb[i];
     };
 
-    float4v acc[4][4];
+    float4v acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
     const int nk = (a.K + BK - 1) / BK;
     load_global();
@@ -157,34 +190,34 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             load_global();
             advance_k();
         }
-        const char *Ab = As + cur * TILE_BYTES + (wm * 64 + (lane & 15)) * PITCH;
-        const char *Bb = Bs + cur * TILE_BYTES + (wn * 64 + (lane & 15)) * PITCH;
+        const char *Ab = As + cur * A_TILE + (wm * (BM / 2) + (lane & 15)) * PITCH;
+        const char *Bb = Bs + cur * B_TILE + (wn * (BN_ / 2) + (lane & 15)) * PITCH;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int koff = s * 64 + (lane >> 4) * 16;
             if constexpr (sizeof(T) == 2) {
-                half8 af[4], bf[4];
+                half8 af[TI], bf[TJ];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * PITCH + koff);
+                for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * PITCH + koff);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * PITCH + koff);
+                for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * PITCH + koff);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < TI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
             } else {
-                float4v af[4], bf[4];
+                float4v af[TI], bf[TJ];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
+                for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
+                for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
+                    for (int i = 0; i < TI; ++i)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
+                        for (int j = 0; j < TJ; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
             }
         }
@@ -192,35 +225,77 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         __syncthreads();
     }
 
-    // ---- epilogue: bias, residual, ReLU, store (C/D: col = lane&15, row = 4*(lane>>4)+r)
+    // ---- epilogue: accumulators -> LDS (fp32, row-major) -> bias / residual /
+    // ReLU -> 16-byte stores of 8 consecutive output channels
+    constexpr int CP = BN_ + 4;  // fp32 pitch (16-B aligned rows, bank spread)
+    float *Cs = reinterpret_cast<float *>(smem);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+                const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
+                Cs[row * CP + col] = acc[i][j][r];
+            }
+    __syncthreads();
     TO *O = reinterpret_cast<TO *>(a.out);
     const TO *RS = reinterpret_cast<const TO *>(a.res);
     const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int gn = n0 + wn * 64 + j * 16 + (lane & 15);
-        if (gn >= a.Cout) continue;
-        const float bv = a.bias ? a.bias[gn] : 0.f;
-        int q = 0, co = gn;
-        if (a.out_mode == 1) {
-            q = gn / Co;
-            co = gn - q * Co;
+    const bool vec_ok = (a.Cout % 8) == 0 && (Co % 8) == 0;
+    constexpr int CPR = BN_ / 8;  // 8-wide chunks per row
+    for (int c = tid; c < BM * CPR; c += CONV_THREADS) {
+        const int row = c / CPR, ch = c - row * CPR;
+        const int gm = m0 + row;
+        if (gm >= a.M) continue;
+        const int gn0 = n0 + ch * 8;
+        if (gn0 >= a.Cout) continue;
+        long long obase;  // output offset of channel gn0
+        int q = 0, co0 = gn0;
+        if (a.out_mode == 0) {
+            obase = (long long)gm * a.Cout + gn0;
+        } else {
+            q = gn0 / Co;
+            co0 = gn0 - q * Co;
+            const int b = gm / ohw, rem = gm - b * ohw;
+            const int y = rem / a.OW, xx = rem - y * a.OW;
+            obase = (((long long)b * (2 * a.OH) + 2 * y + (q >> 1)) * (2 * a.OW) + 2 * xx + (q & 1)) * Co + co0;
         }
+        const float *src = Cs + row * CP + ch * 8;
+        if (vec_ok) {
+            float v[8];
+            const float4 x0 = *reinterpret_cast<const float4 *>(src), x1 = *reinterpret_cast<const float4 *>(src + 4);
+            v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+            if (a.bias) {
+                const float4 b0 = *reinterpret_cast<const float4 *>(a.bias + gn0);
+                const float4 b1 = *reinterpret_cast<const float4 *>(a.bias + gn0 + 4);
+                v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+                v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+            }
+            if (RS) {
+                float rv[8];
+                load8<TO>(RS + obase, rv);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+                for (int k = 0; k < 8; ++k) v[k] += rv[k];
+            }
+            if (a.relu) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gm = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-                if (gm >= a.M) continue;
-                float v = acc[i][j][r] + bv;
-                long long oi;
-                if (a.out_mode == 0) {
-                    oi = (long long)gm * a.Cout + gn;
-                } else {
+                for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+            }
+            store8<TO>(O + obase, v);
+        } else {
+            for (int k = 0; k < 8; ++k) {
+                const int gn = gn0 + k;
+                if (gn >= a.Cout) break;
+                long long oi = obase + k;
+                if (a.out_mode == 1) {
+                    const int qq = gn / Co, co = gn - qq * Co;
                     const int b = gm / ohw, rem = gm - b * ohw;
                     const int y = rem / a.OW, xx = rem - y * a.OW;
-                    oi = (((long long)b * (2 * a.OH) + 2 * y + (q >> 1)) * (2 * a.OW) + 2 * xx + (q & 1)) * Co + co;
+                    oi = (((long long)b * (2 * a.OH) + 2 * y + (qq >> 1)) * (2 * a.OW) + 2 * xx + (qq & 1)) * Co + co;
                 }
+                float v = src[k] + (a.bias ? a.bias[gn] : 0.f);
                 if (RS) v += (float)RS[oi];
                 if (a.relu) v = v > 0.f ? v : 0.f;
                 store_out<TO>(O + oi, v);
@@ -258,19 +333,31 @@ extern "C" int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const voi
     a.K = KH * KW * Cin;
     a.relu = relu;
     a.out_mode = out_mode;
-    const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, BN);
+    const bool narrow = Cout <= 64;  // 64-wide N tile: no wasted MFMA columns for 64-channel layers
+    const int bn = narrow ? 64 : BN;
+    const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_n = tiles_n;
     a.tiles_total = tiles_m * tiles_n;
-    const size_t lds = 4 * (size_t)TILE_BYTES;
+    const size_t lds_main = 2 * (size_t)BM * PITCH + 2 * (size_t)bn * PITCH;
+    const size_t lds_epi = (size_t)BM * (bn + 4) * 4;
+    const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     hipStream_t s = as_stream(stream);
+#define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
+    do {                                                                                                    \
+        if (narrow)                                                                                         \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 64>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);  \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 128>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a); \
+    } while (0)
     if (in_dtype == 1 && out_dtype == 1)
-        hipLaunchKernelGGL((k_conv<_Float16, _Float16>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+        MDX_LAUNCH_CONV(_Float16, _Float16);
     else if (in_dtype == 1 && out_dtype == 0)
-        hipLaunchKernelGGL((k_conv<_Float16, float>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+        MDX_LAUNCH_CONV(_Float16, float);
     else if (in_dtype == 0 && out_dtype == 0)
-        hipLaunchKernelGGL((k_conv<float, float>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+        MDX_LAUNCH_CONV(float, float);
     else
-        hipLaunchKernelGGL((k_conv<float, _Float16>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);
+        MDX_LAUNCH_CONV(float, _Float16);
+#undef MDX_LAUNCH_CONV
     MDX_CHECK_LAUNCH("mdx_conv2d");
     return MDX_OK;
 }

@@ -163,24 +163,54 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
         t[i] = 1.0e6f;
     }
     __syncthreads();
-    // unknown pixels in raster order (interior of the padded frame)
-    int nin = 0;
-    for (long long i0 = 0; i0 < L.np; i0 += INP_SETUP_THREADS) {
-        const long long i = i0 + tid;
-        int in = 0;
-        if (i < L.np) {
-            const int y = (int)(i / PW), x = (int)(i - (long long)y * PW);
-            in = (y >= 1 && y <= H && x >= 1 && x <= W && msk[(long long)(y - 1) * W + x - 1] != 0) ? 1 : 0;
+    // unknown pixels in raster order: each thread owns a contiguous segment of
+    // the padded frame (count, block scan, ordered write)
+    const long long seg = (L.np + INP_SETUP_THREADS - 1) / INP_SETUP_THREADS;
+    const long long s0 = tid * seg, s1 = s0 + seg < L.np ? s0 + seg : L.np;
+    auto is_in = [&](long long i) -> bool {
+        const int y = (int)(i / PW), x = (int)(i - (long long)y * PW);
+        return y >= 1 && y <= H && x >= 1 && x <= W && msk[(long long)(y - 1) * W + x - 1] != 0;
+    };
+    int mine = 0;
+    {
+        // walk rows of the segment without per-pixel division
+        long long i = s0;
+        while (i < s1) {
+            const int y = (int)(i / PW);
+            const long long rowend = ((long long)y + 1) * PW < s1 ? ((long long)y + 1) * PW : s1;
+            if (y >= 1 && y <= H) {
+                const uint8_t *mr = msk + (long long)(y - 1) * W - 1 - (long long)y * PW;
+                for (long long j = i; j < rowend; ++j) {
+                    const int x = (int)(j - (long long)y * PW);
+                    if (x >= 1 && x <= W && mr[j]) ++mine;
+                }
+            }
+            i = rowend;
         }
-        int tot;
-        const int pos = nin + block_scan_excl(in, sh, tot);
-        if (in) {
-            ins[pos] = (int)i;
-            code[i] = pos;
-            lab[pos] = pos;
-        }
-        nin += tot;
     }
+    int nin;
+    int pos = block_scan_excl(mine, sh, nin);
+    {
+        long long i = s0;
+        while (i < s1) {
+            const int y = (int)(i / PW);
+            const long long rowend = ((long long)y + 1) * PW < s1 ? ((long long)y + 1) * PW : s1;
+            if (y >= 1 && y <= H) {
+                const uint8_t *mr = msk + (long long)(y - 1) * W - 1 - (long long)y * PW;
+                for (long long j = i; j < rowend; ++j) {
+                    const int x = (int)(j - (long long)y * PW);
+                    if (x >= 1 && x <= W && mr[j]) {
+                        ins[pos] = (int)j;
+                        code[j] = pos;
+                        lab[pos] = pos;
+                        ++pos;
+                    }
+                }
+            }
+            i = rowend;
+        }
+    }
+    (void)is_in;
     __syncthreads();
     // narrow band: interior 4-neighbours of unknown pixels that are not unknown
     for (int k = tid; k < nin; k += INP_SETUP_THREADS) {

@@ -78,12 +78,12 @@ struct PrepArgs {
 template <typename T>
 __global__ __launch_bounds__(256) void k_preprocess(const uint8_t *__restrict__ fr, int B, int h, int w, int C, int Cp,
                                                     int Hp, int Wp, PrepArgs pa, T *__restrict__ out) {
-    const long long total = (long long)B * Hp * Wp;
-    for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
-        const int b = (int)(p / ((long long)Hp * Wp));
-        const int rem = (int)(p - (long long)b * Hp * Wp);
+    const int total = B * Hp * Wp;  // < 2^31 (checked on the host)
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < total; p += gridDim.x * 256) {
+        const int b = p / (Hp * Wp);
+        const int rem = p - b * Hp * Wp;
         const int y = rem / Wp, x = rem - y * Wp;
-        T *o = out + p * Cp;
+        T *o = out + (long long)p * Cp;
         if (y < h && x < w) {
             const float v = (float)pa.lut[fr[((long long)b * h + y) * w + x]];
             for (int c = 0; c < Cp; ++c) o[c] = c < C ? (T)((v - pa.mean[c]) / pa.stdv[c]) : (T)0.f;
@@ -100,14 +100,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_maxpool(const T *__restrict__ x, int N, int H, int W, int C, int k, int s,
                                                  int p, int OH, int OW, T *__restrict__ out) {
     const int CV = C / 8;
-    const long long total = (long long)N * OH * OW * CV;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-        const int c0 = (int)(i % CV) * 8;
-        long long r = i / CV;
-        const int ox = (int)(r % OW);
+    const int total = N * OH * OW * CV;  // < 2^31 (checked on the host)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        int r = i / CV;
+        const int c0 = (i - r * CV) * 8;
+        const int ox = r % OW;
         r /= OW;
-        const int oy = (int)(r % OH);
-        const int n = (int)(r / OH);
+        const int oy = r % OH;
+        const int n = r / OH;
         float m[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
@@ -157,38 +157,40 @@ __global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int H
     const int nv = cpg / 8;
     float s = 0.f;
     if (vec) {
-        for (long long i = threadIdx.x; i < (long long)HW * nv; i += 256) {
-            const long long px = i / nv, cv = i - px * nv;
-            float v[8];
-            ld8(x + base + px * C + cv * 8, v);
+        for (int px = threadIdx.x; px < HW; px += 256) {
+            const T *xp = x + base + (long long)px * C;
+            for (int cv = 0; cv < nv; ++cv) {
+                float v[8];
+                ld8(xp + cv * 8, v);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) s += v[k];
+                for (int k = 0; k < 8; ++k) s += v[k];
+            }
         }
     } else {
-        for (long long i = threadIdx.x; i < cnt; i += 256) {
-            const long long px = i / cpg, c = i - px * cpg;
-            s += ld(x + base + px * C + c);
-        }
+        for (int px = threadIdx.x; px < HW; px += 256)
+            for (int c = 0; c < cpg; ++c) s += ld(x + base + (long long)px * C + c);
     }
     const float mean = block_sum(s, red) / (float)cnt;
     float s2 = 0.f;
     if (vec) {
-        for (long long i = threadIdx.x; i < (long long)HW * nv; i += 256) {
-            const long long px = i / nv, cv = i - px * nv;
-            float v[8];
-            ld8(x + base + px * C + cv * 8, v);
+        for (int px = threadIdx.x; px < HW; px += 256) {
+            const T *xp = x + base + (long long)px * C;
+            for (int cv = 0; cv < nv; ++cv) {
+                float v[8];
+                ld8(xp + cv * 8, v);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float d = v[k] - mean;
-                s2 += d * d;
+                for (int k = 0; k < 8; ++k) {
+                    const float d = v[k] - mean;
+                    s2 += d * d;
+                }
             }
         }
     } else {
-        for (long long i = threadIdx.x; i < cnt; i += 256) {
-            const long long px = i / cpg, c = i - px * cpg;
-            const float d = ld(x + base + px * C + c) - mean;
-            s2 += d * d;
-        }
+        for (int px = threadIdx.x; px < HW; px += 256)
+            for (int c = 0; c < cpg; ++c) {
+                const float d = ld(x + base + (long long)px * C + c) - mean;
+                s2 += d * d;
+            }
     }
     const float var = block_sum(s2, red) / (float)cnt;
     if (threadIdx.x == 0) {
@@ -204,19 +206,22 @@ __global__ __launch_bounds__(256) void k_gn_apply(const T *__restrict__ x, int N
                                                   const float *__restrict__ stats, const float *__restrict__ gamma,
                                                   const float *__restrict__ beta, const T *__restrict__ up, int fuse,
                                                   T *__restrict__ out) {
-    const long long total = (long long)N * H * W * (C / 8);
+    const int CV = C / 8;
+    const int total = N * H * W * CV;  // < 2^31 (checked on the host)
     const int cpg = C / G;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-        const int c0 = (int)(i % (C / 8)) * 8;
-        const long long pix = i / (C / 8);
-        const int n = (int)(pix / ((long long)H * W));
+    const int HW = H * W;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const int pixi = i / CV;
+        const int c0 = (i - pixi * CV) * 8;
+        const long long pix = pixi;
+        const int n = pixi / HW;
         const int g = c0 / cpg;
         const float mean = stats[2 * (n * G + g)], rstd = stats[2 * (n * G + g) + 1];
         float v[8];
         ld8(x + pix * C + c0, v);
         float u[8];
         if (fuse) {
-            const int rem = (int)(pix - (long long)n * H * W);
+            const int rem = pixi - n * HW;
             const int yy = rem / W, xx = rem - yy * W;
             const int UH = H / 2, UW = W / 2;
             ld8(up + (((long long)n * UH + (yy >> 1)) * UW + (xx >> 1)) * C + c0, u);
@@ -462,22 +467,38 @@ __global__ __launch_bounds__(256) void k_nms_mask(const float *__restrict__ boxe
 }
 
 // one wave per segment: greedy sweep in score order; invalid boxes never keep
-// nor suppress (Detectron2 removes them before NMS)
+// nor suppress (Detectron2 removes them before NMS).  Mask rows are staged
+// 64 at a time into LDS so the serial sweep only touches LDS and registers.
+constexpr int NMS_MAXW = 16;  // pre_topk <= 1024
 __global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, const int *__restrict__ kseg, int cap,
                                                  int words, const unsigned long long *__restrict__ mask,
                                                  int *__restrict__ keep) {
+    __shared__ unsigned long long rows[64][NMS_MAXW + 1];
+    __shared__ int vflag[64];
     const int seg = blockIdx.x, lane = threadIdx.x;
     const int k = kseg[seg];
     const int *vl = valid + (long long)seg * cap;
     const unsigned long long *mk = mask + (long long)seg * cap * words;
     int *kp = keep + (long long)seg * cap;
     unsigned long long removed = 0ull;  // lane w < words holds word w
-    for (int i = 0; i < k; ++i) {
-        const unsigned long long rw = __shfl(removed, i >> 6);
-        const bool sup = (rw >> (i & 63)) & 1ull;
-        const bool ok = !sup && vl[i];
-        if (lane == 0) kp[i] = ok ? 1 : 0;
-        if (ok && lane < words) removed |= mk[(long long)i * words + lane];
+    for (int i0 = 0; i0 < k; i0 += 64) {
+        for (int t = lane; t < 64 * words; t += 64) {
+            const int r = t / words, w = t - r * words;
+            rows[r][w] = (i0 + r < k) ? mk[(long long)(i0 + r) * words + w] : 0ull;
+        }
+        vflag[lane] = (i0 + lane < k) ? vl[i0 + lane] : 0;
+        __syncthreads();
+        const int nr = k - i0 < 64 ? k - i0 : 64;
+        int okbits_lo = 0;
+        for (int r = 0; r < nr; ++r) {
+            const int i = i0 + r;
+            const unsigned long long rw = __shfl(removed, i >> 6);
+            const bool ok = !((rw >> (i & 63)) & 1ull) && vflag[r];
+            if (lane == r) okbits_lo = ok ? 1 : 0;
+            if (ok && lane < words) removed |= rows[r][lane];
+        }
+        if (lane < nr) kp[i0 + lane] = okbits_lo;
+        __syncthreads();
     }
     for (int i = k + lane; i < cap; i += 64) kp[i] = 0;
 }
@@ -959,6 +980,7 @@ extern "C" int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const 
                               mdx_stream_t stream) {
     MDX_REQUIRE(frames && lut && mean && stdv && out, "mdx_preprocess: null pointer");
     MDX_REQUIRE(C >= 1 && C <= 4 && Cp >= C && Cp <= 8 && Hp >= h && Wp >= w, "mdx_preprocess: bad shape");
+    MDX_REQUIRE((long long)B * Hp * Wp < (1ll << 31), "mdx_preprocess: too many pixels");
     PrepArgs pa;
     for (int i = 0; i < 256; ++i) pa.lut[i] = lut[i];
     for (int c = 0; c < 4; ++c) {
@@ -979,6 +1001,7 @@ extern "C" int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const 
 extern "C" int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
                              mdx_stream_t stream) {
     MDX_REQUIRE(x && out && k > 0 && s > 0 && p >= 0 && C % 8 == 0, "mdx_maxpool2d: bad args (C % 8 == 0)");
+    MDX_REQUIRE((long long)N * H * W * C < (1ll << 31), "mdx_maxpool2d: tensor too large");
     const int OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
     const long long total = (long long)N * OH * OW * (C / 8);
     if (dtype == 1)
@@ -997,6 +1020,7 @@ extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, f
     MDX_REQUIRE(x && out && gamma && beta && stats && G > 0 && C % G == 0, "mdx_groupnorm: bad args");
     MDX_REQUIRE(!fuse || (up && H % 2 == 0 && W % 2 == 0), "mdx_groupnorm: fuse needs up and even H, W");
     MDX_REQUIRE(C % 8 == 0 && (C / G) % 8 == 0, "mdx_groupnorm: C and C/G must be multiples of 8");
+    MDX_REQUIRE((long long)N * H * W * C < (1ll << 31), "mdx_groupnorm: tensor too large");
     hipStream_t s = as_stream(stream);
     const long long total = (long long)N * H * W * C;
     if (dtype == 1) {
@@ -1027,7 +1051,8 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     MDX_REQUIRE(head && lvl_h && lvl_w && strides && cell_anchors && out_boxes && out_scores && out_count && workspace,
                 "mdx_rpn_proposals: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && A >= 1 && A <= 4, "mdx_rpn_proposals: L or A out of range");
-    MDX_REQUIRE(pre_topk >= 1 && pre_topk <= TOPK_MAX, "mdx_rpn_proposals: pre_topk must be in [1, %d]", TOPK_MAX);
+    MDX_REQUIRE(pre_topk >= 1 && pre_topk <= TOPK_MAX && (pre_topk + 63) / 64 <= NMS_MAXW,
+                "mdx_rpn_proposals: pre_topk must be in [1, %d]", TOPK_MAX);
     MDX_REQUIRE(post_topk >= 1 && L * pre_topk <= MERGE_MAX, "mdx_rpn_proposals: too many candidates to merge");
     RpnLevels rl{};
     for (int l = 0; l < L; ++l) {
