@@ -126,9 +126,11 @@ int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p
                   mdx_stream_t stream);
 
 /* GroupNorm(G, C, eps) with affine; fuse 1: out = gn + up2(up), 2: (gn + up2(up)) / 2
- * (FPN top-down, nearest x2).  stats: float workspace [N*G*2]. */
+ * (FPN top-down, nearest x2).  workspace: >= mdx_groupnorm_workspace_bytes(N, H, W, G)
+ * bytes (Welford partials + per-group mean/rstd).  C/G must be a multiple of 8. */
+int64_t mdx_groupnorm_workspace_bytes(int N, int H, int W, int G);
 int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, const float *gamma,
-                  const float *beta, const void *up, int fuse, int dtype, void *out, float *stats,
+                  const float *beta, const void *up, int fuse, int dtype, void *out, float *workspace,
                   mdx_stream_t stream);
 
 /* RPN find_top_rpn_proposals: per level head tensor float32 (B,H_l,W_l,A*5)

@@ -142,61 +142,82 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     return s;
 }
 
-// stats of one (image, group); the group's channels are read 8 at a time
-// when C/G is a multiple of 8 (the FPN's 256/32)
+// GroupNorm statistics in two kernels: (1) every block streams a contiguous
+// chunk of pixels (full channel rows, coalesced) and writes a Welford partial
+// (count, mean, M2) per group; (2) one lane per (image, group) merges the
+// partials with Chan's formula.  Lane -> 8-channel octet mapping needs C/G % 8
+// == 0 (the FPN's 256/32).
+constexpr int GN_CHUNK_PIX = 64;
+
 template <typename T>
-__global__ __launch_bounds__(256) void k_gn_stats(const T *__restrict__ x, int HW, int C, int G, float eps,
+__global__ __launch_bounds__(256) void k_gn_partial(const T *__restrict__ x, int HW, int C, int G,
+                                                    float *__restrict__ part) {
+    __shared__ float s_n[256], s_m[256], s_q[256];
+    const int n = blockIdx.y, chunk = blockIdx.x;
+    const int nchunks = gridDim.x;
+    const int CV = C / 8;               // octets per pixel (<= 256)
+    const int rows = 256 / CV;          // pixels processed in parallel
+    const int cv = threadIdx.x % CV, pr = threadIdx.x / CV;
+    const int p0 = chunk * GN_CHUNK_PIX;
+    float cnt = 0.f, mean = 0.f, m2 = 0.f;
+    if (pr < rows) {
+        for (int p = p0 + pr; p < p0 + GN_CHUNK_PIX && p < HW; p += rows) {
+            float v[8];
+            ld8(x + ((long long)n * HW + p) * C + cv * 8, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                cnt += 1.f;
+                const float d = v[k] - mean;
+                mean += d / cnt;
+                m2 += d * (v[k] - mean);
+            }
+        }
+    }
+    s_n[threadIdx.x] = cnt;
+    s_m[threadIdx.x] = mean;
+    s_q[threadIdx.x] = m2;
+    __syncthreads();
+    // merge the lanes of one group: octets g*cpg/8 .. over all pixel rows
+    const int opg = (C / G) / 8;  // octets per group
+    if (threadIdx.x < G) {
+        const int g = threadIdx.x;
+        float N = 0.f, M = 0.f, Q = 0.f;
+        for (int r = 0; r < rows; ++r)
+            for (int o = 0; o < opg; ++o) {
+                const int t = r * CV + g * opg + o;
+                const float nb = s_n[t];
+                if (nb == 0.f) continue;
+                const float tot = N + nb;
+                const float d = s_m[t] - M;
+                M += d * (nb / tot);
+                Q += s_q[t] + d * d * (N * nb / tot);
+                N = tot;
+            }
+        float *pp = part + (((long long)n * G + g) * nchunks + chunk) * 3;
+        pp[0] = N;
+        pp[1] = M;
+        pp[2] = Q;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gn_final(const float *__restrict__ part, int NG, int nchunks, float eps,
                                                   float *__restrict__ stats) {
-    __shared__ float red[8];
-    const int bg = blockIdx.x;
-    const int b = bg / G, g = bg - b * G;
-    const int cpg = C / G;
-    const long long base = (long long)b * HW * C + (long long)g * cpg;
-    const long long cnt = (long long)HW * cpg;
-    const bool vec = (cpg % 8) == 0;
-    const int nv = cpg / 8;
-    float s = 0.f;
-    if (vec) {
-        for (int px = threadIdx.x; px < HW; px += 256) {
-            const T *xp = x + base + (long long)px * C;
-            for (int cv = 0; cv < nv; ++cv) {
-                float v[8];
-                ld8(xp + cv * 8, v);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s += v[k];
-            }
-        }
-    } else {
-        for (int px = threadIdx.x; px < HW; px += 256)
-            for (int c = 0; c < cpg; ++c) s += ld(x + base + (long long)px * C + c);
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= NG) return;
+    const float *pp = part + (long long)i * nchunks * 3;
+    double N = 0.0, M = 0.0, Q = 0.0;
+    for (int c = 0; c < nchunks; ++c) {
+        const double nb = pp[3 * c];
+        if (nb == 0.0) continue;
+        const double tot = N + nb;
+        const double d = (double)pp[3 * c + 1] - M;
+        M += d * (nb / tot);
+        Q += (double)pp[3 * c + 2] + d * d * (N * nb / tot);
+        N = tot;
     }
-    const float mean = block_sum(s, red) / (float)cnt;
-    float s2 = 0.f;
-    if (vec) {
-        for (int px = threadIdx.x; px < HW; px += 256) {
-            const T *xp = x + base + (long long)px * C;
-            for (int cv = 0; cv < nv; ++cv) {
-                float v[8];
-                ld8(xp + cv * 8, v);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float d = v[k] - mean;
-                    s2 += d * d;
-                }
-            }
-        }
-    } else {
-        for (int px = threadIdx.x; px < HW; px += 256)
-            for (int c = 0; c < cpg; ++c) {
-                const float d = ld(x + base + (long long)px * C + c) - mean;
-                s2 += d * d;
-            }
-    }
-    const float var = block_sum(s2, red) / (float)cnt;
-    if (threadIdx.x == 0) {
-        stats[2 * bg] = mean;
-        stats[2 * bg + 1] = 1.0f / sqrtf(var + eps);
-    }
+    const float var = (float)(Q / N);
+    stats[2 * i] = (float)M;
+    stats[2 * i + 1] = 1.0f / sqrtf(var + eps);
 }
 
 // y = (x - mean) * rstd * gamma + beta; optionally fused: y = (y + up(prev)) [/ 2]
@@ -1014,24 +1035,35 @@ extern "C" int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, i
     return MDX_OK;
 }
 
+extern "C" int64_t mdx_groupnorm_workspace_bytes(int N, int H, int W, int G) {
+    const long long nch = ((long long)H * W + GN_CHUNK_PIX - 1) / GN_CHUNK_PIX;
+    return (long long)N * G * 2 * 4 + (long long)N * G * nch * 3 * 4 + 64;
+}
+
 extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, const float *gamma,
-                             const float *beta, const void *up, int fuse, int dtype, void *out, float *stats,
+                             const float *beta, const void *up, int fuse, int dtype, void *out, float *workspace,
                              mdx_stream_t stream) {
-    MDX_REQUIRE(x && out && gamma && beta && stats && G > 0 && C % G == 0, "mdx_groupnorm: bad args");
+    MDX_REQUIRE(x && out && gamma && beta && workspace && G > 0 && C % G == 0, "mdx_groupnorm: bad args");
     MDX_REQUIRE(!fuse || (up && H % 2 == 0 && W % 2 == 0), "mdx_groupnorm: fuse needs up and even H, W");
-    MDX_REQUIRE(C % 8 == 0 && (C / G) % 8 == 0, "mdx_groupnorm: C and C/G must be multiples of 8");
+    MDX_REQUIRE(C % 8 == 0 && (C / G) % 8 == 0 && C / 8 <= 256 && G <= 256,
+                "mdx_groupnorm: C and C/G must be multiples of 8, C <= 2048");
     MDX_REQUIRE((long long)N * H * W * C < (1ll << 31), "mdx_groupnorm: tensor too large");
     hipStream_t s = as_stream(stream);
+    const int HW = H * W;
+    const int nch = (HW + GN_CHUNK_PIX - 1) / GN_CHUNK_PIX;
+    float *stats = workspace;
+    float *part = workspace + 2 * N * G;
     const long long total = (long long)N * H * W * C;
     if (dtype == 1) {
-        hipLaunchKernelGGL(k_gn_stats<_Float16>, dim3(N * G), dim3(256), 0, s, (const _Float16 *)x, H * W, C, G, eps,
-                           stats);
-        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const _Float16 *)x, N, H, W,
-                           C, G, stats, gamma, beta, (const _Float16 *)up, fuse, (_Float16 *)out);
+        hipLaunchKernelGGL(k_gn_partial<_Float16>, dim3(nch, N), dim3(256), 0, s, (const _Float16 *)x, HW, C, G, part);
+        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 255) / 256), dim3(256), 0, s, part, N * G, nch, eps, stats);
+        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const _Float16 *)x, N, H,
+                           W, C, G, stats, gamma, beta, (const _Float16 *)up, fuse, (_Float16 *)out);
     } else {
-        hipLaunchKernelGGL(k_gn_stats<float>, dim3(N * G), dim3(256), 0, s, (const float *)x, H * W, C, G, eps, stats);
-        hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const float *)x, N, H, W, C, G,
-                           stats, gamma, beta, (const float *)up, fuse, (float *)out);
+        hipLaunchKernelGGL(k_gn_partial<float>, dim3(nch, N), dim3(256), 0, s, (const float *)x, HW, C, G, part);
+        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 255) / 256), dim3(256), 0, s, part, N * G, nch, eps, stats);
+        hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const float *)x, N, H, W, C,
+                           G, stats, gamma, beta, (const float *)up, fuse, (float *)out);
     }
     MDX_CHECK_LAUNCH("mdx_groupnorm");
     return MDX_OK;

@@ -181,7 +181,7 @@ class MaskRCNN:
 
     def groupnorm(self, x, N, H, W, C, g, up=None, fuse=0):
         out = torch.empty_like(x)
-        need = N * self.cfg.gn_groups * 2
+        need = (call("mdx_groupnorm_workspace_bytes", N, H, W, self.cfg.gn_groups) + 3) // 4
         if self.gn_stats is None or self.gn_stats.numel() < need:
             self.gn_stats = torch.empty(need, dtype=torch.float32, device=self.device)
         call("mdx_groupnorm", _p(x), N, H, W, C, self.cfg.gn_groups, float(self.cfg.gn_eps), _p(g[0]), _p(g[1]),
