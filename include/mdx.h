@@ -74,10 +74,12 @@ int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t lut[256], u
  * iters_tail=iters) -- M/proc/proc.py:480-515: per frame medianBlur(median_k)
  * (0 = skip; only 3 supported) then morphologyEx(MORPH_OPEN, strel, iters).
  * strel: host uint8 [kh][kw] (each row one contiguous run, kh,kw <= 15).
- * src and out must not alias. */
+ * src, out and workspace (mdx_clean_workspace_bytes; unused when iters == 0)
+ * must not alias. */
+int64_t mdx_clean_workspace_bytes(int64_t n, int H, int W);
 int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k,
                      const uint8_t *strel, int kh, int kw, int iters, uint8_t *out,
-                     mdx_stream_t stream);
+                     uint8_t *workspace, mdx_stream_t stream);
 
 /* get_frame_features(frames, frame_threshold=thr, mask=mask, use_cc=*) +
  * im_moment_features -- M/proc/proc.py:237-302, :518-549.  Largest contour
@@ -114,6 +116,15 @@ int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, 
 int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
                int in_dtype, int out_dtype, void *out, mdx_stream_t stream);
+/* mdx_conv2d with split-K: ksplit K slices write fp32 partials into workspace
+ * (ksplit*M*Cout*4 bytes), a second launch sums them in fixed order and applies
+ * bias/residual/ReLU.  ksplit 0 = choose from the grid size and workspace_bytes
+ * (falls back to 1 slice when it does not pay or does not fit). */
+int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
+int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
+                      int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
+                      int in_dtype, int out_dtype, void *out, int ksplit, void *workspace,
+                      int64_t workspace_bytes, mdx_stream_t stream);
 
 /* scale_raw_frames LUT + replicate 1->C channels + (x - mean[c]) / std[c] + zero
  * pad to (Hp, Wp) with Cp (>= C) channels.  frames uint8 (B,h,w). */

@@ -34,10 +34,14 @@ SIGNATURES = {
     "mdx_inpaint_ns": (I32, [P, P, I64, I32, I32, I32, P, P]),
     "mdx_build_scale_lut": (I32, [F64, F64, I32, P]),
     "mdx_scale_frames": (I32, [P, I64, P, P, P]),
-    "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P]),
+    "mdx_clean_workspace_bytes": (I64, [I64, I32, I32]),
+    "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P, P]),
     "mdx_frame_moments": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P]),
     "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P]),
     "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
+    "mdx_conv2d_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32, I32, I32, I32]),
+    "mdx_conv2d_splitk": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, I32,
+                                P, I64, P]),
     "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),
     "mdx_maxpool2d": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "mdx_groupnorm_workspace_bytes": (I64, [I32, I32, I32, I32]),

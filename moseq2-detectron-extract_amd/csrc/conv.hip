@@ -41,19 +41,6 @@ constexpr int ROWB = 128;          // bytes of K per LDS row
 constexpr int PITCH = ROWB + 16;   // padded row pitch (bytes)
 constexpr int TILE_BYTES = BM * PITCH;
 
-struct ConvArgs {
-    const void *x;
-    const void *w;
-    const float *bias;  // [N] or null
-    const void *res;    // [M][N] (same dtype as out) or null
-    void *out;
-    int H, W, Cin, Cout, KH, KW, stride, pad, OH, OW;
-    int M, K;
-    int relu;
-    int out_mode;  // 0: NHWC, 1: deconv2x2 pixel shuffle
-    int tiles_n, tiles_total;
-};
-
 template <typename TO>
 __device__ __forceinline__ void store_out(TO *p, float v) { *p = (TO)v; }
 
@@ -80,6 +67,69 @@ __device__ __forceinline__ void store8(TO *p, const float *v) {
     } else {
         *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4 *>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
+struct ConvArgs {
+    const void *x;
+    const void *w;
+    const float *bias;  // [N] or null
+    const void *res;    // [M][N] (same dtype as out) or null
+    void *out;
+    int H, W, Cin, Cout, KH, KW, stride, pad, OH, OW;
+    int M, K;
+    int relu;
+    int out_mode;  // 0: NHWC, 1: deconv2x2 pixel shuffle
+    int tiles_n, tiles_total;
+    int ksplit, ksteps;  // split-K: K range of slice z = [z*ksteps*BK, (z+1)*ksteps*BK)
+    float *part;         // [ksplit][M][Cout] fp32 partial sums (ksplit > 1)
+};
+
+// bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
+// the 16-B store (or the scalar path for ragged channel counts)
+template <typename TO>
+__device__ __forceinline__ void finish8(const ConvArgs &a, int gm, int gn0, float *v) {
+    TO *O = reinterpret_cast<TO *>(a.out);
+    const TO *RS = reinterpret_cast<const TO *>(a.res);
+    const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
+    const bool vec_ok = (a.Cout % 8) == 0 && (Co % 8) == 0;
+    const int ohw = a.OH * a.OW;
+    auto out_index = [&](int gn) -> long long {
+        if (a.out_mode == 0) return (long long)gm * a.Cout + gn;
+        const int q = gn / Co, co = gn - q * Co;
+        const int b = gm / ohw, rem = gm - b * ohw;
+        const int y = rem / a.OW, xx = rem - y * a.OW;
+        return (((long long)b * (2 * a.OH) + 2 * y + (q >> 1)) * (2 * a.OW) + 2 * xx + (q & 1)) * Co + co;
+    };
+    if (vec_ok) {
+        const long long obase = out_index(gn0);
+        if (a.bias) {
+            const float4 b0 = *reinterpret_cast<const float4 *>(a.bias + gn0);
+            const float4 b1 = *reinterpret_cast<const float4 *>(a.bias + gn0 + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        if (RS) {
+            float rv[8];
+            load8<TO>(RS + obase, rv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += rv[k];
+        }
+        if (a.relu) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        }
+        store8<TO>(O + obase, v);
+    } else {
+        for (int k = 0; k < 8; ++k) {
+            const int gn = gn0 + k;
+            if (gn >= a.Cout) break;
+            const long long oi = out_index(gn);
+            float x = v[k] + (a.bias ? a.bias[gn] : 0.f);
+            if (RS) x += (float)RS[oi];
+            if (a.relu) x = x > 0.f ? x : 0.f;
+            store_out<TO>(O + oi, x);
+        }
     }
 }
 
@@ -125,10 +175,11 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         a_ix0[i] = ox * a.stride - a.pad;
         a_base[i] = (long long)b * a.H * a.W * a.Cin;
     }
-    int kci = (kc * VEC) % a.Cin;
-    int kr = (kc * VEC) / a.Cin;
+    const int kz = blockIdx.y;
+    int kglob = kz * a.ksteps * BK + kc * VEC;
+    int kci = kglob % a.Cin;
+    int kr = kglob / a.Cin;
     int kkx = kr % a.KW, kky = kr / a.KW;
-    int kglob = kc * VEC;
 
     const T *X = reinterpret_cast<const T *>(a.x);
     const T *Wt = reinterpret_cast<const T *>(a.w);
@@ -178,7 +229,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (a.K + BK - 1) / BK;
+    const int nk_all = (a.K + BK - 1) / BK;
+    const int nk = min(a.ksteps, nk_all - kz * a.ksteps);
     load_global();
     advance_k();
     store_lds(0);
@@ -240,10 +292,6 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
                 Cs[row * CP + col] = acc[i][j][r];
             }
     __syncthreads();
-    TO *O = reinterpret_cast<TO *>(a.out);
-    const TO *RS = reinterpret_cast<const TO *>(a.res);
-    const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
-    const bool vec_ok = (a.Cout % 8) == 0 && (Co % 8) == 0;
     constexpr int CPR = BN_ / 8;  // 8-wide chunks per row
     for (int c = tid; c < BM * CPR; c += CONV_THREADS) {
         const int row = c / CPR, ch = c - row * CPR;
@@ -251,57 +299,37 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         if (gm >= a.M) continue;
         const int gn0 = n0 + ch * 8;
         if (gn0 >= a.Cout) continue;
-        long long obase;  // output offset of channel gn0
-        int q = 0, co0 = gn0;
-        if (a.out_mode == 0) {
-            obase = (long long)gm * a.Cout + gn0;
-        } else {
-            q = gn0 / Co;
-            co0 = gn0 - q * Co;
-            const int b = gm / ohw, rem = gm - b * ohw;
-            const int y = rem / a.OW, xx = rem - y * a.OW;
-            obase = (((long long)b * (2 * a.OH) + 2 * y + (q >> 1)) * (2 * a.OW) + 2 * xx + (q & 1)) * Co + co0;
-        }
         const float *src = Cs + row * CP + ch * 8;
-        if (vec_ok) {
-            float v[8];
-            const float4 x0 = *reinterpret_cast<const float4 *>(src), x1 = *reinterpret_cast<const float4 *>(src + 4);
-            v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-            if (a.bias) {
-                const float4 b0 = *reinterpret_cast<const float4 *>(a.bias + gn0);
-                const float4 b1 = *reinterpret_cast<const float4 *>(a.bias + gn0 + 4);
-                v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-                v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-            }
-            if (RS) {
-                float rv[8];
-                load8<TO>(RS + obase, rv);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] += rv[k];
-            }
-            if (a.relu) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
-            }
-            store8<TO>(O + obase, v);
+        float v[8];
+        const float4 x0 = *reinterpret_cast<const float4 *>(src), x1 = *reinterpret_cast<const float4 *>(src + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        if (a.ksplit > 1) {
+            // raw partial; Cout % 8 == 0 is required for split-K
+            float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
+            *reinterpret_cast<float4 *>(pp) = x0;
+            *reinterpret_cast<float4 *>(pp + 4) = x1;
         } else {
-            for (int k = 0; k < 8; ++k) {
-                const int gn = gn0 + k;
-                if (gn >= a.Cout) break;
-                long long oi = obase + k;
-                if (a.out_mode == 1) {
-                    const int qq = gn / Co, co = gn - qq * Co;
-                    const int b = gm / ohw, rem = gm - b * ohw;
-                    const int y = rem / a.OW, xx = rem - y * a.OW;
-                    oi = (((long long)b * (2 * a.OH) + 2 * y + (qq >> 1)) * (2 * a.OW) + 2 * xx + (qq & 1)) * Co + co;
-                }
-                float v = src[k] + (a.bias ? a.bias[gn] : 0.f);
-                if (RS) v += (float)RS[oi];
-                if (a.relu) v = v > 0.f ? v : 0.f;
-                store_out<TO>(O + oi, v);
-            }
+            finish8<TO>(a, gm, gn0, v);
         }
     }
+}
+
+// split-K reduction: sum the slices (fixed order) and apply the epilogue
+template <typename TO>
+__global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
+    const int cpr = a.Cout / 8;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)a.M * cpr) return;
+    const int gm = (int)(i / cpr), gn0 = (int)(i - (long long)gm * cpr) * 8;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const long long slice = (long long)a.M * a.Cout;
+    const float *pp = a.part + (long long)gm * a.Cout + gn0;
+    for (int z = 0; z < a.ksplit; ++z) {
+        const float4 x0 = *reinterpret_cast<const float4 *>(pp + z * slice);
+        const float4 x1 = *reinterpret_cast<const float4 *>(pp + z * slice + 4);
+        v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w; v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+    }
+    finish8<TO>(a, gm, gn0, v);
 }
 
 }  // namespace mdx
@@ -309,9 +337,42 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
 using namespace mdx;
 
 // dtype codes: 0 = fp32, 1 = fp16
+// split-K slice count for a launch of `tiles` output tiles and nk K-steps:
+// minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
+// with 2 resident workgroups on each of the 256 CUs
+static int choose_ksplit(long long tiles, int nk, long long M, int Cout, long long ws_bytes) {
+    const long long slots = 512;
+    int best = 1;
+    double best_cost = 1e30;
+    for (int ks = 1; ks <= 8; ++ks) {
+        if (ks > 1 && (nk / ks < 4 || (long long)ks * M * Cout * 4 > ws_bytes)) break;
+        const long long waves = (tiles * ks + slots - 1) / slots;
+        const double cost = (double)waves * ((nk + ks - 1) / ks + 4) + (ks > 1 ? 2.0 + ks : 0.0);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = ks;
+        }
+    }
+    return best;
+}
+
+extern "C" int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                              int pad) {
+    const long long OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+    return 8ll * N * OH * OW * Cout * 4;
+}
+
 extern "C" int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                           int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
                           int in_dtype, int out_dtype, void *out, mdx_stream_t stream) {
+    return mdx_conv2d_splitk(x, N, H, W, Cin, w, bias, Cout, KH, KW, stride, pad, residual, relu, out_mode, in_dtype,
+                             out_dtype, out, 1, nullptr, 0, stream);
+}
+
+extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias,
+                                 int Cout, int KH, int KW, int stride, int pad, const void *residual, int relu,
+                                 int out_mode, int in_dtype, int out_dtype, void *out, int ksplit, void *workspace,
+                                 int64_t workspace_bytes, mdx_stream_t stream) {
     MDX_REQUIRE(x && w && out, "mdx_conv2d: null pointer");
     MDX_REQUIRE(in_dtype == 0 || in_dtype == 1, "mdx_conv2d: in_dtype must be 0 (f32) or 1 (f16)");
     MDX_REQUIRE(out_dtype == 0 || out_dtype == 1, "mdx_conv2d: out_dtype must be 0 (f32) or 1 (f16)");
@@ -338,16 +399,28 @@ extern "C" int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const voi
     const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_n = tiles_n;
     a.tiles_total = tiles_m * tiles_n;
+    const int nk = (a.K + (in_dtype == 1 ? 64 : 32) - 1) / (in_dtype == 1 ? 64 : 32);
+    if (ksplit <= 0) ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes) : 1;
+    MDX_REQUIRE(ksplit == 1 || (workspace && Cout % 8 == 0 && (long long)ksplit * M * Cout * 4 <= workspace_bytes),
+                "mdx_conv2d: split-K needs Cout %% 8 == 0 and a workspace of ksplit*M*Cout*4 bytes");
+    ksplit = ksplit > nk ? nk : ksplit;
+    a.ksteps = (nk + ksplit - 1) / ksplit;
+    a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
+    a.part = reinterpret_cast<float *>(workspace);
     const size_t lds_main = 2 * (size_t)BM * PITCH + 2 * (size_t)bn * PITCH;
     const size_t lds_epi = (size_t)BM * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     hipStream_t s = as_stream(stream);
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
+        const dim3 grid(a.tiles_total, a.ksplit);                                                           \
         if (narrow)                                                                                         \
-            hipLaunchKernelGGL((k_conv<TI_, TO_, 64>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a);  \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 64>), grid, dim3(CONV_THREADS), lds, s, a);                 \
         else                                                                                                \
-            hipLaunchKernelGGL((k_conv<TI_, TO_, 128>), dim3(a.tiles_total), dim3(CONV_THREADS), lds, s, a); \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 128>), grid, dim3(CONV_THREADS), lds, s, a);                \
+        if (a.ksplit > 1)                                                                                   \
+            hipLaunchKernelGGL((k_conv_reduce<TO_>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), \
+                               0, s, a);                                                                    \
     } while (0)
     if (in_dtype == 1 && out_dtype == 1)
         MDX_LAUNCH_CONV(_Float16, _Float16);

@@ -82,133 +82,117 @@ __global__ __launch_bounds__(256) void k_scale(const uint8_t *__restrict__ in, i
 }
 
 // ---------------------------------------------------------------------------
-// clean_frames: median3 (replicate border) -> erode^iters -> dilate^iters,
-// fused per output tile.  Pixels outside the image hold the neutral element of
-// the next pass (255 before an erosion, 0 before a dilation), which is exactly
-// OpenCV's morphologyDefaultBorderValue behaviour applied per pass.
+// clean_frames: median3 (replicate border) -> erode^iters -> dilate^iters, one
+// launch per pass over 64x32 output tiles (the frames stay in L2/MALL between
+// passes; a fused multi-pass tile would recompute a 2*iters*rad halo).  Pixels
+// outside the image read as the pass's neutral element (255 for an erosion, 0
+// for a dilation) -- OpenCV's morphologyDefaultBorderValue, applied per pass.
+// Morphology is done separably: per LDS row, the min/max over each distinct
+// strel row span, then per output pixel the combine over the strel rows.
 // ---------------------------------------------------------------------------
 constexpr int CT_W = 64, CT_H = 32, CT_THREADS = 256, MAX_KH = 15;
 
 struct StrelSpans {
-    int kh, ay, ax, rad, nspan;
+    int kh, kw, ay, ax, nspan;
     int8_t j1[MAX_KH], j2[MAX_KH];    // row ky: ones in [j1, j2)
     int8_t sj1[MAX_KH], sj2[MAX_KH];  // distinct spans
     int8_t rspan[MAX_KH];             // row ky -> distinct span index (-1: empty row)
 };
 
-__device__ __forceinline__ uint8_t med3x3(const uint8_t *b, int stride, int ly, int lx) {
-    // exact median of 9 values (sorting network on the 3x3 window)
-    int v[9];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) v[dy * 3 + dx] = b[(ly + dy - 1) * stride + lx + dx - 1];
-#define MDX_S(a, c)            \
-    {                          \
+__device__ __forceinline__ int med9(int *v) {
+#define MDX_S(a, c)               \
+    {                             \
         int lo = min(v[a], v[c]); \
         int hi = max(v[a], v[c]); \
-        v[a] = lo;             \
-        v[c] = hi;             \
+        v[a] = lo;                \
+        v[c] = hi;                \
     }
     MDX_S(1, 2); MDX_S(4, 5); MDX_S(7, 8); MDX_S(0, 1); MDX_S(3, 4); MDX_S(6, 7);
     MDX_S(1, 2); MDX_S(4, 5); MDX_S(7, 8); MDX_S(0, 3); MDX_S(5, 8); MDX_S(4, 7);
     MDX_S(3, 6); MDX_S(1, 4); MDX_S(2, 5); MDX_S(4, 7); MDX_S(4, 2); MDX_S(6, 4);
     MDX_S(4, 2);
 #undef MDX_S
-    return (uint8_t)v[4];
+    return v[4];
 }
 
-__global__ __launch_bounds__(CT_THREADS) void k_clean(const uint8_t *__restrict__ src, int H, int W,
-                                                      int median, StrelSpans st, int iters,
-                                                      uint8_t *__restrict__ out, int tiles_x, int halo) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int TW = CT_W + 2 * halo, TH = CT_H + 2 * halo;
-    uint8_t *A = smem, *B = smem + TW * TH;
-    const int64_t frame = blockIdx.y;
-    const int tx0 = (blockIdx.x % tiles_x) * CT_W - halo;  // global x of local 0
-    const int ty0 = (blockIdx.x / tiles_x) * CT_H - halo;
-    const uint8_t *s = src + frame * (int64_t)H * W;
-
-    // load (replicate border for the median; neutral 255 if no median)
-    for (int i = threadIdx.x; i < TW * TH; i += CT_THREADS) {
-        const int ly = i / TW, lx = i - ly * TW;
-        int gy = ty0 + ly, gx = tx0 + lx;
-        const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-        gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
-        uint8_t v = s[(int64_t)gy * W + gx];
-        if (!median && !inside) v = 255;
-        A[i] = v;
+// medianBlur(3), BORDER_REPLICATE
+__global__ __launch_bounds__(CT_THREADS) void k_median3(const uint8_t *__restrict__ src, int H, int W,
+                                                        uint8_t *__restrict__ out, int tiles_x) {
+    constexpr int LW = CT_W + 2, LH = CT_H + 2;
+    __shared__ uint8_t A[LH * LW];
+    const long long frame = blockIdx.y;
+    const int x0 = (blockIdx.x % tiles_x) * CT_W, y0 = (blockIdx.x / tiles_x) * CT_H;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const uint8_t *s = src + frame * H * W;
+    for (int ly = ty; ly < LH; ly += 4) {
+        const int gy = min(max(y0 + ly - 1, 0), H - 1);
+        for (int lx = tx; lx < LW; lx += 64) {
+            const int gx = min(max(x0 + lx - 1, 0), W - 1);
+            A[ly * LW + lx] = s[gy * W + gx];
+        }
     }
     __syncthreads();
-    int rem = halo;  // valid margin of the current buffer
-    if (median) {
-        rem -= 1;
-        const int lo = halo - rem;
-        const int w = TW - 2 * lo, h = TH - 2 * lo;
-        for (int i = threadIdx.x; i < w * h; i += CT_THREADS) {
-            const int ly = lo + i / w, lx = lo + i % w;
-            const int gy = ty0 + ly, gx = tx0 + lx;
-            const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
-            B[ly * TW + lx] = inside ? med3x3(A, TW, ly, lx) : (uint8_t)255;
-        }
-        __syncthreads();
-        uint8_t *t = A; A = B; B = t;
+    uint8_t *o = out + frame * H * W;
+    const int gx = x0 + tx;
+    if (gx >= W) return;
+#pragma unroll 2
+    for (int r = 0; r < CT_H / 4; ++r) {
+        const int y = ty * (CT_H / 4) + r, gy = y0 + y;
+        if (gy >= H) break;
+        int v[9];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) v[dy * 3 + dx] = A[(y + dy) * LW + tx + dx];
+        o[gy * W + gx] = (uint8_t)med9(v);
     }
-    // per pass: (1) horizontal min/max over each distinct row span into Hs[k]
-    // (2) vertical combine over the strel rows -> B.  Same result as the
-    // direct 2-D scan (min/max are associative), ~3x fewer LDS reads.
-    uint8_t *Hs = smem + 2 * TW * TH;  // [st.nspan][TH][TW]
-    for (int pass = 0; pass < 2 * iters; ++pass) {
-        const bool dil = pass >= iters;
-        const uint8_t outside_next = (pass + 1 >= iters) ? (uint8_t)0 : (uint8_t)255;
-        const int lo_in = halo - rem;  // valid input region [lo_in, T - lo_in)
-        rem -= st.rad;
-        const int lo = halo - rem;
-        {
-            // horizontal: rows of the valid input region, columns of the output region
-            const int w = TW - 2 * lo, h = TH - 2 * lo_in;
-            for (int i = threadIdx.x; i < st.nspan * w * h; i += CT_THREADS) {
-                const int k = i / (w * h), rr = i - k * (w * h);
-                const int ly = lo_in + rr / w, lx = lo + rr % w;
-                const uint8_t *row = A + ly * TW + lx - st.ax;
-                int acc = dil ? 0 : 255;
-                for (int kx = st.sj1[k]; kx < st.sj2[k]; ++kx) {
-                    const int v = row[kx];
-                    acc = dil ? max(acc, v) : min(acc, v);
-                }
-                Hs[(k * TH + ly) * TW + lx] = (uint8_t)acc;
-            }
+}
+
+// one erosion (DIL = false) or dilation (DIL = true) pass
+template <bool DIL>
+__global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict__ src, int H, int W, StrelSpans st,
+                                                      uint8_t *__restrict__ out, int tiles_x) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int LW = CT_W + st.kw - 1, LH = CT_H + st.kh - 1;
+    uint8_t *A = smem;                            // [LH][LW]
+    uint8_t *Hs = smem + ((LH * LW + 15) & ~15);  // [nspan][LH][CT_W]
+    const long long frame = blockIdx.y;
+    const int x0 = (blockIdx.x % tiles_x) * CT_W, y0 = (blockIdx.x / tiles_x) * CT_H;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const uint8_t *s = src + frame * H * W;
+    const uint8_t neutral = DIL ? 0 : 255;
+    for (int ly = ty; ly < LH; ly += 4) {
+        const int gy = y0 + ly - st.ay;
+        const bool yin = gy >= 0 && gy < H;
+        for (int lx = tx; lx < LW; lx += 64) {
+            const int gx = x0 + lx - st.ax;
+            A[ly * LW + lx] = (yin && gx >= 0 && gx < W) ? s[gy * W + gx] : neutral;
         }
-        __syncthreads();
-        const int w = TW - 2 * lo, h = TH - 2 * lo;
-        for (int i = threadIdx.x; i < w * h; i += CT_THREADS) {
-            const int ly = lo + i / w, lx = lo + i % w;
-            const int gy = ty0 + ly, gx = tx0 + lx;
-            const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
-            uint8_t r;
-            if (!inside) {
-                r = outside_next;
-            } else {
-                int acc = dil ? 0 : 255;
-                for (int ky = 0; ky < st.kh; ++ky) {
-                    const int k = st.rspan[ky];
-                    if (k < 0) continue;
-                    const int v = Hs[(k * TH + ly + ky - st.ay) * TW + lx];
-                    acc = dil ? max(acc, v) : min(acc, v);
-                }
-                r = (uint8_t)acc;
-            }
-            B[ly * TW + lx] = r;
-        }
-        __syncthreads();
-        uint8_t *t = A; A = B; B = t;
     }
-    uint8_t *o = out + frame * (int64_t)H * W;
-    for (int i = threadIdx.x; i < CT_W * CT_H; i += CT_THREADS) {
-        const int ly = i / CT_W, lx = i - ly * CT_W;
-        const int gy = ty0 + halo + ly, gx = tx0 + halo + lx;
-        if (gy < H && gx < W) o[(int64_t)gy * W + gx] = A[(ly + halo) * TW + lx + halo];
+    __syncthreads();
+    for (int ly = ty; ly < LH; ly += 4) {
+        const uint8_t *row = A + ly * LW + tx;
+        for (int k = 0; k < st.nspan; ++k) {
+            int acc = neutral;
+            for (int kx = st.sj1[k]; kx < st.sj2[k]; ++kx) acc = DIL ? max(acc, (int)row[kx]) : min(acc, (int)row[kx]);
+            Hs[(k * LH + ly) * CT_W + tx] = (uint8_t)acc;
+        }
+    }
+    __syncthreads();
+    uint8_t *o = out + frame * H * W;
+    const int gx = x0 + tx;
+    if (gx >= W) return;
+    for (int r = 0; r < CT_H / 4; ++r) {
+        const int y = ty * (CT_H / 4) + r, gy = y0 + y;
+        if (gy >= H) break;
+        int acc = neutral;
+        for (int ky = 0; ky < st.kh; ++ky) {
+            const int k = st.rspan[ky];
+            if (k < 0) continue;
+            const int v = Hs[(k * LH + y + ky) * CT_W + tx];
+            acc = DIL ? max(acc, v) : min(acc, v);
+        }
+        o[gy * W + gx] = (uint8_t)acc;
     }
 }
 
@@ -546,19 +530,22 @@ extern "C" int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t 
     return MDX_OK;
 }
 
+extern "C" int64_t mdx_clean_workspace_bytes(int64_t n, int H, int W) { return n * H * W; }
+
 extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k, const uint8_t *strel,
-                                int kh, int kw, int iters, uint8_t *out, mdx_stream_t stream) {
+                                int kh, int kw, int iters, uint8_t *out, uint8_t *workspace, mdx_stream_t stream) {
     MDX_REQUIRE(src && out && src != out, "mdx_clean_frames: null or aliased buffers");
     MDX_REQUIRE(median_k == 0 || median_k == 3, "mdx_clean_frames: median_k must be 0 or 3 (got %d)", median_k);
     MDX_REQUIRE(iters >= 0, "mdx_clean_frames: iters < 0");
+    MDX_REQUIRE(iters == 0 || (workspace && workspace != src && workspace != out),
+                "mdx_clean_frames: the opening needs a distinct workspace of n*H*W bytes");
     StrelSpans st{};
-    st.kh = 0;
     if (iters > 0) {
         MDX_REQUIRE(strel && kh > 0 && kw > 0 && kh <= MAX_KH && kw <= MAX_KH, "mdx_clean_frames: strel %dx%d", kh, kw);
         st.kh = kh;
+        st.kw = kw;
         st.ay = kh / 2;
         st.ax = kw / 2;
-        int rad = std::max(st.ay, kh - 1 - st.ay);
         for (int r = 0; r < kh; ++r) {
             int j1 = -1, j2 = -1;
             for (int c = 0; c < kw; ++c) {
@@ -571,9 +558,7 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
             if (j1 < 0) j1 = j2 = 0;
             st.j1[r] = (int8_t)j1;
             st.j2[r] = (int8_t)j2;
-            if (j2 > j1) rad = std::max(rad, std::max(st.ax - j1, j2 - 1 - st.ax));
         }
-        st.rad = rad;
         st.nspan = 0;
         for (int r = 0; r < kh; ++r) {
             st.rspan[r] = -1;
@@ -590,14 +575,29 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
         }
     }
     if (n == 0) return MDX_OK;
-    const int halo = (median_k ? 1 : 0) + 2 * iters * st.rad;
-    MDX_REQUIRE(halo <= 96, "mdx_clean_frames: halo %d too large", halo);
-    const int tiles_x = (int)ceil_div(W, CT_W), tiles_y = (int)ceil_div(H, CT_H);
-    const size_t lds = (2 + (size_t)std::max(st.nspan, 1)) * (CT_W + 2 * halo) * (CT_H + 2 * halo);
-    MDX_REQUIRE(lds <= 160 * 1024, "mdx_clean_frames: LDS %zu too large", lds);
     MDX_REQUIRE(n <= 65535, "mdx_clean_frames: n > 65535 per call");
-    hipLaunchKernelGGL(k_clean, dim3(tiles_x * tiles_y, (unsigned)n), dim3(CT_THREADS), lds, as_stream(stream), src, H,
-                       W, median_k ? 1 : 0, st, iters, out, tiles_x, halo);
+    MDX_REQUIRE((long long)H * W < (1ll << 31), "mdx_clean_frames: frame too large");
+    hipStream_t s = as_stream(stream);
+    const int tiles_x = (int)ceil_div(W, CT_W), tiles_y = (int)ceil_div(H, CT_H);
+    const dim3 grid(tiles_x * tiles_y, (unsigned)n);
+    const int LW = CT_W + kw - 1, LH = CT_H + kh - 1;
+    const size_t lds = ((size_t)(LH * LW + 15) & ~(size_t)15) + (size_t)std::max(st.nspan, 1) * LH * CT_W;
+    // pass chain: the last pass writes `out`; ping-pong through the workspace
+    const int npass = (median_k ? 1 : 0) + 2 * iters;
+    const uint8_t *cur = src;
+    for (int p = 0; p < npass; ++p) {
+        uint8_t *dst = ((npass - 1 - p) % 2 == 0) ? out : workspace;
+        if (median_k && p == 0) {
+            hipLaunchKernelGGL(k_median3, grid, dim3(CT_THREADS), 0, s, cur, H, W, dst, tiles_x);
+        } else {
+            const int q = p - (median_k ? 1 : 0);
+            if (q < iters)
+                hipLaunchKernelGGL(k_morph<false>, grid, dim3(CT_THREADS), lds, s, cur, H, W, st, dst, tiles_x);
+            else
+                hipLaunchKernelGGL(k_morph<true>, grid, dim3(CT_THREADS), lds, s, cur, H, W, st, dst, tiles_x);
+        }
+        cur = dst;
+    }
     MDX_CHECK_LAUNCH("mdx_clean_frames");
     return MDX_OK;
 }

@@ -159,19 +159,29 @@ __global__ __launch_bounds__(256) void k_gn_partial(const T *__restrict__ x, int
     const int rows = 256 / CV;          // pixels processed in parallel
     const int cv = threadIdx.x % CV, pr = threadIdx.x / CV;
     const int p0 = chunk * GN_CHUNK_PIX;
+    // shifted sums (shift = the lane's first value) -> exact-enough per-lane
+    // (count, mean, M2) for <= GN_CHUNK_PIX*8 values
     float cnt = 0.f, mean = 0.f, m2 = 0.f;
-    if (pr < rows) {
+    if (pr < rows && p0 + pr < HW) {
+        float sh = 0.f, S = 0.f, Q = 0.f;
+        bool first = true;
         for (int p = p0 + pr; p < p0 + GN_CHUNK_PIX && p < HW; p += rows) {
             float v[8];
             ld8(x + ((long long)n * HW + p) * C + cv * 8, v);
+            if (first) {
+                sh = v[0];
+                first = false;
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                cnt += 1.f;
-                const float d = v[k] - mean;
-                mean += d / cnt;
-                m2 += d * (v[k] - mean);
+                const float d = v[k] - sh;
+                S += d;
+                Q += d * d;
             }
+            cnt += 8.f;
         }
+        mean = sh + S / cnt;
+        m2 = fmaxf(Q - S * (S / cnt), 0.f);
     }
     s_n[threadIdx.x] = cnt;
     s_m[threadIdx.x] = mean;
@@ -200,13 +210,15 @@ __global__ __launch_bounds__(256) void k_gn_partial(const T *__restrict__ x, int
     }
 }
 
+// one wave per (image, group): lanes merge strided chunk partials, then a
+// butterfly of Chan merges (fp64)
 __global__ __launch_bounds__(256) void k_gn_final(const float *__restrict__ part, int NG, int nchunks, float eps,
                                                   float *__restrict__ stats) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= NG) return;
     const float *pp = part + (long long)i * nchunks * 3;
     double N = 0.0, M = 0.0, Q = 0.0;
-    for (int c = 0; c < nchunks; ++c) {
+    for (int c = lane; c < nchunks; c += 64) {
         const double nb = pp[3 * c];
         if (nb == 0.0) continue;
         const double tot = N + nb;
@@ -215,9 +227,22 @@ __global__ __launch_bounds__(256) void k_gn_final(const float *__restrict__ part
         Q += (double)pp[3 * c + 2] + d * d * (N * nb / tot);
         N = tot;
     }
-    const float var = (float)(Q / N);
-    stats[2 * i] = (float)M;
-    stats[2 * i + 1] = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double nb = __shfl_xor(N, off), mb = __shfl_xor(M, off), qb = __shfl_xor(Q, off);
+        const double tot = N + nb;
+        if (tot > 0.0) {
+            const double d = mb - M;
+            M += d * (nb / tot);
+            Q += qb + d * d * (N * nb / tot);
+            N = tot;
+        }
+    }
+    if (lane == 0) {
+        const float var = (float)(Q / N);
+        stats[2 * i] = (float)M;
+        stats[2 * i + 1] = 1.0f / sqrtf(var + eps);
+    }
 }
 
 // y = (x - mean) * rstd * gamma + beta; optionally fused: y = (y + up(prev)) [/ 2]
@@ -1056,12 +1081,12 @@ extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, f
     const long long total = (long long)N * H * W * C;
     if (dtype == 1) {
         hipLaunchKernelGGL(k_gn_partial<_Float16>, dim3(nch, N), dim3(256), 0, s, (const _Float16 *)x, HW, C, G, part);
-        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 255) / 256), dim3(256), 0, s, part, N * G, nch, eps, stats);
+        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 3) / 4), dim3(256), 0, s, part, N * G, nch, eps, stats);
         hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const _Float16 *)x, N, H,
                            W, C, G, stats, gamma, beta, (const _Float16 *)up, fuse, (_Float16 *)out);
     } else {
         hipLaunchKernelGGL(k_gn_partial<float>, dim3(nch, N), dim3(256), 0, s, (const float *)x, HW, C, G, part);
-        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 255) / 256), dim3(256), 0, s, part, N * G, nch, eps, stats);
+        hipLaunchKernelGGL(k_gn_final, dim3((N * G + 3) / 4), dim3(256), 0, s, part, N * G, nch, eps, stats);
         hipLaunchKernelGGL(k_gn_apply<float>, dim3(grid_for(total / 8)), dim3(256), 0, s, (const float *)x, N, H, W, C,
                            G, stats, gamma, beta, (const float *)up, fuse, (float *)out);
     }

@@ -26,6 +26,10 @@ from .._lib import MdxError, call
 from .config import ModelConfig
 from .weights import resnet_stage_specs
 
+# fp32 partial-sum workspace for split-K launches of the small-grid layers
+# (res5, ROI heads); the library only splits when the partials fit
+SPLITK_WS_BYTES = 64 << 20
+
 _DT = {"fp32": 0, "fp16": 1}
 
 
@@ -164,6 +168,7 @@ class MaskRCNN:
         self.pixel_mean = np.ascontiguousarray(np.asarray(sd["pixel_mean"].reshape(-1), np.float32))
         self.pixel_std = np.ascontiguousarray(np.asarray(sd["pixel_std"].reshape(-1), np.float32))
         self.gn_stats = None
+        self.splitk_ws = None
 
     # ------------------------------------------------------------ layers
     def conv(self, x, N, H, W, c: Conv, relu, out=None, residual=None, out_f32=False, out_mode=0):
@@ -175,8 +180,11 @@ class MaskRCNN:
                 out = torch.empty((N, 2 * OH, 2 * OW, c.cout // 4), dtype=odt, device=self.device)
             else:
                 out = torch.empty((N, OH, OW, c.cout), dtype=odt, device=self.device)
-        call("mdx_conv2d", _p(x), N, H, W, c.cin, _p(c.w), _p(c.b), c.cout, c.k, c.k, c.stride, c.pad, _p(residual),
-             int(relu), out_mode, self.dcode, 0 if out_f32 else self.dcode, _p(out), _stream())
+        if self.splitk_ws is None:
+            self.splitk_ws = torch.empty(SPLITK_WS_BYTES // 4, dtype=torch.float32, device=self.device)
+        call("mdx_conv2d_splitk", _p(x), N, H, W, c.cin, _p(c.w), _p(c.b), c.cout, c.k, c.k, c.stride, c.pad,
+             _p(residual), int(relu), out_mode, self.dcode, 0 if out_f32 else self.dcode, _p(out), 0,
+             _p(self.splitk_ws), SPLITK_WS_BYTES, _stream())
         return out, OH, OW
 
     def groupnorm(self, x, N, H, W, C, g, up=None, fuse=0):

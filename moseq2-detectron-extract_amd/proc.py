@@ -253,8 +253,9 @@ def clean_frames(frames, prefilter_space=(3,), prefilter_time=None, strel_tail=E
         out.copy_(src)
         return _ret(out, as_np)
     st = np.ascontiguousarray(np.asarray(strel_tail) != 0, np.uint8)
+    ws = torch.empty(call("mdx_clean_workspace_bytes", n, H, W), dtype=torch.uint8, device=src.device)
     call("mdx_clean_frames", _ptr(src), n, H, W, med, st.ctypes.data_as(ctypes.c_void_p), st.shape[0], st.shape[1],
-         iters, _ptr(out), _stream())
+         iters, _ptr(out), _ptr(ws), _stream())
     return _ret(out, as_np)
 
 

@@ -40,9 +40,10 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("ksplit", [1, 3])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d(mdx, dtype, case):
+def test_conv2d(mdx, dtype, case, ksplit):
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
@@ -62,8 +63,16 @@ def test_conv2d(mdx, dtype, case):
     rd = res.cuda() if res is not None else None
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     dc = 1 if dtype == "fp16" else 0
-    call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
-         P(out), None)
+    if ksplit == 1:
+        call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
+             P(out), None)
+    else:
+        if Cout % 8:
+            pytest.skip("split-K needs Cout % 8 == 0")
+        nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
+        ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
+        call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0,
+             dc, dc, P(out), ksplit, P(ws), nb, None)
     got = out.cpu().double()
     scale = want.abs().max().item() + 1e-6
     tol = 2e-3 if dtype == "fp16" else 1e-4
