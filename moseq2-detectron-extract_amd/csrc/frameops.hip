@@ -328,22 +328,42 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
     const int PH = H + 2, PW = W + 2;
     const int nwords = PH * pww;
     if (threadIdx.x == 0) s_best = 0ull;
-    // bit-pack (frame > thr) & mask into LDS: one 64-pixel word per wave step,
-    // lane l reads padded pixel 64*w64 + l (coalesced), __ballot packs the word
+    // bit-pack (frame > thr) & mask into LDS, one padded 32-pixel word per
+    // lane: bit b of word (py, wx) is unpadded pixel (py - 1, 32 wx + b - 1).
+    // Interior words read their 32 pixels [32 wx, 32 wx + 32) with two 16-B
+    // loads (bits 1..31 + the next word's bit 0) plus the byte at 32 wx - 1.
     {
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const int w64s = pww / 2;  // 64-bit words per padded row (pww is even)
-        unsigned long long *bits64 = reinterpret_cast<unsigned long long *>(bits);
-        for (int w = wv; w < PH * w64s; w += MOM_THREADS / 64) {
-            const int py = w / w64s, wx = w - py * w64s;
-            const int x = wx * 64 + lane - 1;
-            bool on = false;
-            if (py >= 1 && py <= H && x >= 0 && x < W) {
-                const long long off = (long long)(py - 1) * W + x;
-                on = (double)fr[off] > thr && (!mk || mk[off]);
+        const bool vec = (W % 16) == 0 && ((reinterpret_cast<uintptr_t>(fr) | reinterpret_cast<uintptr_t>(mk)) & 15) == 0;
+        for (int w = threadIdx.x; w < nwords; w += MOM_THREADS) {
+            const int py = w / pww, wx = w - py * pww;
+            uint32_t word = 0;
+            if (py >= 1 && py <= H) {
+                const uint8_t *fy = fr + (py - 1) * W;
+                const uint8_t *my = mk ? mk + (py - 1) * W : nullptr;
+                const int xb = 32 * wx;  // pixel of bit 1
+                if (vec && xb + 32 <= W) {
+                    uint4 fv[2], mv[2];
+                    fv[0] = *reinterpret_cast<const uint4 *>(fy + xb);
+                    fv[1] = *reinterpret_cast<const uint4 *>(fy + xb + 16);
+                    if (my) {
+                        mv[0] = *reinterpret_cast<const uint4 *>(my + xb);
+                        mv[1] = *reinterpret_cast<const uint4 *>(my + xb + 16);
+                    }
+                    const uint8_t *fe = reinterpret_cast<const uint8_t *>(fv);
+                    const uint8_t *me = reinterpret_cast<const uint8_t *>(mv);
+                    uint32_t u = 0;
+#pragma unroll
+                    for (int k = 0; k < 31; ++k) u |= (uint32_t)((double)fe[k] > thr && (!my || me[k])) << (k + 1);
+                    if (xb > 0) u |= (uint32_t)((double)fy[xb - 1] > thr && (!my || my[xb - 1]));
+                    word = u;
+                } else {
+                    for (int k = 0; k < 32; ++k) {
+                        const int x = xb + k - 1;
+                        if (x >= 0 && x < W) word |= (uint32_t)((double)fy[x] > thr && (!my || my[x])) << k;
+                    }
+                }
             }
-            const unsigned long long word = __ballot(on);
-            if (lane == 0) bits64[w] = word;
+            bits[w] = word;
         }
     }
     __syncthreads();
@@ -608,7 +628,7 @@ extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int
     MDX_REQUIRE(frames && centroid && orientation && axis_length, "mdx_frame_moments: null pointer");
     MDX_REQUIRE(H > 0 && W > 0, "mdx_frame_moments: bad shape");
     if (n == 0) return MDX_OK;
-    const int pww = (int)ceil_div(W + 2, 64) * 2;  // even: rows are whole 64-bit words
+    const int pww = (int)ceil_div(W + 2, 32);
     const size_t lds = (size_t)(H + 2) * pww * 4;
     MDX_REQUIRE(lds <= 120 * 1024, "mdx_frame_moments: frame %dx%d too large for LDS", H, W);
     MDX_REQUIRE(n <= 0x7fffffff, "mdx_frame_moments: n too large");

@@ -34,14 +34,19 @@ constexpr int INP_SETUP_THREADS = 256, INP_MARCH_BLOCKS = 16;
 struct InpLayout {
     long long np;  // padded pixels
     // offsets (in int32 units) of the per-frame arrays
-    long long o_code, o_t, o_ins, o_lab, o_cnt, o_start, o_fill, o_ord, o_scr, o_hdr, total;
+    long long o_code, o_t, o_ins, o_lab, o_cnt, o_start, o_fill, o_ord, o_scr, o_hdr, o_cc, total;
+    int nch;       // compaction chunks of INP_CHUNK unpadded pixels
 };
+
+constexpr int INP_CHUNK = 4096;  // 256 lanes x 16 pixels
 
 static inline InpLayout inp_layout(int H, int W) {
     InpLayout L;
     L.np = (long long)(H + 2) * (W + 2);
     long long o = 0;
     L.o_hdr = o; o += 16;
+    L.nch = (int)(((long long)H * W + INP_CHUNK - 1) / INP_CHUNK);
+    L.o_cc = o; o += (L.nch + 3) / 4 * 4;
     L.o_code = o; o += L.np;
     L.o_t = o; o += L.np;
     L.o_ins = o; o += L.np;
@@ -134,13 +139,97 @@ __device__ __forceinline__ int block_scan_excl(int v, int *sh, int &total) {
     return incl - v;
 }
 
+// code = KNOWN, t = 1e6 over every frame's padded image (wide grid)
+__global__ __launch_bounds__(256) void k_inp_fill(int *__restrict__ ws, InpLayout L, long long n) {
+    const long long per = L.np;
+    const long long total = n * per;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const long long f = i / per, k = i - f * per;
+        int *base = ws + f * L.total;
+        base[L.o_code + k] = C_KNOWN;
+        reinterpret_cast<float *>(base + L.o_t)[k] = 1.0e6f;
+    }
+}
+
+// the 16 mask bytes of lane `tid` in chunk c (unpadded raster order)
+__device__ __forceinline__ void chunk_bytes(const uint8_t *msk, long long HW, int c, int tid, uint8_t *v) {
+    const long long p0 = (long long)c * INP_CHUNK + tid * 16;
+    if (p0 + 16 <= HW && ((reinterpret_cast<uintptr_t>(msk + p0) & 15) == 0)) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(msk + p0);
+        const uint8_t *e = reinterpret_cast<const uint8_t *>(&u);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = e[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = (p0 + k < HW) ? msk[p0 + k] : 0;
+    }
+}
+
+__device__ __forceinline__ int block_sum(int v, int *sh) {
+    int total;
+    block_scan_excl(v, sh, total);
+    return total;
+}
+
+// unknown pixels per chunk
+__global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_count(const uint8_t *__restrict__ invalid, int H, int W,
+                                                                 int *__restrict__ ws, InpLayout L) {
+    __shared__ int sh[INP_SETUP_THREADS];
+    const long long f = blockIdx.y;
+    const int c = blockIdx.x;
+    const long long HW = (long long)H * W;
+    uint8_t v[16];
+    chunk_bytes(invalid + f * HW, HW, c, threadIdx.x, v);
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m += v[k] != 0;
+    const int tot = block_sum(m, sh);
+    if (threadIdx.x == 0) ws[f * L.total + L.o_cc + c] = tot;
+}
+
+// ordered compaction of the unknown pixels: chunk offset = sum of the previous
+// chunks' counts, lane offset = block scan; ins[k] = padded index (raster order)
+__global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_compact(const uint8_t *__restrict__ invalid, int H, int W,
+                                                                   int *__restrict__ ws, InpLayout L) {
+    __shared__ int sh[INP_SETUP_THREADS];
+    const long long f = blockIdx.y;
+    const int c = blockIdx.x, tid = threadIdx.x;
+    int *base = ws + f * L.total;
+    const int *cc = base + L.o_cc;
+    int prev = 0;
+    for (int q = tid; q < c; q += INP_SETUP_THREADS) prev += cc[q];
+    const int off = block_sum(prev, sh);
+    if (cc[c] == 0) return;  // uniform per block
+    const long long HW = (long long)H * W;
+    uint8_t v[16];
+    chunk_bytes(invalid + f * HW, HW, c, tid, v);
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m += v[k] != 0;
+    int tot;
+    int pos = off + block_scan_excl(m, sh, tot);
+    if (!m) return;
+    int *code = base + L.o_code, *ins = base + L.o_ins, *lab = base + L.o_lab;
+    const int PW = W + 2;
+    const long long p0 = (long long)c * INP_CHUNK + tid * 16;
+    for (int k = 0; k < 16; ++k) {
+        if (!v[k]) continue;
+        const long long p = p0 + k;
+        const int y = (int)(p / W), x = (int)(p - (long long)y * W);
+        const int j = (y + 1) * PW + x + 1;
+        ins[pos] = j;
+        code[j] = pos;
+        lab[pos] = pos;
+        ++pos;
+    }
+}
+
 __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *__restrict__ invalid, int H, int W,
                                                                  int range, int *__restrict__ ws, InpLayout L) {
     __shared__ int sh[INP_SETUP_THREADS];
     __shared__ int s_flag;
     const int tid = threadIdx.x;
     const long long f = blockIdx.x;
-    const uint8_t *msk = invalid + f * (long long)H * W;
     int *base = ws + f * L.total;
     int *hdr = base + L.o_hdr;
     int *code = base + L.o_code;
@@ -148,70 +237,13 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
     int *ins = base + L.o_ins, *lab = base + L.o_lab, *cnt = base + L.o_cnt, *start = base + L.o_start;
     int *fill = base + L.o_fill, *ord = base + L.o_ord;
     const int PH = H + 2, PW = W + 2;
-    int any = 0;
-    for (long long i = tid; i < (long long)H * W; i += INP_SETUP_THREADS) any |= msk[i] != 0;
-    if (tid == 0) s_flag = 0;
-    __syncthreads();
-    if (any) atomicOr(&s_flag, 1);
-    __syncthreads();
-    if (!s_flag) {
+    int part = 0;
+    for (int q = tid; q < L.nch; q += INP_SETUP_THREADS) part += base[L.o_cc + q];
+    const int nin = block_sum(part, sh);
+    if (nin == 0) {
         if (tid == 0) hdr[0] = hdr[1] = 0;
         return;
     }
-    for (long long i = tid; i < L.np; i += INP_SETUP_THREADS) {
-        code[i] = C_KNOWN;
-        t[i] = 1.0e6f;
-    }
-    __syncthreads();
-    // unknown pixels in raster order: each thread owns a contiguous segment of
-    // the padded frame (count, block scan, ordered write)
-    const long long seg = (L.np + INP_SETUP_THREADS - 1) / INP_SETUP_THREADS;
-    const long long s0 = tid * seg, s1 = s0 + seg < L.np ? s0 + seg : L.np;
-    auto is_in = [&](long long i) -> bool {
-        const int y = (int)(i / PW), x = (int)(i - (long long)y * PW);
-        return y >= 1 && y <= H && x >= 1 && x <= W && msk[(long long)(y - 1) * W + x - 1] != 0;
-    };
-    int mine = 0;
-    {
-        // walk rows of the segment without per-pixel division
-        long long i = s0;
-        while (i < s1) {
-            const int y = (int)(i / PW);
-            const long long rowend = ((long long)y + 1) * PW < s1 ? ((long long)y + 1) * PW : s1;
-            if (y >= 1 && y <= H) {
-                const uint8_t *mr = msk + (long long)(y - 1) * W - 1 - (long long)y * PW;
-                for (long long j = i; j < rowend; ++j) {
-                    const int x = (int)(j - (long long)y * PW);
-                    if (x >= 1 && x <= W && mr[j]) ++mine;
-                }
-            }
-            i = rowend;
-        }
-    }
-    int nin;
-    int pos = block_scan_excl(mine, sh, nin);
-    {
-        long long i = s0;
-        while (i < s1) {
-            const int y = (int)(i / PW);
-            const long long rowend = ((long long)y + 1) * PW < s1 ? ((long long)y + 1) * PW : s1;
-            if (y >= 1 && y <= H) {
-                const uint8_t *mr = msk + (long long)(y - 1) * W - 1 - (long long)y * PW;
-                for (long long j = i; j < rowend; ++j) {
-                    const int x = (int)(j - (long long)y * PW);
-                    if (x >= 1 && x <= W && mr[j]) {
-                        ins[pos] = (int)j;
-                        code[j] = pos;
-                        lab[pos] = pos;
-                        ++pos;
-                    }
-                }
-            }
-            i = rowend;
-        }
-    }
-    (void)is_in;
-    __syncthreads();
     // narrow band: interior 4-neighbours of unknown pixels that are not unknown
     for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
         const int i = ins[k];
@@ -454,6 +486,11 @@ extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n
     MDX_REQUIRE(n <= 65535, "mdx_inpaint_ns: at most 65535 frames per call");
     const InpLayout L = inp_layout(H, W);
     hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_inp_fill, dim3(2048), dim3(256), 0, s, (int *)workspace, L, (long long)n);
+    hipLaunchKernelGGL(k_inp_count, dim3(L.nch, (unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W,
+                       (int *)workspace, L);
+    hipLaunchKernelGGL(k_inp_compact, dim3(L.nch, (unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W,
+                       (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_setup, dim3((unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W, radius,
                        (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_march, dim3(INP_MARCH_BLOCKS, (unsigned)n), dim3(256), 0, s, frames, H, W, radius,
