@@ -120,6 +120,9 @@ int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const
  * (ksplit*M*Cout*4 bytes), a second launch sums them in fixed order and applies
  * bias/residual/ReLU.  ksplit 0 = choose from the grid size and workspace_bytes
  * (falls back to 1 slice when it does not pay or does not fit). */
+/* Policy for the 256x256 fp16 kernel (Cin % 64 == 0): 0 never, 1 auto (default:
+ * when the layer fills the chip), 2 whenever eligible.  Returns the old mode. */
+int mdx_conv_set_large_tiles(int mode);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

@@ -332,11 +332,178 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
     finish8<TO>(a, gm, gn0, v);
 }
 
+// ---------------------------------------------------------------------------
+// Large-layer kernel (fp16, Cin % 64 == 0): 256x256 tile, 512 threads = 8
+// waves as 2(M) x 4(N), each wave 128x64 = 8x4 MFMA 16x16x32 tiles.  Both
+// operands are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
+// VGPR round trip), two 64 KiB stages, the next K-step's DMA in flight while
+// the current one is multiplied (counted vmcnt + raw s_barrier).  A K-step of
+// 64 halves lies inside one (ky, kx) tap because Cin % 64 == 0, so the
+// implicit-im2col source of each 16-B chunk is a plain per-row offset.
+// LDS image: row r (128 B) holds logical 16-B chunk c at physical chunk
+// c ^ ((r >> 1) & 7) (lane-linear DMA destination, swizzle applied on the
+// global source address); the fragment reads are then bank-conflict-free.
+// ---------------------------------------------------------------------------
+constexpr int G_BM = 256, G_BN = 256, G_THREADS = 512;
+constexpr int G_STAGE = (G_BM + G_BN) * 128;  // bytes per K-step stage
+constexpr int G_EPI_PITCH = 68;               // fp32 pitch of a wave's 64x64 staging block
+constexpr int G_LDS = (2 * G_STAGE > 8 * 64 * G_EPI_PITCH * 4) ? 2 * G_STAGE : 8 * 64 * G_EPI_PITCH * 4;
+
+__device__ __attribute__((aligned(64))) uint4 g_zero16[4];  // zero source for padding / out-of-range rows
+
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+__device__ __forceinline__ void glds16(const void *src, char *dst) {
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)dst, 16, 0, 0);
+}
+
+template <typename TO>
+__global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * G_BM, n0 = tn * G_BN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 2, wn = wid & 3;
+
+    // DMA descriptors: instruction j of wave w fills rows 32w + 8j .. +8
+    const _Float16 *X = reinterpret_cast<const _Float16 *>(a.x);
+    const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
+    const int ohw = a.OH * a.OW;
+    int a_iy0[4], a_ix0[4], a_c[4];
+    long long a_base[4];
+    bool a_ok[4];
+    const _Float16 *b_src[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = 32 * wid + 8 * j + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        a_c[j] = c * 8;
+        const int gm = m0 + r;
+        a_ok[j] = gm < a.M;
+        const int gmc = a_ok[j] ? gm : 0;
+        const int b = gmc / ohw, rem = gmc - b * ohw;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_iy0[j] = oy * a.stride - a.pad;
+        a_ix0[j] = ox * a.stride - a.pad;
+        a_base[j] = (long long)b * a.H * a.W * a.Cin + c * 8;
+        const int gn = n0 + r;
+        b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * 8 : nullptr;
+    }
+    int kglob = 0, kci = 0, kkx = 0, kky = 0;  // uniform: K-step start and its tap
+    auto issue = [&](int stage) {
+        char *As = smem + stage * G_STAGE + 32 * wid * 128;
+        char *Bs = smem + stage * G_STAGE + G_BM * 128 + 32 * wid * 128;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int iy = a_iy0[j] + kky, ix = a_ix0[j] + kkx;
+            const void *src = g_zero16;
+            if (a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                src = X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kci;
+            glds16(src, As + j * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16,
+                                           Bs + j * 1024);
+    };
+    auto advance = [&]() {
+        kglob += 64;
+        kci += 64;
+        if (kci >= a.Cin) {
+            kci = 0;
+            if (++kkx == a.KW) {
+                kkx = 0;
+                ++kky;
+            }
+        }
+    };
+
+    float4v acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.K / 64;
+    const int swz = ((lane & 15) >> 1);  // (row >> 1) & 7 of every fragment row this lane reads
+    issue(0);
+    advance();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+            issue(cur ^ 1);
+            advance();
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        const char *Ab = smem + cur * G_STAGE + (wm * 128 + (lane & 15)) * 128;
+        const char *Bb = smem + cur * G_STAGE + G_BM * 128 + (wn * 64 + (lane & 15)) * 128;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int off = ((4 * s + (lane >> 4)) ^ swz) * 16;
+            half8 bf[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 128 + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const half8 af = *reinterpret_cast<const half8 *>(Ab + i * 16 * 128 + off);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+
+    // epilogue: per wave, two passes of 64 rows x 64 cols through its own LDS block
+    float *Cs = reinterpret_cast<float *>(smem) + wid * 64 * G_EPI_PITCH;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    Cs[(i * 16 + (lane >> 4) * 4 + r) * G_EPI_PITCH + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int item = lane + 64 * q;
+            const int row = item >> 3, ch = item & 7;
+            const int gm = m0 + wm * 128 + 64 * h + row, gn0 = n0 + wn * 64 + ch * 8;
+            if (gm < a.M && gn0 < a.Cout) {
+                const float4 x0 = *reinterpret_cast<const float4 *>(Cs + row * G_EPI_PITCH + ch * 8);
+                const float4 x1 = *reinterpret_cast<const float4 *>(Cs + row * G_EPI_PITCH + ch * 8 + 4);
+                float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                finish8<TO>(a, gm, gn0, v);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
+
 }  // namespace mdx
 
 using namespace mdx;
 
 // dtype codes: 0 = fp32, 1 = fp16
+// large-tile kernel policy (tests): 0 never, 1 auto (default), 2 whenever eligible
+static int g_large_tiles = 1;
+extern "C" int mdx_conv_set_large_tiles(int mode) {
+    const int old = g_large_tiles;
+    g_large_tiles = mode;
+    return old;
+}
+
 // split-K slice count for a launch of `tiles` output tiles and nk K-steps:
 // minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
 // with 2 resident workgroups on each of the 256 CUs
@@ -394,6 +561,25 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.K = KH * KW * Cin;
     a.relu = relu;
     a.out_mode = out_mode;
+    hipStream_t s = as_stream(stream);
+    // large fp16 layers: the 256x256 LDS-DMA kernel when it fills the chip
+    {
+        const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
+        const bool big = Cout >= 192 && t256 >= 384;
+        if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) &&
+            (g_large_tiles == 2 || (g_large_tiles == 1 && big))) {
+            a.tiles_n = (int)ceil_div(Cout, G_BN);
+            a.tiles_total = (int)t256;
+            a.ksplit = 1;
+            a.ksteps = a.K / 64;
+            if (out_dtype == 1)
+                hipLaunchKernelGGL(k_conv256<_Float16>, dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            else
+                hipLaunchKernelGGL(k_conv256<float>, dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            MDX_CHECK_LAUNCH("mdx_conv2d");
+            return MDX_OK;
+        }
+    }
     const bool narrow = Cout <= 64;  // 64-wide N tile: no wasted MFMA columns for 64-channel layers
     const int bn = narrow ? 64 : BN;
     const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
@@ -410,7 +596,6 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     const size_t lds_main = 2 * (size_t)BM * PITCH + 2 * (size_t)bn * PITCH;
     const size_t lds_epi = (size_t)BM * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-    hipStream_t s = as_stream(stream);
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \

@@ -148,11 +148,15 @@ __global__ __launch_bounds__(CT_THREADS) void k_median3(const uint8_t *__restric
     }
 }
 
-// one erosion (DIL = false) or dilation (DIL = true) pass
+// one erosion (DIL = false) or dilation (DIL = true) pass.  The strel tables
+// are copied to LDS once; every table entry is then read once per thread and
+// applied to all of the thread's rows (kernarg arrays indexed at run time
+// would be re-fetched with a scalar load per use).
 template <bool DIL>
 __global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict__ src, int H, int W, StrelSpans st,
                                                       uint8_t *__restrict__ out, int tiles_x) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int8_t s_sj1[MAX_KH], s_sj2[MAX_KH], s_rspan[MAX_KH];
     const int LW = CT_W + st.kw - 1, LH = CT_H + st.kh - 1;
     uint8_t *A = smem;                            // [LH][LW]
     uint8_t *Hs = smem + ((LH * LW + 15) & ~15);  // [nspan][LH][CT_W]
@@ -160,39 +164,55 @@ __global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict_
     const int x0 = (blockIdx.x % tiles_x) * CT_W, y0 = (blockIdx.x / tiles_x) * CT_H;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const uint8_t *s = src + frame * H * W;
-    const uint8_t neutral = DIL ? 0 : 255;
+    const int neutral = DIL ? 0 : 255;
+    if (threadIdx.x < MAX_KH) {
+        s_sj1[threadIdx.x] = st.sj1[threadIdx.x];
+        s_sj2[threadIdx.x] = st.sj2[threadIdx.x];
+        s_rspan[threadIdx.x] = st.rspan[threadIdx.x];
+    }
     for (int ly = ty; ly < LH; ly += 4) {
         const int gy = y0 + ly - st.ay;
         const bool yin = gy >= 0 && gy < H;
         for (int lx = tx; lx < LW; lx += 64) {
             const int gx = x0 + lx - st.ax;
-            A[ly * LW + lx] = (yin && gx >= 0 && gx < W) ? s[gy * W + gx] : neutral;
+            A[ly * LW + lx] = (yin && gx >= 0 && gx < W) ? s[gy * W + gx] : (uint8_t)neutral;
         }
     }
     __syncthreads();
-    for (int ly = ty; ly < LH; ly += 4) {
-        const uint8_t *row = A + ly * LW + tx;
-        for (int k = 0; k < st.nspan; ++k) {
+    const int nsp = st.nspan;
+    for (int k = 0; k < nsp; ++k) {
+        const int j1 = s_sj1[k], j2 = s_sj2[k];
+        for (int ly = ty; ly < LH; ly += 4) {
+            const uint8_t *row = A + ly * LW + tx;
             int acc = neutral;
-            for (int kx = st.sj1[k]; kx < st.sj2[k]; ++kx) acc = DIL ? max(acc, (int)row[kx]) : min(acc, (int)row[kx]);
+            for (int kx = j1; kx < j2; ++kx) acc = DIL ? max(acc, (int)row[kx]) : min(acc, (int)row[kx]);
             Hs[(k * LH + ly) * CT_W + tx] = (uint8_t)acc;
         }
     }
     __syncthreads();
+    constexpr int RPT = CT_H / 4;  // rows per thread
+    const int yb = ty * RPT;
+    int acc[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[r] = neutral;
+    const int kh = st.kh;
+    for (int ky = 0; ky < kh; ++ky) {
+        const int k = s_rspan[ky];
+        if (k < 0) continue;
+        const uint8_t *col = Hs + (k * LH + yb + ky) * CT_W + tx;
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int v = col[r * CT_W];
+            acc[r] = DIL ? max(acc[r], v) : min(acc[r], v);
+        }
+    }
     uint8_t *o = out + frame * H * W;
     const int gx = x0 + tx;
     if (gx >= W) return;
-    for (int r = 0; r < CT_H / 4; ++r) {
-        const int y = ty * (CT_H / 4) + r, gy = y0 + y;
-        if (gy >= H) break;
-        int acc = neutral;
-        for (int ky = 0; ky < st.kh; ++ky) {
-            const int k = st.rspan[ky];
-            if (k < 0) continue;
-            const int v = Hs[(k * LH + y + ky) * CT_W + tx];
-            acc = DIL ? max(acc, v) : min(acc, v);
-        }
-        o[gy * W + gx] = (uint8_t)acc;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int gy = y0 + yb + r;
+        if (gy < H) o[gy * W + gx] = (uint8_t)acc[r];
     }
 }
 
@@ -226,36 +246,60 @@ __device__ __forceinline__ void green_edge(Green &g, long long xi_1, long long y
     g.a02 += dxy * (yi_1 * yii_1 + yi2);
 }
 
-__constant__ int c_dx[8] = {1, 1, 0, -1, -1, -1, 0, 1};
-__constant__ int c_dy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+// direction d: 0 E, 1 NE, 2 N, 3 NW, 4 W, 5 SW, 6 S, 7 SE (y grows down);
+// (dx + 1, dy + 1) packed 2 bits per direction so a lane-varying d needs no
+// table load
+__device__ __forceinline__ int dir_dx(int d) { return (int)((0x901Au >> (2 * d)) & 3u) - 1; }
+__device__ __forceinline__ int dir_dy(int d) { return (int)((0xA901u >> (2 * d)) & 3u) - 1; }
 
 __device__ __forceinline__ int getbit(const uint32_t *bits, int pww, int px, int py) {
     return (bits[py * pww + (px >> 5)] >> (px & 31)) & 1;
 }
 
+// bits (x-1 .. x+1) of padded row y as a 3-bit value
+__device__ __forceinline__ uint32_t row3(const uint32_t *bits, int pww, int x, int y) {
+    const int xm = x - 1, w = xm >> 5, b = xm & 31;
+    const uint32_t *r = bits + y * pww + w;
+    uint64_t v = r[0];
+    if (b > 29) v |= (uint64_t)r[1] << 32;
+    return (uint32_t)(v >> b) & 7u;
+}
+
+// 8-neighbour mask of an interior padded pixel, bit d = direction d
+__device__ __forceinline__ uint32_t nbmask(const uint32_t *bits, int pww, int x, int y) {
+    const uint32_t t = row3(bits, pww, x, y - 1), m = row3(bits, pww, x, y), d = row3(bits, pww, x, y + 1);
+    return ((m >> 2) & 1u) | (((t >> 2) & 1u) << 1) | (((t >> 1) & 1u) << 2) | ((t & 1u) << 3) | ((m & 1u) << 4) |
+           ((d & 1u) << 5) | (((d >> 1) & 1u) << 6) | (((d >> 2) & 1u) << 7);
+}
+
 __device__ Green trace_outer(const uint32_t *bits, int pww, int x0, int y0, long long max_steps) {
     Green g = {0, 0, 0, 0, 0, 0};
+    // first fg neighbour clockwise from W: directions 3, 2, 1, 0, 7, 6, 5 (4 = none)
+    const uint32_t nb0 = nbmask(bits, pww, x0, y0);
     int s = 4;
-    const int s_end = 4;
-    int x1 = 0, y1 = 0;
-    do {
-        s = (s - 1) & 7;
-        x1 = x0 + c_dx[s];
-        y1 = y0 + c_dy[s];
-    } while (!getbit(bits, pww, x1, y1) && s != s_end);
-    if (s == s_end) return g;
+    {
+        int k = 0;
+        for (; k < 7; ++k) {
+            const int d = (3 - k) & 7;
+            if ((nb0 >> d) & 1u) {
+                s = d;
+                break;
+            }
+        }
+        if (k == 7) return g;  // isolated pixel
+    }
+    const int x1 = x0 + dir_dx(s), y1 = y0 + dir_dy(s);
     int x3 = x0, y3 = y0;
     long long px = x0 - 1, py = y0 - 1;
     const long long sx = px, sy = py;
     bool first = true;
     for (long long step = 0; step < max_steps; ++step) {
-        int x4 = 0, y4 = 0;
-        for (int c = 0; c < 8; ++c) {
-            s = (s + 1) & 7;
-            x4 = x3 + c_dx[s];
-            y4 = y3 + c_dy[s];
-            if (getbit(bits, pww, x4, y4)) break;
-        }
+        // next fg neighbour counter-clockwise from s + 1
+        const uint32_t nb = nbmask(bits, pww, x3, y3);
+        const int r = (s + 1) & 7;
+        const uint32_t rot = ((nb | (nb << 8)) >> r) & 0xFFu;
+        s = (r + __builtin_ctz(rot)) & 7;
+        const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
         if (!first) {
             green_edge(g, px, py, x3 - 1, y3 - 1);
             px = x3 - 1;

@@ -37,10 +37,12 @@ CONV_CASES = [
     (300, 1, 1, 1232, 72, 1, 1, 0, False, True),
     (2, 14, 16, 256, 256, 3, 2, 1, True, True),
     (1, 33, 31, 64, 256, 1, 1, 0, True, True),
+    (2, 40, 36, 192, 320, 3, 1, 1, False, True),
+    (600, 1, 1, 1024, 264, 1, 1, 0, False, False),
 ]
 
 
-@pytest.mark.parametrize("ksplit", [1, 3])
+@pytest.mark.parametrize("ksplit", [1, 3, "large"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -63,7 +65,16 @@ def test_conv2d(mdx, dtype, case, ksplit):
     rd = res.cuda() if res is not None else None
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     dc = 1 if dtype == "fp16" else 0
-    if ksplit == 1:
+    if ksplit == "large":
+        if dtype != "fp16" or Cin % 64:
+            pytest.skip("256x256 kernel: fp16, Cin % 64 == 0")
+        old = call("mdx_conv_set_large_tiles", 2)
+        try:
+            call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
+                 dc, P(out), None)
+        finally:
+            call("mdx_conv_set_large_tiles", old)
+    elif ksplit == 1:
         call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
              P(out), None)
     else:
