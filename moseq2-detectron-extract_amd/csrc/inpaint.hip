@@ -14,11 +14,14 @@
 // marched independently -- one lane per cluster -- and the result is
 // bit-identical to the serial algorithm.
 //
-//   k_inp_setup   (one workgroup per frame): flags/T image, raster-ordered
-//                 unknown-pixel list, narrow band, cluster labels (min-label
-//                 propagation + pointer jumping), cluster member lists.
-//   k_inp_march   (one lane per cluster): local FIFO(band) + heap(T, seq) FMM
-//                 with the NS weights, pixel values written in place.
+//   k_inp_fill    code = KNOWN, T = 1e6 over every padded frame (wide grid)
+//   k_inp_count / k_inp_compact  (4096-pixel chunks x frames): raster-ordered
+//                 unknown-pixel list (chunk counts, chunk offsets, block scan)
+//   k_inp_setup   (one workgroup per frame): narrow band, cluster labels
+//                 (min-label propagation + pointer jumping), member lists.
+//   k_inp_march   (one wave per cluster): local FIFO(band) + heap(T, seq) FMM
+//                 with the NS weights (window taps one per lane, summed in
+//                 the serial order), pixel values written in place.
 #include <cmath>
 
 #include "common.h"
@@ -29,7 +32,7 @@ namespace mdx {
 
 // code image: >= 0 unknown (index into the unknown list); -1 KNOWN; -2 BAND
 constexpr int C_KNOWN = -1, C_BAND = -2;
-constexpr int INP_SETUP_THREADS = 256, INP_MARCH_BLOCKS = 16;
+constexpr int INP_SETUP_THREADS = 256, INP_MARCH_BLOCKS = 64;
 
 struct InpLayout {
     long long np;  // padded pixels
@@ -334,9 +337,66 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
     }
 }
 
-__global__ __launch_bounds__(256) void k_inp_march(uint8_t *__restrict__ frames, int H, int W, int range,
-                                                   int *__restrict__ ws, InpLayout L) {
+// One NS window tap (k, l) around the pixel (i, j) being filled: returns the
+// weight w and the product w * I exactly as the serial loop forms them (0, 0
+// for a tap the loop skips, an exact no-op in its running sums).
+__device__ __forceinline__ void ns_tap(int k, int l, int i, int j, int range, int PH, int PW, int W,
+                                       const int *__restrict__ code, const uint8_t *out, float &w_out, float &wi_out) {
+    w_out = 0.f;
+    wi_out = 0.f;
+    const int km = k - 1 + (k == 1), kp = k - 1 - (k == PH - 2);
+    const int lm = l - 1 + (l == 1), lp = l - 1 - (l == PW - 2);
+    if (!(k > 0 && l > 0 && k < PH - 1 && l < PW - 1)) return;
+    if (code[k * PW + l] >= 0) return;
+    if ((l - j) * (l - j) + (k - i) * (k - i) > range * range) return;
+    const float ry = (float)(k - i), rx = (float)(l - j);
+    const float lr = rx * rx + ry * ry;
+    const float dst = (float)(1. / (lr * sqrt((double)lr)));
+    const bool up_ok = code[(k - 1) * PW + l] < 0, dn_ok = code[(k + 1) * PW + l] < 0;
+    const bool lf_ok = code[k * PW + l - 1] < 0, rt_ok = code[k * PW + l + 1] < 0;
+    float gx, gy;
+    if (dn_ok) {
+        if (up_ok)
+            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm]) + abs(out[kp * W + lm] - out[(km - 1) * W + lm]));
+        else
+            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm])) * 2.0f;
+    } else {
+        if (up_ok)
+            gx = (float)(abs(out[kp * W + lm] - out[(km - 1) * W + lm])) * 2.0f;
+        else
+            gx = 0;
+    }
+    if (rt_ok) {
+        if (lf_ok)
+            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm]) + abs(out[km * W + lm] - out[km * W + lm - 1]));
+        else
+            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm])) * 2.0f;
+    } else {
+        if (lf_ok)
+            gy = -(float)(abs(out[km * W + lm] - out[km * W + lm - 1])) * 2.0f;
+        else
+            gy = 0;
+    }
+    const float dot = rx * gx + ry * gy;
+    const float lg = gx * gx + gy * gy;
+    float dir = fabsf(dot / sqrtf(lr * lg));
+    if (!(dir > 0.01f)) dir = 0.000001f;
+    const float w = dst * dir;
+    w_out = w;
+    wi_out = w * (float)out[km * W + lm];
+}
+
+constexpr int MARCH_WAVES = 4, MAX_TAPS = 15 * 15;
+
+// One wave per cluster.  Lane 0 owns the cluster's serial state (member sort,
+// narrow band FIFO, (T, seq) heap); the window of every pixel being filled is
+// evaluated one tap per lane and summed by lane 0 in the serial loop's (k, l)
+// order, so the float sums are the serial ones bit for bit.
+__global__ __launch_bounds__(64 * MARCH_WAVES) void k_inp_march(uint8_t *__restrict__ frames, int H, int W, int range,
+                                                                 int *__restrict__ ws, InpLayout L) {
+    __shared__ float s_w[MARCH_WAVES][MAX_TAPS], s_wi[MARCH_WAVES][MAX_TAPS];
     const long long f = blockIdx.y;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int *base = ws + f * L.total;
     const int ncl = base[L.o_hdr + 1];
     int *code = base + L.o_code;
@@ -347,56 +407,62 @@ __global__ __launch_bounds__(256) void k_inp_march(uint8_t *__restrict__ frames,
     int *scr = base + L.o_scr;
     uint8_t *out = frames + f * (long long)H * W;
     const int PH = H + 2, PW = W + 2;
-    for (int c = blockIdx.x * 256 + threadIdx.x; c < ncl; c += gridDim.x * 256) {
+    const int wside = 2 * range + 1, ntaps = wside * wside;
+    float *tw = s_w[wid], *twi = s_wi[wid];
+    for (int c = blockIdx.x * MARCH_WAVES + wid; c < ncl; c += gridDim.x * MARCH_WAVES) {
         const int s0 = start[c], m = start[c + 1] - s0;
         int *mem = ord + s0;
-        // members in raster order (unknown-list index order == raster order)
-        for (int a = 1; a < m; ++a) {
-            const int v = mem[a];
-            int b = a - 1;
-            while (b >= 0 && mem[b] > v) {
-                mem[b + 1] = mem[b];
-                --b;
-            }
-            mem[b + 1] = v;
-        }
-        // this cluster's narrow band, raster order, unique
         int *band = scr + 7LL * s0;
         HEnt *heap = reinterpret_cast<HEnt *>(band + 4LL * m);
         int nb = 0;
-        for (int a = 0; a < m; ++a) {
-            const int i = ins[mem[a]];
-            const int cand[4] = {i - PW, i - 1, i + 1, i + PW};
-            for (int q = 0; q < 4; ++q) {
-                const int p = cand[q];
-                if (code[p] != C_BAND) continue;
-                // insert sorted, skip duplicates
-                int b = nb - 1;
-                bool dup = false;
-                while (b >= 0 && band[b] >= p) {
-                    if (band[b] == p) {
-                        dup = true;
-                        break;
-                    }
+        if (lane == 0) {
+            // members in raster order (unknown-list index order == raster order)
+            for (int a = 1; a < m; ++a) {
+                const int v = mem[a];
+                int b = a - 1;
+                while (b >= 0 && mem[b] > v) {
+                    mem[b + 1] = mem[b];
                     --b;
                 }
-                if (dup) continue;
-                for (int z = nb; z > b + 1; --z) band[z] = band[z - 1];
-                band[b + 1] = p;
-                ++nb;
+                mem[b + 1] = v;
+            }
+            // this cluster's narrow band, raster order, unique
+            for (int a = 0; a < m; ++a) {
+                const int i = ins[mem[a]];
+                const int cand[4] = {i - PW, i - 1, i + 1, i + PW};
+                for (int q = 0; q < 4; ++q) {
+                    const int p = cand[q];
+                    if (code[p] != C_BAND) continue;
+                    int b = nb - 1;
+                    bool dup = false;
+                    while (b >= 0 && band[b] >= p) {
+                        if (band[b] == p) {
+                            dup = true;
+                            break;
+                        }
+                        --b;
+                    }
+                    if (dup) continue;
+                    for (int z = nb; z > b + 1; --z) band[z] = band[z - 1];
+                    band[b + 1] = p;
+                    ++nb;
+                }
             }
         }
-        int head = 0, hn = 0, seq = nb;
+        int head = 0, hn = 0, seq = __shfl(nb, 0);
         for (;;) {
-            int idx;
-            if (head < nb)
-                idx = band[head++];
-            else if (hn > 0)
-                idx = heap_pop(heap, hn).idx;
-            else
-                break;
+            int idx = -1;
+            if (lane == 0) {
+                if (head < nb)
+                    idx = band[head++];
+                else if (hn > 0)
+                    idx = heap_pop(heap, hn).idx;
+                if (idx >= 0) code[idx] = C_KNOWN;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            idx = __shfl(idx, 0);
+            if (idx < 0) break;
             const int ii = idx / PW, jj = idx - ii * PW;
-            code[idx] = C_KNOWN;
             for (int q = 0; q < 4; ++q) {
                 int i, j;
                 if (q == 0) { i = ii - 1; j = jj; }
@@ -405,62 +471,28 @@ __global__ __launch_bounds__(256) void k_inp_march(uint8_t *__restrict__ frames,
                 else { i = ii; j = jj + 1; }
                 if (i <= 1 || j <= 1 || i > PH - 1 || j > PW - 1) continue;
                 if (code[i * PW + j] < 0) continue;
-                const float dist =
-                    min4f(fm_solve(i - 1, j, i, j - 1, code, t, PW), fm_solve(i + 1, j, i, j - 1, code, t, PW),
-                          fm_solve(i - 1, j, i, j + 1, code, t, PW), fm_solve(i + 1, j, i, j + 1, code, t, PW));
-                float Ia = 0.0f, s = 1.0e-20f;
-                for (int k = i - range; k <= i + range; ++k) {
-                    const int km = k - 1 + (k == 1), kp = k - 1 - (k == PH - 2);
-                    for (int l = j - range; l <= j + range; ++l) {
-                        const int lm = l - 1 + (l == 1), lp = l - 1 - (l == PW - 2);
-                        if (!(k > 0 && l > 0 && k < PH - 1 && l < PW - 1)) continue;
-                        if (code[k * PW + l] >= 0) continue;
-                        if ((l - j) * (l - j) + (k - i) * (k - i) > range * range) continue;
-                        const float ry = (float)(k - i), rx = (float)(l - j);
-                        const float lr = rx * rx + ry * ry;
-                        const float dst = (float)(1. / (lr * sqrt((double)lr)));
-                        const bool up_ok = code[(k - 1) * PW + l] < 0, dn_ok = code[(k + 1) * PW + l] < 0;
-                        const bool lf_ok = code[k * PW + l - 1] < 0, rt_ok = code[k * PW + l + 1] < 0;
-                        float gx, gy;
-                        if (dn_ok) {
-                            if (up_ok)
-                                gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm]) +
-                                             abs(out[kp * W + lm] - out[(km - 1) * W + lm]));
-                            else
-                                gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm])) * 2.0f;
-                        } else {
-                            if (up_ok)
-                                gx = (float)(abs(out[kp * W + lm] - out[(km - 1) * W + lm])) * 2.0f;
-                            else
-                                gx = 0;
-                        }
-                        if (rt_ok) {
-                            if (lf_ok)
-                                gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm]) +
-                                              abs(out[km * W + lm] - out[km * W + lm - 1]));
-                            else
-                                gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm])) * 2.0f;
-                        } else {
-                            if (lf_ok)
-                                gy = -(float)(abs(out[km * W + lm] - out[km * W + lm - 1])) * 2.0f;
-                            else
-                                gy = 0;
-                        }
-                        const float dot = rx * gx + ry * gy;
-                        const float lg = gx * gx + gy * gy;
-                        float dir = fabsf(dot / sqrtf(lr * lg));
-                        if (!(dir > 0.01f)) dir = 0.000001f;
-                        const float w = dst * dir;
-                        Ia += w * (float)out[km * W + lm];
-                        s += w;
-                    }
+                for (int tp = lane; tp < ntaps; tp += 64) {
+                    const int k = i - range + tp / wside, l = j - range + tp % wside;
+                    ns_tap(k, l, i, j, range, PH, PW, W, code, out, tw[tp], twi[tp]);
                 }
-                const double v = (double)Ia / s;
-                const int r = __double2int_rn(v);
-                out[(i - 1) * W + (j - 1)] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
-                t[i * PW + j] = dist;
-                code[i * PW + j] = C_BAND;
-                heap_push(heap, hn, HEnt{dist, seq++, i * PW + j});
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                if (lane == 0) {
+                    const float dist =
+                        min4f(fm_solve(i - 1, j, i, j - 1, code, t, PW), fm_solve(i + 1, j, i, j - 1, code, t, PW),
+                              fm_solve(i - 1, j, i, j + 1, code, t, PW), fm_solve(i + 1, j, i, j + 1, code, t, PW));
+                    float Ia = 0.0f, sw = 1.0e-20f;
+                    for (int tp = 0; tp < ntaps; ++tp) {
+                        Ia += twi[tp];
+                        sw += tw[tp];
+                    }
+                    const double v = (double)Ia / sw;
+                    const int r = __double2int_rn(v);
+                    out[(i - 1) * W + (j - 1)] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+                    t[i * PW + j] = dist;
+                    code[i * PW + j] = C_BAND;
+                    heap_push(heap, hn, HEnt{dist, seq++, i * PW + j});
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             }
         }
     }
@@ -493,8 +525,8 @@ extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n
                        (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_setup, dim3((unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W, radius,
                        (int *)workspace, L);
-    hipLaunchKernelGGL(k_inp_march, dim3(INP_MARCH_BLOCKS, (unsigned)n), dim3(256), 0, s, frames, H, W, radius,
-                       (int *)workspace, L);
+    hipLaunchKernelGGL(k_inp_march, dim3(INP_MARCH_BLOCKS, (unsigned)n), dim3(64 * MARCH_WAVES), 0, s, frames, H, W,
+                       radius, (int *)workspace, L);
     MDX_CHECK_LAUNCH("mdx_inpaint_ns");
     return MDX_OK;
 }
