@@ -133,6 +133,59 @@ __device__ __forceinline__ void finish8(const ConvArgs &a, int gm, int gn0, floa
     }
 }
 
+// NQ epilogue items per lane, residual loads for all of them issued before any
+// store (out and res may alias as far as the compiler knows, so a per-item
+// load -> store sequence would serialise every load behind the previous
+// store).  item(q, gm, gn0, src): row (-1 = skip), first channel, fp32 values.
+template <typename TO, int NQ, typename F>
+__device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
+    TO *O = reinterpret_cast<TO *>(a.out);
+    const TO *RS = reinterpret_cast<const TO *>(a.res);
+    const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
+    const bool vec_ok = (a.Cout % 8) == 0 && (Co % 8) == 0 && a.out_mode == 0;
+    constexpr int RW = sizeof(TO) == 2 ? 1 : 2;  // 16-B words of 8 residual values
+    uint4 rr[NQ][RW];
+    int gms[NQ], gns[NQ];
+    const float *srcs[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        item(q, gms[q], gns[q], srcs[q]);
+        if (gms[q] >= 0 && vec_ok && RS) {
+            const uint4 *rp = reinterpret_cast<const uint4 *>(RS + (long long)gms[q] * a.Cout + gns[q]);
+#pragma unroll
+            for (int w = 0; w < RW; ++w) rr[q][w] = rp[w];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (gms[q] < 0) continue;
+        const float *src = srcs[q];
+        const float4 x0 = *reinterpret_cast<const float4 *>(src), x1 = *reinterpret_cast<const float4 *>(src + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        if (!vec_ok) {
+            finish8<TO>(a, gms[q], gns[q], v);
+            continue;
+        }
+        const int gn0 = gns[q];
+        if (a.bias) {
+            const float4 b0 = *reinterpret_cast<const float4 *>(a.bias + gn0);
+            const float4 b1 = *reinterpret_cast<const float4 *>(a.bias + gn0 + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        if (RS) {
+            const TO *e = reinterpret_cast<const TO *>(&rr[q][0]);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += (float)e[k];
+        }
+        if (a.relu) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        }
+        store8<TO>(O + (long long)gms[q] * a.Cout + gn0, v);
+    }
+}
+
 // BN_: N tile (128 or 64).  4 waves as 2x2; wave tile (BM/2) x (BN_/2) =
 // TI x TJ MFMA tiles of 16x16.
 template <typename T, typename TO, int BN_>
@@ -293,24 +346,29 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             }
     __syncthreads();
     constexpr int CPR = BN_ / 8;  // 8-wide chunks per row
-    for (int c = tid; c < BM * CPR; c += CONV_THREADS) {
-        const int row = c / CPR, ch = c - row * CPR;
-        const int gm = m0 + row;
-        if (gm >= a.M) continue;
-        const int gn0 = n0 + ch * 8;
-        if (gn0 >= a.Cout) continue;
-        const float *src = Cs + row * CP + ch * 8;
-        float v[8];
-        const float4 x0 = *reinterpret_cast<const float4 *>(src), x1 = *reinterpret_cast<const float4 *>(src + 4);
-        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-        if (a.ksplit > 1) {
+    constexpr int NQ = BM * CPR / CONV_THREADS;
+    if (a.ksplit > 1) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = tid + q * CONV_THREADS;
+            const int row = c / CPR, ch = c - row * CPR;
+            const int gm = m0 + row, gn0 = n0 + ch * 8;
+            if (gm >= a.M || gn0 >= a.Cout) continue;
             // raw partial; Cout % 8 == 0 is required for split-K
+            const float *src = Cs + row * CP + ch * 8;
             float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
-            *reinterpret_cast<float4 *>(pp) = x0;
-            *reinterpret_cast<float4 *>(pp + 4) = x1;
-        } else {
-            finish8<TO>(a, gm, gn0, v);
+            *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
+            *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
         }
+    } else {
+        finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+            const int c = tid + q * CONV_THREADS;
+            const int row = c / CPR, ch = c - row * CPR;
+            gm = m0 + row;
+            gn0 = n0 + ch * 8;
+            src = Cs + row * CP + ch * 8;
+            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+        });
     }
 }
 
@@ -475,18 +533,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
                 for (int r = 0; r < 4; ++r)
                     Cs[(i * 16 + (lane >> 4) * 4 + r) * G_EPI_PITCH + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        finish_batch<TO, 8>(a, [&](int q, int &gm, int &gn0, const float *&src) {
             const int item = lane + 64 * q;
             const int row = item >> 3, ch = item & 7;
-            const int gm = m0 + wm * 128 + 64 * h + row, gn0 = n0 + wn * 64 + ch * 8;
-            if (gm < a.M && gn0 < a.Cout) {
-                const float4 x0 = *reinterpret_cast<const float4 *>(Cs + row * G_EPI_PITCH + ch * 8);
-                const float4 x1 = *reinterpret_cast<const float4 *>(Cs + row * G_EPI_PITCH + ch * 8 + 4);
-                float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-                finish8<TO>(a, gm, gn0, v);
-            }
-        }
+            gm = m0 + wm * 128 + 64 * h + row;
+            gn0 = n0 + wn * 64 + ch * 8;
+            src = Cs + row * G_EPI_PITCH + ch * 8;
+            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+        });
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 }

@@ -148,71 +148,107 @@ __global__ __launch_bounds__(CT_THREADS) void k_median3(const uint8_t *__restric
     }
 }
 
-// one erosion (DIL = false) or dilation (DIL = true) pass.  The strel tables
-// are copied to LDS once; every table entry is then read once per thread and
-// applied to all of the thread's rows (kernarg arrays indexed at run time
-// would be re-fetched with a scalar load per use).
+// one erosion (DIL = false) or dilation (DIL = true) pass.  Pixels are held
+// as u16 in LDS so that two of them are combined per v_pk_min/max_u16; each
+// lane owns 4 adjacent columns (two packed dwords).  The strel tables are
+// copied to LDS once (kernarg arrays indexed at run time would be re-fetched
+// with a scalar load per use).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+template <bool DIL>
+__device__ __forceinline__ uint32_t pk_op(uint32_t a, uint32_t b) {
+    const u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+    return __builtin_bit_cast(uint32_t, DIL ? __builtin_elementwise_max(x, y) : __builtin_elementwise_min(x, y));
+}
+
+constexpr int MP_MAXW = CT_W + MAX_KH + 1;  // u16 pixels per LDS row (even, 8-byte aligned rows)
+
 template <bool DIL>
 __global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict__ src, int H, int W, StrelSpans st,
                                                       uint8_t *__restrict__ out, int tiles_x) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int8_t s_sj1[MAX_KH], s_sj2[MAX_KH], s_rspan[MAX_KH];
     const int LW = CT_W + st.kw - 1, LH = CT_H + st.kh - 1;
-    uint8_t *A = smem;                            // [LH][LW]
-    uint8_t *Hs = smem + ((LH * LW + 15) & ~15);  // [nspan][LH][CT_W]
+    const int LP = (LW + 7) & ~3;                                 // u16 pitch (>= LW + 3, multiple of 4)
+    uint16_t *A = reinterpret_cast<uint16_t *>(smem);             // [LH][LP]
+    uint16_t *Hs = A + LH * LP;                                   // [nspan][LH][CT_W]
     const long long frame = blockIdx.y;
     const int x0 = (blockIdx.x % tiles_x) * CT_W, y0 = (blockIdx.x / tiles_x) * CT_H;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const uint8_t *s = src + frame * H * W;
-    const int neutral = DIL ? 0 : 255;
+    const uint32_t neutral = DIL ? 0u : 255u;
     if (threadIdx.x < MAX_KH) {
         s_sj1[threadIdx.x] = st.sj1[threadIdx.x];
         s_sj2[threadIdx.x] = st.sj2[threadIdx.x];
         s_rspan[threadIdx.x] = st.rspan[threadIdx.x];
     }
-    for (int ly = ty; ly < LH; ly += 4) {
-        const int gy = y0 + ly - st.ay;
-        const bool yin = gy >= 0 && gy < H;
-        for (int lx = tx; lx < LW; lx += 64) {
-            const int gx = x0 + lx - st.ax;
-            A[ly * LW + lx] = (yin && gx >= 0 && gx < W) ? s[gy * W + gx] : (uint8_t)neutral;
-        }
-    }
-    __syncthreads();
-    const int nsp = st.nspan;
-    for (int k = 0; k < nsp; ++k) {
-        const int j1 = s_sj1[k], j2 = s_sj2[k];
+    {
+        const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
         for (int ly = ty; ly < LH; ly += 4) {
-            const uint8_t *row = A + ly * LW + tx;
-            int acc = neutral;
-            for (int kx = j1; kx < j2; ++kx) acc = DIL ? max(acc, (int)row[kx]) : min(acc, (int)row[kx]);
-            Hs[(k * LH + ly) * CT_W + tx] = (uint8_t)acc;
+            const int gy = y0 + ly - st.ay;
+            const bool yin = gy >= 0 && gy < H;
+            for (int lx = tx; lx < LP; lx += 64) {
+                const int gx = x0 + lx - st.ax;
+                A[ly * LP + lx] = (uint16_t)((lx < LW && yin && gx >= 0 && gx < W) ? s[gy * W + gx] : neutral);
+            }
         }
     }
     __syncthreads();
-    constexpr int RPT = CT_H / 4;  // rows per thread
-    const int yb = ty * RPT;
-    int acc[RPT];
+    const int g = threadIdx.x & 15, rg = threadIdx.x >> 4;  // column quad, row group
+    const int nsp = st.nspan, kw = st.kw;
+    // horizontal: per LDS row, span min/max for the 4 columns 4g..4g+3
+    for (int ly = rg; ly < LH; ly += 16) {
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(A + ly * LP + 4 * g);
+        uint32_t d[(MAX_KH + 3) / 2 + 1];
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[r] = neutral;
+        for (int m = 0; m < (MAX_KH + 3) / 2 + 1; ++m)
+            if (m <= (kw + 3) / 2) d[m] = row[m];
+        for (int k = 0; k < nsp; ++k) {
+            const int j1 = s_sj1[k], j2 = s_sj2[k];
+            uint32_t a0 = DIL ? 0u : 0x00FF00FFu, a1 = a0;
+#pragma unroll
+            for (int kx = 0; kx < MAX_KH; ++kx) {
+                if (kx < j1 || kx >= j2) continue;
+                // pixels (kx, kx+1) and (kx+2, kx+3) relative to column 4g
+                const uint32_t lo = (kx & 1) ? __builtin_amdgcn_alignbyte(d[kx / 2 + 1], d[kx / 2], 2) : d[kx / 2];
+                const uint32_t hi =
+                    (kx & 1) ? __builtin_amdgcn_alignbyte(d[kx / 2 + 2], d[kx / 2 + 1], 2) : d[kx / 2 + 1];
+                a0 = pk_op<DIL>(a0, lo);
+                a1 = pk_op<DIL>(a1, hi);
+            }
+            uint2 *hp = reinterpret_cast<uint2 *>(Hs + (k * LH + ly) * CT_W + 4 * g);
+            *hp = make_uint2(a0, a1);
+        }
+    }
+    __syncthreads();
+    // vertical combine: rows 2*rg, 2*rg+1 of the output tile
     const int kh = st.kh;
+    uint32_t acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) acc[r][0] = acc[r][1] = DIL ? 0u : 0x00FF00FFu;
+    const int yb = 2 * rg;
     for (int ky = 0; ky < kh; ++ky) {
         const int k = s_rspan[ky];
         if (k < 0) continue;
-        const uint8_t *col = Hs + (k * LH + yb + ky) * CT_W + tx;
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-            const int v = col[r * CT_W];
-            acc[r] = DIL ? max(acc[r], v) : min(acc[r], v);
+        for (int r = 0; r < 2; ++r) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(Hs + (k * LH + yb + r + ky) * CT_W + 4 * g);
+            acc[r][0] = pk_op<DIL>(acc[r][0], v.x);
+            acc[r][1] = pk_op<DIL>(acc[r][1], v.y);
         }
     }
     uint8_t *o = out + frame * H * W;
-    const int gx = x0 + tx;
-    if (gx >= W) return;
+    const int gx = x0 + 4 * g;
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
+    for (int r = 0; r < 2; ++r) {
         const int gy = y0 + yb + r;
-        if (gy < H) o[gy * W + gx] = (uint8_t)acc[r];
+        if (gy >= H || gx >= W) continue;
+        const uint32_t packed = (acc[r][0] & 0xFFu) | ((acc[r][0] >> 8) & 0xFF00u) | ((acc[r][1] & 0xFFu) << 16) |
+                                ((acc[r][1] << 8) & 0xFF000000u);
+        if (gx + 4 <= W && (W & 3) == 0) {
+            *reinterpret_cast<uint32_t *>(o + gy * W + gx) = packed;
+        } else {
+            for (int q = 0; q < 4 && gx + q < W; ++q) o[gy * W + gx + q] = (uint8_t)(packed >> (8 * q));
+        }
     }
 }
 
@@ -644,8 +680,8 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
     hipStream_t s = as_stream(stream);
     const int tiles_x = (int)ceil_div(W, CT_W), tiles_y = (int)ceil_div(H, CT_H);
     const dim3 grid(tiles_x * tiles_y, (unsigned)n);
-    const int LW = CT_W + kw - 1, LH = CT_H + kh - 1;
-    const size_t lds = ((size_t)(LH * LW + 15) & ~(size_t)15) + (size_t)std::max(st.nspan, 1) * LH * CT_W;
+    const int LW = CT_W + kw - 1, LH = CT_H + kh - 1, LP = (LW + 7) & ~3;
+    const size_t lds = 2 * ((size_t)LH * LP + (size_t)std::max(st.nspan, 1) * LH * CT_W);
     // pass chain: the last pass writes `out`; ping-pong through the workspace
     const int npass = (median_k ? 1 : 0) + 2 * iters;
     const uint8_t *cur = src;

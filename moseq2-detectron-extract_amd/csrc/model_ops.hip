@@ -482,45 +482,55 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *
 // ---------------------------------------------------------------------------
 // NMS over score-sorted segments
 // ---------------------------------------------------------------------------
-// mask[seg][i][w]: bit j%64 of word w set when IoU(i, j) > thresh, j > i
+// mask[seg][i][w]: bit j%64 of word w set when IoU(i, j) > thresh, j > i.
+// Block = (word w, 256 rows i, segment): the word's 64 j-boxes are staged in
+// LDS once and read as broadcasts; each lane keeps its i-box in registers.
 __global__ __launch_bounds__(256) void k_nms_mask(const float *__restrict__ boxes, const int *__restrict__ kseg,
                                                   int cap, int words, float thresh,
                                                   unsigned long long *__restrict__ mask) {
-    const int seg = blockIdx.y;
+    __shared__ float4 jb[64];
+    const int seg = blockIdx.z, w = blockIdx.x;
     const int k = kseg[seg];
+    const int j0 = w * 64;
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (j0 >= k || blockIdx.y * 256 >= k) return;  // uniform per block
     const float *bx = boxes + (long long)seg * cap * 4;
-    unsigned long long *mk = mask + (long long)seg * cap * words;
-    for (int t = blockIdx.x * 256 + threadIdx.x; t < k * words; t += gridDim.x * 256) {
-        const int i = t / words, w = t - i * words;
-        const float ix1 = bx[4 * i], iy1 = bx[4 * i + 1], ix2 = bx[4 * i + 2], iy2 = bx[4 * i + 3];
-        const float iarea = (ix2 - ix1) * (iy2 - iy1);
-        unsigned long long bits = 0ull;
-        const int j0 = w * 64;
-        for (int jj = 0; jj < 64; ++jj) {
-            const int j = j0 + jj;
-            if (j <= i || j >= k) continue;
-            const float jx1 = bx[4 * j], jy1 = bx[4 * j + 1], jx2 = bx[4 * j + 2], jy2 = bx[4 * j + 3];
-            const float xx1 = fmaxf(ix1, jx1), yy1 = fmaxf(iy1, jy1);
-            const float xx2 = fminf(ix2, jx2), yy2 = fminf(iy2, jy2);
-            const float w_ = fmaxf(0.f, xx2 - xx1), h_ = fmaxf(0.f, yy2 - yy1);
-            const float inter = w_ * h_;
-            const float jarea = (jx2 - jx1) * (jy2 - jy1);
-            const float ovr = inter / (iarea + jarea - inter);
-            if (ovr > thresh) bits |= 1ull << jj;
-        }
-        mk[(long long)i * words + w] = bits;
+    if (threadIdx.x < 64) {
+        const int j = j0 + threadIdx.x;
+        jb[threadIdx.x] = j < k ? *reinterpret_cast<const float4 *>(bx + 4 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    __syncthreads();
+    if (i >= k) return;
+    const float4 ib = *reinterpret_cast<const float4 *>(bx + 4 * i);
+    const float ix1 = ib.x, iy1 = ib.y, ix2 = ib.z, iy2 = ib.w;
+    const float iarea = (ix2 - ix1) * (iy2 - iy1);
+    unsigned long long bits = 0ull;
+    for (int jj = 0; jj < 64; ++jj) {
+        const int j = j0 + jj;
+        if (j <= i || j >= k) continue;
+        const float4 q = jb[jj];
+        const float jx1 = q.x, jy1 = q.y, jx2 = q.z, jy2 = q.w;
+        const float xx1 = fmaxf(ix1, jx1), yy1 = fmaxf(iy1, jy1);
+        const float xx2 = fminf(ix2, jx2), yy2 = fminf(iy2, jy2);
+        const float w_ = fmaxf(0.f, xx2 - xx1), h_ = fmaxf(0.f, yy2 - yy1);
+        const float inter = w_ * h_;
+        const float jarea = (jx2 - jx1) * (jy2 - jy1);
+        const float ovr = inter / (iarea + jarea - inter);
+        if (ovr > thresh) bits |= 1ull << jj;
+    }
+    mask[((long long)seg * cap + i) * words + w] = bits;
 }
 
 // one wave per segment: greedy sweep in score order; invalid boxes never keep
-// nor suppress (Detectron2 removes them before NMS).  Mask rows are staged
-// 64 at a time into LDS so the serial sweep only touches LDS and registers.
+// nor suppress (Detectron2 removes them before NMS).  Per 64-row chunk the
+// sweep is scalar: the chunk's own removed word and every row's word for the
+// chunk are read with v_readlane, so the serial dependency never waits on
+// memory; the kept rows' full masks are OR-ed into `removed` afterwards.
 constexpr int NMS_MAXW = 16;  // pre_topk <= 1024
 __global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, const int *__restrict__ kseg, int cap,
                                                  int words, const unsigned long long *__restrict__ mask,
                                                  int *__restrict__ keep) {
     __shared__ unsigned long long rows[64][NMS_MAXW + 1];
-    __shared__ int vflag[64];
     const int seg = blockIdx.x, lane = threadIdx.x;
     const int k = kseg[seg];
     const int *vl = valid + (long long)seg * cap;
@@ -532,18 +542,31 @@ __global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, 
             const int r = t / words, w = t - r * words;
             rows[r][w] = (i0 + r < k) ? mk[(long long)(i0 + r) * words + w] : 0ull;
         }
-        vflag[lane] = (i0 + lane < k) ? vl[i0 + lane] : 0;
+        const int vf = (i0 + lane < k) ? vl[i0 + lane] : 0;
         __syncthreads();
+        const int cwi = i0 >> 6;
+        const unsigned long long own = rows[lane][cwi];  // row lane's bits inside this chunk
+        const unsigned long long vmask = __ballot(vf != 0);
+        unsigned long long cw = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(removed >> 32), cwi) << 32) |
+                                (unsigned)__builtin_amdgcn_readlane((unsigned)removed, cwi);
+        const unsigned own_lo = (unsigned)own, own_hi = (unsigned)(own >> 32);
         const int nr = k - i0 < 64 ? k - i0 : 64;
-        int okbits_lo = 0;
+        unsigned long long kept = 0ull;
         for (int r = 0; r < nr; ++r) {
-            const int i = i0 + r;
-            const unsigned long long rw = __shfl(removed, i >> 6);
-            const bool ok = !((rw >> (i & 63)) & 1ull) && vflag[r];
-            if (lane == r) okbits_lo = ok ? 1 : 0;
-            if (ok && lane < words) removed |= rows[r][lane];
+            if (((cw >> r) & 1ull) || !((vmask >> r) & 1ull)) continue;
+            kept |= 1ull << r;
+            cw |= ((unsigned long long)__builtin_amdgcn_readlane(own_hi, r) << 32) |
+                  (unsigned)__builtin_amdgcn_readlane(own_lo, r);
         }
-        if (lane < nr) kp[i0 + lane] = okbits_lo;
+        if (lane < words) {
+            unsigned long long kk = kept;
+            while (kk) {
+                const int r = __builtin_ctzll(kk);
+                kk &= kk - 1;
+                removed |= rows[r][lane];
+            }
+        }
+        if (lane < nr) kp[i0 + lane] = (int)((kept >> lane) & 1ull);
         __syncthreads();
     }
     for (int i = k + lane; i < cap; i += 64) kp[i] = 0;
@@ -1134,7 +1157,7 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     unsigned long long *wmask = (unsigned long long *)ws;
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(k_rpn_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
-    hipLaunchKernelGGL(k_nms_mask, dim3((pre_topk * words + 255) / 256, (unsigned)segs), dim3(256), 0, s, wb, wk,
+    hipLaunchKernelGGL(k_nms_mask, dim3(words, (pre_topk + 255) / 256, (unsigned)segs), dim3(256), 0, s, wb, wk,
                        pre_topk, words, nms_thresh, wmask);
     hipLaunchKernelGGL(k_nms_scan, dim3((unsigned)segs), dim3(64), 0, s, wv, wk, pre_topk, words, wmask, wkeep);
     hipLaunchKernelGGL(k_rpn_merge, dim3(B), dim3(1024), 2 * MERGE_MAX * sizeof(unsigned), s, wb, wsc, wkeep, wk, L,
