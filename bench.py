@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run batches back to back on one stream instead of the two-stream pipeline")
     return ap.parse_args()
 
 
@@ -138,7 +140,7 @@ def main():
     from moseq2_detectron_extract_amd import synth
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     from moseq2_detectron_extract_amd.model.runtime import flops_per_image
-    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
 
     B = args.batch
     cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
@@ -151,23 +153,29 @@ def main():
     if world > 1:
         gather_bufs = [torch.empty((B, 2, 80, 80), dtype=torch.uint8, device="cuda") for _ in range(world)]
 
-    def step(i):
-        raw = raw_all[(i % 2) * B:(i % 2) * B + B]
-        r = ex.step_device(raw)
-        if world > 1:
+    pipe = None if args.no_overlap else OverlappedExtractor(ex)
+
+    def deliver(r):
+        if r is not None and world > 1:
             payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
             dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
-        return r
 
-    for i in range(args.warmup):
-        step(i)
+    def run(nsteps, offset):
+        # nsteps batches through the path; with the pipeline the last batch is
+        # flushed inside, so exactly nsteps batches complete
+        for i in range(nsteps):
+            raw = raw_all[((offset + i) % 2) * B:((offset + i) % 2) * B + B]
+            deliver(ex.step_device(raw) if pipe is None else pipe.submit(raw))
+        if pipe is not None:
+            deliver(pipe.flush())
+
+    run(args.warmup, 0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    run(args.steps, args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -215,7 +223,9 @@ def main():
                                    f"R-CNN {args.dtype}, mask NMS, clean, moments, crop), 512x424 int16 frames",
                        "global_batch": B * world, "per_gpu_batch": B, "frame": [424, 512],
                        "model_gflop_per_frame": round(flops_per_image(cfg) / 1e9, 2),
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}",
+                       "streams": "1" if args.no_overlap else "2 (prep/inpaint/clean of batch i+1 beside the model "
+                                                              "of batch i)"},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

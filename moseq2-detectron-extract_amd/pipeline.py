@@ -109,11 +109,67 @@ class GPUExtractor:
         """One pass over a batch with the angle computed on the device
         (clamp_angles_deg(-rad2deg(orientation)), the non-tracking path
         before flip correction).  Used by bench.py; returns the crops."""
+        return self.back(*self.front(raw))
+
+    def front(self, raw: torch.Tensor):
+        """Model-independent head of the path: prep (+inpaint) and clean."""
         prepped = self.prep(raw)
+        cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
+        return prepped, cleaned
+
+    def back(self, prepped: torch.Tensor, cleaned: torch.Tensor):
+        """Model-dependent tail: forward + selection, moments, angle, crops."""
         inf = self.infer(prepped)
-        cleaned, feats = self.features(prepped, inf["d2_mask"])
+        feats = proc.frame_moments(cleaned, inf["d2_mask"], float(self.cfg.frame_threshold))
         ang = -torch.rad2deg(feats["orientation"])
         ang = torch.where(ang < 0, 360 + ang, ang) % 360
         depth, mask = self.crop(prepped, inf["d2_mask"], feats["centroid"], ang)
         return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
                 "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}
+
+
+class OverlappedExtractor:
+    """Two-stream software pipeline over consecutive batches: the front
+    (prep + inpaint + clean, a few wide-grid frame kernels) of batch i+1 runs
+    on its own stream beside the back (model forward, selection, moments,
+    crops) of batch i, so the frame kernels fill the CUs the convolutions
+    leave idle.  Results come out in submission order, one batch behind.
+
+    submit(raw) -> results of the previous batch (None for the first);
+    flush() -> results of the last submitted batch."""
+
+    def __init__(self, extractor: GPUExtractor):
+        self.ex = extractor
+        self.s_front = torch.cuda.Stream()
+        self.s_back = torch.cuda.Stream()
+        self.pending = None
+
+    def submit(self, raw: torch.Tensor):
+        caller = torch.cuda.current_stream()
+        self.s_front.wait_stream(caller)  # raw produced on the caller's stream
+        with torch.cuda.stream(self.s_front):
+            prepped, cleaned = self.ex.front(raw)
+            ready = torch.cuda.Event()
+            ready.record(self.s_front)
+        raw.record_stream(self.s_front)
+        prev, self.pending = self.pending, (prepped, cleaned, ready)
+        return None if prev is None else self._back(prev)
+
+    def flush(self):
+        prev, self.pending = self.pending, None
+        return None if prev is None else self._back(prev)
+
+    def _back(self, item):
+        prepped, cleaned, ready = item
+        caller = torch.cuda.current_stream()
+        self.s_back.wait_event(ready)
+        self.s_back.wait_stream(caller)
+        with torch.cuda.stream(self.s_back):
+            prepped.record_stream(self.s_back)
+            cleaned.record_stream(self.s_back)
+            out = self.ex.back(prepped, cleaned)
+        caller.wait_stream(self.s_back)
+        for v in out.values():
+            v.record_stream(caller)
+        return out
+

@@ -408,3 +408,24 @@ def test_gpu_extractor_step(mdx):
     prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
     c = r["centroid"].cpu().numpy(); a = r["angle"].cpu().numpy()
     np.testing.assert_array_equal(r["depth_frames"].cpu().numpy(), O.crop_and_rotate_frames(prepped, c, a))
+
+
+def test_overlapped_extractor_matches_serial(mdx):
+    """The two-stream pipeline returns, batch for batch, exactly what the
+    one-stream step returns."""
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
+    s = synth.SyntheticSession(12, seed=5)
+    raw = torch.from_numpy(s.frames(0, 12)).cuda()
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
+    batches = [raw[i:i + 4] for i in range(0, 12, 4)]
+    want = [ex.step_device(b) for b in batches]
+    pipe = OverlappedExtractor(ex)
+    got = [r for r in (pipe.submit(b) for b in batches) if r is not None]
+    got.append(pipe.flush())
+    assert len(got) == 3
+    for w, g in zip(want, got):
+        for k in ("depth_frames", "mask_frames", "centroid", "angle", "keypoints"):
+            torch.testing.assert_close(g[k], w[k], rtol=0, atol=0, equal_nan=True)
