@@ -61,8 +61,8 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
         r = orig(self, x, N, H, W, c, relu, out, residual, out_f32, out_mode)
         e1.record(s)
         OH, OW = r[1], r[2]
-        cin_alg = 3 if c is self.stem else c.cin
-        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * c.k * c.k * cin_alg,
+        kalg = c.kalg or c.k * c.k * c.cin
+        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * kalg,
                     (N * OH * OW, c.cout, c.k * c.k * c.cin, c.k, c.stride, out_mode, residual is not None)))
         return r
 
@@ -167,7 +167,8 @@ def main():
             raw = raw_all[((offset + i) % 2) * B:((offset + i) % 2) * B + B]
             deliver(ex.step_device(raw) if pipe is None else pipe.submit(raw))
         if pipe is not None:
-            deliver(pipe.flush())
+            for r in pipe.flush():
+                deliver(r)
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -224,8 +225,8 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "frame": [424, 512],
                        "model_gflop_per_frame": round(flops_per_image(cfg) / 1e9, 2),
                        "parallelism": f"frame-sharded x{world}",
-                       "streams": "1" if args.no_overlap else "2 (prep/inpaint/clean of batch i+1 beside the model "
-                                                              "of batch i)"},
+                       "streams": "1" if args.no_overlap else "3 (prep/inpaint/clean of batch i+2, model + mask "
+                                                              "selection of batch i+1, moments/crop of batch i)"},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

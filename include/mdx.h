@@ -135,6 +135,14 @@ int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const uint8_t lut
                    const float *std_, int C, int Cp, int Hp, int Wp, int dtype, void *out,
                    mdx_stream_t stream);
 
+/* Same preprocessing written space-to-depth for the stride-2 stem:
+ * out (B, Hp/2+1, Wp/2+1, 16): S2D pixel (Y, X) channel (2*dy+dx)*4 + c holds
+ * padded pixel (2Y-1+dy, 2X-1+dx) channel c (c < C <= 4; other slots 0).
+ * The 7x7/s2/p3 stem equals a 4x4/s1/p1 conv over it with weights
+ * W'[o][ty][tx][(2dy+dx)*4+c] = W[o][c][2ty+dy][2tx+dx] (0 where 2ty+dy = 7). */
+int mdx_preprocess_s2d(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], const float *mean,
+                       const float *stdv, int C, int Hp, int Wp, int dtype, void *out, mdx_stream_t stream);
+
 /* max_pool2d(k, s, p), NHWC. */
 int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
                   mdx_stream_t stream);

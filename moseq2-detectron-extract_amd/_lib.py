@@ -44,6 +44,7 @@ SIGNATURES = {
     "mdx_conv2d_splitk": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, I32,
                                 P, I64, P]),
     "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),
+    "mdx_preprocess_s2d": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, P, P]),
     "mdx_maxpool2d": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "mdx_groupnorm_workspace_bytes": (I64, [I32, I32, I32, I32]),
     "mdx_groupnorm": (I32, [P, I32, I32, I32, I32, I32, F32, P, P, P, I32, I32, P, P, P]),

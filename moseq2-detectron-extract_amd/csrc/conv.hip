@@ -469,16 +469,19 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
         for (int j = 0; j < 4; ++j) glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16,
                                            Bs + j * 1024);
     };
+    // K-step order: 64-channel chunk outer, (ky, kx) tap inner -- the KH*KW
+    // consecutive K-steps of one chunk re-read the same input rows, so the
+    // im2col re-reads hit L2 instead of streaming the whole input per tap.
+    // The weight address follows the (ky, kx, ci) packing, so any order works.
     auto advance = [&]() {
-        kglob += 64;
-        kci += 64;
-        if (kci >= a.Cin) {
-            kci = 0;
-            if (++kkx == a.KW) {
-                kkx = 0;
-                ++kky;
+        if (++kkx == a.KW) {
+            kkx = 0;
+            if (++kky == a.KH) {
+                kky = 0;
+                kci += 64;
             }
         }
+        kglob = (kky * a.KW + kkx) * a.Cin + kci;
     };
 
     float4v acc[8][4];

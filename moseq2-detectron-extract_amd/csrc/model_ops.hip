@@ -93,6 +93,34 @@ __global__ __launch_bounds__(256) void k_preprocess(const uint8_t *__restrict__ 
     }
 }
 
+// Space-to-depth form of the same input for the stride-2 7x7 stem: S2D pixel
+// (Y, X) of shape (Hp/2 + 1, Wp/2 + 1, 16) holds padded-image pixels
+// (2Y - 1 + dy, 2X - 1 + dx) in channels (2 dy + dx) * 4 + c (c < C, rest 0);
+// the stem becomes a 4x4 / stride-1 / pad-1 conv over 16 channels
+// (K = 256 instead of 7*7*8 = 392 with 16-B contiguous channel runs).
+template <typename T>
+__global__ __launch_bounds__(256) void k_preprocess_s2d(const uint8_t *__restrict__ fr, int B, int h, int w, int C,
+                                                        int Hs, int Ws, PrepArgs pa, T *__restrict__ out) {
+    const int total = B * Hs * Ws;
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < total; p += gridDim.x * 256) {
+        const int b = p / (Hs * Ws);
+        const int rem = p - b * Hs * Ws;
+        const int Y = rem / Ws, X = rem - Y * Ws;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int y = 2 * Y - 1 + (q >> 1), x = 2 * X - 1 + (q & 1);
+            const bool in = y >= 0 && y < h && x >= 0 && x < w;
+            const float pix = in ? (float)pa.lut[fr[((long long)b * h + y) * w + x]] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[q * 4 + c] = (in && c < C) ? (pix - pa.mean[c]) / pa.stdv[c] : 0.f;
+        }
+        T *o = out + (long long)p * 16;
+        st8(o, v);
+        st8(o + 8, v + 8);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // maxpool NHWC
 // ---------------------------------------------------------------------------
@@ -1064,6 +1092,30 @@ extern "C" int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const 
         hipLaunchKernelGGL(k_preprocess<float>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames, B, h,
                            w, C, Cp, Hp, Wp, pa, (float *)out);
     MDX_CHECK_LAUNCH("mdx_preprocess");
+    return MDX_OK;
+}
+
+extern "C" int mdx_preprocess_s2d(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], const float *mean,
+                                  const float *stdv, int C, int Hp, int Wp, int dtype, void *out, mdx_stream_t stream) {
+    MDX_REQUIRE(frames && lut && mean && stdv && out, "mdx_preprocess_s2d: null pointer");
+    MDX_REQUIRE(C >= 1 && C <= 4 && Hp >= h && Wp >= w && Hp % 2 == 0 && Wp % 2 == 0,
+                "mdx_preprocess_s2d: bad shape (C <= 4, even Hp, Wp)");
+    const int Hs = Hp / 2 + 1, Ws = Wp / 2 + 1;
+    MDX_REQUIRE((long long)B * Hs * Ws * 16 < (1ll << 31), "mdx_preprocess_s2d: too many pixels");
+    PrepArgs pa;
+    for (int i = 0; i < 256; ++i) pa.lut[i] = lut[i];
+    for (int c = 0; c < 4; ++c) {
+        pa.mean[c] = c < C ? mean[c] : 0.f;
+        pa.stdv[c] = c < C ? stdv[c] : 1.f;
+    }
+    const long long total = (long long)B * Hs * Ws;
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_preprocess_s2d<_Float16>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames,
+                           B, h, w, C, Hs, Ws, pa, (_Float16 *)out);
+    else
+        hipLaunchKernelGGL(k_preprocess_s2d<float>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames, B,
+                           h, w, C, Hs, Ws, pa, (float *)out);
+    MDX_CHECK_LAUNCH("mdx_preprocess_s2d");
     return MDX_OK;
 }
 

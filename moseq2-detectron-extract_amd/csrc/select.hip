@@ -13,47 +13,68 @@
 
 namespace mdx {
 
-constexpr int SEL_MAXD = 8;
+constexpr int SEL_MAXD = 8, SEL_THREADS = 1024;
 
-__global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restrict__ masks,
-                                                         const float *__restrict__ scores,
-                                                         const int *__restrict__ ndet,
-                                                         const float *__restrict__ kpts, int D, int K, long long hw,
-                                                         long long plane, float thr, int *__restrict__ keep_idx,
-                                                         int *__restrict__ nkeep, uint8_t *__restrict__ sel_mask,
-                                                         double *__restrict__ sel_kpts) {
+// DM: compile-time bound on the detections per frame, so the per-lane mask
+// words and pair counters are indexed statically and stay in registers
+template <int DM>
+__global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *__restrict__ masks,
+                                                                 const float *__restrict__ scores,
+                                                                 const int *__restrict__ ndet,
+                                                                 const float *__restrict__ kpts, int D, int K,
+                                                                 long long hw, long long plane, float thr,
+                                                                 int *__restrict__ keep_idx, int *__restrict__ nkeep,
+                                                                 uint8_t *__restrict__ sel_mask,
+                                                                 double *__restrict__ sel_kpts) {
     __shared__ unsigned long long s_cnt[SEL_MAXD * SEL_MAXD];
     __shared__ int s_sel;
     const int b = blockIdx.x;
     const int n = ndet[b];
     const uint8_t *mb = masks + (long long)b * D * plane;
-    for (int i = threadIdx.x; i < SEL_MAXD * SEL_MAXD; i += 256) s_cnt[i] = 0;
+    for (int i = threadIdx.x; i < SEL_MAXD * SEL_MAXD; i += SEL_THREADS) s_cnt[i] = 0;
     __syncthreads();
     if (n > 1) {
         // cnt[i][j] (j >= i): |m_i & m_j| ; cnt[i][i] = area_i.  Mask bytes are
         // 0/1, so the popcount of the AND of 16-byte words counts pixels.
-        unsigned long long loc[SEL_MAXD * (SEL_MAXD + 1) / 2];
-        for (int q = 0; q < SEL_MAXD * (SEL_MAXD + 1) / 2; ++q) loc[q] = 0;
+        constexpr int NP = DM * (DM + 1) / 2;
+        unsigned loc[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) loc[q] = 0;
         const long long nv = (plane % 16 == 0) ? hw / 16 : 0;
-        for (long long v = threadIdx.x; v < nv; v += 256) {
-            uint4 w[SEL_MAXD];
-            for (int i = 0; i < n; ++i) w[i] = reinterpret_cast<const uint4 *>(mb + (long long)i * plane)[v];
+        for (long long v = threadIdx.x; v < nv; v += SEL_THREADS) {
+            uint4 w[DM];
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+                w[i] = i < n ? reinterpret_cast<const uint4 *>(mb + (long long)i * plane)[v] : make_uint4(0, 0, 0, 0);
             int q = 0;
-            for (int i = 0; i < n; ++i)
-                for (int j = i; j < n; ++j, ++q)
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+#pragma unroll
+                for (int j = i; j < DM; ++j, ++q)
                     loc[q] += __popc(w[i].x & w[j].x) + __popc(w[i].y & w[j].y) + __popc(w[i].z & w[j].z) +
                               __popc(w[i].w & w[j].w);
         }
-        for (long long p = nv * 16 + threadIdx.x; p < hw; p += 256) {
-            unsigned m[SEL_MAXD];
-            for (int i = 0; i < n; ++i) m[i] = mb[(long long)i * plane + p] != 0;
+        for (long long p = nv * 16 + threadIdx.x; p < hw; p += SEL_THREADS) {
+            unsigned m[DM];
+#pragma unroll
+            for (int i = 0; i < DM; ++i) m[i] = i < n ? (mb[(long long)i * plane + p] != 0) : 0u;
             int q = 0;
-            for (int i = 0; i < n; ++i)
-                for (int j = i; j < n; ++j, ++q) loc[q] += m[i] & m[j];
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+#pragma unroll
+                for (int j = i; j < DM; ++j, ++q) loc[q] += m[i] & m[j];
         }
+        // wave reduction, then one LDS atomic per wave and pair
         int q = 0;
-        for (int i = 0; i < n; ++i)
-            for (int j = i; j < n; ++j, ++q) atomicAdd(&s_cnt[i * SEL_MAXD + j], loc[q]);
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+#pragma unroll
+            for (int j = i; j < DM; ++j, ++q) {
+                unsigned v = loc[q];
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+                if ((threadIdx.x & 63) == 0 && i < n && j < n) atomicAdd(&s_cnt[i * SEL_MAXD + j], (unsigned long long)v);
+            }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -115,7 +136,14 @@ __global__ __launch_bounds__(256) void k_mask_nms_select(const uint8_t *__restri
     const int s = s_sel;
     uint8_t *o = sel_mask + (long long)b * hw;
     const uint8_t *src = s >= 0 ? mb + (long long)s * plane : nullptr;
-    for (long long p = threadIdx.x; p < hw; p += 256) o[p] = src ? src[p] : (uint8_t)0;
+    long long p0 = 0;
+    if (((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        const long long nv = hw / 16;
+        for (long long v = threadIdx.x; v < nv; v += SEL_THREADS)
+            reinterpret_cast<uint4 *>(o)[v] = src ? reinterpret_cast<const uint4 *>(src)[v] : make_uint4(0, 0, 0, 0);
+        p0 = nv * 16;
+    }
+    for (long long p = p0 + threadIdx.x; p < hw; p += SEL_THREADS) o[p] = src ? src[p] : (uint8_t)0;
 }
 
 }  // namespace mdx
@@ -133,8 +161,13 @@ extern "C" int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, c
     MDX_REQUIRE(plane_stride >= hw, "mdx_mask_nms_select: plane_stride < h*w");
     MDX_REQUIRE(plane_stride % 16 != 0 || ((uintptr_t)masks % 16) == 0, "mdx_mask_nms_select: unaligned masks");
     if (B == 0) return MDX_OK;
-    hipLaunchKernelGGL(k_mask_nms_select, dim3(B), dim3(256), 0, as_stream(stream), masks, scores, ndet, kpts, D, K, hw,
-                       (long long)plane_stride, iou_thresh, keep_idx, nkeep, sel_mask, sel_kpts);
+    if (D <= 4)
+        hipLaunchKernelGGL(k_mask_nms_select<4>, dim3(B), dim3(SEL_THREADS), 0, as_stream(stream), masks, scores, ndet,
+                           kpts, D, K, hw, (long long)plane_stride, iou_thresh, keep_idx, nkeep, sel_mask, sel_kpts);
+    else
+        hipLaunchKernelGGL(k_mask_nms_select<SEL_MAXD>, dim3(B), dim3(SEL_THREADS), 0, as_stream(stream), masks, scores,
+                           ndet, kpts, D, K, hw, (long long)plane_stride, iou_thresh, keep_idx, nkeep, sel_mask,
+                           sel_kpts);
     MDX_CHECK_LAUNCH("mdx_mask_nms_select");
     return MDX_OK;
 }

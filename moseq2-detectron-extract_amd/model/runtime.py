@@ -50,6 +50,7 @@ class Conv:
     k: int
     stride: int
     pad: int
+    kalg: int = 0              # algorithmic K (MACs per output) when the packing pads it; 0 = k*k*cin
 
 
 class MaskRCNN:
@@ -92,10 +93,25 @@ class MaskRCNN:
         bias = sd[p + ".norm.bias"] - sd[p + ".norm.running_mean"] * scale
         return self._conv(w * scale.view(-1, 1, 1, 1), bias, stride, pad, cin_pad)
 
+    def _stem_s2d(self, sd, p) -> Conv:
+        """7x7/s2/p3 stem as a 4x4/s1/p1 conv over the space-to-depth input
+        (mdx_preprocess_s2d): W'[o][ty][tx][(2dy+dx)*4+c] = W[o][c][2ty+dy][2tx+dx]."""
+        w = sd[p + ".weight"]
+        scale = sd[p + ".norm.weight"] * (sd[p + ".norm.running_var"] + 1e-5).rsqrt()
+        bias = sd[p + ".norm.bias"] - sd[p + ".norm.running_mean"] * scale
+        w = w * scale.view(-1, 1, 1, 1)
+        cout, cin, kh, kw = w.shape
+        assert kh == 7 and kw == 7 and cin <= 4
+        w8 = torch.zeros(cout, 4, 8, 8)
+        w8[:, :cin, :7, :7] = w
+        # [o][c][ty][dy][tx][dx] -> [o][ty][tx][dy][dx][c]
+        wp = w8.view(cout, 4, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(cout, 4 * 4 * 16)
+        return Conv(self._dev(wp), self._dev(bias, torch.float32), 16, cout, 4, 1, 1, kalg=49 * cin)
+
     def _pack(self, sd):
         cfg = self.cfg
         bu = "backbone.bottom_up"
-        self.stem = self._conv_bn(sd, f"{bu}.stem.conv1", 2, 3, cin_pad=self.vec)
+        self.stem = self._stem_s2d(sd, f"{bu}.stem.conv1")
         self.blocks: List[dict] = []
         for name, nb, _cin, _bott, _cout, stride in resnet_stage_specs(cfg):
             for b in range(nb):
@@ -203,7 +219,7 @@ class MaskRCNN:
 
     def backbone(self, x, B, Hp, Wp):
         cfg = self.cfg
-        y, H, W = self.conv(x, B, Hp, Wp, self.stem, relu=True)
+        y, H, W = self.conv(x, B, Hp // 2 + 1, Wp // 2 + 1, self.stem, relu=True)
         pooled = torch.empty((B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, self.stem.cout), dtype=self.tdt,
                              device=self.device)
         call("mdx_maxpool2d", _p(y), B, H, W, self.stem.cout, 3, 2, 1, self.dcode, _p(pooled), _stream())
@@ -299,13 +315,12 @@ class MaskRCNN:
         B, h, w = frames.shape
         Hp, Wp = self.padded_size(h, w)
         lut = np.arange(256, dtype=np.uint8) if lut is None else np.ascontiguousarray(lut, np.uint8)
-        Cp = self.vec
-        x = torch.empty((B, Hp, Wp, Cp), dtype=self.tdt, device=self.device)
+        x = torch.empty((B, Hp // 2 + 1, Wp // 2 + 1, 16), dtype=self.tdt, device=self.device)
         C = 3 if cfg.input_format == "RGB" else 1
-        call("mdx_preprocess", _p(frames), B, h, w, lut.ctypes.data_as(ctypes.c_void_p),
+        call("mdx_preprocess_s2d", _p(frames), B, h, w, lut.ctypes.data_as(ctypes.c_void_p),
              self.pixel_mean.ctypes.data_as(ctypes.c_void_p), self.pixel_std.ctypes.data_as(ctypes.c_void_p),
-             C, Cp, Hp, Wp, self.dcode, _p(x), _stream())
-        inter = {"input": x} if intermediates else None
+             C, Hp, Wp, self.dcode, _p(x), _stream())
+        inter = {"input": s2d_to_nhwc(x, Hp, Wp)} if intermediates else None
         res, feats = self.backbone(x, B, Hp, Wp)
         if intermediates:
             inter.update({k: v[0] for k, v in res.items()})
@@ -366,6 +381,14 @@ class MaskRCNN:
         if intermediates:
             out["intermediates"] = inter
         return out
+
+
+def s2d_to_nhwc(x: torch.Tensor, Hp: int, Wp: int) -> torch.Tensor:
+    """(B, Hp/2+1, Wp/2+1, 16) space-to-depth input -> (B, Hp, Wp, 4) NHWC."""
+    B = x.shape[0]
+    t = x.view(B, Hp // 2 + 1, Wp // 2 + 1, 2, 2, 4).permute(0, 1, 3, 2, 4, 5)
+    t = t.reshape(B, Hp + 2, Wp + 2, 4)
+    return t[:, 1:Hp + 1, 1:Wp + 1].contiguous()
 
 
 def flops_per_image(cfg: ModelConfig, h: int = 423, w: int = 511, proposals: int = 1000, dets: int = 4) -> float:

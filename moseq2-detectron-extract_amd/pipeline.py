@@ -117,9 +117,8 @@ class GPUExtractor:
         cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
         return prepped, cleaned
 
-    def back(self, prepped: torch.Tensor, cleaned: torch.Tensor):
-        """Model-dependent tail: forward + selection, moments, angle, crops."""
-        inf = self.infer(prepped)
+    def tail(self, prepped: torch.Tensor, cleaned: torch.Tensor, inf: dict):
+        """Moments of the selected mask, angle, crops."""
         feats = proc.frame_moments(cleaned, inf["d2_mask"], float(self.cfg.frame_threshold))
         ang = -torch.rad2deg(feats["orientation"])
         ang = torch.where(ang < 0, 360 + ang, ang) % 360
@@ -127,49 +126,78 @@ class GPUExtractor:
         return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
                 "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}
 
+    def back(self, prepped: torch.Tensor, cleaned: torch.Tensor):
+        """Model-dependent tail: forward + selection, moments, angle, crops."""
+        return self.tail(prepped, cleaned, self.infer(prepped))
+
 
 class OverlappedExtractor:
-    """Two-stream software pipeline over consecutive batches: the front
-    (prep + inpaint + clean, a few wide-grid frame kernels) of batch i+1 runs
-    on its own stream beside the back (model forward, selection, moments,
-    crops) of batch i, so the frame kernels fill the CUs the convolutions
-    leave idle.  Results come out in submission order, one batch behind.
+    """Three-stage software pipeline over consecutive batches, one HIP stream
+    per stage: front (prep + inpaint + clean) of batch i+2, model forward +
+    mask selection of batch i+1 and tail (moments, angle, crops) of batch i
+    run concurrently, so the frame-side kernels (few, latency-bound
+    workgroups) fill the CUs the convolutions leave idle.  Results come out in
+    submission order, two batches behind.
 
-    submit(raw) -> results of the previous batch (None for the first);
-    flush() -> results of the last submitted batch."""
+    submit(raw) -> results of the batch submitted two calls earlier (or None);
+    flush() -> list of the results still in flight."""
 
     def __init__(self, extractor: GPUExtractor):
         self.ex = extractor
         self.s_front = torch.cuda.Stream()
-        self.s_back = torch.cuda.Stream()
-        self.pending = None
+        self.s_model = torch.cuda.Stream()
+        self.s_tail = torch.cuda.Stream()
+        self.fronted = None   # (prepped, cleaned, event) awaiting the model
+        self.modeled = None   # (prepped, cleaned, inf, event) awaiting the tail
 
-    def submit(self, raw: torch.Tensor):
+    def _front(self, raw):
         caller = torch.cuda.current_stream()
         self.s_front.wait_stream(caller)  # raw produced on the caller's stream
         with torch.cuda.stream(self.s_front):
             prepped, cleaned = self.ex.front(raw)
-            ready = torch.cuda.Event()
-            ready.record(self.s_front)
+            ev = torch.cuda.Event()
+            ev.record(self.s_front)
         raw.record_stream(self.s_front)
-        prev, self.pending = self.pending, (prepped, cleaned, ready)
-        return None if prev is None else self._back(prev)
+        return prepped, cleaned, ev
 
-    def flush(self):
-        prev, self.pending = self.pending, None
-        return None if prev is None else self._back(prev)
+    def _model(self, item):
+        prepped, cleaned, ev = item
+        self.s_model.wait_event(ev)
+        with torch.cuda.stream(self.s_model):
+            prepped.record_stream(self.s_model)
+            inf = self.ex.infer(prepped)
+            ev2 = torch.cuda.Event()
+            ev2.record(self.s_model)
+        return prepped, cleaned, inf, ev2
 
-    def _back(self, item):
-        prepped, cleaned, ready = item
+    def _tail(self, item):
+        prepped, cleaned, inf, ev = item
         caller = torch.cuda.current_stream()
-        self.s_back.wait_event(ready)
-        self.s_back.wait_stream(caller)
-        with torch.cuda.stream(self.s_back):
-            prepped.record_stream(self.s_back)
-            cleaned.record_stream(self.s_back)
-            out = self.ex.back(prepped, cleaned)
-        caller.wait_stream(self.s_back)
+        self.s_tail.wait_event(ev)
+        with torch.cuda.stream(self.s_tail):
+            for t in (prepped, cleaned, *[v for v in inf.values() if torch.is_tensor(v)]):
+                t.record_stream(self.s_tail)
+            out = self.ex.tail(prepped, cleaned, inf)
+        caller.wait_stream(self.s_tail)
         for v in out.values():
             v.record_stream(caller)
         return out
 
+    def submit(self, raw: torch.Tensor):
+        # issue order tail(i-2), model(i-1), front(i): each stage's inputs were
+        # issued a call earlier, so all three run concurrently on the device
+        out = self._tail(self.modeled) if self.modeled is not None else None
+        self.modeled = self._model(self.fronted) if self.fronted is not None else None
+        self.fronted = self._front(raw)
+        return out
+
+    def flush(self):
+        outs = []
+        if self.modeled is not None:
+            outs.append(self._tail(self.modeled))
+        self.modeled = self._model(self.fronted) if self.fronted is not None else None
+        self.fronted = None
+        if self.modeled is not None:
+            outs.append(self._tail(self.modeled))
+        self.modeled = None
+        return outs

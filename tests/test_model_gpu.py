@@ -424,7 +424,7 @@ def test_overlapped_extractor_matches_serial(mdx):
     want = [ex.step_device(b) for b in batches]
     pipe = OverlappedExtractor(ex)
     got = [r for r in (pipe.submit(b) for b in batches) if r is not None]
-    got.append(pipe.flush())
+    got.extend(pipe.flush())
     assert len(got) == 3
     for w, g in zip(want, got):
         for k in ("depth_frames", "mask_frames", "centroid", "angle", "keypoints"):
