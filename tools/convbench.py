@@ -21,6 +21,7 @@ SHAPES = [
 
 
 def main():
+    only = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else None
     import torch
     import mdx_pkg
     mdx_pkg.load()
@@ -39,7 +40,9 @@ def main():
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 10
     print(f"torch copy 256 MiB: {t * 1e3:.1f} us = {2 * (256 << 20) / t / 1e9:.2f} TB/s (read+write)")
-    for (N, H, W, Cin, Cout, k, s, p, res) in SHAPES:
+    for si, (N, H, W, Cin, Cout, k, s, p, res) in enumerate(SHAPES):
+        if only is not None and si not in only:
+            continue
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N, H, W, Cin, device="cuda").half()
         w = (torch.randn(Cout, k * k * Cin, device="cuda") / (k * k * Cin) ** 0.5).half()
