@@ -38,7 +38,7 @@ struct Prec<float> {
 
 constexpr int BM = 128, BN = 128, CONV_THREADS = 256;
 constexpr int ROWB = 128;          // bytes of K per LDS row
-constexpr int PITCH = ROWB + 16;   // padded row pitch (bytes)
+constexpr int PITCH = ROWB;        // row pitch (bytes); 16-B pieces XOR-swizzled by (row >> 1) & 7
 constexpr int TILE_BYTES = BM * PITCH;
 
 template <typename TO>
@@ -267,13 +267,17 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             }
         }
     };
+    // piece kc of row R lives at physical piece kc ^ ((R >> 1) & 7): the
+    // fragment reads (rows l & 15, pieces 4 s + (l >> 4)) are then
+    // bank-conflict-free for every ds_read_b128 lane group
+    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;  // (lrow + 32 i) >> 1 & 7 == lrow >> 1 & 7
     auto store_lds = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(As + buf * A_TILE + (lrow + 32 * i) * PITCH + kc * 16) = ra[i];
+            *reinterpret_cast<uint4 *>(As + buf * A_TILE + (lrow + 32 * i) * PITCH + wpiece) = ra[i];
 #pragma unroll
         for (int i = 0; i < BLOADS; ++i)
-            *reinterpret_cast<uint4 *>(Bs + buf * B_TILE + (lrow + 32 * i) * PITCH + kc * 16) = rb[i];
+            *reinterpret_cast<uint4 *>(Bs + buf * B_TILE + (lrow + 32 * i) * PITCH + wpiece) = rb[i];
     };
 
     float4v acc[TI][TJ];
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         const char *Bb = Bs + cur * B_TILE + (wn * (BN_ / 2) + (lane & 15)) * PITCH;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            const int koff = s * 64 + (lane >> 4) * 16;
+            const int koff = ((4 * s + (lane >> 4)) ^ ((lane & 15) >> 1)) * 16;
             if constexpr (sizeof(T) == 2) {
                 half8 af[TI], bf[TJ];
 #pragma unroll
@@ -394,18 +398,22 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 // Large-layer kernel (fp16, Cin % 64 == 0): 256x256 tile, 512 threads = 8
 // waves as 2(M) x 4(N), each wave 128x64 = 8x4 MFMA 16x16x32 tiles.  Both
 // operands are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
-// VGPR round trip), two 64 KiB stages, the next K-step's DMA in flight while
-// the current one is multiplied (counted vmcnt + raw s_barrier).  A K-step of
-// 64 halves lies inside one (ky, kx) tap because Cin % 64 == 0, so the
-// implicit-im2col source of each 16-B chunk is a plain per-row offset.
-// LDS image: row r (128 B) holds logical 16-B chunk c at physical chunk
-// c ^ ((r >> 1) & 7) (lane-linear DMA destination, swizzle applied on the
-// global source address); the fragment reads are then bank-conflict-free.
+// VGPR round trip) in K-substeps of 32 halves (A 256 x 64 B + B 256 x 64 B =
+// 32 KiB), four substep buffers, three substeps in flight ahead of the one
+// being multiplied (counted vmcnt + raw s_barrier, one barrier per substep).
+// A 64-half chunk of K lies inside one (ky, kx) tap because Cin % 64 == 0, so
+// the implicit-im2col source of each 16-B piece is a plain per-row offset;
+// chunks are visited channel-chunk outer, tap inner (input rows re-read from
+// L2 across the taps).  LDS image: row r (64 B) holds logical 16-B piece c at
+// physical piece c ^ (((r >> 3) & 1) << 1) -- lane-linear DMA destination, the
+// swizzle is applied on the global source address; fragment reads are then
+// bank-conflict-free for the ds_read_b128 lane groups.
 // ---------------------------------------------------------------------------
 constexpr int G_BM = 256, G_BN = 256, G_THREADS = 512;
-constexpr int G_STAGE = (G_BM + G_BN) * 128;  // bytes per K-step stage
-constexpr int G_EPI_PITCH = 68;               // fp32 pitch of a wave's 64x64 staging block
-constexpr int G_LDS = (2 * G_STAGE > 8 * 64 * G_EPI_PITCH * 4) ? 2 * G_STAGE : 8 * 64 * G_EPI_PITCH * 4;
+constexpr int G_SUB = (G_BM + G_BN) * 64;  // bytes per 32-deep K-substep
+constexpr int G_NBUF = 4;
+constexpr int G_EPI_PITCH = 68;            // fp32 pitch of a wave's 64x64 staging block
+constexpr int G_LDS = (G_NBUF * G_SUB > 8 * 64 * G_EPI_PITCH * 4) ? G_NBUF * G_SUB : 8 * 64 * G_EPI_PITCH * 4;
 
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];  // zero source for padding / out-of-range rows
 
@@ -414,6 +422,8 @@ typedef __attribute__((address_space(3))) void *lds_ptr_t;
 __device__ __forceinline__ void glds16(const void *src, char *dst) {
     __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)dst, 16, 0, 0);
 }
+
+__device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 
 template <typename TO>
 __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
@@ -429,19 +439,18 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 2, wn = wid & 3;
 
-    // DMA descriptors: instruction j of wave w fills rows 32w + 8j .. +8
+    // DMA descriptors: instruction j of wave w fills LDS rows 32w + 16j .. +16
     const _Float16 *X = reinterpret_cast<const _Float16 *>(a.x);
     const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
     const int ohw = a.OH * a.OW;
-    int a_iy0[4], a_ix0[4], a_c[4];
-    long long a_base[4];
-    bool a_ok[4];
-    const _Float16 *b_src[4];
+    int a_iy0[2], a_ix0[2];
+    long long a_base[2];
+    bool a_ok[2];
+    const _Float16 *b_src[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int r = 32 * wid + 8 * j + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        a_c[j] = c * 8;
+    for (int j = 0; j < 2; ++j) {
+        const int r = 32 * wid + 16 * j + (lane >> 2);
+        const int c = (lane & 3) ^ g_swz(r);
         const int gm = m0 + r;
         a_ok[j] = gm < a.M;
         const int gmc = a_ok[j] ? gm : 0;
@@ -453,35 +462,35 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
         const int gn = n0 + r;
         b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * 8 : nullptr;
     }
-    int kglob = 0, kci = 0, kkx = 0, kky = 0;  // uniform: K-step start and its tap
-    auto issue = [&](int stage) {
-        char *As = smem + stage * G_STAGE + 32 * wid * 128;
-        char *Bs = smem + stage * G_STAGE + G_BM * 128 + 32 * wid * 128;
+    // issue state (uniform): the 64-chunk being issued and its tap
+    int i_kci = 0, i_kkx = 0, i_kky = 0, i_half = 0;
+    auto issue = [&](int buf) {
+        const int kofs = i_kci + 32 * i_half;
+        const int kglob = (i_kky * a.KW + i_kkx) * a.Cin + kofs;
+        char *As = smem + buf * G_SUB + 32 * wid * 64;
+        char *Bs = smem + buf * G_SUB + G_BM * 64 + 32 * wid * 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int iy = a_iy0[j] + kky, ix = a_ix0[j] + kkx;
-            const void *src = g_zero16;
-            if (a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                src = X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kci;
+        for (int j = 0; j < 2; ++j) {
+            const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
+            const bool ok = a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const void *src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kofs)
+                                 : (const void *)g_zero16;
             glds16(src, As + j * 1024);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16,
-                                           Bs + j * 1024);
-    };
-    // K-step order: 64-channel chunk outer, (ky, kx) tap inner -- the KH*KW
-    // consecutive K-steps of one chunk re-read the same input rows, so the
-    // im2col re-reads hit L2 instead of streaming the whole input per tap.
-    // The weight address follows the (ky, kx, ci) packing, so any order works.
-    auto advance = [&]() {
-        if (++kkx == a.KW) {
-            kkx = 0;
-            if (++kky == a.KH) {
-                kky = 0;
-                kci += 64;
+        for (int j = 0; j < 2; ++j)
+            glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16, Bs + j * 1024);
+        // next substep: half, then tap, then channel chunk
+        if (++i_half == 2) {
+            i_half = 0;
+            if (++i_kkx == a.KW) {
+                i_kkx = 0;
+                if (++i_kky == a.KH) {
+                    i_kky = 0;
+                    i_kci += 64;
+                }
             }
         }
-        kglob = (kky * a.KW + kkx) * a.Cin + kci;
     };
 
     float4v acc[8][4];
@@ -490,39 +499,40 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = a.K / 64;
-    const int swz = ((lane & 15) >> 1);  // (row >> 1) & 7 of every fragment row this lane reads
+    const int T = a.K / 32;  // substeps
+    // fragment rows of this lane: r = 16 i + (lane & 15) (+ multiples of 64)
+    const int off = ((lane >> 4) ^ g_swz(lane & 15)) * 16;
     issue(0);
-    advance();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) {
-            issue(cur ^ 1);
-            advance();
+    if (T > 1) issue(1);
+    if (T > 2) issue(2);
+    for (int t = 0; t < T; ++t) {
+        // substeps issued after t: min(T - 1, t + 2) - t, four DMAs each
+        const int ahead = (T - 1 - t) < 2 ? (T - 1 - t) : 2;
+        if (ahead == 2)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
+        else if (ahead == 1)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        const char *Ab = smem + cur * G_STAGE + (wm * 128 + (lane & 15)) * 128;
-        const char *Bb = smem + cur * G_STAGE + G_BM * 128 + (wn * 64 + (lane & 15)) * 128;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int off = ((4 * s + (lane >> 4)) ^ swz) * 16;
-            half8 bf[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 128 + off);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const half8 af = *reinterpret_cast<const half8 *>(Ab + i * 16 * 128 + off);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
-            }
-        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        // buffer (t + 3) % 4 was read in substep t - 1, which every wave has finished
+        if (t + 3 < T) issue((t + 3) & 3);
+        const char *Ab = smem + (t & 3) * G_SUB + (wm * 128 + (lane & 15)) * 64 + off;
+        const char *Bb = smem + (t & 3) * G_SUB + G_BM * 64 + (wn * 64 + (lane & 15)) * 64 + off;
+        half8 bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const half8 af = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+        }
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 
     // epilogue: per wave, two passes of 64 rows x 64 cols through its own LDS block
     float *Cs = reinterpret_cast<float *>(smem) + wid * 64 * G_EPI_PITCH;

@@ -699,7 +699,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
                                                    const int *__restrict__ counts, T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;
-    const int r = blockIdx.x;
+    // XCD-contiguous ROI ranges: the ROIs of one image (which share its
+    // feature maps) are pooled by the CUs of one XCD / one L2
+    int r;
+    {
+        const int L = blockIdx.x, nwg = gridDim.x;
+        const int q = nwg / 8, rr = nwg % 8, xcd = L % 8;
+        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + L / 8;
+    }
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
     const int CG = C / V;
