@@ -502,35 +502,66 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
     const int T = a.K / 32;  // substeps
     // fragment rows of this lane: r = 16 i + (lane & 15) (+ multiples of 64)
     const int off = ((lane >> 4) ^ g_swz(lane & 15)) * 16;
-    issue(0);
-    if (T > 1) issue(1);
-    if (T > 2) issue(2);
-    for (int t = 0; t < T; ++t) {
-        // substeps issued after t: min(T - 1, t + 2) - t, four DMAs each
-        const int ahead = (T - 1 - t) < 2 ? (T - 1 - t) : 2;
-        if (ahead == 2)
+    const char *Abase = smem + (wm * 128 + (lane & 15)) * 64 + off;
+    const char *Bbase = smem + G_BM * 64 + (wn * 64 + (lane & 15)) * 64 + off;
+    // fragments are register double-buffered: the LDS reads of substep t+1
+    // are in flight while the 32 MFMAs of substep t run from registers
+    half8 fa[2][8], fb[2][4];
+    auto read_frags = [&](int t, int set) {
+        const char *Ab = Abase + (t & 3) * G_SUB;
+        const char *Bb = Bbase + (t & 3) * G_SUB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[set][j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
+    };
+    auto mma = [&](int set) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+    };
+    // wait until substep u has landed (DMAs issued for substeps <= min(T-1, u+2)... counted per thread)
+    auto wait_landed = [&](int u, int issued_upto) {
+        const int ahead = issued_upto - u;
+        if (ahead >= 2)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else if (ahead == 1)
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        // buffer (t + 3) % 4 was read in substep t - 1, which every wave has finished
-        if (t + 3 < T) issue((t + 3) & 3);
-        const char *Ab = smem + (t & 3) * G_SUB + (wm * 128 + (lane & 15)) * 64 + off;
-        const char *Bb = smem + (t & 3) * G_SUB + G_BM * 64 + (wn * 64 + (lane & 15)) * 64 + off;
-        half8 bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const half8 af = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+    };
+    issue(0);
+    if (T > 1) issue(1);
+    if (T > 2) issue(2);
+    int issued = T < 3 ? T - 1 : 2;
+    wait_landed(0, issued);
+    __builtin_amdgcn_s_barrier();
+    read_frags(0, 0);
+    // iteration t: [wait t+1, barrier, DMA t+3, read frags t+1] then MFMAs of t
+    auto step = [&](int t, int cur) {
+        if (t + 1 < T) {
+            wait_landed(t + 1, issued);
+            // drain this wave's pending fragment reads (those of substep t)
+            // before the barrier: after it no wave still reads buffer
+            // (t + 3) & 3 == (t - 1) & 3, which the next DMA overwrites
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (t + 3 < T) {
+                issue((t + 3) & 3);
+                issued = t + 3;
+            }
+            read_frags(t + 1, cur ^ 1);
         }
+        mma(cur);
+    };
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+        step(t, 0);
+        step(t + 1, 1);
     }
+    if (t < T) step(t, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
