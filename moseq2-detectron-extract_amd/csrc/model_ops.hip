@@ -694,28 +694,14 @@ __device__ __forceinline__ void st16(T *p, const float *v) {
     *reinterpret_cast<uint4 *>(p) = u;
 }
 
-// one block per ROI; one lane per (bin, 16-byte channel group)
-template <typename T>
-__global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
-                                                   const int *__restrict__ counts, T *__restrict__ out) {
-    constexpr int V = Vec16<T>::N;
-    // XCD-contiguous ROI ranges: the ROIs of one image (which share its
-    // feature maps) are pooled by the CUs of one XCD / one L2
-    int r;
-    {
-        const int L = blockIdx.x, nwg = gridDim.x;
-        const int q = nwg / 8, rr = nwg % 8, xcd = L % 8;
-        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + L / 8;
-    }
-    const int b = r / rl.per_image, ri = r - b * rl.per_image;
-    const int C = rl.C, P = rl.P;
-    const int CG = C / V;
-    T *o = out + (long long)r * P * P * C;
-    if (ri >= counts[b]) {
-        const float z[V] = {};
-        for (int i = threadIdx.x; i < P * P * CG; i += 256) st16(o + (long long)i * V, z);
-        return;
-    }
+// ROIAlign sample geometry of one ROI (ROIAlignV2 / ROIPooler semantics)
+struct RoiGeom {
+    const void *feat;  // level map of this ROI's image
+    int H, W, gh, gw;
+    float rsw, rsh, bh, bw, count;
+};
+
+__device__ __forceinline__ RoiGeom roi_geom(const RoiLevels &rl, const float *rois, int r, int b, size_t esize) {
     const float x1 = rois[4 * r], y1 = rois[4 * r + 1], x2 = rois[4 * r + 2], y2 = rois[4 * r + 3];
     // level assignment (assign_boxes_to_levels)
     const float area = (x2 - x1) * (y2 - y1);
@@ -724,61 +710,151 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     const float maxl = (float)(rl.min_level + rl.L - 1);
     lv = lv < (float)rl.min_level ? (float)rl.min_level : (lv > maxl ? maxl : lv);
     const int li = (int)lv - rl.min_level;
-    const T *f = reinterpret_cast<const T *>(rl.feat[li]) + (long long)b * rl.H[li] * rl.W[li] * C;
-    const int H = rl.H[li], W = rl.W[li];
+    RoiGeom g;
+    g.H = rl.H[li];
+    g.W = rl.W[li];
+    g.feat = reinterpret_cast<const char *>(rl.feat[li]) + (size_t)b * g.H * g.W * rl.C * esize;
     const float sc = rl.scale[li];
     const float off = rl.aligned ? 0.5f : 0.f;
-    const float rsw = x1 * sc - off, rsh = y1 * sc - off;
+    g.rsw = x1 * sc - off;
+    g.rsh = y1 * sc - off;
     const float rew = x2 * sc - off, reh = y2 * sc - off;
-    float rw = rew - rsw, rh = reh - rsh;
+    float rw = rew - g.rsw, rh = reh - g.rsh;
     if (!rl.aligned) {
         rw = fmaxf(rw, 1.f);
         rh = fmaxf(rh, 1.f);
     }
-    const float bh = rh / (float)P, bw = rw / (float)P;
-    const int gh = rl.sampling > 0 ? rl.sampling : (int)ceilf(rh / (float)P);
-    const int gw = rl.sampling > 0 ? rl.sampling : (int)ceilf(rw / (float)P);
-    const float count = (float)max(gh * gw, 1);
-    for (int t = threadIdx.x; t < P * P * CG; t += 256) {
-        const int cg = t % CG;
-        const int bin = t / CG;
+    const int P = rl.P;
+    g.bh = rh / (float)P;
+    g.bw = rw / (float)P;
+    g.gh = rl.sampling > 0 ? rl.sampling : (int)ceilf(rh / (float)P);
+    g.gw = rl.sampling > 0 ? rl.sampling : (int)ceilf(rw / (float)P);
+    g.count = (float)max(g.gh * g.gw, 1);
+    return g;
+}
+
+// bilinear taps of one sample coordinate along one axis (roi_align_forward's
+// bilinear_interpolate): returns false when the sample is outside (-1, size]
+__device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, float &l) {
+    if (!(v >= -1.0f && v <= (float)size)) return false;  // (also rejects NaN)
+    float vv = v <= 0.f ? 0.f : v;
+    lo = (int)vv;
+    if (lo >= size - 1) {
+        hi = lo = size - 1;
+        vv = (float)lo;
+    } else {
+        hi = lo + 1;
+    }
+    l = vv - (float)lo;
+    return true;
+}
+
+// Grid (ROI, 128-byte channel slice).  The ROI's sample window of the slice
+// is staged in LDS with 16-B loads (every feature pixel fetched once per ROI
+// instead of once per tap of every sample), then every (bin, 16-B group)
+// lane interpolates from LDS.  Windows above ROI_LDS_PX pixels (very
+// elongated proposals) read their taps straight from global memory.
+// Arithmetic (sample positions, weights, accumulation order) is the
+// per-sample formula of the reference kernel in both paths.
+constexpr int ROI_SLICE_B = 128, ROI_LDS_PX = 448;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
+                                                   const int *__restrict__ counts, T *__restrict__ out) {
+    constexpr int V = Vec16<T>::N;          // channels per 16-B group
+    constexpr int SL = ROI_SLICE_B / sizeof(T);  // channels per slice
+    constexpr int G = SL / V;               // 16-B groups per slice (8)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
+    int r;
+    {
+        const int Lb = blockIdx.x, nwg = gridDim.x;
+        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
+        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
+    }
+    const int slice = blockIdx.y;
+    const int b = r / rl.per_image, ri = r - b * rl.per_image;
+    const int C = rl.C, P = rl.P;
+    const int c0 = slice * SL;
+    T *o = out + (long long)r * P * P * C + c0;
+    const int nitems = P * P * G;
+    if (ri >= counts[b]) {
+        const float z[V] = {};
+        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)(i / G) * C + (i % G) * V, z);
+        return;
+    }
+    const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
+    const T *f = reinterpret_cast<const T *>(g.feat) + c0;
+    // window of feature rows / cols the samples touch (sample coordinates are
+    // monotonic in (bin, sub-sample))
+    int ylo = 0, yhi = -1, xlo = 0, xhi = -1;
+    {
+        int lo, hi;
+        float l;
+        const float yf = g.rsh + 0.f * g.bh + (0.f + .5f) * g.bh / (float)g.gh;
+        const float yl_ = g.rsh + (float)(P - 1) * g.bh + ((float)(g.gh - 1) + .5f) * g.bh / (float)g.gh;
+        const float xf = g.rsw + 0.f * g.bw + (0.f + .5f) * g.bw / (float)g.gw;
+        const float xl_ = g.rsw + (float)(P - 1) * g.bw + ((float)(g.gw - 1) + .5f) * g.bw / (float)g.gw;
+        // clamp both ends into the map; outside samples are skipped later
+        const float y0c = fminf(fmaxf(yf, 0.f), (float)g.H), y1c = fminf(fmaxf(yl_, 0.f), (float)g.H);
+        const float x0c = fminf(fmaxf(xf, 0.f), (float)g.W), x1c = fminf(fmaxf(xl_, 0.f), (float)g.W);
+        if (roi_axis(y0c, g.H, lo, hi, l)) ylo = lo;
+        if (roi_axis(y1c, g.H, lo, hi, l)) yhi = hi;
+        if (roi_axis(x0c, g.W, lo, hi, l)) xlo = lo;
+        if (roi_axis(x1c, g.W, lo, hi, l)) xhi = hi;
+    }
+    const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
+    const bool staged = g.gh > 0 && g.gw > 0 && wh > 0 && ww > 0 && wh * ww <= ROI_LDS_PX;
+    if (staged) {
+        const int npx = wh * ww;
+        for (int i = threadIdx.x; i < npx * G; i += 256) {
+            const int px = i / G, cg = i - px * G;
+            const int py = px / ww, pxx = px - py * ww;
+            *reinterpret_cast<uint4 *>(smem + px * ROI_SLICE_B + cg * 16) =
+                *reinterpret_cast<const uint4 *>(f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V);
+        }
+        __syncthreads();
+    }
+    for (int t = threadIdx.x; t < nitems; t += 256) {
+        const int cg = t % G;
+        const int bin = t / G;
         const int ph = bin / P, pw = bin - ph * P;
-        const int c0 = cg * V;
         float acc[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = 0.f;
-        for (int iy = 0; iy < gh; ++iy) {
-            const float y = rsh + (float)ph * bh + ((float)iy + .5f) * bh / (float)gh;
-            for (int ix = 0; ix < gw; ++ix) {
-                const float x = rsw + (float)pw * bw + ((float)ix + .5f) * bw / (float)gw;
-                if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) continue;
-                float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
-                int yl = (int)yy, xl = (int)xx, yh, xh;
-                if (yl >= H - 1) {
-                    yh = yl = H - 1;
-                    yy = (float)yl;
-                } else
-                    yh = yl + 1;
-                if (xl >= W - 1) {
-                    xh = xl = W - 1;
-                    xx = (float)xl;
-                } else
-                    xh = xl + 1;
-                const float ly = yy - (float)yl, lx = xx - (float)xl;
+        for (int iy = 0; iy < g.gh; ++iy) {
+            const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+            int yl, yh;
+            float ly;
+            if (!roi_axis(y, g.H, yl, yh, ly)) continue;
+            for (int ix = 0; ix < g.gw; ++ix) {
+                const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+                int xl, xh;
+                float lx;
+                if (!roi_axis(x, g.W, xl, xh, lx)) continue;
                 const float hy = 1.f - ly, hx = 1.f - lx;
                 const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
                 float v1[V], v2[V], v3[V], v4[V];
-                ld16(f + ((long long)yl * W + xl) * C + c0, v1);
-                ld16(f + ((long long)yl * W + xh) * C + c0, v2);
-                ld16(f + ((long long)yh * W + xl) * C + c0, v3);
-                ld16(f + ((long long)yh * W + xh) * C + c0, v4);
+                if (staged) {
+                    const char *s0 = smem + cg * 16;
+                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xl - xlo) * ROI_SLICE_B), v1);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xh - xlo) * ROI_SLICE_B), v2);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xl - xlo) * ROI_SLICE_B), v3);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xh - xlo) * ROI_SLICE_B), v4);
+                } else {
+                    const T *fc = f + cg * V;
+                    ld16(fc + ((long long)yl * g.W + xl) * C, v1);
+                    ld16(fc + ((long long)yl * g.W + xh) * C, v2);
+                    ld16(fc + ((long long)yh * g.W + xl) * C, v3);
+                    ld16(fc + ((long long)yh * g.W + xh) * C, v4);
+                }
 #pragma unroll
                 for (int i = 0; i < V; ++i) acc[i] += w1 * v1[i] + w2 * v2[i] + w3 * v3[i] + w4 * v4[i];
             }
         }
 #pragma unroll
-        for (int i = 0; i < V; ++i) acc[i] = acc[i] / count;
-        st16(o + (long long)bin * C + c0, acc);
+        for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+        st16(o + (long long)bin * C + cg * V, acc);
     }
 }
 
@@ -1231,7 +1307,7 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
                              void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
-    MDX_REQUIRE(C % (dtype == 1 ? 8 : 4) == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
+    MDX_REQUIRE(C % (dtype == 1 ? 64 : 32) == 0, "mdx_roi_align: C must be a multiple of 128 bytes of channels");
     if (R == 0) return MDX_OK;
     RoiLevels rl{};
     for (int l = 0; l < L; ++l) {
@@ -1243,11 +1319,11 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     if (dtype == 1)
-        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                           (_Float16 *)out);
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (ROI_SLICE_B / 2)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
+                           as_stream(stream), rl, rois, counts, (_Float16 *)out);
     else
-        hipLaunchKernelGGL(k_roi_align<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                           (float *)out);
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (ROI_SLICE_B / 4)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
+                           as_stream(stream), rl, rois, counts, (float *)out);
     MDX_CHECK_LAUNCH("mdx_roi_align");
     return MDX_OK;
 }
