@@ -760,10 +760,11 @@ constexpr int ROI_SLICE_B = 128, ROI_LDS_PX = 448;
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
-                                                   const int *__restrict__ counts, T *__restrict__ out) {
+                                                   const int *__restrict__ counts, int gslice, T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;          // channels per 16-B group
-    constexpr int SL = ROI_SLICE_B / sizeof(T);  // channels per slice
-    constexpr int G = SL / V;               // 16-B groups per slice (8)
+    const int G = gslice;                   // 16-B groups per slice (8, fewer for narrow maps)
+    const int SL = G * V;                   // channels per slice
+    const int PXB = G * 16;                 // LDS bytes per staged pixel
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
     int r;
@@ -810,7 +811,7 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
         for (int i = threadIdx.x; i < npx * G; i += 256) {
             const int px = i / G, cg = i - px * G;
             const int py = px / ww, pxx = px - py * ww;
-            *reinterpret_cast<uint4 *>(smem + px * ROI_SLICE_B + cg * 16) =
+            *reinterpret_cast<uint4 *>(smem + px * PXB + cg * 16) =
                 *reinterpret_cast<const uint4 *>(f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V);
         }
         __syncthreads();
@@ -837,10 +838,10 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
                 float v1[V], v2[V], v3[V], v4[V];
                 if (staged) {
                     const char *s0 = smem + cg * 16;
-                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xl - xlo) * ROI_SLICE_B), v1);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xh - xlo) * ROI_SLICE_B), v2);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xl - xlo) * ROI_SLICE_B), v3);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xh - xlo) * ROI_SLICE_B), v4);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xl - xlo) * PXB), v1);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xh - xlo) * PXB), v2);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xl - xlo) * PXB), v3);
+                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xh - xlo) * PXB), v4);
                 } else {
                     const T *fc = f + cg * V;
                     ld16(fc + ((long long)yl * g.W + xl) * C, v1);
@@ -1307,7 +1308,11 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
                              void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
-    MDX_REQUIRE(C % (dtype == 1 ? 64 : 32) == 0, "mdx_roi_align: C must be a multiple of 128 bytes of channels");
+    const int vch = dtype == 1 ? 8 : 4;  // channels per 16 B
+    MDX_REQUIRE(C % vch == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
+    // channel slice of up to 128 B (8 groups of 16 B) that divides C
+    int gslice = 8;
+    while (gslice > 1 && (C / vch) % gslice) gslice >>= 1;
     if (R == 0) return MDX_OK;
     RoiLevels rl{};
     for (int l = 0; l < L; ++l) {
@@ -1319,11 +1324,11 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     if (dtype == 1)
-        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (ROI_SLICE_B / 2)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
-                           as_stream(stream), rl, rois, counts, (_Float16 *)out);
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * 8)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
+                           as_stream(stream), rl, rois, counts, gslice, (_Float16 *)out);
     else
-        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (ROI_SLICE_B / 4)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
-                           as_stream(stream), rl, rois, counts, (float *)out);
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (gslice * 4)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
+                           as_stream(stream), rl, rois, counts, gslice, (float *)out);
     MDX_CHECK_LAUNCH("mdx_roi_align");
     return MDX_OK;
 }

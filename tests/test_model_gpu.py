@@ -201,14 +201,15 @@ def test_rpn_proposals_from_identical_heads(mdx):
         torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
 
 
-def test_roi_align_matches_oracle(mdx, rt):
+@pytest.mark.parametrize("C", [16, 64])
+def test_roi_align_matches_oracle(mdx, rt, C):
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
     from oracle import model_ref as R
     cfg = ModelConfig()
     g = torch.Generator().manual_seed(5)
-    B, C = 2, 16
+    B = 2
     sizes = {2: (28, 32), 3: (14, 16), 4: (7, 8), 5: (4, 4)}
     feats = {f"p{l}": torch.randn(B, C, *s, generator=g) for l, s in sizes.items()}
     per = 40
