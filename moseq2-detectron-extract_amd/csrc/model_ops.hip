@@ -756,11 +756,13 @@ __device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, fl
 // elongated proposals) read their taps straight from global memory.
 // Arithmetic (sample positions, weights, accumulation order) is the
 // per-sample formula of the reference kernel in both paths.
-constexpr int ROI_SLICE_B = 128, ROI_LDS_PX = 448;
+constexpr int ROI_SLICE_B = 128, ROI_LDS_PX = 160;
+static int g_roi_lds_px = ROI_LDS_PX;  // staging cap in pixels (0: always direct), see mdx_roi_align_set_window
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
-                                                   const int *__restrict__ counts, int gslice, T *__restrict__ out) {
+                                                   const int *__restrict__ counts, int gslice, int lds_px,
+                                                   T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;          // channels per 16-B group
     const int G = gslice;                   // 16-B groups per slice (8, fewer for narrow maps)
     const int SL = G * V;                   // channels per slice
@@ -805,7 +807,7 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
         if (roi_axis(x1c, g.W, lo, hi, l)) xhi = hi;
     }
     const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
-    const bool staged = g.gh > 0 && g.gw > 0 && wh > 0 && ww > 0 && wh * ww <= ROI_LDS_PX;
+    const bool staged = g.gh > 0 && g.gw > 0 && wh > 0 && ww > 0 && wh * ww <= lds_px;
     if (staged) {
         const int npx = wh * ww;
         for (int i = threadIdx.x; i < npx * G; i += 256) {
@@ -1302,6 +1304,12 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     return MDX_OK;
 }
 
+extern "C" int mdx_roi_align_set_window(int max_pixels) {
+    const int old = g_roi_lds_px;
+    g_roi_lds_px = max_pixels < 0 ? 0 : (max_pixels > 1024 ? 1024 : max_pixels);
+    return old;
+}
+
 extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
                              int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
                              int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
@@ -1324,11 +1332,12 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     if (dtype == 1)
-        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * 8)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
-                           as_stream(stream), rl, rois, counts, gslice, (_Float16 *)out);
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * 8)), dim3(256),
+                           (size_t)g_roi_lds_px * gslice * 16, as_stream(stream), rl, rois, counts, gslice,
+                           g_roi_lds_px, (_Float16 *)out);
     else
-        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (gslice * 4)), dim3(256), ROI_LDS_PX * ROI_SLICE_B,
-                           as_stream(stream), rl, rois, counts, gslice, (float *)out);
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (gslice * 4)), dim3(256), (size_t)g_roi_lds_px * gslice * 16,
+                           as_stream(stream), rl, rois, counts, gslice, g_roi_lds_px, (float *)out);
     MDX_CHECK_LAUNCH("mdx_roi_align");
     return MDX_OK;
 }

@@ -1,0 +1,53 @@
+"""Time the box-head ROIAlign on the bench workload's real proposals and FPN
+maps for several LDS staging caps.  Usage: python tools/roibench.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd import proc, synth
+    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    cfg = ModelConfig(score_thresh_test=0.0)
+    pred = Predictor.from_config(cfg, dtype="fp16", seed=0)
+    m = pred.model
+    sess = synth.SyntheticSession(32, seed=1000)
+    raw = torch.from_numpy(sess.frames(0, 32)).cuda()
+    prepped = proc.FramePrep(sess.bground_im, sess.roi, 0, 100, True)(raw)
+    captured = {}
+    orig = m.roi_align
+
+    def cap(feats, props, pcount, R, P, *a, **k):
+        if P == cfg.box_pooler_resolution and "box" not in captured:
+            captured["box"] = (feats, props, pcount, R, P, a, k)
+        return orig(feats, props, pcount, R, P, *a, **k)
+    m.roi_align = cap
+    m.forward(prepped, proc.scale_lut(0, 100))
+    m.roi_align = orig
+    feats, props, pcount, R, P, a, k = captured["box"]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ref = None
+    for px in (0, 64, 96, 128, 160, 224, 320, 448):
+        old = call("mdx_roi_align_set_window", px)
+        for _ in range(2):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e0.record()
+        for _ in range(5):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e1.record()
+        torch.cuda.synchronize()
+        call("mdx_roi_align_set_window", old)
+        if ref is None:
+            ref = out.clone()
+        same = torch.equal(out, ref)
+        print(f"window cap {px:4d} px: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us  identical={same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
