@@ -31,9 +31,23 @@ def main():
     m.forward(prepped, proc.scale_lut(0, 100))
     m.roi_align = orig
     feats, props, pcount, R, P, a, k = captured["box"]
+    # adaptive sampling grid statistics (gh x gw per bin) by level
+    import math
+    b = props.reshape(-1, 4).float()
+    w, h = (b[:, 2] - b[:, 0]).clamp(min=0), (b[:, 3] - b[:, 1]).clamp(min=0)
+    lvl = torch.floor(4 + torch.log2(torch.sqrt(w * h) / 224 + 1e-8)).clamp(2, 5)
+    sc = 2.0 ** (-lvl)
+    gh = torch.ceil(h * sc / P).clamp(min=1)
+    gw = torch.ceil(w * sc / P).clamp(min=1)
+    S = (gh * gw)
+    print(f"ROIs {b.shape[0]}, samples/bin mean {S.mean().item():.2f}, p50 {S.median().item():.0f}, "
+          f"p90 {S.quantile(0.9).item():.0f}, p99 {S.quantile(0.99).item():.0f}, max {S.max().item():.0f}; "
+          f"total samples x bins {float((S * P * P).sum()):.3e}; share of the top 5% ROIs "
+          f"{float(S.sort(descending=True).values[:len(S) // 20].sum() / S.sum()):.2f}")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ref = None
-    for px in (0, 64, 96, 128, 160, 224, 320, 448):
+    caps = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 64, 96, 128, 160, 224, 320, 448]
+    for px in caps:
         old = call("mdx_roi_align_set_window", px)
         for _ in range(2):
             out = orig(feats, props, pcount, R, P, *a, **k)
