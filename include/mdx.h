@@ -166,10 +166,6 @@ int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl
                       float *out_boxes, float *out_scores, int *out_count, void *workspace,
                       mdx_stream_t stream);
 
-/* Tuning knob: largest ROI sample window (pixels) that mdx_roi_align stages
- * in LDS; larger windows read their taps from global memory (0 = never stage,
- * max 1024, default 160).  Returns the previous value. */
-int mdx_roi_align_set_window(int max_pixels);
 /* ROIPooler(ROIAlignV2): rois float32 (R,4) XYXY, R = B*per_image, rows with
  * index >= counts[b] produce zeros.  out (R,P,P,C). */
 int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,

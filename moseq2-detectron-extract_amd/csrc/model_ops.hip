@@ -749,25 +749,21 @@ __device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, fl
     return true;
 }
 
-// Grid (ROI, 128-byte channel slice).  The ROI's sample window of the slice
-// is staged in LDS with 16-B loads (every feature pixel fetched once per ROI
-// instead of once per tap of every sample), then every (bin, 16-B group)
-// lane interpolates from LDS.  Windows above ROI_LDS_PX pixels (very
-// elongated proposals) read their taps straight from global memory.
-// Arithmetic (sample positions, weights, accumulation order) is the
-// per-sample formula of the reference kernel in both paths.
-constexpr int ROI_SLICE_B = 128, ROI_LDS_PX = 160;
-static int g_roi_lds_px = ROI_LDS_PX;  // staging cap in pixels (0: always direct), see mdx_roi_align_set_window
+// One workgroup per ROI, all channels.  The bilinear tap rows/cols and
+// fractions of the ROI's P*gh sample rows and P*gw sample columns are
+// computed once into LDS (the sample-coordinate arithmetic -- including its
+// divisions -- is the same for every channel, so per-lane recomputation made
+// the kernel VALU-bound); each (bin, 16-B channel group) lane then only
+// gathers and blends.  Arithmetic (sample positions, weights, accumulation
+// order) is the reference kernel's per-sample formula.
+constexpr int ROI_TAB = 256;  // max P*gh (and P*gw) held in the tables
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
-                                                   const int *__restrict__ counts, int gslice, int lds_px,
-                                                   T *__restrict__ out) {
-    constexpr int V = Vec16<T>::N;          // channels per 16-B group
-    const int G = gslice;                   // 16-B groups per slice (8, fewer for narrow maps)
-    const int SL = G * V;                   // channels per slice
-    const int PXB = G * 16;                 // LDS bytes per staged pixel
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+                                                   const int *__restrict__ counts, T *__restrict__ out) {
+    constexpr int V = Vec16<T>::N;  // channels per 16-B group
+    __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
+    __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
     int r;
     {
@@ -775,82 +771,84 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
         const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
         r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
     }
-    const int slice = blockIdx.y;
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
-    const int c0 = slice * SL;
-    T *o = out + (long long)r * P * P * C + c0;
-    const int nitems = P * P * G;
+    const int CG = C / V;
+    T *o = out + (long long)r * P * P * C;
+    const int nitems = P * P * CG;
     if (ri >= counts[b]) {
         const float z[V] = {};
-        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)(i / G) * C + (i % G) * V, z);
+        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)i * V, z);
         return;
     }
     const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
-    const T *f = reinterpret_cast<const T *>(g.feat) + c0;
-    // window of feature rows / cols the samples touch (sample coordinates are
-    // monotonic in (bin, sub-sample))
-    int ylo = 0, yhi = -1, xlo = 0, xhi = -1;
-    {
-        int lo, hi;
-        float l;
-        const float yf = g.rsh + 0.f * g.bh + (0.f + .5f) * g.bh / (float)g.gh;
-        const float yl_ = g.rsh + (float)(P - 1) * g.bh + ((float)(g.gh - 1) + .5f) * g.bh / (float)g.gh;
-        const float xf = g.rsw + 0.f * g.bw + (0.f + .5f) * g.bw / (float)g.gw;
-        const float xl_ = g.rsw + (float)(P - 1) * g.bw + ((float)(g.gw - 1) + .5f) * g.bw / (float)g.gw;
-        // clamp both ends into the map; outside samples are skipped later
-        const float y0c = fminf(fmaxf(yf, 0.f), (float)g.H), y1c = fminf(fmaxf(yl_, 0.f), (float)g.H);
-        const float x0c = fminf(fmaxf(xf, 0.f), (float)g.W), x1c = fminf(fmaxf(xl_, 0.f), (float)g.W);
-        if (roi_axis(y0c, g.H, lo, hi, l)) ylo = lo;
-        if (roi_axis(y1c, g.H, lo, hi, l)) yhi = hi;
-        if (roi_axis(x0c, g.W, lo, hi, l)) xlo = lo;
-        if (roi_axis(x1c, g.W, lo, hi, l)) xhi = hi;
-    }
-    const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
-    const bool staged = g.gh > 0 && g.gw > 0 && wh > 0 && ww > 0 && wh * ww <= lds_px;
-    if (staged) {
-        const int npx = wh * ww;
-        for (int i = threadIdx.x; i < npx * G; i += 256) {
-            const int px = i / G, cg = i - px * G;
-            const int py = px / ww, pxx = px - py * ww;
-            *reinterpret_cast<uint4 *>(smem + px * PXB + cg * 16) =
-                *reinterpret_cast<const uint4 *>(f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V);
+    const T *f = reinterpret_cast<const T *>(g.feat);
+    const int ny = P * g.gh, nx = P * g.gw;
+    const bool tab = g.gh > 0 && g.gw > 0 && ny <= ROI_TAB && nx <= ROI_TAB;
+    if (tab) {
+        for (int e = threadIdx.x; e < ny; e += 256) {
+            const int ph = e / g.gh, iy = e - ph * g.gh;
+            const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+            int lo, hi;
+            float l;
+            const bool ok = roi_axis(y, g.H, lo, hi, l);
+            s_y0[e] = ok ? lo : -1;
+            s_y1[e] = hi;
+            s_ly[e] = l;
+        }
+        for (int e = threadIdx.x; e < nx; e += 256) {
+            const int pw = e / g.gw, ix = e - pw * g.gw;
+            const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+            int lo, hi;
+            float l;
+            const bool ok = roi_axis(x, g.W, lo, hi, l);
+            s_x0[e] = ok ? lo : -1;
+            s_x1[e] = hi;
+            s_lx[e] = l;
         }
         __syncthreads();
     }
     for (int t = threadIdx.x; t < nitems; t += 256) {
-        const int cg = t % G;
-        const int bin = t / G;
+        const int bin = t / CG, cg = t - bin * CG;
         const int ph = bin / P, pw = bin - ph * P;
+        const T *fc = f + cg * V;
         float acc[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = 0.f;
         for (int iy = 0; iy < g.gh; ++iy) {
-            const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
             int yl, yh;
             float ly;
-            if (!roi_axis(y, g.H, yl, yh, ly)) continue;
+            if (tab) {
+                const int e = ph * g.gh + iy;
+                yl = s_y0[e];
+                yh = s_y1[e];
+                ly = s_ly[e];
+                if (yl < 0) continue;
+            } else {
+                const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+                if (!roi_axis(y, g.H, yl, yh, ly)) continue;
+            }
+            const T *r0 = fc + (long long)yl * g.W * C, *r1 = fc + (long long)yh * g.W * C;
             for (int ix = 0; ix < g.gw; ++ix) {
-                const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
                 int xl, xh;
                 float lx;
-                if (!roi_axis(x, g.W, xl, xh, lx)) continue;
+                if (tab) {
+                    const int e = pw * g.gw + ix;
+                    xl = s_x0[e];
+                    xh = s_x1[e];
+                    lx = s_lx[e];
+                    if (xl < 0) continue;
+                } else {
+                    const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+                    if (!roi_axis(x, g.W, xl, xh, lx)) continue;
+                }
                 const float hy = 1.f - ly, hx = 1.f - lx;
                 const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
                 float v1[V], v2[V], v3[V], v4[V];
-                if (staged) {
-                    const char *s0 = smem + cg * 16;
-                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xl - xlo) * PXB), v1);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yl - ylo) * ww + xh - xlo) * PXB), v2);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xl - xlo) * PXB), v3);
-                    ld16(reinterpret_cast<const T *>(s0 + ((yh - ylo) * ww + xh - xlo) * PXB), v4);
-                } else {
-                    const T *fc = f + cg * V;
-                    ld16(fc + ((long long)yl * g.W + xl) * C, v1);
-                    ld16(fc + ((long long)yl * g.W + xh) * C, v2);
-                    ld16(fc + ((long long)yh * g.W + xl) * C, v3);
-                    ld16(fc + ((long long)yh * g.W + xh) * C, v4);
-                }
+                ld16(r0 + (long long)xl * C, v1);
+                ld16(r0 + (long long)xh * C, v2);
+                ld16(r1 + (long long)xl * C, v3);
+                ld16(r1 + (long long)xh * C, v4);
 #pragma unroll
                 for (int i = 0; i < V; ++i) acc[i] += w1 * v1[i] + w2 * v2[i] + w3 * v3[i] + w4 * v4[i];
             }
@@ -1304,23 +1302,13 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     return MDX_OK;
 }
 
-extern "C" int mdx_roi_align_set_window(int max_pixels) {
-    const int old = g_roi_lds_px;
-    g_roi_lds_px = max_pixels < 0 ? 0 : (max_pixels > 1024 ? 1024 : max_pixels);
-    return old;
-}
-
 extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
                              int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
                              int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
                              void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
-    const int vch = dtype == 1 ? 8 : 4;  // channels per 16 B
-    MDX_REQUIRE(C % vch == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
-    // channel slice of up to 128 B (8 groups of 16 B) that divides C
-    int gslice = 8;
-    while (gslice > 1 && (C / vch) % gslice) gslice >>= 1;
+    MDX_REQUIRE(C % (dtype == 1 ? 8 : 4) == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
     if (R == 0) return MDX_OK;
     RoiLevels rl{};
     for (int l = 0; l < L; ++l) {
@@ -1332,12 +1320,11 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     if (dtype == 1)
-        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * 8)), dim3(256),
-                           (size_t)g_roi_lds_px * gslice * 16, as_stream(stream), rl, rois, counts, gslice,
-                           g_roi_lds_px, (_Float16 *)out);
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                           (_Float16 *)out);
     else
-        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (gslice * 4)), dim3(256), (size_t)g_roi_lds_px * gslice * 16,
-                           as_stream(stream), rl, rois, counts, gslice, g_roi_lds_px, (float *)out);
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                           (float *)out);
     MDX_CHECK_LAUNCH("mdx_roi_align");
     return MDX_OK;
 }

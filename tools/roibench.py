@@ -12,7 +12,6 @@ def main():
     import mdx_pkg
     mdx_pkg.load()
     from moseq2_detectron_extract_amd import proc, synth
-    from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     cfg = ModelConfig(score_thresh_test=0.0)
     pred = Predictor.from_config(cfg, dtype="fp16", seed=0)
@@ -46,21 +45,14 @@ def main():
           f"{float(S.sort(descending=True).values[:len(S) // 20].sum() / S.sum()):.2f}")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ref = None
-    caps = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 64, 96, 128, 160, 224, 320, 448]
-    for px in caps:
-        old = call("mdx_roi_align_set_window", px)
-        for _ in range(2):
-            out = orig(feats, props, pcount, R, P, *a, **k)
-        e0.record()
-        for _ in range(5):
-            out = orig(feats, props, pcount, R, P, *a, **k)
-        e1.record()
-        torch.cuda.synchronize()
-        call("mdx_roi_align_set_window", old)
-        if ref is None:
-            ref = out.clone()
-        same = torch.equal(out, ref)
-        print(f"window cap {px:4d} px: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us  identical={same}", flush=True)
+    for _ in range(2):
+        out = orig(feats, props, pcount, R, P, *a, **k)
+    e0.record()
+    for _ in range(5):
+        out = orig(feats, props, pcount, R, P, *a, **k)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"box ROIAlign: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
 
 
 if __name__ == "__main__":
