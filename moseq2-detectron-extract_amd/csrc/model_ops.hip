@@ -749,21 +749,25 @@ __device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, fl
     return true;
 }
 
-// One workgroup per ROI, all channels.  The bilinear tap rows/cols and
-// fractions of the ROI's P*gh sample rows and P*gw sample columns are
-// computed once into LDS (the sample-coordinate arithmetic -- including its
-// divisions -- is the same for every channel, so per-lane recomputation made
-// the kernel VALU-bound); each (bin, 16-B channel group) lane then only
-// gathers and blends.  Arithmetic (sample positions, weights, accumulation
-// order) is the reference kernel's per-sample formula.
-constexpr int ROI_TAB = 256;  // max P*gh (and P*gw) held in the tables
+// Grid (ROI, channel slice of up to 128 B).  Per workgroup: (1) the bilinear
+// tap rows/cols and fractions of the ROI's P*gh sample rows and P*gw sample
+// columns are computed once into LDS (the coordinate arithmetic -- including
+// its divisions -- is the same for every channel); (2) the slice of the ROI's
+// sample window is staged in LDS with 16-B loads, so each feature pixel is
+// fetched once per ROI instead of once per tap of every sample (windows above
+// ROI_WIN_PX pixels read their taps from global memory); (3) every (bin,
+// 16-B group) lane gathers and blends.  Arithmetic (sample positions,
+// weights, accumulation order) is the reference kernel's per-sample formula.
+constexpr int ROI_TAB = 256;     // max P*gh (and P*gw) held in the tables
+constexpr int ROI_WIN_PX = 224;  // staged window cap (pixels x 128 B)
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
-                                                   const int *__restrict__ counts, T *__restrict__ out) {
+                                                   const int *__restrict__ counts, int gslice, T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;  // channels per 16-B group
     __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
+    __shared__ __attribute__((aligned(16))) char s_win[ROI_WIN_PX * 128];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
     int r;
     {
@@ -771,20 +775,22 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
         const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
         r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
     }
+    const int G = gslice, PXB = G * 16;  // 16-B groups per slice, LDS bytes per pixel
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
-    const int CG = C / V;
-    T *o = out + (long long)r * P * P * C;
-    const int nitems = P * P * CG;
+    const int c0 = blockIdx.y * G * V;
+    T *o = out + (long long)r * P * P * C + c0;
+    const int nitems = P * P * G;
     if (ri >= counts[b]) {
         const float z[V] = {};
-        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)i * V, z);
+        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)(i / G) * C + (i % G) * V, z);
         return;
     }
     const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
-    const T *f = reinterpret_cast<const T *>(g.feat);
+    const T *f = reinterpret_cast<const T *>(g.feat) + c0;
     const int ny = P * g.gh, nx = P * g.gw;
     const bool tab = g.gh > 0 && g.gw > 0 && ny <= ROI_TAB && nx <= ROI_TAB;
+    int ylo = 0, yhi = -1, xlo = 0, xhi = -1;
     if (tab) {
         for (int e = threadIdx.x; e < ny; e += 256) {
             const int ph = e / g.gh, iy = e - ph * g.gh;
@@ -807,11 +813,43 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
             s_lx[e] = l;
         }
         __syncthreads();
+        // window: rows/cols touched by the valid samples (tables are monotonic)
+        for (int e = 0; e < ny; ++e)
+            if (s_y0[e] >= 0) {
+                ylo = s_y0[e];
+                break;
+            }
+        for (int e = ny - 1; e >= 0; --e)
+            if (s_y0[e] >= 0) {
+                yhi = s_y1[e];
+                break;
+            }
+        for (int e = 0; e < nx; ++e)
+            if (s_x0[e] >= 0) {
+                xlo = s_x0[e];
+                break;
+            }
+        for (int e = nx - 1; e >= 0; --e)
+            if (s_x0[e] >= 0) {
+                xhi = s_x1[e];
+                break;
+            }
+    }
+    const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
+    const bool staged = tab && wh > 0 && ww > 0 && wh * ww <= ROI_WIN_PX;
+    if (staged) {
+        const int npx = wh * ww;
+        for (int i = threadIdx.x; i < npx * G; i += 256) {
+            const int px = i / G, cg = i - px * G;
+            const int py = px / ww, pxx = px - py * ww;
+            *reinterpret_cast<uint4 *>(s_win + px * PXB + cg * 16) =
+                *reinterpret_cast<const uint4 *>(f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V);
+        }
+        __syncthreads();
     }
     for (int t = threadIdx.x; t < nitems; t += 256) {
-        const int bin = t / CG, cg = t - bin * CG;
+        const int bin = t / G, cg = t - bin * G;
         const int ph = bin / P, pw = bin - ph * P;
-        const T *fc = f + cg * V;
         float acc[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -828,7 +866,6 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
                 const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
                 if (!roi_axis(y, g.H, yl, yh, ly)) continue;
             }
-            const T *r0 = fc + (long long)yl * g.W * C, *r1 = fc + (long long)yh * g.W * C;
             for (int ix = 0; ix < g.gw; ++ix) {
                 int xl, xh;
                 float lx;
@@ -845,10 +882,20 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
                 const float hy = 1.f - ly, hx = 1.f - lx;
                 const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
                 float v1[V], v2[V], v3[V], v4[V];
-                ld16(r0 + (long long)xl * C, v1);
-                ld16(r0 + (long long)xh * C, v2);
-                ld16(r1 + (long long)xl * C, v3);
-                ld16(r1 + (long long)xh * C, v4);
+                if (staged) {
+                    const char *w0 = s_win + cg * 16;
+                    const int a0 = (yl - ylo) * ww - xlo, a1 = (yh - ylo) * ww - xlo;
+                    ld16(reinterpret_cast<const T *>(w0 + (a0 + xl) * PXB), v1);
+                    ld16(reinterpret_cast<const T *>(w0 + (a0 + xh) * PXB), v2);
+                    ld16(reinterpret_cast<const T *>(w0 + (a1 + xl) * PXB), v3);
+                    ld16(reinterpret_cast<const T *>(w0 + (a1 + xh) * PXB), v4);
+                } else {
+                    const T *fc = f + cg * V;
+                    ld16(fc + ((long long)yl * g.W + xl) * C, v1);
+                    ld16(fc + ((long long)yl * g.W + xh) * C, v2);
+                    ld16(fc + ((long long)yh * g.W + xl) * C, v3);
+                    ld16(fc + ((long long)yh * g.W + xh) * C, v4);
+                }
 #pragma unroll
                 for (int i = 0; i < V; ++i) acc[i] += w1 * v1[i] + w2 * v2[i] + w3 * v3[i] + w4 * v4[i];
             }
@@ -1308,8 +1355,12 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
                              void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
-    MDX_REQUIRE(C % (dtype == 1 ? 8 : 4) == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
+    const int vch = dtype == 1 ? 8 : 4;  // channels per 16 B
+    MDX_REQUIRE(C % vch == 0, "mdx_roi_align: C must be a multiple of 16 bytes of channels");
     if (R == 0) return MDX_OK;
+    // channel slice of up to 128 B (8 groups of 16 B) that divides C
+    int gslice = 8;
+    while (gslice > 1 && (C / vch) % gslice) gslice >>= 1;
     RoiLevels rl{};
     for (int l = 0; l < L; ++l) {
         rl.feat[l] = feats[l];
@@ -1320,11 +1371,11 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     if (dtype == 1)
-        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                           (_Float16 *)out);
+        hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * vch)), dim3(256), 0, as_stream(stream), rl,
+                           rois, counts, gslice, (_Float16 *)out);
     else
-        hipLaunchKernelGGL(k_roi_align<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                           (float *)out);
+        hipLaunchKernelGGL(k_roi_align<float>, dim3(R, C / (gslice * vch)), dim3(256), 0, as_stream(stream), rl, rois,
+                           counts, gslice, (float *)out);
     MDX_CHECK_LAUNCH("mdx_roi_align");
     return MDX_OK;
 }
