@@ -123,6 +123,9 @@ int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const
 /* Policy for the 256x256 fp16 kernel (Cin % 64 == 0): 0 never, 1 auto (default:
  * when the layer fills the chip), 2 whenever eligible.  Returns the old mode. */
 int mdx_conv_set_large_tiles(int mode);
+/* Layers with KH*KW*Cin <= kmax use the 64-wide output-channel tile (more
+ * workgroups per CU for HBM-bound small-K layers).  Returns the old value. */
+int mdx_conv_set_narrow_kmax(int kmax);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

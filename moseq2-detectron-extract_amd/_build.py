@@ -76,7 +76,22 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link of libmdx.so failed:\n{r.stderr[-6000:]}")
+        check_symbols()
     return LIB
+
+
+def check_symbols() -> None:
+    """A shared link does not reject undefined symbols; a kernel whose host
+    stub was not emitted only fails at dlopen on the GPU box.  Refuse the
+    library here instead."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-u", "-C", LIB], capture_output=True, text=True)
+    if r.returncode != 0:
+        return
+    bad = [ln.strip() for ln in r.stdout.splitlines() if "mdx::" in ln]
+    if bad:
+        os.remove(LIB)
+        raise RuntimeError("libmdx.so has undefined symbols of its own:\n" + "\n".join(bad[:20]))
 
 
 if __name__ == "__main__":

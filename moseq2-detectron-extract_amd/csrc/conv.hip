@@ -194,9 +194,10 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     constexpr int TI = BM / 32, TJ = BN_ / 32;
     constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
     constexpr int BLOADS = BN_ * 8 / CONV_THREADS;  // 16-B chunks of B per thread
+    constexpr int STAGE = A_TILE + B_TILE;  // one K-step buffer: A tile then B tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *As = smem;                   // [2][BM][PITCH]
-    char *Bs = smem + 2 * A_TILE;      // [2][BN_][PITCH]
+    char *As = smem;                   // buffer b: A at b * STAGE, B at b * STAGE + A_TILE
+    char *Bs = smem + A_TILE;          // (a one-step K needs buffer 0 only)
 
     // XCD-contiguous remap of the linear block id (bijective)
     int tile;
@@ -274,10 +275,10 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     auto store_lds = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(As + buf * A_TILE + (lrow + 32 * i) * PITCH + wpiece) = ra[i];
+            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = ra[i];
 #pragma unroll
         for (int i = 0; i < BLOADS; ++i)
-            *reinterpret_cast<uint4 *>(Bs + buf * B_TILE + (lrow + 32 * i) * PITCH + wpiece) = rb[i];
+            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = rb[i];
     };
 
     float4v acc[TI][TJ];
@@ -299,8 +300,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             load_global();
             advance_k();
         }
-        const char *Ab = As + cur * A_TILE + (wm * (BM / 2) + (lane & 15)) * PITCH;
-        const char *Bb = Bs + cur * B_TILE + (wn * (BN_ / 2) + (lane & 15)) * PITCH;
+        const char *Ab = As + cur * STAGE + (wm * (BM / 2) + (lane & 15)) * PITCH;
+        const char *Bb = Bs + cur * STAGE + (wn * (BN_ / 2) + (lane & 15)) * PITCH;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int koff = ((4 * s + (lane >> 4)) ^ ((lane & 15) >> 1)) * 16;
@@ -334,45 +335,56 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         __syncthreads();
     }
 
-    // ---- epilogue: accumulators -> LDS (fp32, row-major) -> bias / residual /
-    // ReLU -> 16-byte stores of 8 consecutive output channels
+    // ---- epilogue, in two halves of BM/2 rows (the LDS image is half the
+    // tile, so a one-step-K launch fits 4 workgroups per CU): the waves owning
+    // the half write their accumulators to LDS (fp32, row-major), then all
+    // threads apply bias / residual / ReLU and store 8 consecutive output
+    // channels per 16-byte store
     constexpr int CP = BN_ + 4;  // fp32 pitch (16-B aligned rows, bank spread)
+    constexpr int HM = BM / 2;
     float *Cs = reinterpret_cast<float *>(smem);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-                const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
-                Cs[row * CP + col] = acc[i][j][r];
-            }
-    __syncthreads();
     constexpr int CPR = BN_ / 8;  // 8-wide chunks per row
-    constexpr int NQ = BM * CPR / CONV_THREADS;
-    if (a.ksplit > 1) {
+    constexpr int NQ = HM * CPR / CONV_THREADS;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int c = tid + q * CONV_THREADS;
-            const int row = c / CPR, ch = c - row * CPR;
-            const int gm = m0 + row, gn0 = n0 + ch * 8;
-            if (gm >= a.M || gn0 >= a.Cout) continue;
-            // raw partial; Cout % 8 == 0 is required for split-K
-            const float *src = Cs + row * CP + ch * 8;
-            float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
-            *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
-            *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
+    for (int h = 0; h < 2; ++h) {
+        if (wm == h) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = i * 16 + (lane >> 4) * 4 + r;
+                        const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
+                        Cs[row * CP + col] = acc[i][j][r];
+                    }
         }
-    } else {
-        finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
-            const int c = tid + q * CONV_THREADS;
-            const int row = c / CPR, ch = c - row * CPR;
-            gm = m0 + row;
-            gn0 = n0 + ch * 8;
-            src = Cs + row * CP + ch * 8;
-            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
-        });
+        __syncthreads();
+        const int mh = m0 + h * HM;
+        if (a.ksplit > 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                const int gm = mh + row, gn0 = n0 + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) continue;
+                // raw partial; Cout % 8 == 0 is required for split-K
+                const float *src = Cs + row * CP + ch * 8;
+                float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
+                *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
+                *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
+            }
+        } else {
+            finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                gm = mh + row;
+                gn0 = n0 + ch * 8;
+                src = Cs + row * CP + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+            });
+        }
+        if (h == 0) __syncthreads();
     }
 }
 
@@ -601,6 +613,15 @@ extern "C" int mdx_conv_set_large_tiles(int mode) {
     g_large_tiles = mode;
     return old;
 }
+// layers with K <= g_narrow_kmax use the 64-wide N tile (4 workgroups per CU:
+// the HBM-bound small-K 1x1 convs need the memory parallelism more than the
+// wider tile's A-operand reuse)
+static int g_narrow_kmax = 128;
+extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
+    const int old = g_narrow_kmax;
+    g_narrow_kmax = kmax;
+    return old;
+}
 
 // split-K slice count for a launch of `tiles` output tiles and nk K-steps:
 // minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
@@ -664,7 +685,7 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     {
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
         const bool big = Cout >= 192 && t256 >= 384;
-        if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) &&
+        if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) && KH * KW * Cin > g_narrow_kmax &&
             (g_large_tiles == 2 || (g_large_tiles == 1 && big))) {
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
@@ -678,7 +699,9 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
             return MDX_OK;
         }
     }
-    const bool narrow = Cout <= 64;  // 64-wide N tile: no wasted MFMA columns for 64-channel layers
+    // 64-wide N tile: no wasted MFMA columns for 64-channel layers; more
+    // workgroups per CU for the small-K layers
+    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax;
     const int bn = narrow ? 64 : BN;
     const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_n = tiles_n;
@@ -691,8 +714,10 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.ksteps = (nk + ksplit - 1) / ksplit;
     a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
     a.part = reinterpret_cast<float *>(workspace);
-    const size_t lds_main = 2 * (size_t)BM * PITCH + 2 * (size_t)bn * PITCH;
-    const size_t lds_epi = (size_t)BM * (bn + 4) * 4;
+    // stage buffers: one when the whole K is one step, else two; epilogue
+    // image: half the tile in fp32
+    const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
+    const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \

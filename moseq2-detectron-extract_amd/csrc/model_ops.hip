@@ -759,6 +759,11 @@ __device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, fl
 // 16-B group) lane gathers and blends.  Arithmetic (sample positions,
 // weights, accumulation order) is the reference kernel's per-sample formula.
 constexpr int ROI_TAB = 256;     // max P*gh (and P*gw) held in the tables
+
+// one 16-B LDS-DMA piece per lane: LDS destination = lds_base + 16 * lane
+__device__ __forceinline__ void roi_glds16(const void *src, char *lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
 constexpr int ROI_WIN_PX = 224;  // staged window cap (pixels x 128 B)
 
 template <typename T>
@@ -838,13 +843,23 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
     const bool staged = tab && wh > 0 && ww > 0 && wh * ww <= ROI_WIN_PX;
     if (staged) {
-        const int npx = wh * ww;
-        for (int i = threadIdx.x; i < npx * G; i += 256) {
+        // LDS-DMA: piece i (pixel i / G, 16-B group i % G) lands at byte 16 i
+        // of the window, i.e. wave-uniform base + 16 * lane, so every piece
+        // of the window is one global_load_lds_dwordx4 and all of a thread's
+        // (<= ROI_STAGE) pieces are in flight together.  Lanes past the end
+        // re-fetch piece 0 into the unused tail of the window.
+        const int npc = wh * ww * G;
+        const int nrounds = (npc + 255) / 256;
+        for (int j = 0; j < nrounds; ++j) {
+            const int i0 = j * 256 + (threadIdx.x & ~63);
+            int i = i0 + (threadIdx.x & 63);
+            i = i < npc ? i : 0;
             const int px = i / G, cg = i - px * G;
             const int py = px / ww, pxx = px - py * ww;
-            *reinterpret_cast<uint4 *>(s_win + px * PXB + cg * 16) =
-                *reinterpret_cast<const uint4 *>(f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V);
+            const T *src = f + ((long long)(ylo + py) * g.W + xlo + pxx) * C + cg * V;
+            roi_glds16(src, s_win + i0 * 16);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     for (int t = threadIdx.x; t < nitems; t += 256) {

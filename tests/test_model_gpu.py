@@ -201,8 +201,8 @@ def test_rpn_proposals_from_identical_heads(mdx):
         torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("C", [16, 64])
-def test_roi_align_matches_oracle(mdx, rt, C):
+@pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True)])
+def test_roi_align_matches_oracle(mdx, rt, C, half):
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
@@ -212,24 +212,28 @@ def test_roi_align_matches_oracle(mdx, rt, C):
     B = 2
     sizes = {2: (28, 32), 3: (14, 16), 4: (7, 8), 5: (4, 4)}
     feats = {f"p{l}": torch.randn(B, C, *s, generator=g) for l, s in sizes.items()}
+    if half:  # fp16-representable inputs; the kernel accumulates in fp32 and rounds once
+        feats = {k: v.half().float() for k, v in feats.items()}
     per = 40
     xy = torch.rand(B, per, 2, generator=g) * torch.tensor([120.0, 100.0])
     wh = torch.rand(B, per, 2, generator=g) ** 2 * 110 + 0.5
     boxes = torch.cat([xy, xy + wh], -1)
     counts = torch.tensor([per, per - 7], dtype=torch.int32)
     want = R.pooler(feats, [boxes[0], boxes[1, :per - 7]], 7, cfg)
-    fl = [feats[f"p{l}"].permute(0, 2, 3, 1).contiguous().cuda() for l in (2, 3, 4, 5)]
-    out = torch.empty(B * per, 7, 7, C, device="cuda")
+    fdt = torch.float16 if half else torch.float32
+    fl = [feats[f"p{l}"].permute(0, 2, 3, 1).contiguous().to(fdt).cuda() for l in (2, 3, 4, 5)]
+    out = torch.empty(B * per, 7, 7, C, device="cuda", dtype=fdt)
     ptrs = (ctypes.c_void_p * 4)(*[f.data_ptr() for f in fl])
     ia = lambda v: (ctypes.c_int * 4)(*v)  # noqa: E731
     sc = (ctypes.c_float * 4)(*[0.25, 0.125, 0.0625, 0.03125])
     bd, cd = boxes.contiguous().cuda(), counts.cuda()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4, 2, C,
-         P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, 0, P(out), None)
-    got = out.cpu().permute(0, 3, 1, 2)
+         P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(out), None)
+    got = out.cpu().float().permute(0, 3, 1, 2)
     got = torch.cat([got[:per], got[per:2 * per - 7]])
-    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+    tol = 2e-3 if half else 1e-5
+    torch.testing.assert_close(got, want, rtol=tol, atol=tol)
     assert out[2 * per - 7:].abs().max().item() == 0  # padded rows are zero
 
 

@@ -17,6 +17,9 @@ SHAPES = [
     (32, 112, 128, 256, 256, 3, 1, 1, False),   # fpn output p2
     (32, 56, 64, 128, 512, 1, 1, 0, True),      # res3 conv3
     (32000, 1, 1, 12544, 1024, 1, 1, 0, False),  # fc1
+    (32, 225, 257, 16, 64, 4, 1, 1, False),     # stem (space-to-depth 4x4)
+    (32, 112, 128, 256, 15, 1, 1, 0, False),    # rpn head p2
+    (32, 28, 32, 256, 1024, 1, 1, 0, True),     # res4 conv3
 ]
 
 
@@ -53,8 +56,9 @@ def main():
         flops = 2.0 * M * Cout * k * k * Cin
         byts = 2.0 * (x.numel() + w.numel() + out.numel() + (r.numel() if res else 0))
         line = f"M={M:7d} N={Cout:5d} K={k * k * Cin:6d} res={int(res)}:"
-        for mode in (0, 2):
+        for mode, nk in ((0, 0), (2, 0), (0, 1 << 20)):
             old = call("mdx_conv_set_large_tiles", mode)
+            oldk = call("mdx_conv_set_narrow_kmax", nk)
 
             def go():
                 call("mdx_conv2d_splitk", P(x), N, H, W, Cin, P(w), P(b), Cout, k, k, s, p, P(r), 1, 0, 1, 1,
@@ -67,8 +71,9 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             call("mdx_conv_set_large_tiles", old)
+            call("mdx_conv_set_narrow_kmax", oldk)
             t = e0.elapsed_time(e1) / 10 * 1e-3
-            line += f"  [{'128' if mode == 0 else '256'}] {t * 1e6:7.1f}us {flops / t / 1e12:6.1f}TF {byts / t / 1e12:5.2f}TB/s"
+            line += f"  [{'64' if nk else ('128' if mode == 0 else '256')}] {t * 1e6:7.1f}us {flops / t / 1e12:6.1f}TF {byts / t / 1e12:5.2f}TB/s"
         print(line, flush=True)
 
 
