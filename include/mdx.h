@@ -176,6 +176,12 @@ int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const 
                   int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
                   void *out, mdx_stream_t stream);
 
+/* ROIAlign kernel choice: 0 = one workgroup per (ROI, 128-B channel slice)
+ * with the sample window staged in LDS; 1 (default), 2, 3 = one workgroup per
+ * ROI over all channels, taps gathered from the map, 1/2/4 items per thread
+ * in lockstep.  Returns the old mode. */
+int mdx_roi_align_set_mode(int mode);
+
 /* fast_rcnn_inference_single_image + detector_postprocess for 1 class:
  * pred float32 (B*R, ld_pred) = [cls0, bg, dx, dy, dw, dh].  Outputs
  * (B,D,4), (B,D), int64 (B,D), ndet (B). */

@@ -755,7 +755,7 @@ __device__ __forceinline__ bool roi_axis(float v, int size, int &lo, int &hi, fl
 // its divisions -- is the same for every channel); (2) the slice of the ROI's
 // sample window is staged in LDS with 16-B loads, so each feature pixel is
 // fetched once per ROI instead of once per tap of every sample (windows above
-// ROI_WIN_PX pixels read their taps from global memory); (3) every (bin,
+// ROI_WIN_BYTES read their taps from global memory); (3) every (bin,
 // 16-B group) lane gathers and blends.  Arithmetic (sample positions,
 // weights, accumulation order) is the reference kernel's per-sample formula.
 constexpr int ROI_TAB = 256;     // max P*gh (and P*gw) held in the tables
@@ -764,7 +764,7 @@ constexpr int ROI_TAB = 256;     // max P*gh (and P*gw) held in the tables
 __device__ __forceinline__ void roi_glds16(const void *src, char *lds_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
 }
-constexpr int ROI_WIN_PX = 224;  // staged window cap (pixels x 128 B)
+constexpr int ROI_WIN_BYTES = 224 * 128;  // staged window cap (pixels x slice bytes)
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__restrict__ rois,
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     constexpr int V = Vec16<T>::N;  // channels per 16-B group
     __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
-    __shared__ __attribute__((aligned(16))) char s_win[ROI_WIN_PX * 128];
+    __shared__ __attribute__((aligned(16))) char s_win[ROI_WIN_BYTES];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
     int r;
     {
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
             }
     }
     const int wh = yhi - ylo + 1, ww = xhi - xlo + 1;
-    const bool staged = tab && wh > 0 && ww > 0 && wh * ww <= ROI_WIN_PX;
+    const bool staged = tab && wh > 0 && ww > 0 && wh * ww * PXB <= ROI_WIN_BYTES;
     if (staged) {
         // LDS-DMA: piece i (pixel i / G, 16-B group i % G) lands at byte 16 i
         // of the window, i.e. wave-uniform base + 16 * lane, so every piece
@@ -919,6 +919,154 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
         for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
         st16(o + (long long)bin * C + cg * V, acc);
     }
+}
+
+// One workgroup per ROI over all C channels (grid R).  The bilinear tap
+// tables of the ROI's P*gh sample rows / P*gw sample columns are built once in
+// LDS; then items (bin, 16-B channel group), group fastest, gather their taps
+// straight from the NHWC map (a wave-instruction reads whole 512-B pixel
+// rows), accumulate in the reference's per-sample order and store 16 B.
+// Every thread owns ~P*P*C/(8*256) items, so the ROI's fixed costs (count and
+// box loads, level, tables) are paid once for all channels.
+template <typename T, int ROI_NI>
+__global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const float *__restrict__ rois,
+                                                        const int *__restrict__ counts, T *__restrict__ out) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
+    __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
+    int r;
+    {
+        const int Lb = blockIdx.x, nwg = gridDim.x;
+        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
+        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
+    }
+    const int b = r / rl.per_image, ri = r - b * rl.per_image;
+    const int C = rl.C, P = rl.P;
+    const int G = C / V;  // 16-B groups per pixel
+    T *o = out + (long long)r * P * P * C;
+    const int nitems = P * P * G;
+    if (ri >= counts[b]) {
+        const float z[V] = {};
+        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)i * V, z);
+        return;
+    }
+    const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
+    const T *f = reinterpret_cast<const T *>(g.feat);
+    const int ny = P * g.gh, nx = P * g.gw;
+    const bool tab = g.gh > 0 && g.gw > 0 && ny <= ROI_TAB && nx <= ROI_TAB;
+    if (tab) {
+        for (int e = threadIdx.x; e < ny; e += 256) {
+            const int ph = e / g.gh, iy = e - ph * g.gh;
+            const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+            int lo, hi;
+            float l;
+            const bool ok = roi_axis(y, g.H, lo, hi, l);
+            s_y0[e] = ok ? lo : -1;
+            s_y1[e] = hi;
+            s_ly[e] = l;
+        }
+        for (int e = threadIdx.x; e < nx; e += 256) {
+            const int pw = e / g.gw, ix = e - pw * g.gw;
+            const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+            int lo, hi;
+            float l;
+            const bool ok = roi_axis(x, g.W, lo, hi, l);
+            s_x0[e] = ok ? lo : -1;
+            s_x1[e] = hi;
+            s_lx[e] = l;
+        }
+        __syncthreads();
+    }
+    // ROI_NI items per thread in lockstep (gh, gw are uniform over the ROI),
+    // so 4 * ROI_NI tap loads are in flight per sample
+    for (int t0 = threadIdx.x; t0 < nitems; t0 += 256 * ROI_NI) {
+        int ph[ROI_NI], pw[ROI_NI];
+        const T *fc[ROI_NI];
+        float acc[ROI_NI][V];
+#pragma unroll
+        for (int k = 0; k < ROI_NI; ++k) {
+            int t = t0 + k * 256;
+            t = t < nitems ? t : t0;  // idle slots recompute item t0 (not stored)
+            const int bin = t / G, cg = t - bin * G;
+            ph[k] = bin / P;
+            pw[k] = bin - ph[k] * P;
+            fc[k] = f + cg * V;
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[k][i] = 0.f;
+        }
+        for (int iy = 0; iy < g.gh; ++iy) {
+            int yl[ROI_NI], yh[ROI_NI];
+            float ly[ROI_NI];
+#pragma unroll
+            for (int k = 0; k < ROI_NI; ++k) {
+                if (tab) {
+                    const int e = ph[k] * g.gh + iy;
+                    yl[k] = s_y0[e];
+                    yh[k] = s_y1[e];
+                    ly[k] = s_ly[e];
+                } else {
+                    const float y = g.rsh + (float)ph[k] * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+                    if (!roi_axis(y, g.H, yl[k], yh[k], ly[k])) yl[k] = -1;
+                }
+            }
+            for (int ix = 0; ix < g.gw; ++ix) {
+                float v[ROI_NI][4][V], w[ROI_NI][4];
+                bool ok[ROI_NI];
+#pragma unroll
+                for (int k = 0; k < ROI_NI; ++k) {
+                    int xl, xh;
+                    float lx;
+                    if (tab) {
+                        const int e = pw[k] * g.gw + ix;
+                        xl = s_x0[e];
+                        xh = s_x1[e];
+                        lx = s_lx[e];
+                    } else {
+                        const float x = g.rsw + (float)pw[k] * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+                        if (!roi_axis(x, g.W, xl, xh, lx)) xl = -1;
+                    }
+                    ok[k] = yl[k] >= 0 && xl >= 0;
+                    const float hy = 1.f - ly[k], hx = 1.f - lx;
+                    w[k][0] = hy * hx;
+                    w[k][1] = hy * lx;
+                    w[k][2] = ly[k] * hx;
+                    w[k][3] = ly[k] * lx;
+                    const int y0 = ok[k] ? yl[k] : 0, y1 = ok[k] ? yh[k] : 0;
+                    const int x0 = ok[k] ? xl : 0, x1 = ok[k] ? xh : 0;
+                    const T *r0 = fc[k] + (long long)y0 * g.W * C, *r1 = fc[k] + (long long)y1 * g.W * C;
+                    ld16(r0 + (long long)x0 * C, v[k][0]);
+                    ld16(r0 + (long long)x1 * C, v[k][1]);
+                    ld16(r1 + (long long)x0 * C, v[k][2]);
+                    ld16(r1 + (long long)x1 * C, v[k][3]);
+                }
+#pragma unroll
+                for (int k = 0; k < ROI_NI; ++k) {
+                    if (!ok[k]) continue;
+#pragma unroll
+                    for (int i = 0; i < V; ++i)
+                        acc[k][i] += w[k][0] * v[k][0][i] + w[k][1] * v[k][1][i] + w[k][2] * v[k][2][i] +
+                                     w[k][3] * v[k][3][i];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < ROI_NI; ++k) {
+            const int t = t0 + k * 256;
+            if (t >= nitems) continue;
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[k][i] = acc[k][i] / g.count;
+            st16(o + (long long)t * V, acc[k]);
+        }
+    }
+}
+
+// kernel choice (tests / microbenchmarks): 0 slice + LDS window; 1, 2, 3:
+// full-channel rows with 1, 2, 4 items per thread in lockstep
+static int g_roi_mode = 1;
+extern "C" int mdx_roi_align_set_mode(int mode) {
+    const int old = g_roi_mode;
+    g_roi_mode = mode;
+    return old;
 }
 
 // ---------------------------------------------------------------------------
@@ -1385,7 +1533,24 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     }
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
-    if (dtype == 1)
+    if (g_roi_mode >= 1 && g_roi_mode <= 3) {
+#define MDX_ROI_FULL(NI_)                                                                                     \
+    do {                                                                                                      \
+        if (dtype == 1)                                                                                       \
+            hipLaunchKernelGGL((k_roi_align_full<_Float16, NI_>), dim3(R), dim3(256), 0, as_stream(stream), rl, \
+                               rois, counts, (_Float16 *)out);                                                \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_roi_align_full<float, NI_>), dim3(R), dim3(256), 0, as_stream(stream), rl,    \
+                               rois, counts, (float *)out);                                                   \
+    } while (0)
+        if (g_roi_mode == 1)
+            MDX_ROI_FULL(1);
+        else if (g_roi_mode == 2)
+            MDX_ROI_FULL(2);
+        else
+            MDX_ROI_FULL(4);
+#undef MDX_ROI_FULL
+    } else if (dtype == 1)
         hipLaunchKernelGGL(k_roi_align<_Float16>, dim3(R, C / (gslice * vch)), dim3(256), 0, as_stream(stream), rl,
                            rois, counts, gslice, (_Float16 *)out);
     else

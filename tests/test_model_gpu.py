@@ -201,8 +201,9 @@ def test_rpn_proposals_from_identical_heads(mdx):
         torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True)])
-def test_roi_align_matches_oracle(mdx, rt, C, half):
+def test_roi_align_matches_oracle(mdx, rt, C, half, mode):
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
@@ -228,8 +229,12 @@ def test_roi_align_matches_oracle(mdx, rt, C, half):
     sc = (ctypes.c_float * 4)(*[0.25, 0.125, 0.0625, 0.03125])
     bd, cd = boxes.contiguous().cuda(), counts.cuda()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4, 2, C,
-         P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(out), None)
+    old = call("mdx_roi_align_set_mode", mode)
+    try:
+        call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4, 2,
+             C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(out), None)
+    finally:
+        call("mdx_roi_align_set_mode", old)
     got = out.cpu().float().permute(0, 3, 1, 2)
     got = torch.cat([got[:per], got[per:2 * per - 7]])
     tol = 2e-3 if half else 1e-5

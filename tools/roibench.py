@@ -43,17 +43,22 @@ def main():
           f"p90 {S.quantile(0.9).item():.0f}, p99 {S.quantile(0.99).item():.0f}, max {S.max().item():.0f}; "
           f"total samples x bins {float((S * P * P).sum()):.3e}; share of the top 5% ROIs "
           f"{float(S.sort(descending=True).values[:len(S) // 20].sum() / S.sum()):.2f}")
+    from moseq2_detectron_extract_amd._lib import call
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ref = None
-    for _ in range(2):
-        out = orig(feats, props, pcount, R, P, *a, **k)
-    e0.record()
-    for _ in range(5):
-        out = orig(feats, props, pcount, R, P, *a, **k)
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"box ROIAlign: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
-
+    outs = {}
+    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4")):
+        old = call("mdx_roi_align_set_mode", mode)
+        for _ in range(2):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e0.record()
+        for _ in range(5):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e1.record()
+        torch.cuda.synchronize()
+        call("mdx_roi_align_set_mode", old)
+        outs[mode] = out.float()
+        print(f"box ROIAlign [{name}]: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
+    print("max |diff| between kernels:", max((outs[0] - outs[m]).abs().max().item() for m in outs))
 
 if __name__ == "__main__":
     main()
