@@ -101,6 +101,19 @@ int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, 
                     uint8_t *out0, uint8_t *out1, mdx_stream_t stream);
 
 
+/* Per-frame reductions of compute_scalars (M/proc/scalars.py:79-103) over
+ * frames * masks (uint8 product, M/pipeline/process_features_step.py:165):
+ * area_px[i] = #{p : min_height < v < max_height}, height_ave[i] = mean of
+ * those v (0 when none).  masks may be NULL (all ones).  With K > 0 also the
+ * keypoint z lookup of keypoints_to_dict (M/proc/keypoints.py:122-130):
+ * z_data[i][k] = z_frames[i][clip(floor(y))][clip(floor(x))] for keypoints
+ * float64 [n][K][3] (NaN -> index 0, numpy's cast).  area_px int64 [n],
+ * height_ave / z_data float64. */
+int mdx_frame_scalars(const uint8_t *frames, const uint8_t *masks, int64_t n, int H, int W,
+                      double min_height, double max_height, const double *keypoints, int K,
+                      const uint8_t *z_frames, int64_t *area_px, double *height_ave, double *z_data,
+                      mdx_stream_t stream);
+
 /* ---------------------------------------------------------------------
  * Mask/Keypoint R-CNN forward (Predictor.__call__, M/model/predict.py:53-102,
  * Detectron2 GeneralizedRCNN built by M/model/config.py:21-94).  Tensors are

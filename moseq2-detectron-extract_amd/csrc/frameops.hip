@@ -582,6 +582,88 @@ __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// per-frame reductions of compute_scalars (M/proc/scalars.py:79-103) on
+// frames * masks (M/pipeline/process_features_step.py:165) and the keypoint
+// z lookup of keypoints_to_dict (M/proc/keypoints.py:122-130).  One
+// workgroup per frame; 16-B loads; integer sums (exact).
+// ---------------------------------------------------------------------------
+constexpr int SC_THREADS = 256;
+
+// np.clip(np.floor(v).astype(int), 0, hi): NaN / +-inf / |v| >= 2^63 become
+// INT64_MIN on x86 (cvttsd2si's integer indefinite) and clip to 0
+__device__ __forceinline__ int np_floor_clip(double v, int hi) {
+    if (!(fabs(v) < 9.2233720368547758e18)) return 0;
+    const double fl = floor(v);
+    return fl < 0.0 ? 0 : (fl > (double)hi ? hi : (int)fl);
+}
+
+__device__ __forceinline__ void sc_acc1(uint32_t f8, uint32_t m8, double lo, double hi, unsigned &cnt,
+                                        unsigned &sum) {
+    const uint32_t v = (f8 * m8) & 255u;  // uint8 product
+    const bool in = (double)v > lo && (double)v < hi;
+    cnt += in;
+    sum += in ? v : 0u;
+}
+
+__device__ __forceinline__ void sc_acc(uint32_t fw, uint32_t mw, double lo, double hi, unsigned &cnt,
+                                       unsigned &sum) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sc_acc1((fw >> (8 * b)) & 255u, (mw >> (8 * b)) & 255u, lo, hi, cnt, sum);
+}
+
+__global__ __launch_bounds__(SC_THREADS) void k_frame_scalars(const uint8_t *__restrict__ frames,
+                                                              const uint8_t *__restrict__ masks, int H, int W,
+                                                              double lo, double hi, const double *__restrict__ kpts,
+                                                              int K, const uint8_t *__restrict__ zsrc,
+                                                              long long *__restrict__ area,
+                                                              double *__restrict__ mean_h, double *__restrict__ z) {
+    __shared__ unsigned long long s_c, s_s;
+    const int64_t f = blockIdx.x;
+    const int64_t hw = (int64_t)H * W;
+    const uint8_t *fr = frames + f * hw;
+    const uint8_t *mk = masks ? masks + f * hw : nullptr;
+    if (threadIdx.x == 0) s_c = s_s = 0ull;
+    __syncthreads();
+    unsigned cnt = 0, sum = 0;  // <= 256 * 255 per lane per 16-B word: no overflow at frame sizes < 2^24
+    int64_t p0 = 0;
+    if ((((uintptr_t)fr | (uintptr_t)mk) & 15) == 0) {
+        const int64_t nv = hw / 16;
+        for (int64_t v = threadIdx.x; v < nv; v += SC_THREADS) {
+            const uint4 a = reinterpret_cast<const uint4 *>(fr)[v];
+            const uint4 m = mk ? reinterpret_cast<const uint4 *>(mk)[v] : make_uint4(0x01010101u, 0x01010101u,
+                                                                                     0x01010101u, 0x01010101u);
+            sc_acc(a.x, m.x, lo, hi, cnt, sum);
+            sc_acc(a.y, m.y, lo, hi, cnt, sum);
+            sc_acc(a.z, m.z, lo, hi, cnt, sum);
+            sc_acc(a.w, m.w, lo, hi, cnt, sum);
+        }
+        p0 = nv * 16;
+    }
+    for (int64_t p = p0 + threadIdx.x; p < hw; p += SC_THREADS)
+        sc_acc1(fr[p], mk ? mk[p] : 1u, lo, hi, cnt, sum);
+    unsigned long long c = cnt, sm = sum;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o);
+        sm += __shfl_xor(sm, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&s_c, c);
+        atomicAdd(&s_s, sm);
+    }
+    if (kpts && zsrc && threadIdx.x < K) {
+        const double *kp = kpts + (f * K + threadIdx.x) * 3;
+        const int x = np_floor_clip(kp[0], W - 1), y = np_floor_clip(kp[1], H - 1);
+        z[f * K + threadIdx.x] = (double)zsrc[f * hw + (int64_t)y * W + x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        area[f] = (long long)s_c;
+        // np.mean over the selected uint8 values: exact integer sum / count
+        mean_h[f] = s_c ? (double)s_s / (double)s_c : 0.0;
+    }
+}
+
 }  // namespace mdx
 
 using namespace mdx;
@@ -728,5 +810,22 @@ extern "C" int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t
     hipLaunchKernelGGL(k_crop, dim3((unsigned)n), dim3(256), 0, as_stream(stream), src0, src1, H, W, center,
                        angle_deg, cw, ch, out0, out1);
     MDX_CHECK_LAUNCH("mdx_crop_rotate");
+    return MDX_OK;
+}
+
+extern "C" int mdx_frame_scalars(const uint8_t *frames, const uint8_t *masks, int64_t n, int H, int W,
+                                 double min_height, double max_height, const double *keypoints, int K,
+                                 const uint8_t *z_frames, int64_t *area_px, double *height_ave, double *z_data,
+                                 mdx_stream_t stream) {
+    MDX_REQUIRE(frames && area_px && height_ave, "mdx_frame_scalars: null pointer");
+    MDX_REQUIRE(H > 0 && W > 0 && (int64_t)H * W < (1ll << 24), "mdx_frame_scalars: bad frame %dx%d", H, W);
+    MDX_REQUIRE(K >= 0 && K <= SC_THREADS, "mdx_frame_scalars: K must be in [0, %d]", SC_THREADS);
+    MDX_REQUIRE(K == 0 || (keypoints && z_frames && z_data), "mdx_frame_scalars: keypoints need z_frames and z_data");
+    if (n == 0) return MDX_OK;
+    MDX_REQUIRE(n <= 0x7fffffff, "mdx_frame_scalars: n too large");
+    hipLaunchKernelGGL(k_frame_scalars, dim3((unsigned)n), dim3(SC_THREADS), 0, as_stream(stream), frames, masks, H, W,
+                       min_height, max_height, K ? keypoints : nullptr, K, K ? z_frames : nullptr,
+                       (long long *)area_px, height_ave, z_data);
+    MDX_CHECK_LAUNCH("mdx_frame_scalars");
     return MDX_OK;
 }

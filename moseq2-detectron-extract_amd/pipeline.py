@@ -25,6 +25,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
+from . import features as F
 from . import proc
 from ._lib import call
 
@@ -125,6 +126,46 @@ class GPUExtractor:
         depth, mask = self.crop(prepped, inf["d2_mask"], feats["centroid"], ang)
         return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
                 "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}
+
+    def process_chunk(self, raw, frame_idxs=None, offset: int = 0, true_depth: float = 673.1) -> dict:
+        """One chunk through ProduceFramesStep -> InferenceStep ->
+        ProcessFeaturesStep with tracking off (--no-use-tracking), returning
+        the data dict the reference's writer consumes
+        (M/pipeline/produce_frames_step.py:33-38, inference_step.py:71,
+        process_features_step.py:163-199; M/io/result.py:106-130).
+
+        Device: prep/inpaint, model + mask NMS + instance 0, clean, moments,
+        scalar reductions + keypoint z, crops.  Host (as in the reference, and
+        sequential over the chunk): angle flips + iterative 180-degree filter
+        (M/proc/proc.py:827-839), scalar and keypoint tables."""
+        cfg = self.cfg
+        raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+        n = raw.shape[0]
+        frame_idxs = np.arange(n) if frame_idxs is None else np.asarray(frame_idxs)
+        prepped = self.prep(raw)
+        inf = self.infer(prepped)
+        d2 = inf["d2_mask"]
+        cleaned, feats = self.features(prepped, d2)
+        area, hmean, z = F.frame_scalars(prepped, d2, cfg.min_height, cfg.max_height,
+                                         keypoints=inf["sel_keypoints"], z_frames=cleaned)
+        cen = feats["centroid"].cpu().numpy()
+        ori = feats["orientation"].cpu().numpy()
+        axl = feats["axis_length"].cpu().numpy()
+        kp = inf["sel_keypoints"].cpu().numpy()
+        angles, flips = F.finalize_angles(ori, axl, cen, kp)
+        track = {"centroid": cen, "orientation": np.array(angles), "axis_length": axl, "contour": []}
+        scalars = F.compute_scalars(None, track, cfg.min_height, cfg.max_height, true_depth,
+                                    reductions=(area.cpu().numpy(), hmean.cpu().numpy()))
+        keypoints = F.keypoints_to_dict(kp, None, cen, track["orientation"], true_depth=true_depth,
+                                        z_data=z.cpu().numpy())
+        depth, mask = self.crop(prepped, d2, torch.from_numpy(cen).cuda(), torch.from_numpy(track["orientation"]).cuda())
+        return {
+            "chunk": prepped, "frame_idxs": frame_idxs, "offset": offset,
+            "features": {"cleaned_frames": cleaned, "masks": d2, "features": track, "flips": flips,
+                         "keypoints": kp, "num_instances": inf["nkeep"].cpu().numpy()},
+            "scalars": scalars, "keypoints": keypoints,
+            "depth_frames": depth.cpu().numpy(), "mask_frames": mask.cpu().numpy(),
+        }
 
     def back(self, prepped: torch.Tensor, cleaned: torch.Tensor):
         """Model-dependent tail: forward + selection, moments, angle, crops."""

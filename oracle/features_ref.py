@@ -3,6 +3,9 @@ INFRASTRUCTURE ONLY).
 
 * nms_mask_instances  M/pipeline/process_features_step.py:63-113 (mask-IoU
   NMS with the reference's deletion quirk), on (n, H, W) bool masks + scores.
+* frame_scalars_ref   the per-frame reductions of compute_scalars
+  (M/proc/scalars.py:79-103) and the keypoint z lookup of keypoints_to_dict
+  (M/proc/keypoints.py:122-130) -- checker of mdx_frame_scalars.
 """
 from __future__ import annotations
 
@@ -34,3 +37,25 @@ def nms_mask_instances(masks: np.ndarray, scores: np.ndarray, iou_threshold: flo
         over = np.where(ious > iou_threshold)[0]
         idxs = np.delete(idxs, np.unique(np.concatenate(([last], over))))
     return [int(orig[p]) for p in pick]
+
+
+def frame_scalars_ref(frames, masks, min_height, max_height, keypoints=None, z_frames=None):
+    """(area_px int64 (n,), height_ave float64 (n,), z_data float64 (n,K) | None),
+    literally as the reference computes them."""
+    fm = frames if masks is None else frames * masks          # uint8 product
+    masked = np.logical_and(fm > min_height, fm < max_height)
+    area = np.sum(masked, axis=(1, 2)).astype(np.int64)
+    hmean = np.zeros(fm.shape[0])
+    for i in range(fm.shape[0]):
+        if area[i] > 0:
+            hmean[i] = np.mean(fm[i, masked[i]])
+    z = None
+    if keypoints is not None:
+        zf = frames if z_frames is None else z_frames
+        with np.errstate(invalid="ignore"):
+            x = np.clip(np.floor(keypoints[:, :, 0]).astype(int), 0, zf.shape[2] - 1)
+            y = np.clip(np.floor(keypoints[:, :, 1]).astype(int), 0, zf.shape[1] - 1)
+        z = np.zeros((zf.shape[0], keypoints.shape[1]))
+        for k in range(keypoints.shape[1]):
+            z[:, k] = zf[np.arange(zf.shape[0]), y[:, k], x[:, k]]
+    return area, hmean, z

@@ -148,3 +148,42 @@ def test_inpaint_dense_holes(mdx, p, seed):
     got = proc.fill_invalid_pixels(f.copy(), m)
     want = O.inpaint_ns(f, m)
     np.testing.assert_array_equal(got, want)
+
+
+def test_frame_scalars_matches_oracle(mdx):
+    """Area / mean height of frames*masks and the keypoint z lookup, bit-exact
+    against the numpy restatement (NaN / inf / out-of-range keypoints included)."""
+    from oracle import features_ref as FR
+    from moseq2_detectron_extract_amd import features as F
+    rng = np.random.default_rng(21)
+    fr = rng.integers(0, 140, size=(7, 61, 83), dtype=np.uint8)   # W not a multiple of 16: ragged tail path
+    mk = (rng.random(fr.shape) < 0.5).astype(np.uint8)
+    mk[2] = 0
+    kp = np.concatenate([rng.uniform(-20, 100, (7, 8, 2)), rng.random((7, 8, 1))], -1)
+    kp[1, 3, :2] = [np.nan, 4.0]; kp[4, 0, :2] = [np.inf, -np.inf]; kp[5, 5, :2] = [1e300, -1e300]
+    zf = rng.integers(0, 255, size=fr.shape, dtype=np.uint8)
+    for lo, hi in ((10, 100), (0, 100), (-1, 256)):
+        a, h, z = F.frame_scalars(fr, mk, lo, hi, keypoints=kp, z_frames=zf)
+        ra, rh, rz = FR.frame_scalars_ref(fr, mk, lo, hi, keypoints=kp, z_frames=zf)
+        np.testing.assert_array_equal(a.cpu().numpy(), ra)
+        np.testing.assert_array_equal(h.cpu().numpy(), rh)
+        np.testing.assert_array_equal(z.cpu().numpy(), rz)
+
+
+def test_compute_scalars_and_keypoints_on_device_match_reference(mdx):
+    """compute_scalars / keypoints_to_dict with their reductions on the GPU
+    against the reference's own outputs (tests/golden/ref_features.npz)."""
+    import os
+    import torch
+    from moseq2_detectron_extract_amd import features as F
+    gf = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_features.npz")))
+    fr, mk = gf["sc_frames"], gf["sc_masks"]
+    tf = {k: gf[f"sc_tf_{k}"] for k in ("centroid", "axis_length", "orientation")}
+    for mh, xh, td in [(10, 100, 673.1), (0, 100, 650.0)]:
+        got = F.compute_scalars(torch.from_numpy(fr * mk).cuda(), tf, mh, xh, td)
+        for k, v in got.items():
+            np.testing.assert_allclose(v, gf[f"sc_{mh}_{xh}_{k}"], rtol=4e-16, atol=0, err_msg=k)
+    kd = F.keypoints_to_dict(gf["kd_kp"], torch.from_numpy(gf["kd_frames"]).cuda(), gf["kd_cen"], gf["kd_ang"],
+                             true_depth=660.0)
+    for i, k in enumerate(list(gf["kd_keys"])):
+        np.testing.assert_allclose(kd[k], gf[f"kd_{i}"], rtol=1e-12, atol=1e-9, equal_nan=True, err_msg=k)

@@ -439,3 +439,34 @@ def test_overlapped_extractor_matches_serial(mdx):
     for w, g in zip(want, got):
         for k in ("depth_frames", "mask_frames", "centroid", "angle", "keypoints"):
             torch.testing.assert_close(g[k], w[k], rtol=0, atol=0, equal_nan=True)
+
+
+def test_process_chunk_data_dict(mdx):
+    """Full chunk through the device path (tracking off): the writer's data
+    dict, with crops equal to the oracle crop at the host-final angles and
+    scalars equal to the oracle reductions fed through the same host code."""
+    from moseq2_detectron_extract_amd import features as F
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    from oracle import features_ref as FR
+    from oracle import frameops as O
+    s = synth.SyntheticSession(6, seed=4)
+    raw = s.frames(0, 6)
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
+    d = ex.process_chunk(raw, np.arange(100, 106), 0, true_depth=s.true_depth)
+    for k in ("chunk", "frame_idxs", "offset", "features", "scalars", "keypoints", "depth_frames", "mask_frames"):
+        assert k in d
+    assert d["depth_frames"].shape == (6, 80, 80) and d["mask_frames"].dtype == np.uint8
+    assert set(d["scalars"]) == set(F.scalar_attributes())
+    assert set(d["keypoints"]) == set(F.keypoint_attributes())
+    tr = d["features"]["features"]
+    prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
+    d2 = d["features"]["masks"].cpu().numpy()
+    np.testing.assert_array_equal(d["depth_frames"], O.crop_and_rotate_frames(prepped, tr["centroid"], tr["orientation"]))
+    np.testing.assert_array_equal(d["mask_frames"], O.crop_and_rotate_frames(d2, tr["centroid"], tr["orientation"]))
+    area, hmean, _ = FR.frame_scalars_ref(prepped, d2, 0, 100)
+    want = F.compute_scalars(None, tr, 0, 100, s.true_depth, reductions=(area, hmean))
+    for k in want:
+        np.testing.assert_array_equal(d["scalars"][k], want[k], err_msg=k)
