@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="run batches back to back on one stream instead of the two-stream pipeline")
+                    help="run batches back to back on one stream instead of the multi-stream pipeline")
+    ap.add_argument("--model-streams", type=int, default=2,
+                    help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
 
 
@@ -153,7 +155,7 @@ def main():
     if world > 1:
         gather_bufs = [torch.empty((B, 2, 80, 80), dtype=torch.uint8, device="cuda") for _ in range(world)]
 
-    pipe = None if args.no_overlap else OverlappedExtractor(ex)
+    pipe = None if args.no_overlap else OverlappedExtractor(ex, args.model_streams)
 
     def deliver(r):
         if r is not None and world > 1:
@@ -225,8 +227,9 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "frame": [424, 512],
                        "model_gflop_per_frame": round(flops_per_image(cfg) / 1e9, 2),
                        "parallelism": f"frame-sharded x{world}",
-                       "streams": "1" if args.no_overlap else "3 (prep/inpaint/clean of batch i+2, model + mask "
-                                                              "selection of batch i+1, moments/crop of batch i)"},
+                       "streams": "1" if args.no_overlap else f"{2 + args.model_streams} (prep/inpaint/clean of the "
+                                  f"newest batch, {args.model_streams} model forwards + mask selection of the next "
+                                  f"batches, moments/crop of the oldest)"},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

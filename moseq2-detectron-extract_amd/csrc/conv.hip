@@ -421,11 +421,23 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 // swizzle is applied on the global source address; fragment reads are then
 // bank-conflict-free for the ds_read_b128 lane groups.
 // ---------------------------------------------------------------------------
-constexpr int G_BM = 256, G_BN = 256, G_THREADS = 512;
-constexpr int G_SUB = (G_BM + G_BN) * 64;  // bytes per 32-deep K-substep
-constexpr int G_NBUF = 4;
-constexpr int G_EPI_PITCH = 68;            // fp32 pitch of a wave's 64x64 staging block
-constexpr int G_LDS = (G_NBUF * G_SUB > 8 * 64 * G_EPI_PITCH * 4) ? G_NBUF * G_SUB : 8 * 64 * G_EPI_PITCH * 4;
+// NW waves (8: 256x256 tile, 4: 128x128 tile); tile = 32 NW rows of A and of
+// B.  Waves form WM_(2) x (NW/2); wave tile (BM/2) x (BN/(NW/2)).
+template <int NW>
+struct GTile {
+    static constexpr int THREADS = 64 * NW, BM = 32 * NW, BN = 32 * NW;
+    static constexpr int WM = 2, WN = NW / 2;
+    static constexpr int WROWS = BM / WM, WCOLS = BN / WN;      // wave tile
+    static constexpr int TI = WROWS / 16, TJ = WCOLS / 16;      // MFMA tiles per wave
+    static constexpr int SUB = (BM + BN) * 64;                  // bytes per 32-deep K-substep
+    static constexpr int NBUF = 4;
+    static constexpr int EPI_PITCH = 68;                        // fp32 pitch of a wave's 64-column block
+    static constexpr int EPI_ROWS = 64;                         // rows per epilogue pass
+    static constexpr int EPI = NW * EPI_ROWS * EPI_PITCH * 4;
+    static constexpr int LDS = NBUF * SUB > EPI ? NBUF * SUB : EPI;
+};
+constexpr int G_BM = GTile<8>::BM, G_BN = GTile<8>::BN, G_THREADS = GTile<8>::THREADS;
+constexpr int G_LDS = GTile<8>::LDS;
 
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];  // zero source for padding / out-of-range rows
 
@@ -437,8 +449,10 @@ __device__ __forceinline__ void glds16(const void *src, char *dst) {
 
 __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-template <typename TO>
-__global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
+template <typename TO, int NW, bool g_setprio>
+__global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
+    using GT = GTile<NW>;
+    constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int tile;
     {
@@ -447,9 +461,9 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
         tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
     }
     const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int m0 = tm * G_BM, n0 = tn * G_BN;
+    const int m0 = tm * GT::BM, n0 = tn * GT::BN;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 2, wn = wid & 3;
+    const int wm = wid / GT::WN, wn = wid - wm * GT::WN;
 
     // DMA descriptors: instruction j of wave w fills LDS rows 32w + 16j .. +16
     const _Float16 *X = reinterpret_cast<const _Float16 *>(a.x);
@@ -479,8 +493,8 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
     auto issue = [&](int buf) {
         const int kofs = i_kci + 32 * i_half;
         const int kglob = (i_kky * a.KW + i_kkx) * a.Cin + kofs;
-        char *As = smem + buf * G_SUB + 32 * wid * 64;
-        char *Bs = smem + buf * G_SUB + G_BM * 64 + 32 * wid * 64;
+        char *As = smem + buf * SUB + 32 * wid * 64;
+        char *Bs = smem + buf * SUB + BM * 64 + 32 * wid * 64;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
@@ -505,36 +519,38 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
         }
     };
 
-    float4v acc[8][4];
+    float4v acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
     const int T = a.K / 32;  // substeps
     // fragment rows of this lane: r = 16 i + (lane & 15) (+ multiples of 64)
     const int off = ((lane >> 4) ^ g_swz(lane & 15)) * 16;
-    const char *Abase = smem + (wm * 128 + (lane & 15)) * 64 + off;
-    const char *Bbase = smem + G_BM * 64 + (wn * 64 + (lane & 15)) * 64 + off;
+    const char *Abase = smem + (wm * GT::WROWS + (lane & 15)) * 64 + off;
+    const char *Bbase = smem + BM * 64 + (wn * GT::WCOLS + (lane & 15)) * 64 + off;
     // fragments are register double-buffered: the LDS reads of substep t+1
-    // are in flight while the 32 MFMAs of substep t run from registers
-    half8 fa[2][8], fb[2][4];
+    // are in flight while the MFMAs of substep t run from registers
+    half8 fa[2][TI], fb[2][TJ];
     auto read_frags = [&](int t, int set) {
-        const char *Ab = Abase + (t & 3) * G_SUB;
-        const char *Bb = Bbase + (t & 3) * G_SUB;
+        const char *Ab = Abase + (t & 3) * SUB;
+        const char *Bb = Bbase + (t & 3) * SUB;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[set][j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
+        for (int j = 0; j < TJ; ++j) fb[set][j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
+        for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
     };
     auto mma = [&](int set) {
+        if (g_setprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TJ; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+        if (g_setprio) __builtin_amdgcn_s_setprio(0);
     };
-    // wait until substep u has landed (DMAs issued for substeps <= min(T-1, u+2)... counted per thread)
+    // wait until substep u has landed (4 DMAs per thread per substep)
     auto wait_landed = [&](int u, int issued_upto) {
         const int ahead = issued_upto - u;
         if (ahead >= 2)
@@ -577,24 +593,28 @@ __global__ __launch_bounds__(G_THREADS, 1) void k_conv256(ConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
-    // epilogue: per wave, two passes of 64 rows x 64 cols through its own LDS block
-    float *Cs = reinterpret_cast<float *>(smem) + wid * 64 * G_EPI_PITCH;
+    // epilogue: per wave, passes of 64 rows x WCOLS (= 64) columns through its
+    // own LDS block
+    static_assert(GT::WCOLS == 64, "epilogue stages 64-column wave blocks");
+    constexpr int NPASS = GT::WROWS / GT::EPI_ROWS;
+    constexpr int IPP = GT::EPI_ROWS / 16;  // MFMA row tiles per pass
+    float *Cs = reinterpret_cast<float *>(smem) + wid * GT::EPI_ROWS * GT::EPI_PITCH;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NPASS; ++h) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < IPP; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TJ; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    Cs[(i * 16 + (lane >> 4) * 4 + r) * G_EPI_PITCH + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
+                    Cs[(i * 16 + (lane >> 4) * 4 + r) * GT::EPI_PITCH + j * 16 + (lane & 15)] = acc[IPP * h + i][j][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         finish_batch<TO, 8>(a, [&](int q, int &gm, int &gn0, const float *&src) {
             const int item = lane + 64 * q;
             const int row = item >> 3, ch = item & 7;
-            gm = m0 + wm * 128 + 64 * h + row;
-            gn0 = n0 + wn * 64 + ch * 8;
-            src = Cs + row * G_EPI_PITCH + ch * 8;
+            gm = m0 + wm * GT::WROWS + GT::EPI_ROWS * h + row;
+            gn0 = n0 + wn * GT::WCOLS + ch * 8;
+            src = Cs + row * GT::EPI_PITCH + ch * 8;
             if (gm >= a.M || gn0 >= a.Cout) gm = -1;
         });
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -611,6 +631,22 @@ static int g_large_tiles = 1;
 extern "C" int mdx_conv_set_large_tiles(int mode) {
     const int old = g_large_tiles;
     g_large_tiles = mode;
+    return old;
+}
+// 128x128 LDS-DMA kernel policy: 0 never, 1 when the layer has at least
+// g_dma128_min_tiles tiles (and no wider kernel was chosen), 2 whenever eligible
+static int g_dma128 = 0, g_dma128_min_tiles = 0;
+// s_setprio(1) around the MFMA cluster of the LDS-DMA kernels (experiment knob)
+static int g_prio = 0;
+extern "C" int mdx_conv_set_mfma_prio(int on) {
+    const int old = g_prio;
+    g_prio = on;
+    return old;
+}
+extern "C" int mdx_conv_set_dma128(int mode, int min_tiles) {
+    const int old = g_dma128;
+    g_dma128 = mode;
+    g_dma128_min_tiles = min_tiles;
     return old;
 }
 // layers with K <= g_narrow_kmax use the 64-wide N tile (4 workgroups per CU:
@@ -681,20 +717,39 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.relu = relu;
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
-    // large fp16 layers: the 256x256 LDS-DMA kernel when it fills the chip
-    {
+    // fp16 layers with Cin % 64 == 0: the LDS-DMA pipelined kernels -- the
+    // 256x256 tile when it fills the chip, else (policy) the 128x128 tile
+    if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) && KH * KW * Cin > g_narrow_kmax) {
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
         const bool big = Cout >= 192 && t256 >= 384;
-        if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) && KH * KW * Cin > g_narrow_kmax &&
-            (g_large_tiles == 2 || (g_large_tiles == 1 && big))) {
+        if (g_large_tiles == 2 || (g_large_tiles == 1 && big)) {
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
             a.ksplit = 1;
             a.ksteps = a.K / 64;
-            if (out_dtype == 1)
-                hipLaunchKernelGGL(k_conv256<_Float16>, dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            if (out_dtype == 1 && g_prio)
+                hipLaunchKernelGGL((k_convg<_Float16, 8, true>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            else if (out_dtype == 1)
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
             else
-                hipLaunchKernelGGL(k_conv256<float>, dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            MDX_CHECK_LAUNCH("mdx_conv2d");
+            return MDX_OK;
+        }
+        const long long t128 = ceil_div(M, 128) * ceil_div(Cout, 128);
+        if (g_dma128 == 2 || (g_dma128 == 1 && Cout > 64 && t128 >= g_dma128_min_tiles)) {
+            using G4 = GTile<4>;
+            a.tiles_n = (int)ceil_div(Cout, G4::BN);
+            a.tiles_total = (int)t128;
+            a.ksplit = 1;
+            a.ksteps = a.K / 64;
+            if (out_dtype == 1 && g_prio)
+                hipLaunchKernelGGL((k_convg<_Float16, 4, true>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
+            else if (out_dtype == 1)
+                hipLaunchKernelGGL((k_convg<_Float16, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s,
+                                   a);
+            else
+                hipLaunchKernelGGL((k_convg<float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }

@@ -183,10 +183,22 @@ class MaskRCNN:
             self.kp_deconv_b = self._dev(sd["roi_heads.keypoint_head.score_lowres.bias"], torch.float32)
         self.pixel_mean = np.ascontiguousarray(np.asarray(sd["pixel_mean"].reshape(-1), np.float32))
         self.pixel_std = np.ascontiguousarray(np.asarray(sd["pixel_std"].reshape(-1), np.float32))
-        self.gn_stats = None
-        self.splitk_ws = None
+        # per-stream workspaces: forwards of different batches may run
+        # concurrently on different HIP streams (pipeline.OverlappedExtractor)
+        self._ws = {}
+        self._keep = {}
 
     # ------------------------------------------------------------ layers
+    def workspace(self, name: str, nbytes: int) -> torch.Tensor:
+        """Scratch buffer `name` of >= nbytes owned by the current stream (work
+        on one stream is ordered, so reuse within it is safe)."""
+        key = (torch.cuda.current_stream().cuda_stream, name)
+        t = self._ws.get(key)
+        if t is None or t.numel() * 4 < nbytes:
+            t = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=self.device)
+            self._ws[key] = t
+        return t
+
     def conv(self, x, N, H, W, c: Conv, relu, out=None, residual=None, out_f32=False, out_mode=0):
         OH = (H + 2 * c.pad - c.k) // c.stride + 1
         OW = (W + 2 * c.pad - c.k) // c.stride + 1
@@ -196,20 +208,17 @@ class MaskRCNN:
                 out = torch.empty((N, 2 * OH, 2 * OW, c.cout // 4), dtype=odt, device=self.device)
             else:
                 out = torch.empty((N, OH, OW, c.cout), dtype=odt, device=self.device)
-        if self.splitk_ws is None:
-            self.splitk_ws = torch.empty(SPLITK_WS_BYTES // 4, dtype=torch.float32, device=self.device)
+        ws = self.workspace("splitk", SPLITK_WS_BYTES)
         call("mdx_conv2d_splitk", _p(x), N, H, W, c.cin, _p(c.w), _p(c.b), c.cout, c.k, c.k, c.stride, c.pad,
              _p(residual), int(relu), out_mode, self.dcode, 0 if out_f32 else self.dcode, _p(out), 0,
-             _p(self.splitk_ws), SPLITK_WS_BYTES, _stream())
+             _p(ws), SPLITK_WS_BYTES, _stream())
         return out, OH, OW
 
     def groupnorm(self, x, N, H, W, C, g, up=None, fuse=0):
         out = torch.empty_like(x)
-        need = (call("mdx_groupnorm_workspace_bytes", N, H, W, self.cfg.gn_groups) + 3) // 4
-        if self.gn_stats is None or self.gn_stats.numel() < need:
-            self.gn_stats = torch.empty(need, dtype=torch.float32, device=self.device)
+        ws = self.workspace("gn", call("mdx_groupnorm_workspace_bytes", N, H, W, self.cfg.gn_groups))
         call("mdx_groupnorm", _p(x), N, H, W, C, self.cfg.gn_groups, float(self.cfg.gn_eps), _p(g[0]), _p(g[1]),
-             _p(up), fuse, self.dcode, _p(out), _p(self.gn_stats), _stream())
+             _p(up), fuse, self.dcode, _p(out), _p(ws), _stream())
         return out
 
     # ------------------------------------------------------------ forward
@@ -282,7 +291,7 @@ class MaskRCNN:
              self.cell_anchors.ctypes.data_as(ctypes.c_void_p), float(cfg.anchor_offset), h, w,
              cfg.rpn_pre_nms_topk_test, post, float(cfg.rpn_nms_thresh), float(cfg.rpn_min_box_size),
              float(cfg.bbox_reg_clamp), _p(boxes), _p(scores), _p(counts), _p(ws_), _stream())
-        self._keep = (heads, ws_)  # keep alive until the stream consumes them
+        self._keep[torch.cuda.current_stream().cuda_stream] = (heads, ws_)  # alive until the stream consumes them
         return boxes, scores, counts
 
     def roi_align(self, feats, rois, counts, per_image, P):

@@ -18,6 +18,7 @@ h5 schema drop in unchanged.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
@@ -173,23 +174,28 @@ class GPUExtractor:
 
 
 class OverlappedExtractor:
-    """Three-stage software pipeline over consecutive batches, one HIP stream
-    per stage: front (prep + inpaint + clean) of batch i+2, model forward +
-    mask selection of batch i+1 and tail (moments, angle, crops) of batch i
-    run concurrently, so the frame-side kernels (few, latency-bound
-    workgroups) fill the CUs the convolutions leave idle.  Results come out in
-    submission order, two batches behind.
+    """Software pipeline over consecutive batches on separate HIP streams:
+    front (prep + inpaint + clean) of batch i+2, model forward + mask
+    selection of batch i+1 and tail (moments, angle, crops) of batch i run
+    concurrently, so the frame-side kernels (few, latency-bound workgroups)
+    fill the CUs the convolutions leave idle.  With model_streams=2 the
+    forwards of consecutive batches alternate between two streams and
+    overlap each other too (the RPN / NMS / post-processing kernels and the
+    small late layers of one forward leave most CUs idle).  Results come out
+    in submission order, model_streams + 1 batches behind.
 
-    submit(raw) -> results of the batch submitted two calls earlier (or None);
+    submit(raw) -> results of the batch submitted model_streams + 1 calls
+    earlier (or None);
     flush() -> list of the results still in flight."""
 
-    def __init__(self, extractor: GPUExtractor):
+    def __init__(self, extractor: GPUExtractor, model_streams: int = 2):
         self.ex = extractor
         self.s_front = torch.cuda.Stream()
-        self.s_model = torch.cuda.Stream()
+        self.s_models = [torch.cuda.Stream() for _ in range(max(1, model_streams))]
+        self.n_model = 0
         self.s_tail = torch.cuda.Stream()
-        self.fronted = None   # (prepped, cleaned, event) awaiting the model
-        self.modeled = None   # (prepped, cleaned, inf, event) awaiting the tail
+        self.fronted = None            # (prepped, cleaned, event) awaiting the model
+        self.modeled = collections.deque()  # (prepped, cleaned, inf, event) awaiting the tail
 
     def _front(self, raw):
         caller = torch.cuda.current_stream()
@@ -203,12 +209,14 @@ class OverlappedExtractor:
 
     def _model(self, item):
         prepped, cleaned, ev = item
-        self.s_model.wait_event(ev)
-        with torch.cuda.stream(self.s_model):
-            prepped.record_stream(self.s_model)
+        sm = self.s_models[self.n_model % len(self.s_models)]
+        self.n_model += 1
+        sm.wait_event(ev)
+        with torch.cuda.stream(sm):
+            prepped.record_stream(sm)
             inf = self.ex.infer(prepped)
             ev2 = torch.cuda.Event()
-            ev2.record(self.s_model)
+            ev2.record(sm)
         return prepped, cleaned, inf, ev2
 
     def _tail(self, item):
@@ -225,20 +233,25 @@ class OverlappedExtractor:
         return out
 
     def submit(self, raw: torch.Tensor):
-        # issue order tail(i-2), model(i-1), front(i): each stage's inputs were
-        # issued a call earlier, so all three run concurrently on the device
-        out = self._tail(self.modeled) if self.modeled is not None else None
-        self.modeled = self._model(self.fronted) if self.fronted is not None else None
+        # issue order: tail of the oldest modeled batch (once `depth` forwards
+        # are in flight), forward of the fronted batch, front of `raw`; every
+        # stage's inputs were issued on an earlier call, so the stages (and up
+        # to `depth` forwards) run concurrently on the device
+        out = None
+        if len(self.modeled) >= len(self.s_models):
+            out = self._tail(self.modeled.popleft())
+        if self.fronted is not None:
+            self.modeled.append(self._model(self.fronted))
         self.fronted = self._front(raw)
         return out
 
     def flush(self):
         outs = []
-        if self.modeled is not None:
-            outs.append(self._tail(self.modeled))
-        self.modeled = self._model(self.fronted) if self.fronted is not None else None
-        self.fronted = None
-        if self.modeled is not None:
-            outs.append(self._tail(self.modeled))
-        self.modeled = None
+        if self.fronted is not None:
+            if len(self.modeled) >= len(self.s_models):
+                outs.append(self._tail(self.modeled.popleft()))
+            self.modeled.append(self._model(self.fronted))
+            self.fronted = None
+        while self.modeled:
+            outs.append(self._tail(self.modeled.popleft()))
         return outs

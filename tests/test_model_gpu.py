@@ -42,7 +42,7 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -65,15 +65,19 @@ def test_conv2d(mdx, dtype, case, ksplit):
     rd = res.cuda() if res is not None else None
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     dc = 1 if dtype == "fp16" else 0
-    if ksplit == "large":
+    if ksplit in ("large", "dma128"):
         if dtype != "fp16" or Cin % 64:
-            pytest.skip("256x256 kernel: fp16, Cin % 64 == 0")
-        old = call("mdx_conv_set_large_tiles", 2)
+            pytest.skip("LDS-DMA kernels: fp16, Cin % 64 == 0")
+        old_nk = call("mdx_conv_set_narrow_kmax", 0)
+        old = call("mdx_conv_set_large_tiles", 2 if ksplit == "large" else 0)
+        old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
         try:
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
         finally:
             call("mdx_conv_set_large_tiles", old)
+            call("mdx_conv_set_narrow_kmax", old_nk)
+            call("mdx_conv_set_dma128", old_d, 0)
     elif ksplit == 1:
         call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
              P(out), None)
