@@ -140,10 +140,11 @@ int mdx_conv_set_large_tiles(int mode);
  * workgroups per CU for HBM-bound small-K layers).  Returns the old value. */
 int mdx_conv_set_narrow_kmax(int kmax);
 /* Policy for the 128x128 LDS-DMA fp16 kernel (Cin % 64 == 0): 0 never, 1 when
- * the layer has >= min_tiles 128x128 tiles and the 256x256 kernel was not
- * chosen, 2 whenever eligible.  Returns the old mode. */
+ * the layer has >= min_tiles 128x128 tiles, 2 whenever eligible (default 0:
+ * slower than the 256x256 / split-K kernels inside the full forward).
+ * Returns the old mode. */
 int mdx_conv_set_dma128(int mode, int min_tiles);
-/* s_setprio(1) around the MFMA cluster of the LDS-DMA kernels (0/1). */
+/* Issue the LDS-DMA pieces between the MFMAs of the LDS-DMA kernels (0/1). */
 int mdx_conv_set_mfma_prio(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,

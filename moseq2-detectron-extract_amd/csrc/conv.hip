@@ -449,7 +449,7 @@ __device__ __forceinline__ void glds16(const void *src, char *dst) {
 
 __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-template <typename TO, int NW, bool g_setprio>
+template <typename TO, int NW, bool ILV>
 __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
@@ -490,22 +490,27 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     }
     // issue state (uniform): the 64-chunk being issued and its tap
     int i_kci = 0, i_kkx = 0, i_kky = 0, i_half = 0;
-    auto issue = [&](int buf) {
+    // DMA piece p of the substep being issued into buffer buf: p = 0, 1 the A
+    // rows of instruction j = p, p = 2, 3 the B rows of j = p - 2
+    auto issue_piece = [&](int buf, int p) {
         const int kofs = i_kci + 32 * i_half;
-        const int kglob = (i_kky * a.KW + i_kkx) * a.Cin + kofs;
-        char *As = smem + buf * SUB + 32 * wid * 64;
-        char *Bs = smem + buf * SUB + BM * 64 + 32 * wid * 64;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        if (p < 2) {
+            const int j = p;
             const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
             const bool ok = a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
             const void *src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kofs)
                                  : (const void *)g_zero16;
-            glds16(src, As + j * 1024);
+            glds16(src, smem + buf * SUB + 32 * wid * 64 + j * 1024);
+        } else {
+            const int j = p - 2;
+            const int kglob = (i_kky * a.KW + i_kkx) * a.Cin + kofs;
+            glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16,
+                   smem + buf * SUB + BM * 64 + 32 * wid * 64 + j * 1024);
         }
+    };
+    auto issue = [&](int buf) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-            glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16, Bs + j * 1024);
+        for (int p = 0; p < 4; ++p) issue_piece(buf, p);
         // next substep: half, then tap, then channel chunk
         if (++i_half == 2) {
             i_half = 0;
@@ -542,13 +547,11 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
     };
     auto mma = [&](int set) {
-        if (g_setprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
-        if (g_setprio) __builtin_amdgcn_s_setprio(0);
     };
     // wait until substep u has landed (4 DMAs per thread per substep)
     auto wait_landed = [&](int u, int issued_upto) {
@@ -568,6 +571,15 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     read_frags(0, 0);
     // iteration t: [wait t+1, barrier, DMA t+3, read frags t+1] then MFMAs of t
+    // MFMAs q0 .. q1 - 1 of the wave's TI x TJ tile loop
+    auto mma_range = [&](int set, int q0, int q1) {
+#pragma unroll
+        for (int q = 0; q < TI * TJ; ++q) {
+            if (q < q0 || q >= q1) continue;
+            const int i = q / TJ, j = q - i * TJ;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+        }
+    };
     auto step = [&](int t, int cur) {
         if (t + 1 < T) {
             wait_landed(t + 1, issued);
@@ -576,11 +588,37 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
             // (t + 3) & 3 == (t - 1) & 3, which the next DMA overwrites
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
+            read_frags(t + 1, cur ^ 1);
             if (t + 3 < T) {
+                if (ILV) {
+                    // the four DMA pieces ride in the MFMA issue gaps instead of
+                    // stalling every wave right after the barrier
+                    constexpr int QP = TI * TJ / 4;
+                    const int buf = (t + 3) & 3;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        issue_piece(buf, p);
+                        __builtin_amdgcn_sched_barrier(0);
+                        mma_range(cur, p * QP, (p + 1) * QP);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (++i_half == 2) {
+                        i_half = 0;
+                        if (++i_kkx == a.KW) {
+                            i_kkx = 0;
+                            if (++i_kky == a.KH) {
+                                i_kky = 0;
+                                i_kci += 64;
+                            }
+                        }
+                    }
+                    issued = t + 3;
+                    return;
+                }
                 issue((t + 3) & 3);
                 issued = t + 3;
             }
-            read_frags(t + 1, cur ^ 1);
         }
         mma(cur);
     };
@@ -635,9 +673,9 @@ extern "C" int mdx_conv_set_large_tiles(int mode) {
 }
 // 128x128 LDS-DMA kernel policy: 0 never, 1 when the layer has at least
 // g_dma128_min_tiles tiles (and no wider kernel was chosen), 2 whenever eligible
-static int g_dma128 = 0, g_dma128_min_tiles = 0;
-// s_setprio(1) around the MFMA cluster of the LDS-DMA kernels (experiment knob)
-static int g_prio = 0;
+static int g_dma128 = 0, g_dma128_min_tiles = 1536;
+// DMA pieces interleaved with the MFMAs in the 128x128 LDS-DMA kernel (0/1)
+static int g_prio = 1;
 extern "C" int mdx_conv_set_mfma_prio(int on) {
     const int old = g_prio;
     g_prio = on;
@@ -718,24 +756,10 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
     // fp16 layers with Cin % 64 == 0: the LDS-DMA pipelined kernels -- the
-    // 256x256 tile when it fills the chip, else (policy) the 128x128 tile
+    // 128x128 tile (DMA pieces interleaved with the MFMAs) for layers with
+    // many tiles, the 256x256 tile by policy, else the register-staged kernel
+    // (with split-K) below, which serves the small grids better
     if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) && KH * KW * Cin > g_narrow_kmax) {
-        const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && t256 >= 384;
-        if (g_large_tiles == 2 || (g_large_tiles == 1 && big)) {
-            a.tiles_n = (int)ceil_div(Cout, G_BN);
-            a.tiles_total = (int)t256;
-            a.ksplit = 1;
-            a.ksteps = a.K / 64;
-            if (out_dtype == 1 && g_prio)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, true>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
-            else if (out_dtype == 1)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
-            else
-                hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
-            MDX_CHECK_LAUNCH("mdx_conv2d");
-            return MDX_OK;
-        }
         const long long t128 = ceil_div(M, 128) * ceil_div(Cout, 128);
         if (g_dma128 == 2 || (g_dma128 == 1 && Cout > 64 && t128 >= g_dma128_min_tiles)) {
             using G4 = GTile<4>;
@@ -750,6 +774,21 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
                                    a);
             else
                 hipLaunchKernelGGL((k_convg<float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
+            MDX_CHECK_LAUNCH("mdx_conv2d");
+            return MDX_OK;
+        }
+        const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
+        const bool big = Cout >= 192 && t256 >= 384;
+        if (g_large_tiles == 2 || (g_large_tiles == 1 && big)) {
+            a.tiles_n = (int)ceil_div(Cout, G_BN);
+            a.tiles_total = (int)t256;
+            a.ksplit = 1;
+            a.ksteps = a.K / 64;
+            // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
+            if (out_dtype == 1)
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            else
+                hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }

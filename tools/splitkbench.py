@@ -57,7 +57,7 @@ def main():
                     go()
             except Exception as ex:  # split not allowed for this shape
                 call("mdx_conv_set_large_tiles", old)
-                call("mdx_conv_set_dma128", old_d, 0)
+                call("mdx_conv_set_dma128", old_d, 1536)
                 line += f"  ks{ks}: n/a"
                 continue
             e0.record()
@@ -66,10 +66,10 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             call("mdx_conv_set_large_tiles", old)
-            d = call("mdx_conv_set_dma128", old_d, 0)
+            d = call("mdx_conv_set_dma128", old_d, 1536)
             pr = call("mdx_conv_set_mfma_prio", oldp)
             t = e0.elapsed_time(e1) / 20 * 1e-3
-            tag = ("dma128" if d == 2 else ("auto" if ks == 0 else f"ks{ks}")) + ("+prio" if pr else "")
+            tag = ("dma128" if d == 2 else ("auto" if ks == 0 else f"ks{ks}")) + ("+ilv" if pr else "")
             line += f"  {tag}:{t * 1e6:6.1f}us/{flops / t / 1e12:4.0f}TF"
         print(line, flush=True)
 
