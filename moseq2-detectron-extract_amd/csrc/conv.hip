@@ -83,6 +83,7 @@ struct ConvArgs {
     int tiles_n, tiles_total;
     int ksplit, ksteps;  // split-K: K range of slice z = [z*ksteps*BK, (z+1)*ksteps*BK)
     float *part;         // [ksplit][M][Cout] fp32 partial sums (ksplit > 1)
+    int xbytes, wbytes;  // operand sizes for the range-checked buffer descriptors (< 2^31)
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -235,26 +236,33 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     int kr = kglob / a.Cin;
     int kkx = kr % a.KW, kky = kr / a.KW;
 
-    const T *X = reinterpret_cast<const T *>(a.x);
-    const T *Wt = reinterpret_cast<const T *>(a.w);
-    uint4 ra[4], rb[BLOADS];
+    // two register stages: the global loads of K-step t + 2 are issued while
+    // step t is multiplied, and stored to LDS at the end of step t + 1
+    uint4 ra[2][4], rb[2][BLOADS];
 
-    auto load_global = [&]() {
+    // buffer loads through range-checked descriptors: a padding / out-of-range
+    // piece gets an offset past the end and reads zeros from the hardware, so
+    // every lane issues every load with no branch (a per-piece "load or zero"
+    // select compiles to a branch + vmcnt(0) around each load)
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
         const bool kok = kglob < a.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                v = *reinterpret_cast<const uint4 *>(X + a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci);
-            ra[i] = v;
+            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const unsigned off =
+                (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * (long long)sizeof(T));
+            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < BLOADS; ++i) {
             const int gn = n0 + lrow + 32 * i;
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (kok && gn < a.Cout) u = *reinterpret_cast<const uint4 *>(Wt + (long long)gn * a.K + kglob);
-            rb[i] = u;
+            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * (long long)sizeof(T));
+            Bv[i] = __builtin_bit_cast(uint4,
+                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
         }
     };
     auto advance_k = [&]() {
@@ -272,13 +280,13 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     // fragment reads (rows l & 15, pieces 4 s + (l >> 4)) are then
     // bank-conflict-free for every ds_read_b128 lane group
     const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;  // (lrow + 32 i) >> 1 & 7 == lrow >> 1 & 7
-    auto store_lds = [&](int buf) {
+    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = ra[i];
+            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = A[i];
 #pragma unroll
         for (int i = 0; i < BLOADS; ++i)
-            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = rb[i];
+            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
     };
 
     float4v acc[TI][TJ];
@@ -289,15 +297,21 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
 
     const int nk_all = (a.K + BK - 1) / BK;
     const int nk = min(a.ksteps, nk_all - kz * a.ksteps);
-    load_global();
+    load_global(ra[0], rb[0]);
     advance_k();
-    store_lds(0);
+    store_lds(0, ra[0], rb[0]);
+    if (nk > 1) {
+        load_global(ra[1], rb[1]);
+        advance_k();
+    }
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
+    // iteration kt: registers [kt & 1] are free (their step is in LDS), [(kt +
+    // 1) & 1] hold step kt + 1
+    auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
+                     const uint4 (&Bs_)[BLOADS]) {
         const int cur = kt & 1;
-        const bool more = kt + 1 < nk;
-        if (more) {
-            load_global();
+        if (kt + 2 < nk) {
+            load_global(Ai, Bi);
             advance_k();
         }
         const char *Ab = As + cur * STAGE + (wm * (BM / 2) + (lane & 15)) * PITCH;
@@ -331,9 +345,15 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
             }
         }
-        if (more) store_lds(cur ^ 1);
+        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
         __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+        kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+        kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
     }
+    if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
 
     // ---- epilogue, in two halves of BM/2 rows (the LDS image is half the
     // tile, so a one-step-K launch fits 4 workgroups per CU): the waves owning
@@ -752,6 +772,13 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     MDX_REQUIRE(M < (1ll << 31), "mdx_conv2d: M too large");
     a.M = (int)M;
     a.K = KH * KW * Cin;
+    {
+        const long long es = in_dtype == 1 ? 2 : 4;
+        const long long xb = (long long)N * H * W * Cin * es, wb = (long long)Cout * a.K * es;
+        MDX_REQUIRE(xb < (1ll << 31) && wb < (1ll << 31), "mdx_conv2d: operands above 2 GiB are not supported");
+        a.xbytes = (int)xb;
+        a.wbytes = (int)wb;
+    }
     a.relu = relu;
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
