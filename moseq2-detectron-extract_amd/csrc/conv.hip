@@ -84,6 +84,7 @@ struct ConvArgs {
     int ksplit, ksteps;  // split-K: K range of slice z = [z*ksteps*BK, (z+1)*ksteps*BK)
     float *part;         // [ksplit][M][Cout] fp32 partial sums (ksplit > 1)
     int xbytes, wbytes;  // operand sizes for the range-checked buffer descriptors (< 2^31)
+    int rbytes;          // residual size (bytes), same purpose
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -149,12 +150,21 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
     int gms[NQ], gns[NQ];
     const float *srcs[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        item(q, gms[q], gns[q], srcs[q]);
-        if (gms[q] >= 0 && vec_ok && RS) {
-            const uint4 *rp = reinterpret_cast<const uint4 *>(RS + (long long)gms[q] * a.Cout + gns[q]);
+    for (int q = 0; q < NQ; ++q) item(q, gms[q], gns[q], srcs[q]);
+    if (vec_ok && RS) {
+        // residual rows through a range-checked descriptor: skipped items read
+        // zeros past the end, so all loads issue back to back (no per-item
+        // branch and vmcnt(0))
+        const __amdgpu_buffer_rsrc_t rr_d = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
+                                                                            0x00020000);
 #pragma unroll
-            for (int w = 0; w < RW; ++w) rr[q][w] = rp[w];
+        for (int q = 0; q < NQ; ++q) {
+            const unsigned off = gms[q] >= 0
+                                     ? (unsigned)(((long long)gms[q] * a.Cout + gns[q]) * (long long)sizeof(TO))
+                                     : 0xFFFFFFE0u;
+#pragma unroll
+            for (int w = 0; w < RW; ++w)
+                rr[q][w] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr_d, off + 16u * w, 0, 0));
         }
     }
 #pragma unroll
@@ -778,6 +788,9 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
         MDX_REQUIRE(xb < (1ll << 31) && wb < (1ll << 31), "mdx_conv2d: operands above 2 GiB are not supported");
         a.xbytes = (int)xb;
         a.wbytes = (int)wb;
+        const long long rb = residual ? M * Cout * (out_dtype == 1 ? 2 : 4) : 0;
+        MDX_REQUIRE(rb < (1ll << 31), "mdx_conv2d: residual above 2 GiB is not supported");
+        a.rbytes = (int)rb;
     }
     a.relu = relu;
     a.out_mode = out_mode;
