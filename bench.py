@@ -48,14 +48,28 @@ def parse():
     return ap.parse_args()
 
 
+KERNEL_SYMBOLS = {  # MDX_CONV_KERNEL_* -> rocprofv3 symbol (fp16 in / fp16 out)
+    0: "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE",
+    1: "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE",
+    2: "_ZN3mdx7k_convgIDF16_Li8ELb0EEEvNS_8ConvArgsE",
+    3: "_ZN3mdx7k_convgIDF16_Li4ELb1EEEvNS_8ConvArgsE",
+}
+KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
+                2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM"}
+
+
 def conv_roofline(extractor, raw, steps=3, dump=None):
-    """Time every conv launch of a step with HIP events on the launch stream;
-    returns (algorithmic conv FLOP per step, conv seconds per step, launches)."""
+    """Time every conv launch of a step with HIP events on the launch stream
+    and tag it with the kernel the library chose (mdx_conv2d_last_plan).
+    Returns {kernel id: [algorithmic FLOP, seconds, launches]} per step plus
+    the totals over all conv launches."""
+    import ctypes
     import torch
+    from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import runtime as RT
-    model = extractor.predictor.model
     rec = []
     orig = RT.MaskRCNN.conv
+    kid, ksp = ctypes.c_int(), ctypes.c_int()
 
     def timed(self, x, N, H, W, c, relu, out=None, residual=None, out_f32=False, out_mode=0):
         s = torch.cuda.current_stream()
@@ -63,9 +77,11 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
         e0.record(s)
         r = orig(self, x, N, H, W, c, relu, out, residual, out_f32, out_mode)
         e1.record(s)
+        call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ksp))
         OH, OW = r[1], r[2]
         kalg = c.kalg or c.k * c.k * c.cin
-        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * kalg,
+        key = kid.value if not out_f32 else kid.value + 10  # fp32-output instances are other symbols
+        rec.append((e0, e1, 2.0 * N * OH * OW * c.cout * kalg, key, ksp.value,
                     (N * OH * OW, c.cout, c.k * c.k * c.cin, c.k, c.stride, out_mode, residual is not None)))
         return r
 
@@ -76,16 +92,48 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
         torch.cuda.synchronize()
     finally:
         RT.MaskRCNN.conv = orig
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in rec)
-    fl = sum(f for _, _, f, _ in rec)
+    per = {}
+    for e0, e1, f, key, ks, _ in rec:
+        d = per.setdefault(key, [0.0, 0.0, 0, 0])
+        d[0] += f / steps
+        d[1] += e0.elapsed_time(e1) * 1e-3 / steps
+        d[2] += 1.0 / steps
+        d[3] = max(d[3], ks)
     if dump:
-        per = len(rec) // steps
+        n = len(rec) // steps
         rows = [{"M": sh[0], "N": sh[1], "K": sh[2], "k": sh[3], "stride": sh[4], "mode": sh[5], "res": sh[6],
-                 "us": e0.elapsed_time(e1) * 1e3, "tflops": f / (e0.elapsed_time(e1) * 1e-3) / 1e12}
-                for e0, e1, f, sh in rec[-per:]]
+                 "kernel": key, "ksplit": ks, "us": e0.elapsed_time(e1) * 1e3,
+                 "tflops": f / (e0.elapsed_time(e1) * 1e-3) / 1e12}
+                for e0, e1, f, key, ks, sh in rec[-n:]]
         with open(dump, "w") as fh:
             json.dump(rows, fh, indent=0)
-    return fl / steps, ms / 1e3 / steps, len(rec) // steps
+    return per
+
+
+def roofline_line(per, dtype):
+    """Roofline object for the dominant conv kernel (most time per step)."""
+    peak = 2500.0 if dtype == "fp16" else 157.3
+    key = max(per, key=lambda k: per[k][1])
+    fl, sec, n, ks = per[key]
+    ach = fl / sec / 1e12
+    traffic = None
+    sym = KERNEL_SYMBOLS.get(key)
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_kernels.json")
+    if sym and os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                traffic = json.load(fh)["kernels"].get(sym, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    tot_f = sum(v[0] for v in per.values())
+    tot_s = sum(v[1] for v in per.values())
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": traffic,
+            "kernel": f"{KERNEL_NAMES.get(key, key)} ({sym}): {n:.0f} launches/step, "
+                      f"{fl / n / 1e9:.1f} GFLOP and {sec / n * 1e6:.1f} us per launch (HIP events on the launch "
+                      f"stream; traffic = PMC HBM bytes per launch)",
+            "all_conv": {"launches": round(sum(v[2] for v in per.values())), "tflop_per_step": round(tot_f / 1e12, 3),
+                         "ms_per_step": round(tot_s * 1e3, 3), "achieved": round(tot_f / tot_s / 1e12, 1)}}
 
 
 def cpu_baseline(nframes: int, dtype_cfg):
@@ -197,21 +245,8 @@ def main():
 
     roof = None
     if not args.no_roofline:
-        fl, sec, nl = conv_roofline(ex, raw_all[:B], dump=args.dump_convs)
-        peak = 2500.0 if args.dtype == "fp16" else 157.3
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "conv_pmc_summary.json")
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as fh:
-                    traffic = json.load(fh).get("hbm_bytes_per_step")
-            except Exception:
-                traffic = None
-        ach = fl / sec / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": traffic,
-                "kernel": f"k_conv<{args.dtype}> implicit-GEMM, {nl} launches/step, {fl / 1e12:.3f} TFLOP/step "
-                          f"in {sec * 1e3:.2f} ms (HIP events on the launch stream)"}
+        per = conv_roofline(ex, raw_all[:B], dump=args.dump_convs)
+        roof = roofline_line(per, args.dtype)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

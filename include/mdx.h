@@ -146,6 +146,11 @@ int mdx_conv_set_narrow_kmax(int kmax);
 int mdx_conv_set_dma128(int mode, int min_tiles);
 /* Issue the LDS-DMA pieces between the MFMAs of the LDS-DMA kernels (0/1). */
 int mdx_conv_set_mfma_prio(int on);
+/* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
+ * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
+ * K slices launched (the split-K reduction is a second launch). */
+enum { MDX_CONV_KERNEL_REG128 = 0, MDX_CONV_KERNEL_REG64 = 1, MDX_CONV_KERNEL_DMA256 = 2, MDX_CONV_KERNEL_DMA128 = 3 };
+int mdx_conv2d_last_plan(int *kernel, int *ksplit);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

@@ -693,6 +693,9 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
 
 using namespace mdx;
 
+// kernel chosen by the calling thread's last mdx_conv2d* call (measurement)
+static thread_local int t_plan_kernel = -1, t_plan_ksplit = 0;
+
 // dtype codes: 0 = fp32, 1 = fp16
 // large-tile kernel policy (tests): 0 never, 1 auto (default), 2 whenever eligible
 static int g_large_tiles = 1;
@@ -814,6 +817,8 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
                                    a);
             else
                 hipLaunchKernelGGL((k_convg<float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
+            t_plan_kernel = MDX_CONV_KERNEL_DMA128;
+            t_plan_ksplit = 1;
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
@@ -829,6 +834,8 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
                 hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
             else
                 hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+            t_plan_kernel = MDX_CONV_KERNEL_DMA256;
+            t_plan_ksplit = 1;
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
@@ -873,6 +880,15 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
+    t_plan_kernel = narrow ? MDX_CONV_KERNEL_REG64 : MDX_CONV_KERNEL_REG128;
+    t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d");
+    return MDX_OK;
+}
+
+extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
+    MDX_REQUIRE(kernel && ksplit, "mdx_conv2d_last_plan: null pointer");
+    *kernel = t_plan_kernel;
+    *ksplit = t_plan_ksplit;
     return MDX_OK;
 }

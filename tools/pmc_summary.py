@@ -41,6 +41,11 @@ def main():
         "top_kernels": dict(sorted(((k[:80], v) for k, v in kernels.items()),
                                    key=lambda kv: -kv[1]["hbm_bytes_per_step"])[:15]),
     }
+    summary["kernels"] = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_step"] / max(v["launches_per_step"], 1e-9),
+                              "fetch_bytes_per_launch": v["fetch_bytes_per_step"] / max(v["launches_per_step"], 1e-9),
+                              "write_bytes_per_launch": v["write_bytes_per_step"] / max(v["launches_per_step"], 1e-9),
+                              "launches_per_step": v["launches_per_step"]}
+                          for k, v in kernels.items()}
     with open(out, "w") as fh:
         json.dump(summary, fh, indent=1)
     print(json.dumps({k: summary[k] for k in ("hbm_bytes_per_step", "conv_launches_per_step")}))
