@@ -142,15 +142,17 @@ __device__ __forceinline__ int block_scan_excl(int v, int *sh, int &total) {
     return incl - v;
 }
 
-// code = KNOWN, t = 1e6 over every frame's padded image (wide grid)
-__global__ __launch_bounds__(256) void k_inp_fill(int *__restrict__ ws, InpLayout L, long long n) {
-    const long long per = L.np;
-    const long long total = n * per;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-        const long long f = i / per, k = i - f * per;
-        int *base = ws + f * L.total;
-        base[L.o_code + k] = C_KNOWN;
-        reinterpret_cast<float *>(base + L.o_t)[k] = 1.0e6f;
+// code = KNOWN, t = 1e6 over every frame's padded image; grid (pixel
+// blocks, frame), 32-bit indices (a 64-bit division per element made this
+// kernel cost more than the march itself)
+__global__ __launch_bounds__(256) void k_inp_fill(int *__restrict__ ws, InpLayout L) {
+    int *base = ws + (long long)blockIdx.y * L.total;
+    int *code = base + L.o_code;
+    float *t = reinterpret_cast<float *>(base + L.o_t);
+    const int np = (int)L.np;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < np; k += gridDim.x * 256) {
+        code[k] = C_KNOWN;
+        t[k] = 1.0e6f;
     }
 }
 
@@ -518,7 +520,9 @@ extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n
     MDX_REQUIRE(n <= 65535, "mdx_inpaint_ns: at most 65535 frames per call");
     const InpLayout L = inp_layout(H, W);
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(k_inp_fill, dim3(2048), dim3(256), 0, s, (int *)workspace, L, (long long)n);
+    MDX_REQUIRE(L.np < (1ll << 31), "mdx_inpaint_ns: frame too large");
+    hipLaunchKernelGGL(k_inp_fill, dim3((unsigned)ceil_div(L.np, 1024), (unsigned)n), dim3(256), 0, s,
+                       (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_count, dim3(L.nch, (unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W,
                        (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_compact, dim3(L.nch, (unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W,

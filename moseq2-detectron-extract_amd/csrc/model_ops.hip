@@ -566,11 +566,16 @@ __global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, 
     int *kp = keep + (long long)seg * cap;
     unsigned long long removed = 0ull;  // lane w < words holds word w
     for (int i0 = 0; i0 < k; i0 += 64) {
+        // unconditional loads from a clamped row (a "load or zero" select
+        // compiles to a branch + vmcnt(0) per load), then the select
         for (int t = lane; t < 64 * words; t += 64) {
             const int r = t / words, w = t - r * words;
-            rows[r][w] = (i0 + r < k) ? mk[(long long)(i0 + r) * words + w] : 0ull;
+            const int rc = i0 + r < k ? i0 + r : k - 1;
+            const unsigned long long v = mk[(long long)rc * words + w];
+            rows[r][w] = (i0 + r < k) ? v : 0ull;
         }
-        const int vf = (i0 + lane < k) ? vl[i0 + lane] : 0;
+        const int vraw = vl[i0 + lane < k ? i0 + lane : k - 1];
+        const int vf = (i0 + lane < k) ? vraw : 0;
         __syncthreads();
         const int cwi = i0 >> 6;
         const unsigned long long own = rows[lane][cwi];  // row lane's bits inside this chunk
