@@ -476,3 +476,26 @@ def test_process_chunk_data_dict(mdx):
     want = F.compute_scalars(None, tr, 0, 100, s.true_depth, reductions=(area, hmean))
     for k in want:
         np.testing.assert_array_equal(d["scalars"][k], want[k], err_msg=k)
+
+
+def test_extract_session_from_dat(mdx, tmp_path):
+    """A synthetic session written as depth.dat, streamed chunk by chunk to
+    HBM and extracted; equals process_chunk on the same frames, and a 2-rank
+    split covers exactly the same frames."""
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.extract import extract_session
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    s = synth.SyntheticSession(10, seed=6)
+    s.write(str(tmp_path))
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    cfg = ExtractConfig(chunk_size=4, batch_size=4)
+    out = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth)
+    assert out["frames"].shape == (10, 80, 80) and list(out["frame_idxs"]) == list(range(10))
+    ex = GPUExtractor(s.bground_im, s.roi, pred, cfg)
+    d = ex.process_chunk(s.frames(4, 8), np.arange(4, 8), true_depth=s.true_depth)
+    np.testing.assert_array_equal(out["frames"][4:8], d["depth_frames"])
+    np.testing.assert_array_equal(out["scalars/area_px"][4:8], d["scalars"]["area_px"])
+    halves = [extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
+                              world=2, rank=r) for r in (0, 1)]
+    np.testing.assert_array_equal(np.concatenate([h["frame_idxs"] for h in halves]), np.arange(10))
