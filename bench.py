@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="run batches back to back on one stream instead of the multi-stream pipeline")
     ap.add_argument("--dma128", type=int, default=None, help="conv kernel policy knob (mdx_conv_set_dma128)")
+    ap.add_argument("--prio256", type=int, default=None, help="conv knob (mdx_conv_set_mfma_prio256)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -196,6 +197,9 @@ def main():
     if args.dma128 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_dma128", args.dma128, 1536)
+    if args.prio256 is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_mfma_prio256", args.prio256)
     B = args.batch
     cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
     pred = Predictor.from_config(cfg, dtype=args.dtype, seed=0)

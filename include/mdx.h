@@ -146,6 +146,8 @@ int mdx_conv_set_narrow_kmax(int kmax);
 int mdx_conv_set_dma128(int mode, int min_tiles);
 /* Issue the LDS-DMA pieces between the MFMAs of the LDS-DMA kernels (0/1). */
 int mdx_conv_set_mfma_prio(int on);
+/* s_setprio(1) around the MFMA bursts of the 256x256 LDS-DMA kernel (0/1). */
+int mdx_conv_set_mfma_prio256(int on);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */

@@ -479,7 +479,7 @@ __device__ __forceinline__ void glds16(const void *src, char *dst) {
 
 __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-template <typename TO, int NW, bool ILV>
+template <typename TO, int NW, bool ILV, bool PRIO = false>
 __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
@@ -577,11 +577,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
     };
     auto mma = [&](int set) {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);  // the wave in its MFMA burst keeps the issue slots
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
     };
     // wait until substep u has landed (4 DMAs per thread per substep)
     auto wait_landed = [&](int u, int issued_upto) {
@@ -709,6 +711,13 @@ extern "C" int mdx_conv_set_large_tiles(int mode) {
 static int g_dma128 = 0, g_dma128_min_tiles = 1536;
 // DMA pieces interleaved with the MFMAs in the 128x128 LDS-DMA kernel (0/1)
 static int g_prio = 1;
+// s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
+static int g_prio8 = 0;
+extern "C" int mdx_conv_set_mfma_prio256(int on) {
+    const int old = g_prio8;
+    g_prio8 = on;
+    return old;
+}
 extern "C" int mdx_conv_set_mfma_prio(int on) {
     const int old = g_prio;
     g_prio = on;
@@ -830,7 +839,10 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
             a.ksplit = 1;
             a.ksteps = a.K / 64;
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
-            if (out_dtype == 1)
+            if (out_dtype == 1 && g_prio8)
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false, true>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s,
+                                   a);
+            else if (out_dtype == 1)
                 hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
             else
                 hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
