@@ -44,6 +44,7 @@ def parse():
                     help="run batches back to back on one stream instead of the multi-stream pipeline")
     ap.add_argument("--dma128", type=int, default=None, help="conv kernel policy knob (mdx_conv_set_dma128)")
     ap.add_argument("--prio256", type=int, default=None, help="conv knob (mdx_conv_set_mfma_prio256)")
+    ap.add_argument("--stream1x1", type=int, default=None, help="conv knob (mdx_conv_set_stream1x1)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -54,9 +55,11 @@ KERNEL_SYMBOLS = {  # MDX_CONV_KERNEL_* -> rocprofv3 symbol (fp16 in / fp16 out)
     1: "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE",
     2: "_ZN3mdx7k_convgIDF16_Li8ELb0EEEvNS_8ConvArgsE",
     3: "_ZN3mdx7k_convgIDF16_Li4ELb1EEEvNS_8ConvArgsE",
+    4: "k_conv1x1_stream<KC> (three instances by K)",
 }
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
-                2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM"}
+                2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
+                4: "k_conv1x1_stream streaming 1x1 GEMM"}
 
 
 def conv_roofline(extractor, raw, steps=3, dump=None):
@@ -197,6 +200,9 @@ def main():
     if args.dma128 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_dma128", args.dma128, 1536)
+    if args.stream1x1 is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_stream1x1", args.stream1x1, 65536)
     if args.prio256 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_mfma_prio256", args.prio256)

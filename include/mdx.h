@@ -151,7 +151,17 @@ int mdx_conv_set_mfma_prio256(int on);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */
-enum { MDX_CONV_KERNEL_REG128 = 0, MDX_CONV_KERNEL_REG64 = 1, MDX_CONV_KERNEL_DMA256 = 2, MDX_CONV_KERNEL_DMA128 = 3 };
+enum {
+    MDX_CONV_KERNEL_REG128 = 0,
+    MDX_CONV_KERNEL_REG64 = 1,
+    MDX_CONV_KERNEL_DMA256 = 2,
+    MDX_CONV_KERNEL_DMA128 = 3,
+    MDX_CONV_KERNEL_STREAM1X1 = 4
+};
+/* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
+ * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256
+ * only when Cout == 64), 2 for every eligible layer with M >= min_m. */
+int mdx_conv_set_stream1x1(int mode, int min_m);
 int mdx_conv2d_last_plan(int *kernel, int *ksplit);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,

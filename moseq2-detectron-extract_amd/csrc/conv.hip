@@ -451,6 +451,124 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 // swizzle is applied on the global source address; fragment reads are then
 // bank-conflict-free for the ds_read_b128 lane groups.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Streaming 1x1 kernel for HBM-bound layers (fp16, stride 1, K = Cin in
+// {64, 128, 256}, Cout % 64 == 0): out = act(X W^T + b (+ res)) with M in the
+// hundreds of thousands and a small K.  Workgroup = 4 waves = 128 pixels x 64
+// output channels; the 64 x K weight slice is staged in LDS once, the
+// activations go straight from HBM into MFMA operand registers (no LDS pass,
+// no barrier in the loop), and the product is formed transposed (D = W X^T)
+// so each lane ends with 4 consecutive channels of one pixel: 8-byte
+// residual loads and stores, no LDS epilogue.
+//   lane l, MFMA 16x16x32:  W operand  = W[n0 + 16 ns + (l & 15)][32 kc + 8 (l >> 4) ..+8]
+//                           X operand  = X[m0 + 16 ms + (l & 15)][32 kc + 8 (l >> 4) ..+8]
+//                           D[ms][ns][r] = out[m0 + 16 ms + (l & 15)][n0 + 16 ns + 4 (l >> 4) + r]
+// ---------------------------------------------------------------------------
+template <int KC>
+__global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
+    constexpr int K = 32 * KC, WPITCH = 2 * K + 16;  // LDS row pitch (bytes): +16 spreads rows over banks
+    __shared__ __attribute__((aligned(16))) char sw[64 * WPITCH];
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int n0 = tn * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
+    // stage the 64 x K weight slice
+    for (int i = tid; i < 64 * K / 8; i += 256) {
+        const int r = i / (K / 8), c = i - r * (K / 8);
+        *reinterpret_cast<uint4 *>(sw + r * WPITCH + c * 16) =
+            *reinterpret_cast<const uint4 *>(Wt + (long long)(n0 + r) * K + c * 8);
+    }
+    // this wave's 32 pixels and their activation fragments
+    const int m0 = tm * 128 + wid * 32;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    half8 xf[2][KC];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+        const int m = m0 + 16 * ms + (lane & 15);
+        const unsigned base = (unsigned)((long long)m * K * 2) + 16u * (lane >> 4);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+            xf[ms][kc] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rx, m < a.M ? base + 64u * kc : 0xFFFFFFF0u, 0, 0));
+    }
+    __syncthreads();
+    float4v acc[2][4];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = float4v{0.f, 0.f, 0.f, 0.f};
+    const char *wl = sw + (lane & 15) * WPITCH + 16 * (lane >> 4);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+        half8 wf[4];
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) wf[ns] = *reinterpret_cast<const half8 *>(wl + 16 * ns * WPITCH + 64 * kc);
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns)
+                acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ns], xf[ms][kc], acc[ms][ns], 0, 0, 0);
+    }
+    // epilogue: bias, residual, ReLU, fp16, 8-byte stores
+    const int cq = 4 * (lane >> 4);
+    float bv[4][4];
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) {
+        const float4 b4 = a.bias ? *reinterpret_cast<const float4 *>(a.bias + n0 + 16 * ns + cq)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[ns][0] = b4.x; bv[ns][1] = b4.y; bv[ns][2] = b4.z; bv[ns][3] = b4.w;
+    }
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    half4 rr[2][4];
+    if (a.res) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
+                                                                            0x00020000);
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms) {
+            const int m = m0 + 16 * ms + (lane & 15);
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns) {
+                const unsigned off = m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 16 * ns + cq) * 2) : 0xFFFFFFF0u;
+                rr[ms][ns] = __builtin_bit_cast(half4, __builtin_amdgcn_raw_buffer_load_b64(rd, off, 0, 0));
+            }
+        }
+    }
+    _Float16 *O = reinterpret_cast<_Float16 *>(a.out);
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+        const int m = m0 + 16 * ms + (lane & 15);
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) {
+            half4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[ms][ns][r] + bv[ns][r];
+                if (a.res) v += (float)rr[ms][ns][r];
+                if (a.relu) v = v > 0.f ? v : 0.f;
+                o[r] = (_Float16)v;
+            }
+            *reinterpret_cast<half4 *>(O + (long long)m * a.Cout + n0 + 16 * ns + cq) = o;
+        }
+    }
+}
+
+// streaming 1x1 kernel policy: 0 never, 1 for eligible layers with M >= g_stream_min_m (default),
+// 2 also for K = 256 layers with Cout > 64
+static int g_stream1x1 = 1, g_stream_min_m = 65536;
+extern "C" int mdx_conv_set_stream1x1(int mode, int min_m) {
+    const int old = g_stream1x1;
+    g_stream1x1 = mode;
+    g_stream_min_m = min_m;
+    return old;
+}
+
 // NW waves (8: 256x256 tile, 4: 128x128 tile); tile = 32 NW rows of A and of
 // B.  Waves form WM_(2) x (NW/2); wave tile (BM/2) x (BN/(NW/2)).
 template <int NW>
@@ -807,6 +925,25 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.relu = relu;
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
+    // HBM-bound 1x1 layers: the streaming kernel
+    if (g_stream1x1 && in_dtype == 1 && out_dtype == 1 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+        pad == 0 && (Cin == 64 || Cin == 128 || (Cin == 256 && (Cout == 64 || g_stream1x1 == 2))) && Cout % 64 == 0 &&
+        (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m) {
+        // (K = 256 with Cout > 64 stays on the 256x256 kernel: measured faster)
+        a.tiles_n = Cout / 64;
+        a.tiles_total = (int)(ceil_div(M, 128) * a.tiles_n);
+        a.ksplit = 1;
+        if (Cin == 64)
+            hipLaunchKernelGGL(k_conv1x1_stream<2>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else if (Cin == 128)
+            hipLaunchKernelGGL(k_conv1x1_stream<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_conv1x1_stream<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        t_plan_kernel = MDX_CONV_KERNEL_STREAM1X1;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
     // fp16 layers with Cin % 64 == 0: the LDS-DMA pipelined kernels -- the
     // 128x128 tile (DMA pieces interleaved with the MFMAs) for layers with
     // many tiles, the 256x256 tile by policy, else the register-staged kernel

@@ -39,10 +39,12 @@ CONV_CASES = [
     (1, 33, 31, 64, 256, 1, 1, 0, True, True),
     (2, 40, 36, 192, 320, 3, 1, 1, False, True),
     (600, 1, 1, 1024, 264, 1, 1, 0, False, False),
+    (2, 20, 30, 128, 192, 1, 1, 0, True, True),
+    (1, 17, 19, 256, 64, 1, 1, 0, False, False),
 ]
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128", "stream"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -65,7 +67,19 @@ def test_conv2d(mdx, dtype, case, ksplit):
     rd = res.cuda() if res is not None else None
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     dc = 1 if dtype == "fp16" else 0
-    if ksplit in ("large", "dma128"):
+    if ksplit == "stream":
+        if dtype != "fp16" or k != 1 or s != 1 or Cin not in (64, 128, 256) or Cout % 64:
+            pytest.skip("streaming 1x1 kernel: fp16, 1x1/s1, Cin in {64,128,256}, Cout % 64 == 0")
+        old = call("mdx_conv_set_stream1x1", 2, 0)
+        try:
+            call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
+                 dc, P(out), None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            assert kid.value == 4
+        finally:
+            call("mdx_conv_set_stream1x1", old, 65536)
+    elif ksplit in ("large", "dma128"):
         if dtype != "fp16" or Cin % 64:
             pytest.skip("LDS-DMA kernels: fp16, Cin % 64 == 0")
         old_nk = call("mdx_conv_set_narrow_kmax", 0)
