@@ -3,6 +3,12 @@ without its control plane): frame source -> GPUExtractor.process_chunk per
 chunk -> results in the writer's layout (M/io/result.py:106-130), optionally
 restricted to this rank's chunk-aligned shard.
 
+With tracking on and more than one rank the chunk loop runs in two device
+passes around the exchange step (shard.tracking_exchange): pass 1 keeps each
+chunk's prepped / mask / cleaned frames resident in HBM (3 x 216 KB per frame:
+a 1M-frame session over 8 GPUs holds ~81 GB per GPU, well inside 288 GB) and
+ships its feature records to rank 0; pass 2 crops at the tracked values.
+
 The h5 writer itself is not rebuilt (h5py is absent from this image); the
 results are returned as arrays keyed like the h5 datasets and can be saved as
 ``.npz``.
@@ -15,6 +21,7 @@ import numpy as np
 
 from .pipeline import ExtractConfig, GPUExtractor
 from .session import RawDepthSource
+from .shard import tracking_exchange
 
 
 def shard_chunk_range(nchunks: int, world: int, rank: int):
@@ -26,7 +33,8 @@ def shard_chunk_range(nchunks: int, world: int, rank: int):
 
 def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predictor,
                     config: ExtractConfig = ExtractConfig(), true_depth: float = 673.1,
-                    frame_trim=(0, 0), world: int = 1, rank: int = 0, out_npz: Optional[str] = None) -> Dict:
+                    frame_trim=(0, 0), world: int = 1, rank: int = 0, out_npz: Optional[str] = None,
+                    exchange: Optional[bool] = None) -> Dict:
     """Extract every chunk of the session (or of this rank's shard).  Returns
     {'frames': uint8 (n,80,80), 'frames_mask': uint8 (n,80,80),
     'scalars/<name>': (n,), 'keypoints/<name>': (n,), 'flips': bool (n,),
@@ -38,8 +46,20 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         c0, c1 = shard_chunk_range(len(batches), world, rank)
         batches = batches[c0:c1]
     parts = []
-    for idx, raw in src.iterate(device=True, batches=batches):
-        parts.append(ex.process_chunk(raw, np.asarray(idx), offset=0, true_depth=true_depth))
+    if exchange is None:  # two passes around the exchange step (needs torch.distributed initialised)
+        exchange = world > 1 and config.use_tracking
+    if exchange:
+        states = []
+        for idx, raw in src.iterate(device=True, batches=batches):
+            st, host = ex.features_pass(raw)
+            states.append((np.asarray(idx), st, host))
+        tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
+        for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
+            parts.append(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth))
+        states.clear()
+    else:
+        for idx, raw in src.iterate(device=True, batches=batches):
+            parts.append(ex.process_chunk(raw, np.asarray(idx), offset=0, true_depth=true_depth))
     src.close()
     out: Dict[str, np.ndarray] = {}
     if not parts:

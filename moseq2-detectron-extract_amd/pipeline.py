@@ -28,6 +28,7 @@ import torch
 
 from . import features as F
 from . import proc
+from . import tracking as TR
 from ._lib import call
 
 
@@ -52,6 +53,7 @@ class ExtractConfig:
     iters_tail: int = 3
     mask_iou_threshold: float = 0.5
     fix_invalid_pixels: bool = True
+    use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -83,6 +85,9 @@ class GPUExtractor:
         self.lut = proc.scale_lut(config.min_height, config.max_height)
         self.predictor = predictor
         self.strel = proc.ELLIPSE9
+        # ProcessFeaturesStep's Kalman trackers (process_features_step.py:40-51),
+        # carried from chunk to chunk
+        self.point_tracker, self.angle_tracker = TR.make_trackers() if config.use_tracking else (None, None)
 
     def infer(self, prepped: torch.Tensor):
         """Model forward over a prepped chunk in batch_size slices
@@ -128,45 +133,73 @@ class GPUExtractor:
         return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
                 "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}
 
-    def process_chunk(self, raw, frame_idxs=None, offset: int = 0, true_depth: float = 673.1) -> dict:
-        """One chunk through ProduceFramesStep -> InferenceStep ->
-        ProcessFeaturesStep with tracking off (--no-use-tracking), returning
-        the data dict the reference's writer consumes
-        (M/pipeline/produce_frames_step.py:33-38, inference_step.py:71,
-        process_features_step.py:163-199; M/io/result.py:106-130).
-
-        Device: prep/inpaint, model + mask NMS + instance 0, clean, moments,
-        scalar reductions + keypoint z, crops.  Host (as in the reference, and
-        sequential over the chunk): angle flips + iterative 180-degree filter
-        (M/proc/proc.py:827-839), scalar and keypoint tables."""
-        cfg = self.cfg
+    def features_pass(self, raw):
+        """Device part of one chunk up to the sequential host step: prep
+        (+inpaint), model + mask NMS + instance 0, clean, moments.  Returns
+        (device state kept for finish_chunk, host per-frame features
+        {centroid, orientation (rad), axis_length, keypoints (n,K,3)})."""
         raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
-        n = raw.shape[0]
-        frame_idxs = np.arange(n) if frame_idxs is None else np.asarray(frame_idxs)
         prepped = self.prep(raw)
         inf = self.infer(prepped)
         d2 = inf["d2_mask"]
         cleaned, feats = self.features(prepped, d2)
+        host = {"centroid": feats["centroid"].cpu().numpy(), "orientation": feats["orientation"].cpu().numpy(),
+                "axis_length": feats["axis_length"].cpu().numpy(), "keypoints": inf["sel_keypoints"].cpu().numpy()}
+        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": inf["nkeep"].cpu().numpy()}
+        return state, host
+
+    def finish_chunk(self, state: dict, centroid, keypoints, angles, flips, axis_length, frame_idxs=None,
+                     offset: int = 0, true_depth: float = 673.1) -> dict:
+        """Device part after the host angle step: scalar reductions + keypoint
+        z at the final keypoints, host scalar / keypoint tables, crops at the
+        final centroid and angle; returns the writer's data dict."""
+        cfg = self.cfg
+        prepped, d2, cleaned = state["prepped"], state["d2"], state["cleaned"]
+        n = prepped.shape[0]
+        frame_idxs = np.arange(n) if frame_idxs is None else np.asarray(frame_idxs)
         area, hmean, z = F.frame_scalars(prepped, d2, cfg.min_height, cfg.max_height,
-                                         keypoints=inf["sel_keypoints"], z_frames=cleaned)
-        cen = feats["centroid"].cpu().numpy()
-        ori = feats["orientation"].cpu().numpy()
-        axl = feats["axis_length"].cpu().numpy()
-        kp = inf["sel_keypoints"].cpu().numpy()
-        angles, flips = F.finalize_angles(ori, axl, cen, kp)
-        track = {"centroid": cen, "orientation": np.array(angles), "axis_length": axl, "contour": []}
+                                         keypoints=np.ascontiguousarray(keypoints, dtype=np.float64), z_frames=cleaned)
+        track = {"centroid": centroid, "orientation": np.array(angles), "axis_length": axis_length, "contour": []}
         scalars = F.compute_scalars(None, track, cfg.min_height, cfg.max_height, true_depth,
                                     reductions=(area.cpu().numpy(), hmean.cpu().numpy()))
-        keypoints = F.keypoints_to_dict(kp, None, cen, track["orientation"], true_depth=true_depth,
-                                        z_data=z.cpu().numpy())
-        depth, mask = self.crop(prepped, d2, torch.from_numpy(cen).cuda(), torch.from_numpy(track["orientation"]).cuda())
+        kpd = F.keypoints_to_dict(keypoints, None, centroid, track["orientation"], true_depth=true_depth,
+                                  z_data=z.cpu().numpy())
+        depth, mask = self.crop(prepped, d2, torch.from_numpy(np.ascontiguousarray(centroid, dtype=np.float64)).cuda(),
+                                torch.from_numpy(track["orientation"]).cuda())
         return {
             "chunk": prepped, "frame_idxs": frame_idxs, "offset": offset,
             "features": {"cleaned_frames": cleaned, "masks": d2, "features": track, "flips": flips,
-                         "keypoints": kp, "num_instances": inf["nkeep"].cpu().numpy()},
-            "scalars": scalars, "keypoints": keypoints,
+                         "keypoints": keypoints, "num_instances": state["nkeep"]},
+            "scalars": scalars, "keypoints": kpd,
             "depth_frames": depth.cpu().numpy(), "mask_frames": mask.cpu().numpy(),
         }
+
+    def host_angles(self, host: dict):
+        """The sequential host step of instances_to_features
+        (M/proc/proc.py:720-839): the tracking branch (Kalman smoothing +
+        tracker-assisted flips; tracker state carried to the next chunk) or
+        keypoint flips + iterative 180-degree filtering.  Returns (centroid,
+        keypoints, angles deg, flips)."""
+        if self.cfg.use_tracking:
+            return TR.track_features(self.point_tracker, self.angle_tracker, host["centroid"], host["keypoints"],
+                                     host["orientation"], host["axis_length"])
+        angles, flips = F.finalize_angles(host["orientation"], host["axis_length"], host["centroid"],
+                                          host["keypoints"])
+        return host["centroid"], host["keypoints"], angles, flips
+
+    def process_chunk(self, raw, frame_idxs=None, offset: int = 0, true_depth: float = 673.1) -> dict:
+        """One chunk through ProduceFramesStep -> InferenceStep ->
+        ProcessFeaturesStep, returning the data dict the reference's writer
+        consumes (M/pipeline/produce_frames_step.py:33-38, inference_step.py:71,
+        process_features_step.py:163-199; M/io/result.py:106-130).
+
+        Device: prep/inpaint, model + mask NMS + instance 0, clean, moments,
+        scalar reductions + keypoint z, crops.  Host (as in the reference, and
+        sequential over frames and chunks): the angle / tracking step
+        (host_angles), scalar and keypoint tables."""
+        state, host = self.features_pass(raw)
+        cen, kp, angles, flips = self.host_angles(host)
+        return self.finish_chunk(state, cen, kp, angles, flips, host["axis_length"], frame_idxs, offset, true_depth)
 
     def back(self, prepped: torch.Tensor, cleaned: torch.Tensor):
         """Model-dependent tail: forward + selection, moments, angle, crops."""

@@ -461,10 +461,12 @@ def test_overlapped_extractor_matches_serial(mdx):
             torch.testing.assert_close(g[k], w[k], rtol=0, atol=0, equal_nan=True)
 
 
-def test_process_chunk_data_dict(mdx):
-    """Full chunk through the device path (tracking off): the writer's data
-    dict, with crops equal to the oracle crop at the host-final angles and
-    scalars equal to the oracle reductions fed through the same host code."""
+@pytest.mark.parametrize("use_tracking", [False, True])
+def test_process_chunk_data_dict(mdx, use_tracking):
+    """Full chunk through the device path (tracking off and on): the writer's
+    data dict, with crops equal to the oracle crop at the host-final centroid
+    and angles, scalars equal to the oracle reductions fed through the same
+    host code, and keypoint z read at the final (smoothed) keypoints."""
     from moseq2_detectron_extract_amd import features as F
     from moseq2_detectron_extract_amd import synth
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
@@ -474,7 +476,7 @@ def test_process_chunk_data_dict(mdx):
     s = synth.SyntheticSession(6, seed=4)
     raw = s.frames(0, 6)
     pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
-    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
+    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4, use_tracking=use_tracking))
     d = ex.process_chunk(raw, np.arange(100, 106), 0, true_depth=s.true_depth)
     for k in ("chunk", "frame_idxs", "offset", "features", "scalars", "keypoints", "depth_frames", "mask_frames"):
         assert k in d
@@ -486,10 +488,17 @@ def test_process_chunk_data_dict(mdx):
     d2 = d["features"]["masks"].cpu().numpy()
     np.testing.assert_array_equal(d["depth_frames"], O.crop_and_rotate_frames(prepped, tr["centroid"], tr["orientation"]))
     np.testing.assert_array_equal(d["mask_frames"], O.crop_and_rotate_frames(d2, tr["centroid"], tr["orientation"]))
-    area, hmean, _ = FR.frame_scalars_ref(prepped, d2, 0, 100)
+    kp = d["features"]["keypoints"]
+    area, hmean, z = FR.frame_scalars_ref(prepped, d2, 0, 100, keypoints=kp,
+                                          z_frames=d["features"]["cleaned_frames"].cpu().numpy())
     want = F.compute_scalars(None, tr, 0, 100, s.true_depth, reductions=(area, hmean))
     for k in want:
         np.testing.assert_array_equal(d["scalars"][k], want[k], err_msg=k)
+    wkp = F.keypoints_to_dict(kp, None, tr["centroid"], tr["orientation"], true_depth=s.true_depth, z_data=z)
+    for k in wkp:
+        np.testing.assert_array_equal(d["keypoints"][k], wkp[k], err_msg=k)
+    if use_tracking:
+        assert ex.point_tracker.is_initialized and ex.angle_tracker.is_initialized
 
 
 def test_extract_session_from_dat(mdx, tmp_path):
@@ -503,7 +512,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
     s = synth.SyntheticSession(10, seed=6)
     s.write(str(tmp_path))
     pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
-    cfg = ExtractConfig(chunk_size=4, batch_size=4)
+    cfg = ExtractConfig(chunk_size=4, batch_size=4, use_tracking=False)
     out = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth)
     assert out["frames"].shape == (10, 80, 80) and list(out["frame_idxs"]) == list(range(10))
     ex = GPUExtractor(s.bground_im, s.roi, pred, cfg)
@@ -513,3 +522,30 @@ def test_extract_session_from_dat(mdx, tmp_path):
     halves = [extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
                               world=2, rank=r) for r in (0, 1)]
     np.testing.assert_array_equal(np.concatenate([h["frame_idxs"] for h in halves]), np.arange(10))
+    # tracking on: the session equals process_chunk chunk after chunk on one
+    # extractor (the trackers carry their state across chunks)
+    cfg_t = ExtractConfig(chunk_size=4, batch_size=4, use_tracking=True)
+    out_t = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_t, true_depth=s.true_depth)
+    ex_t = GPUExtractor(s.bground_im, s.roi, pred, cfg_t)
+    ds = [ex_t.process_chunk(s.frames(a, min(a + 4, 10)), np.arange(a, min(a + 4, 10)), true_depth=s.true_depth)
+          for a in (0, 4, 8)]
+    np.testing.assert_array_equal(out_t["frames"], np.concatenate([d["depth_frames"] for d in ds]))
+    np.testing.assert_array_equal(out_t["scalars/angle"], np.concatenate([d["scalars"]["angle"] for d in ds]))
+    np.testing.assert_array_equal(out_t["flips"], np.concatenate([d["features"]["flips"] for d in ds]))
+    # the two-pass path around the rank-0 exchange (a 1-rank gloo group here;
+    # world 2-3 exchanges are covered on CPU in test_shard.py)
+    import socket
+    import torch.distributed as dist
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        out_x = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_t,
+                                true_depth=s.true_depth, exchange=True)
+    finally:
+        dist.destroy_process_group()
+    assert set(out_x) == set(out_t)
+    for k in out_t:
+        np.testing.assert_array_equal(out_x[k], out_t[k], err_msg=k)

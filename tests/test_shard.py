@@ -80,3 +80,72 @@ def test_gather_results_world2_gloo(mdx):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == list(range(2500))
+
+
+def _chunk_feats(n_chunks, chunk, seed=11):
+    """Per-chunk host feature records as GPUExtractor.features_pass returns them."""
+    rng = np.random.default_rng(seed)
+    n = n_chunks * chunk
+    t = np.arange(n)
+    cen = np.stack([200 + 30 * np.sin(t / 20), 180 + 20 * np.cos(t / 30)], 1) + rng.normal(0, 1, (n, 2))
+    ang = (t * 2.0) % 360
+    kp = np.zeros((n, 8, 3))
+    for k in range(8):
+        d = (3.5 - k) * 6
+        kp[:, k, 0] = cen[:, 0] + d * np.cos(np.deg2rad(ang))
+        kp[:, k, 1] = cen[:, 1] - d * np.sin(np.deg2rad(ang))
+        kp[:, k, 2] = 0.8
+    kp[:, :, :2] += rng.normal(0, 1, (n, 8, 2))
+    ori = -np.deg2rad(ang + np.where(t % 17 == 0, 180, 0))
+    axl = np.stack([np.full(n, 40.0), np.full(n, 14.0)], 1)
+    cen[7] = np.nan
+    kp[9] = np.nan
+    return [{"centroid": cen[i:i + chunk], "orientation": ori[i:i + chunk], "axis_length": axl[i:i + chunk],
+             "keypoints": kp[i:i + chunk]} for i in range(0, n, chunk)]
+
+
+def _track_worker(rank, world, port, q, n_chunks, chunk):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.extract import shard_chunk_range
+    from moseq2_detectron_extract_amd.shard import tracking_exchange
+    from moseq2_detectron_extract_amd.tracking import make_trackers
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    feats = _chunk_feats(n_chunks, chunk)
+    c0, c1 = shard_chunk_range(len(feats), world, rank)
+    p, a = make_trackers() if rank == 0 else (None, None)
+    res = tracking_exchange(feats[c0:c1], p, a)
+    q.put((rank, [[np.asarray(x).tolist() for x in r] for r in res]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_chunks", [(2, 3), (3, 2)])
+def test_tracking_exchange_equals_sequential(mdx, world, n_chunks):
+    """Rank 0 tracks every rank's chunks in session order: the scattered
+    results equal one process running the tracking branch chunk by chunk
+    (bit-exact), including a rank that owns no chunk (world 3, 2 chunks)."""
+    from moseq2_detectron_extract_amd.tracking import make_trackers, track_features
+    chunk = 40
+    feats = _chunk_feats(n_chunks, chunk)
+    p, a = make_trackers()
+    want = [track_features(p, a, f["centroid"], f["keypoints"], f["orientation"], f["axis_length"]) for f in feats]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_track_worker, args=(r, world, port, q, n_chunks, chunk)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    flat = [r for k in sorted(got) for r in got[k]]
+    assert len(flat) == len(want)
+    for g, w in zip(flat, want):
+        for gx, wx in zip(g, w):
+            np.testing.assert_array_equal(np.asarray(gx, dtype=np.asarray(wx).dtype), wx)
