@@ -114,6 +114,15 @@ int mdx_frame_scalars(const uint8_t *frames, const uint8_t *masks, int64_t n, in
                       const uint8_t *z_frames, int64_t *area_px, double *height_ave, double *z_data,
                       mdx_stream_t stream);
 
+/* Session background, get_bground_im M/proc/roi.py:293-307
+ * as find_roi calls it (M/io/session.py:212-213): every frame int16 [n][H][W]
+ * is median-blurred (cv2.medianBlur, BORDER_REPLICATE, med_scale 3 or 5) into
+ * `work` (int16, n*H*W, caller-owned), then out[H][W] (float64) =
+ * np.median(work, axis=0): the middle value, or the mean of the two middle
+ * values for even n; NaN when n == 0.  n <= 65535. */
+int mdx_bground_median(const int16_t *frames, int64_t n, int H, int W, int med_scale, int16_t *work,
+                       double *out, mdx_stream_t stream);
+
 /* ---------------------------------------------------------------------
  * Mask/Keypoint R-CNN forward (Predictor.__call__, M/model/predict.py:53-102,
  * Detectron2 GeneralizedRCNN built by M/model/config.py:21-94).  Tensors are

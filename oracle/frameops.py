@@ -156,3 +156,13 @@ def crop_and_rotate_frames(frames, centers, angles, crop_size=(80, 80)):
     out = np.empty((n, crop_size[1], crop_size[0]), np.uint8)
     _lib().orc_crop_rotate(_p(frames), n, H, W, _p(c), _p(a), crop_size[0], crop_size[1], _p(out))
     return out
+
+
+def bground_ref(frames, med_scale=5):
+    """get_bground_im (M/proc/roi.py:293-307): per-frame medianBlur(med_scale)
+    (BORDER_REPLICATE == scipy 'nearest'), then np.median over frames."""
+    from scipy.ndimage import median_filter
+    f = np.asarray(frames).copy()
+    for i in range(f.shape[0]):
+        f[i] = median_filter(f[i], size=med_scale, mode="nearest")
+    return np.median(f, axis=0)
