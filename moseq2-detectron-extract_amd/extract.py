@@ -15,11 +15,14 @@ results are returned as arrays keyed like the h5 datasets and can be saved as
 """
 from __future__ import annotations
 
+import os
+import uuid
 from typing import Dict, Optional
 
 import numpy as np
 
 from .pipeline import ExtractConfig, GPUExtractor
+from .results import KeypointsTSVWriter, create_extract_h5, open_results, write_extracted_chunk_to_h5
 from .session import RawDepthSource
 from .shard import tracking_exchange
 
@@ -34,7 +37,8 @@ def shard_chunk_range(nchunks: int, world: int, rank: int):
 def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predictor,
                     config: ExtractConfig = ExtractConfig(), true_depth: float = 673.1,
                     frame_trim=(0, 0), world: int = 1, rank: int = 0, out_npz: Optional[str] = None,
-                    exchange: Optional[bool] = None) -> Dict:
+                    exchange: Optional[bool] = None, output_dir: Optional[str] = None,
+                    first_frame: Optional[np.ndarray] = None, status: Optional[dict] = None) -> Dict:
     """Extract every chunk of the session (or of this rank's shard).  Returns
     {'frames': uint8 (n,80,80), 'frames_mask': uint8 (n,80,80),
     'scalars/<name>': (n,), 'keypoints/<name>': (n,), 'flips': bool (n,),
@@ -62,6 +66,9 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
             parts.append(ex.process_chunk(raw, np.asarray(idx), offset=0, true_depth=true_depth))
     src.close()
     out: Dict[str, np.ndarray] = {}
+    if output_dir:
+        _write_outputs(output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}"), parts, src, bground_im,
+                       roi, true_depth, config, first_frame, status)
     if not parts:
         return out
     out["frame_idxs"] = np.concatenate([p["frame_idxs"] for p in parts])
@@ -75,3 +82,26 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     if out_npz:
         np.savez_compressed(out_npz, **out)
     return out
+
+
+def _write_outputs(output_dir, parts, src, bground_im, roi, true_depth, config, first_frame, status):
+    """results_00.h5 (or .npz without h5py) + keypoints_00.tsv, as
+    ResultWriterStep writes them (M/pipeline/write_results_step.py)."""
+    os.makedirs(output_dir, exist_ok=True)
+    ts_file = os.path.join(os.path.dirname(os.path.abspath(src.path)), "depth_ts.txt")
+    nframes = src.last_frame_idx
+    ts = np.loadtxt(ts_file)[:nframes] if os.path.exists(ts_file) else np.arange(nframes) * (1000 / 30)
+    cfg = {"nframes": nframes, "crop_size": config.crop_size, "frame_dtype": "uint8", "timestamps": ts,
+           "flip_classifier": "keypoints", "true_depth": true_depth, "roi": roi,
+           "first_frame": first_frame if first_frame is not None else src.read([0])[0], "bground_im": bground_im}
+    status = status or {"uuid": str(uuid.uuid4()), "parameters": {k: v for k, v in vars(config).items()},
+                        "metadata": {}}
+    h5 = open_results(output_dir)
+    tsv = KeypointsTSVWriter(output_dir)
+    try:
+        create_extract_h5(h5, cfg, status)
+        for d in parts:
+            write_extracted_chunk_to_h5(h5, d)
+            tsv.write(d)
+    finally:
+        h5.close()

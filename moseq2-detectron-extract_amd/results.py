@@ -1,0 +1,215 @@
+"""Result writers: the extraction h5 layout and the
+keypoints TSV, fed by the writer data dict GPUExtractor.process_chunk returns.
+
+=============================  =============================================
+this module                    reference (M/ = moseq2_detectron_extract/)
+=============================  =============================================
+create_extract_h5              M/io/result.py:14-103
+write_extracted_chunk_to_h5    M/io/result.py:106-130
+dict_to_h5                     M/io/util.py:136-176
+KeypointsTSVWriter             ResultWriterStep.__process_csv
+                               M/pipeline/write_results_step.py:54-73
+open_results                   ResultWriterStep.__init_h5 :34-39
+=============================  =============================================
+
+h5py is not installed in this image's interpreter, so ``open_results`` falls
+back to ``MemoryH5``: the same dataset tree (names, shapes, dtypes,
+descriptions) held in numpy arrays and saved as one ``.npz`` (dataset path ->
+array) on close; with h5py present it opens a real ``results_XX.h5``.  The
+TSV is appended chunk by chunk (the reference rewrites the whole table after
+every chunk: O(n^2) in the session length); the file bytes are the same.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import numpy as np
+
+from .features import keypoint_attributes, scalar_attributes
+
+PACKAGE_VERSION = "moseq2-detectron-extract-amd v0.1"
+
+
+class MemoryDataset:
+    """numpy-backed stand-in for h5py.Dataset (assignment casts like h5py)."""
+
+    def __init__(self, data: np.ndarray):
+        self.data = data
+        self.attrs: Dict[str, object] = {}
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+    @property
+    def dtype(self):
+        return self.data.dtype
+
+    def __getitem__(self, idx):
+        return self.data[idx]
+
+    def __setitem__(self, idx, value):
+        self.data[idx] = np.asarray(value).astype(self.data.dtype)
+
+
+class MemoryH5:
+    """Minimal h5py.File stand-in: a flat tree of datasets keyed by path."""
+
+    def __init__(self, path: Optional[str] = None):
+        self.path = path
+        self.datasets: Dict[str, MemoryDataset] = {}
+
+    @staticmethod
+    def _key(name: str) -> str:
+        return name.strip("/")
+
+    def create_dataset(self, name, shape=None, dtype=None, data=None, compression=None, **kw):
+        key = self._key(name)
+        if key in self.datasets:
+            raise ValueError(f"dataset {key} exists")
+        if data is not None:
+            arr = np.array(data, dtype=dtype) if dtype is not None else np.array(data)
+            if shape is not None:
+                arr = arr.reshape(shape)
+        else:
+            arr = np.zeros(() if shape is None else shape, dtype=dtype or "float32")
+        ds = MemoryDataset(arr)
+        self.datasets[key] = ds
+        return ds
+
+    def __setitem__(self, name, value):
+        self.create_dataset(name, data=value)
+
+    def __getitem__(self, name) -> MemoryDataset:
+        return self.datasets[self._key(name)]
+
+    def __contains__(self, name) -> bool:
+        return self._key(name) in self.datasets
+
+    def close(self):
+        if self.path:
+            np.savez_compressed(self.path, **{k: v.data for k, v in self.datasets.items()})
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def open_results(output_dir: str, bg_roi_index: int = 0):
+    """results_XX.h5 via h5py when importable, else a MemoryH5 saved as
+    results_XX.npz."""
+    try:
+        import h5py
+    except ImportError:
+        return MemoryH5(os.path.join(output_dir, f"results_{bg_roi_index:02d}.npz"))
+    return h5py.File(os.path.join(output_dir, f"results_{bg_roi_index:02d}.h5"), mode="w")
+
+
+def dict_to_h5(h5_file, data: dict, root: str = "/", annotations: Optional[dict] = None) -> None:
+    """Nested dict -> datasets under `root` (None -> empty string dataset)."""
+    if not root.endswith("/"):
+        root = root + "/"
+    annotations = annotations or {}
+    for key, item in data.items():
+        dest = root + key
+        if isinstance(item, dict):
+            dict_to_h5(h5_file, item, dest)
+            continue
+        if isinstance(item, (np.ndarray, np.int64, np.float64, str, bytes)):
+            h5_file[dest] = item
+        elif isinstance(item, (tuple, list)):
+            h5_file[dest] = np.asarray(item)
+        elif isinstance(item, (int, float)):
+            h5_file[dest] = np.asarray([item])[0]
+        elif item is None:
+            h5_file[dest] = ""
+        else:
+            raise ValueError(f"Cannot save {type(item)} type to key {dest}")
+        if key in annotations:
+            h5_file[dest].attrs["description"] = "" if annotations[key] is None else annotations[key]
+
+
+def create_extract_h5(h5_file, config_data: dict, status_dict: dict) -> None:
+    """Datasets and metadata of an extraction result file (layout, dtypes and
+    descriptions of M/io/result.py:14-103)."""
+    nframes = config_data["nframes"]
+    crop = config_data["crop_size"]
+    h5_file.create_dataset("metadata/uuid", data=status_dict["uuid"])
+    for name, desc in scalar_attributes().items():
+        h5_file.create_dataset(f"scalars/{name}", (nframes,), "float32", compression="gzip")
+        h5_file[f"scalars/{name}"].attrs["description"] = desc
+    for name, desc in keypoint_attributes().items():
+        h5_file.create_dataset(f"keypoints/{name}", (nframes,), "float32", compression="gzip")
+        h5_file[f"keypoints/{name}"].attrs["description"] = desc
+    h5_file.create_dataset("timestamps", compression="gzip", data=config_data["timestamps"])
+    h5_file["timestamps"].attrs["description"] = "Depth video timestamps"
+    h5_file.create_dataset("frames", (nframes, crop[0], crop[1]), config_data["frame_dtype"], compression="gzip")
+    h5_file["frames"].attrs["description"] = "3D Numpy array of depth frames (nframes x w x h, in mm)"
+    if config_data.get("use_tracking_model", False):
+        h5_file.create_dataset("frames_mask", (nframes, crop[0], crop[1]), "float32", compression="gzip")
+        h5_file["frames_mask"].attrs["description"] = "Log-likelihood values from the tracking model (nframes x w x h)"
+    else:
+        h5_file.create_dataset("frames_mask", (nframes, crop[0], crop[1]), "bool", compression="gzip")
+        h5_file["frames_mask"].attrs["description"] = "Boolean mask, false=not mouse, true=mouse"
+    if config_data.get("flip_classifier") is not None:
+        h5_file.create_dataset("metadata/extraction/flips", (nframes,), "bool", compression="gzip")
+        h5_file["metadata/extraction/flips"].attrs["description"] = \
+            "Output from flip classifier, false=no flip, true=flip"
+    h5_file.create_dataset("metadata/extraction/true_depth", data=config_data["true_depth"])
+    h5_file["metadata/extraction/true_depth"].attrs["description"] = "Detected true depth of arena floor in mm"
+    h5_file.create_dataset("metadata/extraction/roi", data=config_data["roi"], compression="gzip")
+    h5_file["metadata/extraction/roi"].attrs["description"] = "ROI mask"
+    h5_file.create_dataset("metadata/extraction/first_frame", data=config_data["first_frame"], compression="gzip")
+    h5_file["metadata/extraction/first_frame"].attrs["description"] = "First frame of depth dataset"
+    h5_file.create_dataset("metadata/extraction/background", data=config_data["bground_im"], compression="gzip")
+    h5_file["metadata/extraction/background"].attrs["description"] = "Computed background image"
+    h5_file.create_dataset("metadata/extraction/extract_version", data=PACKAGE_VERSION)
+    h5_file["metadata/extraction/extract_version"].attrs["description"] = "Version of moseq2-extract"
+    dict_to_h5(h5_file, status_dict.get("parameters", {}), "metadata/extraction/parameters")
+    for key, value in status_dict.get("metadata", {}).items():
+        if isinstance(value, list) and len(value) > 0 and isinstance(value[0], str):
+            value = [v.encode("utf8") for v in value]
+        if value is not None:
+            h5_file.create_dataset(f"metadata/acquisition/{key}", data=value)
+        else:
+            h5_file.create_dataset(f"metadata/acquisition/{key}", dtype="f")
+
+
+def write_extracted_chunk_to_h5(h5_file, results: dict) -> None:
+    """Scalars, crops, masks, flips and keypoints of one chunk at rows
+    results['frame_idxs'] (data sliced from results['offset'], as the
+    reference does -- which requires offset 0 in practice)."""
+    rows = results["frame_idxs"]
+    off = results["offset"]
+    for name, vals in results["scalars"].items():
+        h5_file[f"scalars/{name}"][rows] = np.asarray(vals)[off:]
+    h5_file["frames"][rows] = results["depth_frames"][off:]
+    h5_file["frames_mask"][rows] = results["mask_frames"][off:]
+    h5_file["metadata/extraction/flips"][rows] = np.asarray(results["features"]["flips"])[off:]
+    for name, vals in results["keypoints"].items():
+        h5_file[f"keypoints/{name}"][rows] = np.asarray(vals)[off:]
+
+
+class KeypointsTSVWriter:
+    """keypoints_XX.tsv: Frame_Idx, Flip, Centroid_X, Centroid_Y, Angle, then
+    every keypoint field, one row per frame, appended per chunk."""
+
+    def __init__(self, output_dir: str, bg_roi_index: int = 0):
+        self.path = os.path.join(output_dir, f"keypoints_{bg_roi_index:02d}.tsv")
+        self._header = True
+
+    def write(self, data: dict) -> None:
+        import pandas as pd
+        feats = data["features"]
+        cen = np.asarray(feats["features"]["centroid"])
+        cols = {"Frame_Idx": np.asarray(data["frame_idxs"]), "Flip": np.asarray(feats["flips"]),
+                "Centroid_X": cen[:, 0], "Centroid_Y": cen[:, 1],
+                "Angle": np.asarray(feats["features"]["orientation"])}
+        for k, v in data["keypoints"].items():
+            cols[k] = np.asarray(v)
+        df = pd.DataFrame(cols)
+        df.to_csv(self.path, sep="\t", index=False, mode="w" if self._header else "a", header=self._header)
+        self._header = False

@@ -546,6 +546,13 @@ def test_extract_session_from_dat(mdx, tmp_path):
                                 true_depth=s.true_depth, exchange=True)
     finally:
         dist.destroy_process_group()
+    # writers: the h5 tree (npz without h5py) + keypoints TSV of the same run
+    extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_t, true_depth=s.true_depth,
+                    output_dir=str(tmp_path / "out"))
+    res = np.load(str(tmp_path / "out" / "results_00.npz"))
+    np.testing.assert_array_equal(res["frames"], out_t["frames"])
+    np.testing.assert_array_equal(res["scalars/angle"], out_t["scalars/angle"].astype(np.float32))
+    assert (tmp_path / "out" / "keypoints_00.tsv").read_text().count("\n") == 11
     assert set(out_x) == set(out_t)
     for k in out_t:
         np.testing.assert_array_equal(out_x[k], out_t[k], err_msg=k)

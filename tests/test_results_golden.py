@@ -1,0 +1,85 @@
+"""Result writers (results.py) against the reference's own
+write_extracted_chunk_to_h5 (real h5py) and ResultWriterStep's keypoints TSV
+(tests/golden/make_golden_results.py): identical dataset contents and
+identical TSV bytes."""
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def g():
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "ref_results.npz")))
+
+
+@pytest.fixture(scope="module")
+def RS():
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd import results
+    return results
+
+
+def _chunks(g):
+    out = []
+    for i in range(2):
+        p = f"c{i}_"
+        out.append({
+            "frame_idxs": g[p + "frame_idxs"], "offset": int(g[p + "offset"]),
+            "depth_frames": g[p + "depth_frames"], "mask_frames": g[p + "mask_frames"],
+            "scalars": {k[len(p + "scalars/"):]: g[k] for k in g if k.startswith(p + "scalars/")},
+            "keypoints": {k[len(p + "keypoints/"):]: g[k] for k in g if k.startswith(p + "keypoints/")},
+            "features": {"flips": g[p + "flips"],
+                         "features": {"centroid": g[p + "centroid"], "orientation": g[p + "orientation"]}},
+        })
+    return out
+
+
+def test_h5_layout_and_chunk_writes(g, RS, tmp_path):
+    n = int(g["nframes"])
+    cfg = {"nframes": n, "crop_size": (80, 80), "frame_dtype": "uint8", "timestamps": np.arange(n) * 33.3,
+           "flip_classifier": "keypoints", "true_depth": 673.5, "roi": np.ones((4, 5), bool),
+           "first_frame": np.zeros((4, 5), np.int16), "bground_im": np.full((4, 5), 670.0)}
+    status = {"uuid": "abc", "parameters": {"chunk_size": 1000, "bg_roi_depth_range": (650, 750), "x": None,
+                                            "nested": {"a": 1.5}},
+              "metadata": {"SubjectName": "m1", "Tags": ["a", "b"], "Empty": None}}
+    path = str(tmp_path / "r.npz")
+    h = RS.MemoryH5(path)
+    RS.create_extract_h5(h, cfg, status)
+    for c in _chunks(g):
+        RS.write_extracted_chunk_to_h5(h, c)
+    want = {k[3:]: g[k] for k in g if k.startswith("h5/")}
+    for k, v in want.items():
+        assert h[k].dtype == v.dtype, k
+        np.testing.assert_array_equal(h[k][()], v, err_msg=k)
+    assert set(RS.scalar_attributes()) <= {k.split("/", 1)[1] for k in want if k.startswith("scalars/")}
+    assert h["frames_mask"].attrs["description"].startswith("Boolean mask")
+    h.close()
+    saved = np.load(path)
+    np.testing.assert_array_equal(saved["frames"], want["frames"])
+    assert float(saved["metadata/extraction/true_depth"]) == 673.5
+    assert list(saved["metadata/extraction/parameters/bg_roi_depth_range"]) == [650, 750]
+
+
+def test_overlapping_chunk_raises_like_reference(g, RS):
+    h = RS.MemoryH5()
+    n = int(g["nframes"])
+    for k in ("frames", "frames_mask"):
+        h.create_dataset(k, (n, 80, 80), "uint8" if k == "frames" else "bool")
+    h.create_dataset("metadata/extraction/flips", (n,), "bool")
+    c = _chunks(g)[0]
+    c = dict(c, offset=2, scalars={}, keypoints={})
+    with pytest.raises(ValueError):
+        RS.write_extracted_chunk_to_h5(h, c)
+
+
+def test_keypoints_tsv_bytes(g, RS, tmp_path):
+    w = RS.KeypointsTSVWriter(str(tmp_path))
+    for c in _chunks(g):
+        w.write(c)
+    with open(w.path, "rb") as fh:
+        got = fh.read()
+    assert got == bytes(g["tsv"])
