@@ -26,6 +26,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# One HIP hardware queue per stream of the overlapped pipeline (default, front,
+# two model forwards, tail): with HIP's default of 4 the tail shares a queue
+# with a model stream, and its wait for one forward blocks the next forward
+# queued behind it (measured +2.7 % with 8).  Read at HIP initialisation.
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 
 def parse():
@@ -38,6 +43,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=50, choices=[50, 101])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--issue-stream", type=int, default=1, help="issue the pipeline from a pool stream (1) or the NULL stream (0)")
     ap.add_argument("--cpu-sample-frames", type=int, default=2)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     ap.add_argument("--no-overlap", action="store_true",
@@ -219,12 +225,29 @@ def main():
 
     pipe = None if args.no_overlap else OverlappedExtractor(ex, args.model_streams)
 
+    gstream = torch.cuda.Stream() if world > 1 else None
+
     def deliver(r):
         if r is not None and world > 1:
-            payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
-            dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
+            # on a side stream, so the hand-off never orders the caller's
+            # stream (and the pipeline's next fronts) behind this batch
+            with torch.cuda.stream(gstream):
+                if "ready" in r:
+                    gstream.wait_event(r["ready"])
+                payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
+                dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
+
+    # the loop issues from a pool stream, not HIP's legacy NULL stream: an
+    # event recorded on the NULL stream also waits for all earlier work of
+    # every blocking stream, which would order each front behind the
+    # previous forward
+    issue_stream = torch.cuda.Stream() if args.issue_stream else torch.cuda.current_stream()
 
     def run(nsteps, offset):
+        with torch.cuda.stream(issue_stream):
+            run_(nsteps, offset)
+
+    def run_(nsteps, offset):
         # nsteps batches through the path; with the pipeline the last batch is
         # flushed inside, so exactly nsteps batches complete
         for i in range(nsteps):

@@ -223,9 +223,11 @@ int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const 
                   void *out, mdx_stream_t stream);
 
 /* ROIAlign kernel choice: 0 = one workgroup per (ROI, 128-B channel slice)
- * with the sample window staged in LDS; 1 (default), 2, 3 = one workgroup per
+ * with the sample window staged in LDS; 1, 2, 3 = one workgroup per
  * ROI over all channels, taps gathered from the map, 1/2/4 items per thread
- * in lockstep.  Returns the old mode. */
+ * in lockstep; 4 (default) = one workgroup per ROI, separable form (per-bin row and
+ * column weight sums, (gh+1)(gw+1) taps per output instead of 4 gh gw).
+ * Returns the old mode. */
 int mdx_roi_align_set_mode(int mode);
 
 /* fast_rcnn_inference_single_image + detector_postprocess for 1 class:

@@ -1067,7 +1067,161 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
 
 // kernel choice (tests / microbenchmarks): 0 slice + LDS window; 1, 2, 3:
 // full-channel rows with 1, 2, 4 items per thread in lockstep
-static int g_roi_mode = 1;
+// Separable form of the same average (mode 4): a sample's bilinear weights
+// factor into a row part and a column part, so the bin average over its gh x gw
+// sample grid is sum_r sum_c A[r] B[c] F[r][c] / count, with A[r] (B[c]) the
+// summed row (column) weights of the bin's sample rows (columns).  With the
+// adaptive grid (gh = ceil(bin height)) samples are <= 1 px apart and a bin
+// touches gh + 1 rows: (gh+1)(gw+1) 16-B taps per output group instead of
+// 4 gh gw (16 instead of 36 at 3 x 3) -- the tap loads through the texture
+// path are what bound this kernel.  Rounding differs from the per-sample sum
+// (fp32, ~1 ulp); bins needing more than ROI_RMAX rows or columns (fixed
+// sampling ratios) take the per-sample path.
+constexpr int ROI_RMAX = 8, ROI_PMAX = 16;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float *__restrict__ rois,
+                                                       const int *__restrict__ counts, T *__restrict__ out) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ int s_r0[ROI_PMAX], s_nr[ROI_PMAX], s_c0[ROI_PMAX], s_nc[ROI_PMAX];
+    __shared__ float s_A[ROI_PMAX][ROI_RMAX], s_B[ROI_PMAX][ROI_RMAX];
+    __shared__ int s_bad;
+    int r;
+    {
+        const int Lb = blockIdx.x, nwg = gridDim.x;
+        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
+        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
+    }
+    const int b = r / rl.per_image, ri = r - b * rl.per_image;
+    const int C = rl.C, P = rl.P;
+    const int G = C / V;
+    T *o = out + (long long)r * P * P * C;
+    const int nitems = P * P * G;
+    if (ri >= counts[b]) {
+        const float z[V] = {};
+        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)i * V, z);
+        return;
+    }
+    const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
+    const T *f = reinterpret_cast<const T *>(g.feat);
+    if (threadIdx.x == 0) s_bad = P > ROI_PMAX;
+    __syncthreads();
+    // row tables by lanes 0..P-1 of wave 0, column tables by wave 1
+    const int w = threadIdx.x >> 6, lidx = threadIdx.x & 63;
+    if (w < 2 && lidx < P && P <= ROI_PMAX) {
+        const bool rows = w == 0;
+        const int n = rows ? g.gh : g.gw, size = rows ? g.H : g.W;
+        const float st = rows ? g.rsh : g.rsw, bsz = rows ? g.bh : g.bw;
+        float wt[ROI_RMAX];
+#pragma unroll
+        for (int j = 0; j < ROI_RMAX; ++j) wt[j] = 0.f;
+        int base = -1, cnt = 0;
+        bool bad = false;
+        for (int i = 0; i < n; ++i) {
+            const float v = st + (float)lidx * bsz + ((float)i + .5f) * bsz / (float)n;
+            int lo, hi;
+            float l;
+            if (!roi_axis(v, size, lo, hi, l)) continue;
+            if (base < 0) base = lo;
+            const int a = lo - base, c = hi - base;
+            if (c >= ROI_RMAX) {
+                bad = true;
+                break;
+            }
+#pragma unroll
+            for (int j = 0; j < ROI_RMAX; ++j) wt[j] += (j == a ? 1.f - l : 0.f) + (j == c ? l : 0.f);
+            cnt = c + 1 > cnt ? c + 1 : cnt;
+        }
+        if (bad) s_bad = 1;
+        if (rows) {
+            s_r0[lidx] = base < 0 ? 0 : base;
+            s_nr[lidx] = cnt;
+#pragma unroll
+            for (int j = 0; j < ROI_RMAX; ++j) s_A[lidx][j] = wt[j];
+        } else {
+            s_c0[lidx] = base < 0 ? 0 : base;
+            s_nc[lidx] = cnt;
+#pragma unroll
+            for (int j = 0; j < ROI_RMAX; ++j) s_B[lidx][j] = wt[j];
+        }
+    }
+    __syncthreads();
+    if (s_bad) {
+        // per-sample path (the reference formula), taps from global memory
+        for (int t = threadIdx.x; t < nitems; t += 256) {
+            const int bin = t / G, cg = t - bin * G;
+            const int ph = bin / P, pw = bin - ph * P;
+            const T *fc = f + cg * V;
+            float acc[V];
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[i] = 0.f;
+            for (int iy = 0; iy < g.gh; ++iy) {
+                const float y = g.rsh + (float)ph * g.bh + ((float)iy + .5f) * g.bh / (float)g.gh;
+                int yl, yh;
+                float ly;
+                if (!roi_axis(y, g.H, yl, yh, ly)) continue;
+                for (int ix = 0; ix < g.gw; ++ix) {
+                    const float x = g.rsw + (float)pw * g.bw + ((float)ix + .5f) * g.bw / (float)g.gw;
+                    int xl, xh;
+                    float lx;
+                    if (!roi_axis(x, g.W, xl, xh, lx)) continue;
+                    const float hy = 1.f - ly, hx = 1.f - lx;
+                    float v1[V], v2[V], v3[V], v4[V];
+                    ld16(fc + ((long long)yl * g.W + xl) * C, v1);
+                    ld16(fc + ((long long)yl * g.W + xh) * C, v2);
+                    ld16(fc + ((long long)yh * g.W + xl) * C, v3);
+                    ld16(fc + ((long long)yh * g.W + xh) * C, v4);
+#pragma unroll
+                    for (int i = 0; i < V; ++i)
+                        acc[i] += hy * hx * v1[i] + hy * lx * v2[i] + ly * hx * v3[i] + ly * lx * v4[i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+            st16(o + (long long)t * V, acc);
+        }
+        return;
+    }
+    for (int t = threadIdx.x; t < nitems; t += 256) {
+        const int bin = t / G, cg = t - bin * G;
+        const int ph = bin / P, pw = bin - ph * P;
+        const int nr = s_nr[ph], nc = s_nc[pw];
+        const T *fc = f + ((long long)s_r0[ph] * g.W + s_c0[pw]) * C + cg * V;
+        float acc[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        // two rows x four columns of taps per round, all eight loads issued
+        // before any is consumed (the kernel is bound by load latency):
+        // out-of-range taps re-read the last valid pixel with weight 0
+        for (int j = 0; j < nr; j += 2) {
+            const bool two = j + 1 < nr;
+            const float a0 = s_A[ph][j], a1 = two ? s_A[ph][j + 1] : 0.f;
+            const T *rp0 = fc + (long long)j * g.W * C;
+            const T *rp1 = two ? rp0 + (long long)g.W * C : rp0;
+            for (int kc = 0; kc < nc; kc += 4) {
+                float v[8][V];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = kc + u < nc ? kc + u : nc - 1;
+                    ld16(rp0 + (long long)k * C, v[u]);
+                    ld16(rp1 + (long long)k * C, v[4 + u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float bk = kc + u < nc ? s_B[pw][kc + u] : 0.f;
+                    const float w0 = a0 * bk, w1 = a1 * bk;
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] += w0 * v[u][i] + w1 * v[4 + u][i];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+        st16(o + (long long)t * V, acc);
+    }
+}
+
+static int g_roi_mode = 4;
 extern "C" int mdx_roi_align_set_mode(int mode) {
     const int old = g_roi_mode;
     g_roi_mode = mode;
@@ -1538,7 +1692,14 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     }
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
-    if (g_roi_mode >= 1 && g_roi_mode <= 3) {
+    if (g_roi_mode == 4 && P <= ROI_PMAX) {
+        if (dtype == 1)
+            hipLaunchKernelGGL(k_roi_align_sep<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                               (_Float16 *)out);
+        else
+            hipLaunchKernelGGL(k_roi_align_sep<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                               (float *)out);
+    } else if (g_roi_mode >= 1 && g_roi_mode <= 4) {
 #define MDX_ROI_FULL(NI_)                                                                                     \
     do {                                                                                                      \
         if (dtype == 1)                                                                                       \

@@ -230,9 +230,11 @@ class OverlappedExtractor:
         self.fronted = None            # (prepped, cleaned, event) awaiting the model
         self.modeled = collections.deque()  # (prepped, cleaned, inf, event) awaiting the tail
 
-    def _front(self, raw):
+    def _front(self, raw, raw_ready):
         caller = torch.cuda.current_stream()
-        self.s_front.wait_stream(caller)  # raw produced on the caller's stream
+        # raw was produced on the caller's stream before this submit; wait for
+        # exactly that, not for the tail hand-offs queued on it since
+        self.s_front.wait_event(raw_ready)
         with torch.cuda.stream(self.s_front):
             prepped, cleaned = self.ex.front(raw)
             ev = torch.cuda.Event()
@@ -260,9 +262,22 @@ class OverlappedExtractor:
             for t in (prepped, cleaned, *[v for v in inf.values() if torch.is_tensor(v)]):
                 t.record_stream(self.s_tail)
             out = self.ex.tail(prepped, cleaned, inf)
-        caller.wait_stream(self.s_tail)
+            ready = torch.cuda.Event()
+            ready.record(self.s_tail)
         for v in out.values():
             v.record_stream(caller)
+        # the caller's stream does NOT wait here: a wait queued on it would
+        # hold back every later front (and through it the next forwards)
+        # until this batch's tail is done; consumers wait on out["ready"]
+        # (OverlappedExtractor.wait) or call flush()
+        out["ready"] = ready
+        return out
+
+    @staticmethod
+    def wait(out, stream=None):
+        """Make `stream` (default: current) wait until a submit() result is
+        complete."""
+        (stream or torch.cuda.current_stream()).wait_event(out["ready"])
         return out
 
     def submit(self, raw: torch.Tensor):
@@ -270,12 +285,14 @@ class OverlappedExtractor:
         # are in flight), forward of the fronted batch, front of `raw`; every
         # stage's inputs were issued on an earlier call, so the stages (and up
         # to `depth` forwards) run concurrently on the device
+        raw_ready = torch.cuda.Event()
+        raw_ready.record(torch.cuda.current_stream())
         out = None
         if len(self.modeled) >= len(self.s_models):
             out = self._tail(self.modeled.popleft())
         if self.fronted is not None:
             self.modeled.append(self._model(self.fronted))
-        self.fronted = self._front(raw)
+        self.fronted = self._front(raw, raw_ready)
         return out
 
     def flush(self):
@@ -287,4 +304,5 @@ class OverlappedExtractor:
             self.fronted = None
         while self.modeled:
             outs.append(self._tail(self.modeled.popleft()))
+        torch.cuda.current_stream().wait_stream(self.s_tail)  # every result so far is complete
         return outs

@@ -46,7 +46,7 @@ def main():
     from moseq2_detectron_extract_amd._lib import call
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     outs = {}
-    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4")):
+    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4"), (4, "separable")):
         old = call("mdx_roi_align_set_mode", mode)
         for _ in range(2):
             out = orig(feats, props, pcount, R, P, *a, **k)
@@ -59,6 +59,27 @@ def main():
         outs[mode] = out.float()
         print(f"box ROIAlign [{name}]: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
     print("max |diff| between kernels:", max((outs[0] - outs[m]).abs().max().item() for m in outs))
+    # locality experiment: ROIs of each image ordered by level, then position
+    pr = props.reshape(pcount.shape[0], -1, 4)
+    cy = (pr[..., 1] + pr[..., 3]) / 2
+    cx = (pr[..., 0] + pr[..., 2]) / 2
+    wv, hv = (pr[..., 2] - pr[..., 0]).clamp(min=0), (pr[..., 3] - pr[..., 1]).clamp(min=0)
+    lv = torch.floor(4 + torch.log2(torch.sqrt(wv * hv) / 224 + 1e-8)).clamp(2, 5)
+    key = lv * 1e6 + torch.floor(cy / 32) * 1e3 + cx
+    order = key.argsort(dim=1)
+    ps = torch.gather(pr, 1, order[..., None].expand(-1, -1, 4)).reshape(props.shape).contiguous()
+    for mode in (1, 4):
+        old = call("mdx_roi_align_set_mode", mode)
+        for _ in range(2):
+            out = orig(feats, ps, pcount, R, P, *a, **k)
+        e0.record()
+        for _ in range(5):
+            out = orig(feats, ps, pcount, R, P, *a, **k)
+        e1.record()
+        torch.cuda.synchronize()
+        call("mdx_roi_align_set_mode", old)
+        print(f"box ROIAlign [mode {mode}, ROIs sorted by level/position]: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us",
+              flush=True)
 
 if __name__ == "__main__":
     main()
