@@ -597,6 +597,15 @@ __device__ __forceinline__ void glds16(const void *src, char *dst) {
 
 __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 
+// s_waitcnt the compiler's waitcnt pass can see (an inline-asm waitcnt is
+// opaque to it: it then re-waits for loads this one already drained), fenced
+// by empty memory clobbers so no memory operation moves across it.
+// gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14
+#define MDX_WAIT_VM(n) \
+    do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_waitcnt(0x0F70 | (n)); asm volatile("" ::: "memory"); } while (0)
+#define MDX_WAIT_LGKM0() \
+    do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_waitcnt(0xC07F); asm volatile("" ::: "memory"); } while (0)
+
 template <typename TO, int NW, bool ILV, bool PRIO = false>
 __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
@@ -707,11 +716,11 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     auto wait_landed = [&](int u, int issued_upto) {
         const int ahead = issued_upto - u;
         if (ahead >= 2)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            MDX_WAIT_VM(8);
         else if (ahead == 1)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            MDX_WAIT_VM(4);
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            MDX_WAIT_VM(0);
     };
     issue(0);
     if (T > 1) issue(1);
@@ -736,8 +745,9 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
             // drain this wave's pending fragment reads (those of substep t)
             // before the barrier: after it no wave still reads buffer
             // (t + 3) & 3 == (t - 1) & 3, which the next DMA overwrites
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            MDX_WAIT_LGKM0();
             __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
             read_frags(t + 1, cur ^ 1);
             if (t + 3 < T) {
                 if (ILV) {
@@ -769,6 +779,12 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
                 issue((t + 3) & 3);
                 issued = t + 3;
             }
+        } else {
+            // last substep: an explicit wait on this path too (taken once), so
+            // the two paths joining before mma() agree that the current set's
+            // reads are drained; otherwise the compiler waits for the NEXT
+            // set's reads before the MFMAs of every odd step
+            MDX_WAIT_LGKM0();
         }
         mma(cur);
     };
