@@ -171,6 +171,15 @@ enum {
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256
  * only when Cout == 64), 2 for every eligible layer with M >= min_m. */
 int mdx_conv_set_stream1x1(int mode, int min_m);
+
+/* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
+ * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1
+ * when the split reaches >= 192 workgroups with >= min_sub 32-deep substeps
+ * per slice, 2 whenever possible (tests).  Measured slower than the 128-row
+ * kernel on every such layer of the bench (short slices: pipeline fill/drain
+ * and the fp32 partial round trip), hence off.  Slices are summed in fixed order by
+ * the split-K reduction.  Returns the old mode. */
+int mdx_conv_set_split256(int mode, int min_sub);
 int mdx_conv2d_last_plan(int *kernel, int *ksplit);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,

@@ -646,7 +646,18 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * 8 : nullptr;
     }
     // issue state (uniform): the 64-chunk being issued and its tap
-    int i_kci = 0, i_kkx = 0, i_kky = 0, i_half = 0;
+    // split-K: slice z = blockIdx.y multiplies substeps [s0, s0 + T) of the
+    // K order (channel chunk outer, tap, half inner)
+    const int s0 = (int)blockIdx.y * a.ksteps;
+    int i_kci, i_kkx, i_kky, i_half;
+    {
+        const int q = s0 >> 1, taps = a.KH * a.KW;
+        i_half = s0 & 1;
+        const int tap = q % taps;
+        i_kci = (q / taps) * 64;
+        i_kky = tap / a.KW;
+        i_kkx = tap - i_kky * a.KW;
+    }
     // DMA piece p of the substep being issued into buffer buf: p = 0, 1 the A
     // rows of instruction j = p, p = 2, 3 the B rows of j = p - 2
     auto issue_piece = [&](int buf, int p) {
@@ -687,7 +698,7 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    const int T = a.K / 32;  // substeps
+    const int T = min(a.K / 32 - s0, a.ksteps);  // substeps of this slice
     // fragment rows of this lane: r = 16 i + (lane & 15) (+ multiples of 64)
     const int off = ((lane >> 4) ^ g_swz(lane & 15)) * 16;
     const char *Abase = smem + (wm * GT::WROWS + (lane & 15)) * 64 + off;
@@ -813,14 +824,30 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
                 for (int r = 0; r < 4; ++r)
                     Cs[(i * 16 + (lane >> 4) * 4 + r) * GT::EPI_PITCH + j * 16 + (lane & 15)] = acc[IPP * h + i][j][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        finish_batch<TO, 8>(a, [&](int q, int &gm, int &gn0, const float *&src) {
-            const int item = lane + 64 * q;
-            const int row = item >> 3, ch = item & 7;
-            gm = m0 + wm * GT::WROWS + GT::EPI_ROWS * h + row;
-            gn0 = n0 + wn * GT::WCOLS + ch * 8;
-            src = Cs + row * GT::EPI_PITCH + ch * 8;
-            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
-        });
+        if (a.ksplit > 1) {
+            // raw fp32 partial of this K slice (k_conv_reduce sums the slices)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int item = lane + 64 * q;
+                const int row = item >> 3, ch = item & 7;
+                const int gm = m0 + wm * GT::WROWS + GT::EPI_ROWS * h + row;
+                const int gn0 = n0 + wn * GT::WCOLS + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) continue;
+                const float *src = Cs + row * GT::EPI_PITCH + ch * 8;
+                float *pp = a.part + ((long long)blockIdx.y * a.M + gm) * a.Cout + gn0;
+                *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
+                *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
+            }
+        } else {
+            finish_batch<TO, 8>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+                const int item = lane + 64 * q;
+                const int row = item >> 3, ch = item & 7;
+                gm = m0 + wm * GT::WROWS + GT::EPI_ROWS * h + row;
+                gn0 = n0 + wn * GT::WCOLS + ch * 8;
+                src = Cs + row * GT::EPI_PITCH + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+            });
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 }
@@ -845,6 +872,15 @@ extern "C" int mdx_conv_set_large_tiles(int mode) {
 static int g_dma128 = 0, g_dma128_min_tiles = 1536;
 // DMA pieces interleaved with the MFMAs in the 128x128 LDS-DMA kernel (0/1)
 static int g_prio = 1;
+// split-K on the 256x256 kernel for few-tile deep-K layers (0 off -- default, measured slower --, 1 auto,
+// 2 whenever Cout % 256 == 0 -- tests) and the minimum substeps (of 32) per slice
+static int g_split256 = 0, g_split256_min_sub = 18;
+extern "C" int mdx_conv_set_split256(int mode, int min_sub) {
+    const int old = g_split256;
+    g_split256 = mode;
+    g_split256_min_sub = min_sub;
+    return old;
+}
 // s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
 static int g_prio8 = 0;
 extern "C" int mdx_conv_set_mfma_prio256(int on) {
@@ -971,7 +1007,7 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
             a.tiles_n = (int)ceil_div(Cout, G4::BN);
             a.tiles_total = (int)t128;
             a.ksplit = 1;
-            a.ksteps = a.K / 64;
+            a.ksteps = a.K / 32;
             if (out_dtype == 1 && g_prio)
                 hipLaunchKernelGGL((k_convg<_Float16, 4, true>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
             else if (out_dtype == 1)
@@ -986,21 +1022,43 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
         const bool big = Cout >= 192 && t256 >= 384;
-        if (g_large_tiles == 2 || (g_large_tiles == 1 && big)) {
+        // split-K on the 256x256 kernel for layers with few tiles but a deep
+        // K (res4/res5 and head 3x3 convs): enough slices to fill the chip
+        int ks256 = 1;
+        if (!big && g_split256 && workspace && Cout % 256 == 0 && ksplit <= 1) {
+            const int nsub = a.K / 32;
+            for (int k = 2; k <= 8; ++k) {
+                if (nsub / k < g_split256_min_sub || (long long)k * M * Cout * 4 > workspace_bytes) break;
+                ks256 = k;
+                if (t256 * k >= 256) break;
+            }
+            if (g_split256 == 1 && t256 * ks256 < 192) ks256 = 1;  // still too few workgroups: the 128-row kernel
+        }
+        if (g_large_tiles == 2 || (g_large_tiles == 1 && big) || ks256 > 1) {
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
-            a.ksplit = 1;
-            a.ksteps = a.K / 64;
+            a.ksplit = ks256;
+            a.ksteps = (a.K / 32 + ks256 - 1) / ks256;
+            a.ksplit = (a.K / 32 + a.ksteps - 1) / a.ksteps;
+            a.part = reinterpret_cast<float *>(workspace);
+            const dim3 grid256((unsigned)a.tiles_total, (unsigned)a.ksplit);
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
             if (out_dtype == 1 && g_prio8)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false, true>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s,
-                                   a);
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else if (out_dtype == 1)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else
-                hipLaunchKernelGGL((k_convg<float, 8, false>), dim3(a.tiles_total), dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
+            if (a.ksplit > 1) {
+                if (out_dtype == 1)
+                    hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)),
+                                       dim3(256), 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_conv_reduce<float>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)),
+                                       dim3(256), 0, s, a);
+            }
             t_plan_kernel = MDX_CONV_KERNEL_DMA256;
-            t_plan_ksplit = 1;
+            t_plan_ksplit = a.ksplit;
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }

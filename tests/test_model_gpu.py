@@ -41,10 +41,11 @@ CONV_CASES = [
     (600, 1, 1, 1024, 264, 1, 1, 0, False, False),
     (2, 20, 30, 128, 192, 1, 1, 0, True, True),
     (1, 17, 19, 256, 64, 1, 1, 0, False, False),
+    (1, 12, 10, 128, 512, 3, 1, 1, True, True),
 ]
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128", "stream"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128", "stream", "split256"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -79,6 +80,22 @@ def test_conv2d(mdx, dtype, case, ksplit):
             assert kid.value == 4
         finally:
             call("mdx_conv_set_stream1x1", old, 65536)
+    elif ksplit == "split256":
+        if dtype != "fp16" or Cin % 64 or Cout % 256:
+            pytest.skip("256x256 split-K: fp16, Cin % 64 == 0, Cout % 256 == 0")
+        nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
+        ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
+        old_nk = call("mdx_conv_set_narrow_kmax", 0)
+        old = call("mdx_conv_set_split256", 2, 1)
+        try:
+            call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu),
+                 0, dc, dc, P(out), 0, P(ws), nb, None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            assert kid.value == 2 and (ks_.value > 1 or Cin * k * k <= 32)
+        finally:
+            call("mdx_conv_set_split256", old, 18)
+            call("mdx_conv_set_narrow_kmax", old_nk)
     elif ksplit in ("large", "dma128"):
         if dtype != "fp16" or Cin % 64:
             pytest.skip("LDS-DMA kernels: fp16, Cin % 64 == 0")
