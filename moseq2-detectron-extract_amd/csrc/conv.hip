@@ -478,6 +478,30 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
     const int n0 = tn * 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
+    const int m0 = tm * 128 + wid * 32;
+    // Output layout of the epilogue: per pixel row and pair of 16-channel
+    // blocks (2p, 2p+1), lane group g = lane >> 4 owns 8 consecutive channels
+    // -- block 2p + (g & 1), channels 8 (g >> 1) .. +8 -- after one exchange
+    // with lane ^ 16, so residual loads and output stores are 16 B per lane
+    // (8-B accesses run at ~0.6x the 16-B rate).
+    const int g = lane >> 4;
+    const int ch_in_pair = 16 * (g & 1) + 8 * (g >> 1);  // channel offset within a 32-channel pair
+    // residual first: its loads are the longest stream and depend on nothing
+    half8 rr[2][2];
+    if (a.res) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
+                                                                            0x00020000);
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms) {
+            const int m = m0 + 16 * ms + (lane & 15);
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const unsigned off =
+                    m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 32 * pp + ch_in_pair) * 2) : 0xFFFFFFF0u;
+                rr[ms][pp] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
+            }
+        }
+    }
     // stage the 64 x K weight slice
     for (int i = tid; i < 64 * K / 8; i += 256) {
         const int r = i / (K / 8), c = i - r * (K / 8);
@@ -485,7 +509,6 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
             *reinterpret_cast<const uint4 *>(Wt + (long long)(n0 + r) * K + c * 8);
     }
     // this wave's 32 pixels and their activation fragments
-    const int m0 = tm * 128 + wid * 32;
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
     half8 xf[2][KC];
 #pragma unroll
@@ -515,46 +538,44 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
             for (int ns = 0; ns < 4; ++ns)
                 acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ns], xf[ms][kc], acc[ms][ns], 0, 0, 0);
     }
-    // epilogue: bias, residual, ReLU, fp16, 8-byte stores
-    const int cq = 4 * (lane >> 4);
-    float bv[4][4];
-#pragma unroll
-    for (int ns = 0; ns < 4; ++ns) {
-        const float4 b4 = a.bias ? *reinterpret_cast<const float4 *>(a.bias + n0 + 16 * ns + cq)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        bv[ns][0] = b4.x; bv[ns][1] = b4.y; bv[ns][2] = b4.z; bv[ns][3] = b4.w;
-    }
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    half4 rr[2][4];
-    if (a.res) {
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
-                                                                            0x00020000);
-#pragma unroll
-        for (int ms = 0; ms < 2; ++ms) {
-            const int m = m0 + 16 * ms + (lane & 15);
-#pragma unroll
-            for (int ns = 0; ns < 4; ++ns) {
-                const unsigned off = m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 16 * ns + cq) * 2) : 0xFFFFFFF0u;
-                rr[ms][ns] = __builtin_bit_cast(half4, __builtin_amdgcn_raw_buffer_load_b64(rd, off, 0, 0));
-            }
-        }
-    }
+    // epilogue: exchange halves with lane ^ 16, bias, residual, ReLU, fp16,
+    // 16-byte stores
+    const bool odd = (g & 1) != 0;
     _Float16 *O = reinterpret_cast<_Float16 *>(a.out);
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-        const int m = m0 + 16 * ms + (lane & 15);
-        if (m >= a.M) continue;
+    for (int pp = 0; pp < 2; ++pp) {
+        const int c0 = n0 + 32 * pp + ch_in_pair;
+        float bv[8];
 #pragma unroll
-        for (int ns = 0; ns < 4; ++ns) {
-            half4 o;
+        for (int h = 0; h < 2; ++h) {
+            const float4 b4 = a.bias ? *reinterpret_cast<const float4 *>(a.bias + c0 + 4 * h)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            bv[4 * h] = b4.x; bv[4 * h + 1] = b4.y; bv[4 * h + 2] = b4.z; bv[4 * h + 3] = b4.w;
+        }
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms) {
+            // even groups keep block 2pp and receive its upper 4 channels; odd
+            // groups keep block 2pp+1 and receive its lower 4 channels
+            float v[8];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v = acc[ms][ns][r] + bv[ns][r];
-                if (a.res) v += (float)rr[ms][ns][r];
-                if (a.relu) v = v > 0.f ? v : 0.f;
-                o[r] = (_Float16)v;
+                const float keep = odd ? acc[ms][2 * pp + 1][r] : acc[ms][2 * pp][r];
+                const float send = odd ? acc[ms][2 * pp][r] : acc[ms][2 * pp + 1][r];
+                const float recv = __shfl_xor(send, 16);
+                v[odd ? 4 + r : r] = keep;
+                v[odd ? r : 4 + r] = recv;
             }
-            *reinterpret_cast<half4 *>(O + (long long)m * a.Cout + n0 + 16 * ns + cq) = o;
+            const int m = m0 + 16 * ms + (lane & 15);
+            if (m >= a.M) continue;
+            half8 o;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                float x = v[r] + bv[r];
+                if (a.res) x += (float)rr[ms][pp][r];
+                if (a.relu) x = x > 0.f ? x : 0.f;
+                o[r] = (_Float16)x;
+            }
+            *reinterpret_cast<half8 *>(O + (long long)m * a.Cout + c0) = o;
         }
     }
 }
