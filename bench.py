@@ -62,10 +62,11 @@ KERNEL_SYMBOLS = {  # MDX_CONV_KERNEL_* -> rocprofv3 symbol (fp16 in / fp16 out)
     2: "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0EEEvNS_8ConvArgsE",
     3: "_ZN3mdx7k_convgIDF16_Li4ELb1ELb0EEEvNS_8ConvArgsE",
     4: "k_conv1x1_stream<KC> (three instances by K)",
+    5: "k_conv1x1_head<KC> (three instances by K)",
 }
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
-                4: "k_conv1x1_stream streaming 1x1 GEMM"}
+                4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1"}
 
 
 def conv_roofline(extractor, raw, steps=3, dump=None):

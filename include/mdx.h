@@ -165,7 +165,8 @@ enum {
     MDX_CONV_KERNEL_REG64 = 1,
     MDX_CONV_KERNEL_DMA256 = 2,
     MDX_CONV_KERNEL_DMA128 = 3,
-    MDX_CONV_KERNEL_STREAM1X1 = 4
+    MDX_CONV_KERNEL_STREAM1X1 = 4,
+    MDX_CONV_KERNEL_HEAD1X1 = 5
 };
 /* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256

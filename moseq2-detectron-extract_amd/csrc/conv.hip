@@ -580,6 +580,58 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
     }
 }
 
+// Narrow-output streaming 1x1 kernel (RPN head: 256 -> 15 logits/deltas,
+// fp32 out): one 16-row MFMA block of output channels (rows >= Cout read as
+// zero weights), no LDS and no barrier -- each wave loads its 16 x K weight
+// fragments straight from L2 and streams 32 pixels' activations into the B
+// operands, so the launch runs at the activation read rate.
+template <int KC>
+__global__ __launch_bounds__(256) void k_conv1x1_head(ConvArgs a) {
+    constexpr int K = 32 * KC;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int m0 = (int)blockIdx.x * 128 + wid * 32;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    half8 xf[2][KC], wf[KC];
+    const int orow = lane & 15;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+        wf[kc] = __builtin_bit_cast(
+            half8, __builtin_amdgcn_raw_buffer_load_b128(
+                       rw, orow < a.Cout ? (unsigned)((orow * K + 8 * (lane >> 4) + 32 * kc) * 2) : 0xFFFFFFF0u, 0, 0));
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+        const int m = m0 + 16 * ms + (lane & 15);
+        const unsigned base = (unsigned)((long long)m * K * 2) + 16u * (lane >> 4);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+            xf[ms][kc] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rx, m < a.M ? base + 64u * kc : 0xFFFFFFF0u, 0, 0));
+    }
+    float4v acc[2] = {float4v{0.f, 0.f, 0.f, 0.f}, float4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+            acc[ms] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[kc], xf[ms][kc], acc[ms], 0, 0, 0);
+    // D[och = 4 (lane >> 4) + r][pixel = lane & 15]
+    const int oc = 4 * (lane >> 4);
+    float* O = reinterpret_cast<float *>(a.out);
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+        const int m = m0 + 16 * ms + (lane & 15);
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = oc + r;
+            if (c >= a.Cout) continue;
+            float v = acc[ms][r] + (a.bias ? a.bias[c] : 0.f);
+            if (a.relu) v = v > 0.f ? v : 0.f;
+            O[(long long)m * a.Cout + c] = v;
+        }
+    }
+}
+
 // streaming 1x1 kernel policy: 0 never, 1 for eligible layers with M >= g_stream_min_m (default),
 // 2 also for K = 256 layers with Cout > 64
 static int g_stream1x1 = 1, g_stream_min_m = 65536;
@@ -999,6 +1051,22 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
     // HBM-bound 1x1 layers: the streaming kernel
+    if (g_stream1x1 && in_dtype == 1 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+        pad == 0 && !residual && (Cin == 64 || Cin == 128 || Cin == 256) && Cout <= 16 && (ksplit == 1 || ksplit == 0)) {
+        a.tiles_n = 1;
+        a.tiles_total = (int)ceil_div(M, 128);
+        a.ksplit = 1;
+        if (Cin == 64)
+            hipLaunchKernelGGL(k_conv1x1_head<2>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else if (Cin == 128)
+            hipLaunchKernelGGL(k_conv1x1_head<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_conv1x1_head<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        t_plan_kernel = MDX_CONV_KERNEL_HEAD1X1;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
     if (g_stream1x1 && in_dtype == 1 && out_dtype == 1 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
         pad == 0 && (Cin == 64 || Cin == 128 || (Cin == 256 && (Cout == 64 || g_stream1x1 == 2))) && Cout % 64 == 0 &&
         (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m) {

@@ -45,6 +45,29 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("Cin,Cout,M", [(256, 15, 5000), (64, 16, 130), (128, 3, 77), (256, 12, 128)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_head_1x1_fp32_out(mdx, Cin, Cout, M, relu):
+    """Narrow-output streaming 1x1 kernel (RPN head): fp16 in, fp32 out."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(Cin + Cout + M)
+    x = torch.randn(1, M, 1, Cin, generator=g).half()
+    w = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).half()
+    b = torch.randn(Cout, generator=g)
+    want = _conv_ref(x.float(), w.float(), b, 1, 0, None, relu)
+    out = torch.empty(1, M, 1, Cout, dtype=torch.float32, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    xd, wd, bd = x.cuda(), w.reshape(Cout, Cin).contiguous().cuda(), b.cuda()
+    call("mdx_conv2d", P(xd), 1, M, 1, Cin, P(wd), P(bd), Cout, 1, 1, 1, 0, None, int(relu), 0, 1, 0, P(out), None)
+    kid, ks_ = ctypes.c_int(), ctypes.c_int()
+    call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+    assert kid.value == 5
+    got = out.cpu().double()
+    err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-6)
+    assert err < 1e-3, err
+
+
 @pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128", "stream", "split256"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
