@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--dma128", type=int, default=None, help="conv kernel policy knob (mdx_conv_set_dma128)")
     ap.add_argument("--prio256", type=int, default=None, help="conv knob (mdx_conv_set_mfma_prio256)")
     ap.add_argument("--stream1x1", type=int, default=None, help="conv knob (mdx_conv_set_stream1x1)")
+    ap.add_argument("--stream-min-m", type=int, default=65536, help="conv knob (mdx_conv_set_stream1x1 min_m)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -209,7 +210,7 @@ def main():
         call("mdx_conv_set_dma128", args.dma128, 1536)
     if args.stream1x1 is not None:
         from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_stream1x1", args.stream1x1, 65536)
+        call("mdx_conv_set_stream1x1", args.stream1x1, args.stream_min_m)
     if args.prio256 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_mfma_prio256", args.prio256)

@@ -823,8 +823,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
         }
     };
+    // Every step -- the last one too -- waits, crosses the barrier and reads
+    // the next fragment set (after the last substep: a harmless read of a
+    // stale buffer).  With no path skipping the reads, the compiler's waitcnt
+    // pass sees the same state on every path into mma() and never waits for
+    // the set being read before the MFMAs of the other one.
     auto step = [&](int t, int cur) {
-        if (t + 1 < T) {
+        {
             wait_landed(t + 1, issued);
             // drain this wave's pending fragment reads (those of substep t)
             // before the barrier: after it no wave still reads buffer
@@ -863,12 +868,6 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
                 issue((t + 3) & 3);
                 issued = t + 3;
             }
-        } else {
-            // last substep: an explicit wait on this path too (taken once), so
-            // the two paths joining before mma() agree that the current set's
-            // reads are drained; otherwise the compiler waits for the NEXT
-            // set's reads before the MFMAs of every odd step
-            MDX_WAIT_LGKM0();
         }
         mma(cur);
     };
