@@ -181,6 +181,11 @@ int mdx_conv_set_stream1x1(int mode, int min_m);
  * and the fp32 partial round trip), hence off.  Slices are summed in fixed order by
  * the split-K reduction.  Returns the old mode. */
 int mdx_conv_set_split256(int mode, int min_sub);
+
+/* 256x256 LDS-DMA kernel schedule: 1 = issue each substep's DMA after its
+ * MFMA burst (address arithmetic overlaps the burst), 0 (default) = before.
+ * Returns the old setting. */
+int mdx_conv_set_dma_after(int on);
 int mdx_conv2d_last_plan(int *kernel, int *ksplit);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,

@@ -679,7 +679,7 @@ __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 #define MDX_WAIT_LGKM0() \
     do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_waitcnt(0xC07F); asm volatile("" ::: "memory"); } while (0)
 
-template <typename TO, int NW, bool ILV, bool PRIO = false>
+template <typename TO, int NW, bool ILV, bool PRIO = false, bool DMA_AFTER = false>
 __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
@@ -865,11 +865,20 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
                     issued = t + 3;
                     return;
                 }
-                issue((t + 3) & 3);
-                issued = t + 3;
+                if (!DMA_AFTER) {
+                    issue((t + 3) & 3);
+                    issued = t + 3;
+                }
             }
         }
         mma(cur);
+        if (DMA_AFTER && t + 3 < T) {
+            // MFMAs first: right after the barrier every wave has its
+            // operands, and the DMA address arithmetic then overlaps the tail
+            // of the SIMD's MFMA bursts
+            issue((t + 3) & 3);
+            issued = t + 3;
+        }
     };
     int t = 0;
     for (; t + 1 < T; t += 2) {
@@ -951,6 +960,13 @@ extern "C" int mdx_conv_set_split256(int mode, int min_sub) {
     const int old = g_split256;
     g_split256 = mode;
     g_split256_min_sub = min_sub;
+    return old;
+}
+// 256x256 kernel: issue the next DMA after the MFMA burst instead of before (0/1)
+static int g_dma_after = 0;
+extern "C" int mdx_conv_set_dma_after(int on) {
+    const int old = g_dma_after;
+    g_dma_after = on;
     return old;
 }
 // s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
@@ -1131,7 +1147,9 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
             a.part = reinterpret_cast<float *>(workspace);
             const dim3 grid256((unsigned)a.tiles_total, (unsigned)a.ksplit);
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
-            if (out_dtype == 1 && g_prio8)
+            if (out_dtype == 1 && g_dma_after)
+                hipLaunchKernelGGL((k_convg<_Float16, 8, false, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
+            else if (out_dtype == 1 && g_prio8)
                 hipLaunchKernelGGL((k_convg<_Float16, 8, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else if (out_dtype == 1)
                 hipLaunchKernelGGL((k_convg<_Float16, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);

@@ -126,6 +126,7 @@ def test_conv2d(mdx, dtype, case, ksplit):
         old = call("mdx_conv_set_large_tiles", 2 if ksplit == "large" else 0)
         old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
         old_i = call("mdx_conv_set_mfma_prio", int(case[0] % 2 == 0))  # both DMA schedules across the cases
+        old_da = call("mdx_conv_set_dma_after", int(case[1] % 2 == 0))
         try:
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
@@ -134,6 +135,7 @@ def test_conv2d(mdx, dtype, case, ksplit):
             call("mdx_conv_set_narrow_kmax", old_nk)
             call("mdx_conv_set_dma128", old_d, 1536)
             call("mdx_conv_set_mfma_prio", old_i)
+            call("mdx_conv_set_dma_after", old_da)
     elif ksplit == 1:
         call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
              P(out), None)

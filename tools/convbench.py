@@ -29,6 +29,9 @@ def main():
     import mdx_pkg
     mdx_pkg.load()
     from moseq2_detectron_extract_amd._lib import call
+    for kv in sys.argv[2:]:  # knob=value, e.g. dma_after=1 -> mdx_conv_set_dma_after(1)
+        name, val = kv.split("=")
+        call(f"mdx_conv_set_{name}", int(val))
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     ws = torch.empty(64 << 18, dtype=torch.float32, device="cuda")
     copy_src = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
