@@ -415,6 +415,39 @@ def test_forward_fp16_close_to_fp32(small_case):
         assert err < 3e-2, f"{k}: fp16 relative L2 error {err:.2e}"
 
 
+def test_forward_r101_matches_oracle(mdx):
+    """ResNet101-FPN (BASELINE config 5's backbone): fp32 features and
+    detections against the oracle on a small image."""
+    from moseq2_detectron_extract_amd.model import ModelConfig
+    from oracle import model_ref as R
+    cfg = ModelConfig(depth=101, score_thresh_test=0.0)
+    sd, m = _model(cfg, seed=3)
+    imgs = np.random.default_rng(1).integers(0, 256, size=(1, 96, 120, 1), dtype=np.uint8)
+    out = m.forward(torch.from_numpy(imgs[..., 0]).cuda(), intermediates=True)
+    want, inter = R.forward(sd, cfg, imgs)
+    for k in ("res4", "res5", "p2", "p5"):
+        got = out["intermediates"][k].cpu().permute(0, 3, 1, 2).double()
+        w = inter[k].double()
+        err = (got - w).abs().max().item() / (w.abs().max().item() + 1e-9)
+        assert err < 3e-4, f"{k}: rel err {err:.2e}"
+    n = int(out["ndet"][0])
+    assert n == len(want[0]["pred_boxes"])
+    torch.testing.assert_close(out["scores"][0, :n].cpu(), want[0]["scores"], rtol=1e-3, atol=1e-4)
+
+
+def test_forward_r101_fp16_batch64_runs(mdx):
+    """Config 5 shape: R101-FPN fp16, batch 64, full 512x424 frames; every
+    image yields the fixed number of detections with finite outputs."""
+    from moseq2_detectron_extract_amd.model import ModelConfig
+    cfg = ModelConfig(depth=101, score_thresh_test=0.0)
+    _, m = _model(cfg, seed=4, dtype="fp16")
+    x = torch.from_numpy(np.random.default_rng(2).integers(0, 256, size=(64, 423, 511), dtype=np.uint8)).cuda()
+    out = m.forward(x)
+    torch.cuda.synchronize()
+    assert out["ndet"].shape == (64,) and int(out["ndet"].min()) >= 1
+    assert torch.isfinite(out["boxes"]).all() and torch.isfinite(out["keypoints"]).all()
+
+
 def test_predictor_instances(mdx):
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     p = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
