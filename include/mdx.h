@@ -123,6 +123,14 @@ int mdx_frame_scalars(const uint8_t *frames, const uint8_t *masks, int64_t n, in
 int mdx_bground_median(const int16_t *frames, int64_t n, int H, int W, int med_scale, int16_t *work,
                        double *out, mdx_stream_t stream);
 
+/* Host (CPU) function: iterative_filter_angles (M/proc/proc.py:627-654) over
+ * float64 angles[n] with the moving median of filter_angles (:600-624,
+ * bottleneck move_median, min_count 1): repeat until np.allclose(curr, last)
+ * or max_iters; out[n] the filtered angles, flips[n] = isclose(|out - in|,
+ * 180).  Bit-identical to the numpy code; runs without the GIL. */
+int mdx_iterative_filter_angles(const double *angles, int64_t n, int window, double tolerance, int max_iters,
+                                double *out, uint8_t *flips);
+
 /* ---------------------------------------------------------------------
  * Mask/Keypoint R-CNN forward (Predictor.__call__, M/model/predict.py:53-102,
  * Detectron2 GeneralizedRCNN built by M/model/config.py:21-94).  Tensors are

@@ -40,6 +40,7 @@ SIGNATURES = {
     "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P]),
     "mdx_frame_scalars": (I32, [P, P, I64, I32, I32, F64, F64, P, I32, P, P, P, P, P]),
     "mdx_bground_median": (I32, [P, I64, I32, I32, I32, P, P, P]),
+    "mdx_iterative_filter_angles": (I32, [P, I64, I32, F64, I32, P, P]),
     "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
     "mdx_conv_set_large_tiles": (I32, [I32]),
     "mdx_conv_set_narrow_kmax": (I32, [I32]),

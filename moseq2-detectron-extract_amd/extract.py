@@ -59,11 +59,13 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
             states.append((np.asarray(idx), st, host))
         tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
         for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
-            parts.append(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth))
+            parts.append(_lighten(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)))
         states.clear()
+    elif config.overlap_host:
+        parts = _run_overlapped(src, batches, ex, true_depth)
     else:
         for idx, raw in src.iterate(device=True, batches=batches):
-            parts.append(ex.process_chunk(raw, np.asarray(idx), offset=0, true_depth=true_depth))
+            parts.append(_lighten(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
     src.close()
     out: Dict[str, np.ndarray] = {}
     if output_dir:
@@ -105,3 +107,71 @@ def _write_outputs(output_dir, parts, src, bground_im, roi, true_depth, config, 
             tsv.write(d)
     finally:
         h5.close()
+
+
+def _lighten(d: dict) -> dict:
+    """Drop a finished chunk's device frames (prepped, cleaned, masks: 650 KB
+    per frame) once its host results exist; the writer needs none of them."""
+    d["chunk"] = None
+    d["features"]["cleaned_frames"] = None
+    d["features"]["masks"] = None
+    return d
+
+
+def _run_overlapped(src, batches, ex, true_depth):
+    """Chunk loop with the host step off the critical path: the calling thread
+    runs each chunk's device pass (prep, model, clean, moments) and hands it
+    to a worker thread, which runs the sequential host step (angles / Kalman
+    tracking, in chunk order) and the small device tail (scalars, keypoint z,
+    crops) on its own stream while the next chunk's device pass runs."""
+    import queue
+    import threading
+
+    import torch
+    q: "queue.Queue" = queue.Queue(maxsize=2)
+    parts, err = [], []
+    dev = torch.cuda.current_device()
+
+    def worker():
+        try:
+            torch.cuda.set_device(dev)
+            ws = torch.cuda.Stream()
+            while True:
+                item = q.get()
+                if item is None:
+                    return
+                if err:
+                    continue
+                idx, st, host, ev = item
+                ws.wait_event(ev)
+                with torch.cuda.stream(ws):
+                    for t in (st["prepped"], st["d2"], st["cleaned"]):
+                        t.record_stream(ws)
+                    cen, kp, ang, fl = ex.host_angles(host)
+                    d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
+                parts.append(_lighten(d))
+        except BaseException as e:  # surfaced by the caller
+            err.append(e)
+
+    import sys
+    # the worker's host step is many short numpy calls: a short GIL switch
+    # interval keeps the launching thread from waiting out the default 5 ms
+    old_si = sys.getswitchinterval()
+    sys.setswitchinterval(1e-4)
+    t = threading.Thread(target=worker, daemon=True)
+    t.start()
+    try:
+        for idx, raw in src.iterate(device=True, batches=batches):
+            if err:
+                break
+            st, host = ex.features_pass(raw)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            q.put((np.asarray(idx), st, host, ev))
+    finally:
+        q.put(None)
+        t.join()
+        sys.setswitchinterval(old_si)
+    if err:
+        raise err[0]
+    return parts

@@ -183,6 +183,34 @@ def compute_keypoint_alignment_scores(keypoints: np.ndarray, expected_alignment:
 # ---------------------------------------------------------------------------
 # angle filtering
 # ---------------------------------------------------------------------------
+def _nan_median_small(v: np.ndarray, min_count: int) -> float:
+    v = v[~np.isnan(v)]
+    if len(v) < max(min_count, 1):
+        return np.nan
+    v = np.sort(v)
+    c = len(v)
+    return v[(c - 1) // 2] if c % 2 else (v[c // 2 - 1] + v[c // 2]) / 2
+
+
+def _move_median3(x: np.ndarray, min_count: int) -> np.ndarray:
+    """Window-3 moving median (the angle filter's case): median of three by
+    min/max for full windows (exact); the two leading partial windows and the
+    windows holding a NaN (min/max propagate it) are recomputed one by one."""
+    n = x.shape[0]
+    out = np.empty(n)
+    if n >= 3:
+        p, q, r = x[:-2], x[1:-1], x[2:]
+        out[2:] = np.maximum(np.minimum(p, q), np.minimum(np.maximum(p, q), r))
+        if min_count > 3:
+            out[2:] = np.nan
+    for i in range(min(n, 2)):
+        out[i] = _nan_median_small(x[:i + 1], min_count)
+    if n >= 3:
+        for i in (np.flatnonzero(np.isnan(out[2:])) + 2).tolist():
+            out[i] = _nan_median_small(x[i - 2:i + 1], min_count)
+    return out
+
+
 def move_median(a: np.ndarray, window: int, min_count: Optional[int] = None, axis: int = -1) -> np.ndarray:
     """bottleneck.move_median: median of the trailing `window` values (the
     first window-1 outputs use the values available), NaNs ignored, NaN where
@@ -196,16 +224,20 @@ def move_median(a: np.ndarray, window: int, min_count: Optional[int] = None, axi
     out_dtype = np.float32 if a.dtype == np.float32 else np.float64
     x = np.moveaxis(a.astype(np.float64), axis, -1)
     n = x.shape[-1]
+    if window == 3 and x.ndim == 1:
+        return _move_median3(x, min_count).astype(out_dtype)
     pad = np.full(x.shape[:-1] + (window - 1,), np.nan)
     xp = np.concatenate([pad, x], axis=-1)
     win = np.lib.stride_tricks.sliding_window_view(xp, window, axis=-1)[..., :n, :]
     cnt = np.sum(~np.isnan(win), axis=-1)
-    with np.errstate(all="ignore"):
-        import warnings
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore", RuntimeWarning)
-            med = np.nanmedian(win, axis=-1) if win.size else np.empty(win.shape[:-1])
-    med = np.where(cnt >= min_count, med, np.nan)
+    # exact median of the non-NaN values of each window: sort (NaNs go last)
+    # and pick the middle one, or the mean of the middle two for even counts
+    srt = np.sort(win, axis=-1)
+    c = np.maximum(cnt, 1)
+    lo = np.take_along_axis(srt, ((c - 1) // 2)[..., None], axis=-1)[..., 0]
+    hi = np.take_along_axis(srt, (c // 2)[..., None], axis=-1)[..., 0]
+    med = np.where(c % 2 == 1, lo, (lo + hi) / 2)
+    med = np.where((cnt >= min_count) & (cnt > 0), med, np.nan)
     return np.moveaxis(med, -1, axis).astype(out_dtype)
 
 
@@ -224,7 +256,23 @@ def filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60) ->
 
 def iterative_filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60,
                             max_iters: int = 1000) -> Tuple[np.ndarray, np.ndarray]:
-    """filter_angles until it stops changing (M/proc/proc.py:627-654)."""
+    """filter_angles until it stops changing (M/proc/proc.py:627-654).  Runs
+    in libmdx (mdx_iterative_filter_angles, host code, bit-identical to
+    iterative_filter_angles_numpy) without holding the GIL: the reference
+    loops up to 1000 times whenever an angle is NaN."""
+    a = np.ascontiguousarray(angles, dtype=np.float64)
+    if a.ndim != 1 or window > 8:
+        return iterative_filter_angles_numpy(angles, window, tolerance, max_iters)
+    out = np.empty_like(a)
+    flips = np.empty(a.shape, dtype=np.uint8)
+    call("mdx_iterative_filter_angles", a.ctypes.data_as(ctypes.c_void_p), a.shape[0], int(window), float(tolerance),
+         int(max_iters), out.ctypes.data_as(ctypes.c_void_p), flips.ctypes.data_as(ctypes.c_void_p))
+    return out, flips.astype(bool)
+
+
+def iterative_filter_angles_numpy(angles: np.ndarray, window: int = 3, tolerance: float = 60,
+                                  max_iters: int = 1000) -> Tuple[np.ndarray, np.ndarray]:
+    """The same loop in numpy (the reference's formulation)."""
     last = np.copy(angles)
     iterations = 0
     while True:

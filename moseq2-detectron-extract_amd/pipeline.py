@@ -54,6 +54,8 @@ class ExtractConfig:
     mask_iou_threshold: float = 0.5
     fix_invalid_pixels: bool = True
     use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
+    model_streams: int = 2           # forwards of consecutive batches in flight within a chunk
+    overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -88,18 +90,45 @@ class GPUExtractor:
         # ProcessFeaturesStep's Kalman trackers (process_features_step.py:40-51),
         # carried from chunk to chunk
         self.point_tracker, self.angle_tracker = TR.make_trackers() if config.use_tracking else (None, None)
+        self._streams = []
 
     def infer(self, prepped: torch.Tensor):
         """Model forward over a prepped chunk in batch_size slices
-        (InferenceStep.process); returns concatenated device outputs."""
+        (InferenceStep.process); returns concatenated device outputs.  The
+        slices alternate over `config.model_streams` HIP streams, so up to
+        that many forwards are in flight (their small late kernels fill each
+        other's gaps, as in OverlappedExtractor)."""
         outs = []
         n = prepped.shape[0]
         bs = min(self.cfg.batch_size, n)
-        for i in range(0, n, bs):
-            o = self.predictor.run(prepped[i:i + bs], self.lut)
-            sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
-            o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+        cur = torch.cuda.current_stream()
+        ns = max(1, int(self.cfg.model_streams))
+        if ns > 1 and n > bs:
+            if len(self._streams) < ns:
+                self._streams = [torch.cuda.Stream() for _ in range(ns)]
+            ready = torch.cuda.Event()
+            ready.record(cur)
+        for k, i in enumerate(range(0, n, bs)):
+            if ns > 1 and n > bs:
+                st = self._streams[k % ns]
+                st.wait_event(ready)
+                with torch.cuda.stream(st):
+                    prepped.record_stream(st)
+                    o = self.predictor.run(prepped[i:i + bs], self.lut)
+                    sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
+                    o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+                for v in o.values():
+                    for t in (v if isinstance(v, (list, tuple)) else (v,)):
+                        if torch.is_tensor(t):
+                            t.record_stream(cur)
+            else:
+                o = self.predictor.run(prepped[i:i + bs], self.lut)
+                sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
+                o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
             outs.append(o)
+        if ns > 1 and n > bs:
+            for st in self._streams[:ns]:
+                cur.wait_stream(st)
         keys = ("boxes", "scores", "classes", "ndet", "keypoints", "d2_mask", "sel_keypoints", "nkeep", "keep_idx")
         return {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
 

@@ -105,3 +105,25 @@ def test_keypoints_to_dict(gf, F):
 def test_attribute_tables(F):
     assert len(F.scalar_attributes()) == 17
     assert len(F.keypoint_attributes()) == 8 * 2 * 6
+
+
+def test_iterative_filter_angles_native_matches_numpy(F):
+    """libmdx's host loop (mdx_iterative_filter_angles) vs the numpy
+    formulation, bit for bit: NaN (1000-iteration runs), constant series,
+    max_iters cut-offs, windows 1..5, empty and 1-element series."""
+    rng = np.random.default_rng(4)
+    for trial in range(120):
+        n = int(rng.integers(0, 200))
+        a = rng.uniform(0, 360, n)
+        if n:
+            a[rng.random(n) < 0.3] += 180
+        if trial % 3 == 0 and n:
+            a[rng.integers(0, n)] = np.nan
+        if trial % 7 == 0 and n:
+            a[:] = a[0]
+        for w in (1, 2, 3, 5):
+            mi = int(rng.integers(0, 20)) if trial % 2 else 1000
+            o1, f1 = F.iterative_filter_angles(a, w, 60, mi)
+            o2, f2 = F.iterative_filter_angles_numpy(a, w, 60, mi)
+            np.testing.assert_array_equal(o1, o2)
+            np.testing.assert_array_equal(f1, f2)
