@@ -61,8 +61,8 @@ def parse():
 KERNEL_SYMBOLS = {  # MDX_CONV_KERNEL_* -> rocprofv3 symbol (fp16 in / fp16 out)
     0: "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE",
     1: "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE",
-    2: "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0EEEvNS_8ConvArgsE",
-    3: "_ZN3mdx7k_convgIDF16_Li4ELb1ELb0EEEvNS_8ConvArgsE",
+    2: "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
+    3: "_ZN3mdx7k_convgIDF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
     4: "k_conv1x1_stream<KC> (three instances by K)",
     5: "k_conv1x1_head<KC> (three instances by K)",
 }
