@@ -289,6 +289,16 @@ int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, const float 
                         const float *kpts, int B, int D, int K, int h, int w, float iou_thresh, int *keep_idx,
                         int *nkeep, uint8_t *sel_mask, double *sel_kpts, mdx_stream_t stream);
 
+/* Centres of the kept detections for the instance tracker
+ * (ProcessFeaturesStep.__instances_to_detections,
+ * M/pipeline/process_features_step.py:116-130): per frame b and kept slot
+ * s < nkeep[b], scipy center_of_mass (row, col) of mask plane keep_idx[b,s], or
+ * the box centre (x, y) when that mask is empty.  masks/plane_stride/keep_idx/
+ * nkeep as mdx_mask_nms_select, boxes float32 (B,D,4) XYXY -> centers float64
+ * (B,D,2), NaN for slots >= nkeep. */
+int mdx_mask_centers(const uint8_t *masks, int64_t plane_stride, const int *keep_idx, const int *nkeep,
+                     const float *boxes, int B, int D, int h, int w, double *centers, mdx_stream_t stream);
+
 /* heatmaps_to_keypoints: maps float32 (B*D, K, M, M) -> (B*D, K, 3) [x, y, score]. */
 int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
                               int K, int M, float *out, mdx_stream_t stream);

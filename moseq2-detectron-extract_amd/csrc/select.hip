@@ -146,6 +146,73 @@ __global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *
     for (long long p = p0 + threadIdx.x; p < hw; p += SEL_THREADS) o[p] = src ? src[p] : (uint8_t)0;
 }
 
+// Centres of the kept detections for the instance tracker
+// (ProcessFeaturesStep.__instances_to_detections, process_features_step.py:
+// 116-130): scipy.ndimage.center_of_mass of each kept mask = (sum rows / area,
+// sum cols / area) -- integer sums, so the fp64 quotients are exact -- and the
+// box centre (x, y) when the mask is empty (the reference's fallback, in its
+// (x, y) order).  One workgroup per (frame, kept slot).
+constexpr int CEN_THREADS = 256;
+
+__global__ __launch_bounds__(CEN_THREADS) void k_mask_centers(const uint8_t *__restrict__ masks, long long plane,
+                                                             const int *__restrict__ keep_idx,
+                                                             const int *__restrict__ nkeep,
+                                                             const float *__restrict__ boxes, int D, int h, int w,
+                                                             double *__restrict__ centers) {
+    __shared__ unsigned long long s_acc[3][CEN_THREADS / 64];
+    const int b = blockIdx.x / D, slot = blockIdx.x % D;
+    double *out = centers + ((long long)b * D + slot) * 2;
+    if (slot >= nkeep[b]) {
+        if (threadIdx.x == 0) out[0] = out[1] = __builtin_nan("");
+        return;
+    }
+    const int j = keep_idx[b * D + slot];
+    const uint8_t *m = masks + ((long long)b * D + j) * plane;
+    unsigned long long area = 0, sy = 0, sx = 0;
+    // one image row per wave iteration; mask bytes are 0/1
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int y = wave; y < h; y += CEN_THREADS / 64) {
+        const uint8_t *row = m + (long long)y * w;
+        unsigned ra = 0, rx = 0;
+        for (int x = lane; x < w; x += 64) {
+            const unsigned v = row[x] != 0;
+            ra += v;
+            rx += v * (unsigned)x;
+        }
+        area += ra;
+        sy += (unsigned long long)ra * (unsigned)y;
+        sx += rx;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        area += __shfl_xor(area, off);
+        sy += __shfl_xor(sy, off);
+        sx += __shfl_xor(sx, off);
+    }
+    if (lane == 0) {
+        s_acc[0][wave] = area;
+        s_acc[1][wave] = sy;
+        s_acc[2][wave] = sx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, ty = 0, tx = 0;
+        for (int q = 0; q < CEN_THREADS / 64; ++q) {
+            a += s_acc[0][q];
+            ty += s_acc[1][q];
+            tx += s_acc[2][q];
+        }
+        if (a > 0) {
+            out[0] = (double)ty / (double)a;
+            out[1] = (double)tx / (double)a;
+        } else {  // Boxes.get_centers(): float32 (x0 + x1) / 2, (y0 + y1) / 2
+            const float *bx = boxes + ((long long)b * D + j) * 4;
+            out[0] = (double)((bx[0] + bx[2]) * 0.5f);
+            out[1] = (double)((bx[1] + bx[3]) * 0.5f);
+        }
+    }
+}
+
 }  // namespace mdx
 
 using namespace mdx;
@@ -169,5 +236,18 @@ extern "C" int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, c
                            ndet, kpts, D, K, hw, (long long)plane_stride, iou_thresh, keep_idx, nkeep, sel_mask,
                            sel_kpts);
     MDX_CHECK_LAUNCH("mdx_mask_nms_select");
+    return MDX_OK;
+}
+
+extern "C" int mdx_mask_centers(const uint8_t *masks, int64_t plane_stride, const int *keep_idx, const int *nkeep,
+                                const float *boxes, int B, int D, int h, int w, double *centers,
+                                mdx_stream_t stream) {
+    MDX_REQUIRE(masks && keep_idx && nkeep && boxes && centers, "mdx_mask_centers: null pointer");
+    MDX_REQUIRE(D >= 1 && D <= SEL_MAXD && h > 0 && w > 0, "mdx_mask_centers: bad shape");
+    MDX_REQUIRE(plane_stride >= (int64_t)h * w, "mdx_mask_centers: plane_stride < h*w");
+    if (B == 0) return MDX_OK;
+    hipLaunchKernelGGL(k_mask_centers, dim3(B * D), dim3(CEN_THREADS), 0, as_stream(stream), masks,
+                       (long long)plane_stride, keep_idx, nkeep, boxes, D, h, w, centers);
+    MDX_CHECK_LAUNCH("mdx_mask_centers");
     return MDX_OK;
 }

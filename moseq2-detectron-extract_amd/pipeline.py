@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from . import features as F
+from . import instances as INS
 from . import proc
 from . import tracking as TR
 from ._lib import call
@@ -56,6 +57,8 @@ class ExtractConfig:
     use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
     model_streams: int = 2           # forwards of consecutive batches in flight within a chunk
     overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
+    select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
+    expected_instances: int = 1      # --expected-instances (M/cli.py:341)
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -78,6 +81,20 @@ def mask_nms_select(out: dict, iou_thresh: float = 0.5):
     return sel, kp, nkeep, keep_idx
 
 
+def mask_centers(out: dict, keep_idx: torch.Tensor, nkeep: torch.Tensor):
+    """Centres of the kept detections (center_of_mass of each kept mask, box
+    centre when empty) for the instance tracker: float64 (B,D,2)."""
+    masks = out["masks"]
+    B, D, h, w = masks.shape
+    mbuf, plane = out.get("mask_planes", (None, None))
+    if mbuf is None:
+        mbuf, plane = masks.contiguous(), h * w
+    cen = torch.empty((B, D, 2), dtype=torch.float64, device=masks.device)
+    call("mdx_mask_centers", _p(mbuf), int(plane), _p(keep_idx), _p(nkeep), _p(out["boxes"]), B, D, h, w, _p(cen),
+         _stream())
+    return cen
+
+
 class GPUExtractor:
     """Chunk processor of the hot path on the current GPU."""
 
@@ -90,6 +107,10 @@ class GPUExtractor:
         # ProcessFeaturesStep's Kalman trackers (process_features_step.py:40-51),
         # carried from chunk to chunk
         self.point_tracker, self.angle_tracker = TR.make_trackers() if config.use_tracking else (None, None)
+        # ProcessFeaturesStep's norfair instance tracker (process_features_step.py:35-38), per session
+        self.instance_tracker = INS.InstanceTracker(config.expected_instances)
+        self._frames_seen = 0
+        self._tail_dets = {}  # session frame -> (mask planes (D,h,w), keypoints (D,K,3), keep_idx row)
         self._streams = []
 
     def infer(self, prepped: torch.Tensor):
@@ -117,6 +138,8 @@ class GPUExtractor:
                     o = self.predictor.run(prepped[i:i + bs], self.lut)
                     sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
                     o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+                    if self.cfg.select_instances:
+                        o["centers"] = mask_centers(o, keep_idx, nkeep)
                 for v in o.values():
                     for t in (v if isinstance(v, (list, tuple)) else (v,)):
                         if torch.is_tensor(t):
@@ -125,12 +148,60 @@ class GPUExtractor:
                 o = self.predictor.run(prepped[i:i + bs], self.lut)
                 sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
                 o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+                if self.cfg.select_instances:
+                    o["centers"] = mask_centers(o, keep_idx, nkeep)
             outs.append(o)
         if ns > 1 and n > bs:
             for st in self._streams[:ns]:
                 cur.wait_stream(st)
         keys = ("boxes", "scores", "classes", "ndet", "keypoints", "d2_mask", "sel_keypoints", "nkeep", "keep_idx")
+        keys += ("centers",) if "centers" in outs[0] else ()
         return {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
+
+    def select_instances(self, inf: dict):
+        """ProcessFeaturesStep.__select_instances (process_features_step.py:
+        133-160) over a chunk, after the GPU mask NMS: the kept detections'
+        centres go through the session's norfair-semantics tracker on the host
+        (instances.InstanceTracker); frames whose picked instance differs from
+        the NMS result (more than one tracked object) get the picked
+        detection's mask plane and keypoints copied into d2_mask /
+        sel_keypoints on the device, and num_instances = the number picked.
+        Rewrites inf in place; returns the host nkeep (num_instances)."""
+        nkeep = inf["nkeep"].cpu().numpy().astype(np.int64)
+        cen = inf["centers"].cpu().numpy()
+        n = len(nkeep)
+        f0 = self._frames_seen
+        changes = INS.select_chunk(self.instance_tracker, nkeep, cen, f0)
+        masks = inf["masks"]
+        bs = masks[0].shape[0]
+        if changes:
+            keep = inf["keep_idx"].cpu().numpy()
+            d2, skp = inf["d2_mask"], inf["sel_keypoints"]
+            for f, sel in changes.items():
+                nkeep[f] = len(sel)
+                if not sel:
+                    d2[f].zero_()
+                    skp[f].fill_(float("nan"))
+                    continue
+                g, slot = sel[0]
+                if g >= f0:
+                    j = int(keep[g - f0, slot])
+                    plane = masks[(g - f0) // bs][(g - f0) % bs, j]
+                    kp = inf["keypoints"][g - f0, j]
+                else:  # a detection of the previous chunk's last frames
+                    planes, kps, krow = self._tail_dets[g]
+                    plane, kp = planes[int(krow[slot])], kps[int(krow[slot])]
+                d2[f].copy_(plane)
+                skp[f].copy_(kp)
+        # the tracker's live objects are at most pointwise_hit_counter_max
+        # frames old, so the last frames' detections are all a later chunk needs
+        tail = {}
+        keep_rows = inf["keep_idx"][max(0, n - INS.POINTWISE_HIT_COUNTER_MAX):].cpu().numpy()
+        for r, f in enumerate(range(max(0, n - INS.POINTWISE_HIT_COUNTER_MAX), n)):
+            tail[f0 + f] = (masks[f // bs][f % bs].clone(), inf["keypoints"][f].clone(), keep_rows[r])
+        self._tail_dets = tail
+        self._frames_seen = f0 + n
+        return nkeep
 
     def features(self, prepped: torch.Tensor, d2_mask: torch.Tensor):
         """clean_frames(iters_tail=3) + get_frame_features(mask=d2, thr=3)."""
@@ -170,11 +241,14 @@ class GPUExtractor:
         raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
         prepped = self.prep(raw)
         inf = self.infer(prepped)
+        # clean is independent of the selection: queued before the host step
+        cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
+        nkeep = self.select_instances(inf) if self.cfg.select_instances else inf["nkeep"].cpu().numpy()
         d2 = inf["d2_mask"]
-        cleaned, feats = self.features(prepped, d2)
+        feats = proc.frame_moments(cleaned, d2, float(self.cfg.frame_threshold))
         host = {"centroid": feats["centroid"].cpu().numpy(), "orientation": feats["orientation"].cpu().numpy(),
                 "axis_length": feats["axis_length"].cpu().numpy(), "keypoints": inf["sel_keypoints"].cpu().numpy()}
-        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": inf["nkeep"].cpu().numpy()}
+        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": nkeep}
         return state, host
 
     def finish_chunk(self, state: dict, centroid, keypoints, angles, flips, axis_length, frame_idxs=None,

@@ -590,10 +590,18 @@ def test_extract_session_from_dat(mdx, tmp_path):
     cfg = ExtractConfig(chunk_size=4, batch_size=4, use_tracking=False)
     out = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth)
     assert out["frames"].shape == (10, 80, 80) and list(out["frame_idxs"]) == list(range(10))
+    # the norfair instance tracker carries its state from chunk to chunk
     ex = GPUExtractor(s.bground_im, s.roi, pred, cfg)
+    ex.process_chunk(s.frames(0, 4), np.arange(0, 4), true_depth=s.true_depth)
     d = ex.process_chunk(s.frames(4, 8), np.arange(4, 8), true_depth=s.true_depth)
     np.testing.assert_array_equal(out["frames"][4:8], d["depth_frames"])
     np.testing.assert_array_equal(out["scalars/area_px"][4:8], d["scalars"]["area_px"])
+    # without the instance tracker (instance 0 after mask NMS) chunks are independent
+    cfg_n = ExtractConfig(chunk_size=4, batch_size=4, use_tracking=False, select_instances=False)
+    out_n = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_n, true_depth=s.true_depth)
+    d = GPUExtractor(s.bground_im, s.roi, pred, cfg_n).process_chunk(s.frames(4, 8), np.arange(4, 8),
+                                                                     true_depth=s.true_depth)
+    np.testing.assert_array_equal(out_n["frames"][4:8], d["depth_frames"])
     halves = [extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
                               world=2, rank=r) for r in (0, 1)]
     np.testing.assert_array_equal(np.concatenate([h["frame_idxs"] for h in halves]), np.arange(10))
