@@ -299,6 +299,15 @@ int mdx_mask_nms_select(const uint8_t *masks, int64_t plane_stride, const float 
 int mdx_mask_centers(const uint8_t *masks, int64_t plane_stride, const int *keep_idx, const int *nkeep,
                      const float *boxes, int B, int D, int h, int w, double *centers, mdx_stream_t stream);
 
+/* Instance-selection fix-up (ProcessFeaturesStep.__select_instances,
+ * M/pipeline/process_features_step.py:150-158, then instance 0 of
+ * mask_and_keypoints_from_model_output, M/proc/proc.py:680-684): for i < n,
+ * plane dst_idx[i] of dst (planes of plane_bytes) <- the plane_bytes at the
+ * device address src_ptrs[i] (0 = all-zero plane, the empty-instances case).
+ * src_ptrs / dst_idx are device arrays. */
+int mdx_gather_planes(const uint64_t *src_ptrs, const int *dst_idx, uint8_t *dst, int64_t plane_bytes, int n,
+                      mdx_stream_t stream);
+
 /* heatmaps_to_keypoints: maps float32 (B*D, K, M, M) -> (B*D, K, 3) [x, y, score]. */
 int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
                               int K, int M, float *out, mdx_stream_t stream);

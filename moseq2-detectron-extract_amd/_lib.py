@@ -71,6 +71,7 @@ SIGNATURES = {
     "mdx_heatmaps_to_keypoints": (I32, [P, P, P, I32, I32, I32, I32, P, P]),
     "mdx_mask_nms_select": (I32, [P, I64, P, P, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P]),
     "mdx_mask_centers": (I32, [P, I64, P, P, P, I32, I32, I32, I32, P, P]),
+    "mdx_gather_planes": (I32, [P, P, P, I64, I32, P]),
 }
 
 

@@ -213,6 +213,22 @@ __global__ __launch_bounds__(CEN_THREADS) void k_mask_centers(const uint8_t *__r
     }
 }
 
+// Plane gather for the instance-selection fix-up: dst plane dst_idx[i] <-
+// the hw bytes at src[i] (a device address; 0 = zero plane).  One launch for
+// every changed frame of a chunk instead of a copy per frame.
+constexpr int GATH_THREADS = 256;
+
+__global__ __launch_bounds__(GATH_THREADS) void k_gather_planes(const unsigned long long *__restrict__ src,
+                                                               const int *__restrict__ dst_idx,
+                                                               uint8_t *__restrict__ dst, long long hw) {
+    const int i = blockIdx.y;
+    const uint8_t *s = reinterpret_cast<const uint8_t *>(src[i]);
+    uint8_t *d = dst + (long long)dst_idx[i] * hw;
+    const long long step = (long long)gridDim.x * GATH_THREADS;
+    for (long long p = (long long)blockIdx.x * GATH_THREADS + threadIdx.x; p < hw; p += step)
+        d[p] = s ? s[p] : (uint8_t)0;
+}
+
 }  // namespace mdx
 
 using namespace mdx;
@@ -249,5 +265,18 @@ extern "C" int mdx_mask_centers(const uint8_t *masks, int64_t plane_stride, cons
     hipLaunchKernelGGL(k_mask_centers, dim3(B * D), dim3(CEN_THREADS), 0, as_stream(stream), masks,
                        (long long)plane_stride, keep_idx, nkeep, boxes, D, h, w, centers);
     MDX_CHECK_LAUNCH("mdx_mask_centers");
+    return MDX_OK;
+}
+
+extern "C" int mdx_gather_planes(const uint64_t *src_ptrs, const int *dst_idx, uint8_t *dst, int64_t plane_bytes,
+                                 int n, mdx_stream_t stream) {
+    MDX_REQUIRE(src_ptrs && dst_idx && dst, "mdx_gather_planes: null pointer");
+    MDX_REQUIRE(plane_bytes > 0 && n >= 0 && n <= 65535, "mdx_gather_planes: bad size");
+    if (n == 0) return MDX_OK;
+    const long long per = (plane_bytes + GATH_THREADS - 1) / GATH_THREADS;
+    const int bx = (int)(per < 64 ? per : 64);
+    hipLaunchKernelGGL(k_gather_planes, dim3(bx, n), dim3(GATH_THREADS), 0, as_stream(stream),
+                       reinterpret_cast<const unsigned long long *>(src_ptrs), dst_idx, dst, (long long)plane_bytes);
+    MDX_CHECK_LAUNCH("mdx_gather_planes");
     return MDX_OK;
 }

@@ -56,6 +56,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         states = []
         for idx, raw in src.iterate(device=True, batches=batches):
             st, host = ex.features_pass(raw)
+            ex.select_instances(st, host)
             states.append((np.asarray(idx), st, host))
         tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
         for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
@@ -147,6 +148,7 @@ def _run_overlapped(src, batches, ex, true_depth):
                 with torch.cuda.stream(ws):
                     for t in (st["prepped"], st["d2"], st["cleaned"]):
                         t.record_stream(ws)
+                    ex.select_instances(st, host)
                     cen, kp, ang, fl = ex.host_angles(host)
                     d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
                 parts.append(_lighten(d))

@@ -35,6 +35,7 @@ tests/test_instances.py.
 from __future__ import annotations
 
 import math
+import struct
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -43,6 +44,7 @@ DIST_THRESHOLD = 50.0
 HIT_COUNTER_MAX = 3
 POINTWISE_HIT_COUNTER_MAX = 4
 INITIALIZATION_DELAY = 0
+_F32 = struct.Struct("f")
 KF_R, KF_Q, KF_POS_VAR, KF_POS_VEL_COV, KF_VEL_VAR = 4.0, 0.1, 10.0, 0.0, 1.0
 
 
@@ -98,30 +100,31 @@ class InstanceTracker:
         for o in objs:
             o.step()
         nd, no = len(points), len(objs)
-        unmatched = list(range(nd))
+        unmatched = range(nd)
         if nd and no:
-            dm = np.empty((nd, no), dtype=np.float32)
+            # float32 distance matrix; greedy matching = repeated argmin with
+            # detection-major tie-breaking, i.e. ascending (distance, det, obj)
+            cand = []
             for i in range(nd):
                 py, px = float(points[i][0]), float(points[i][1])
                 for j, o in enumerate(objs):
                     dy, dx = py - o.pos[0], px - o.pos[1]
-                    dm[i, j] = math.sqrt(dy * dy + dx * dx)
-            if np.isnan(dm).any():
-                raise ValueError("Received nan values from distance function")
-            pairs = []
-            cur = dm.min()
-            while cur < DIST_THRESHOLD:
-                k = int(dm.argmin())
-                i, j = divmod(k, no)
-                pairs.append((i, j))
-                dm[i, :] = DIST_THRESHOLD + 1
-                dm[:, j] = DIST_THRESHOLD + 1
-                cur = dm.min()
-            if pairs:
-                taken = {i for i, _ in pairs}
-                unmatched = [i for i in range(nd) if i not in taken]
-                for i, j in pairs:
-                    objs[j].hit(points[i], det_ids[i])
+                    d = _F32.unpack(_F32.pack(math.sqrt(dy * dy + dx * dx)))[0]
+                    if d != d:
+                        raise ValueError("Received nan values from distance function")
+                    cand.append((d, i, j))
+            cand.sort()
+            used_i, used_j = set(), set()
+            for d, i, j in cand:
+                if d >= DIST_THRESHOLD:
+                    break
+                if i in used_i or j in used_j:
+                    continue
+                used_i.add(i)
+                used_j.add(j)
+                objs[j].hit(points[i], det_ids[i])
+            if used_i:
+                unmatched = [i for i in range(nd) if i not in used_i]
         for i in unmatched:
             self.objects.append(_Object(points[i], det_ids[i]))
         return [o for o in self.objects if o.hit_counter >= 0]
@@ -146,10 +149,12 @@ def select_chunk(tracker: InstanceTracker, nkeep: np.ndarray, centers: np.ndarra
     kept slot).  Returns {chunk frame: list of picked detection ids} for the
     frames whose instances change."""
     changes = {}
-    for f in range(len(nkeep)):
-        k = int(nkeep[f])
+    nk = np.asarray(nkeep).tolist()
+    cen = np.asarray(centers, dtype=np.float64).tolist()
+    for f in range(len(nk)):
+        k = nk[f]
         g = frame0 + f
-        sel = tracker.select([centers[f, s] for s in range(k)], [(g, s) for s in range(k)])
+        sel = tracker.select(cen[f][:k], [(g, s) for s in range(k)])
         if sel is not None:
             if len(sel) == k and all(d == (g, s) for s, d in enumerate(sel)):
                 continue  # same instances, same order

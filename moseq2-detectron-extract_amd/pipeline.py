@@ -158,50 +158,69 @@ class GPUExtractor:
         keys += ("centers",) if "centers" in outs[0] else ()
         return {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
 
-    def select_instances(self, inf: dict):
+    def select_instances(self, state: dict, host: dict):
         """ProcessFeaturesStep.__select_instances (process_features_step.py:
         133-160) over a chunk, after the GPU mask NMS: the kept detections'
         centres go through the session's norfair-semantics tracker on the host
-        (instances.InstanceTracker); frames whose picked instance differs from
-        the NMS result (more than one tracked object) get the picked
-        detection's mask plane and keypoints copied into d2_mask /
-        sel_keypoints on the device, and num_instances = the number picked.
-        Rewrites inf in place; returns the host nkeep (num_instances)."""
-        nkeep = inf["nkeep"].cpu().numpy().astype(np.int64)
-        cen = inf["centers"].cpu().numpy()
+        (instances.InstanceTracker).  Frames whose picked instance differs
+        from the NMS result (more than one tracked object) get the picked
+        detection's mask plane copied into the d2 masks on the device and its
+        keypoints, num_instances = the number picked, and the chunk's moments
+        are recomputed.  Part of the sequential host step (chunks in session
+        order); rewrites state / host in place."""
+        inf = state.pop("inf", None)
+        if inf is None:
+            return
+        nkeep = state["nkeep"].astype(np.int64)
         n = len(nkeep)
         f0 = self._frames_seen
-        changes = INS.select_chunk(self.instance_tracker, nkeep, cen, f0)
+        changes = INS.select_chunk(self.instance_tracker, nkeep, host["centers"], f0)
         masks = inf["masks"]
         bs = masks[0].shape[0]
+        keep = inf["keep_idx"].cpu().numpy()
         if changes:
-            keep = inf["keep_idx"].cpu().numpy()
-            d2, skp = inf["d2_mask"], inf["sel_keypoints"]
+            d2 = state["d2"]
+            kph = host["keypoints"]
+            det_kp = inf["keypoints"].cpu().numpy()
+            hw = d2.shape[1] * d2.shape[2]
+            src, dst = [], []
             for f, sel in changes.items():
                 nkeep[f] = len(sel)
+                dst.append(f)
                 if not sel:
-                    d2[f].zero_()
-                    skp[f].fill_(float("nan"))
+                    src.append(0)
+                    kph[f] = np.nan
                     continue
                 g, slot = sel[0]
                 if g >= f0:
                     j = int(keep[g - f0, slot])
-                    plane = masks[(g - f0) // bs][(g - f0) % bs, j]
-                    kp = inf["keypoints"][g - f0, j]
+                    src.append(masks[(g - f0) // bs][(g - f0) % bs, j].data_ptr())
+                    kph[f] = det_kp[g - f0, j]
                 else:  # a detection of the previous chunk's last frames
                     planes, kps, krow = self._tail_dets[g]
-                    plane, kp = planes[int(krow[slot])], kps[int(krow[slot])]
-                d2[f].copy_(plane)
-                skp[f].copy_(kp)
+                    src.append(planes[int(krow[slot])].data_ptr())
+                    kph[f] = kps[int(krow[slot])]
+            tab = torch.from_numpy(np.asarray(src, dtype=np.uint64).view(np.int64)).to(d2.device)
+            didx = torch.from_numpy(np.asarray(dst, dtype=np.int32)).to(d2.device)
+            for c in range(0, len(dst), 65535):
+                call("mdx_gather_planes", _p(tab[c:]), _p(didx[c:]), _p(d2), hw, min(65535, len(dst) - c), _stream())
+            feats = proc.frame_moments(state["cleaned"], d2, float(self.cfg.frame_threshold))
+            for k in ("centroid", "orientation", "axis_length"):
+                host[k] = feats[k].cpu().numpy()
+            state["nkeep"] = nkeep
         # the tracker's live objects are at most pointwise_hit_counter_max
         # frames old, so the last frames' detections are all a later chunk needs
         tail = {}
-        keep_rows = inf["keep_idx"][max(0, n - INS.POINTWISE_HIT_COUNTER_MAX):].cpu().numpy()
-        for r, f in enumerate(range(max(0, n - INS.POINTWISE_HIT_COUNTER_MAX), n)):
-            tail[f0 + f] = (masks[f // bs][f % bs].clone(), inf["keypoints"][f].clone(), keep_rows[r])
+        kp_tail = None
+        for f in range(max(0, n - INS.POINTWISE_HIT_COUNTER_MAX), n):
+            if kp_tail is None:
+                kp_tail = inf["keypoints"][f:].cpu().numpy()
+                t0 = f
+            tail[f0 + f] = (masks[f // bs][f % bs].clone(), kp_tail[f - t0], keep[f])
         self._tail_dets = tail
         self._frames_seen = f0 + n
-        return nkeep
+        # the copies / clones above read the chunk's mask planes, freed on return
+        torch.cuda.current_stream().synchronize()
 
     def features(self, prepped: torch.Tensor, d2_mask: torch.Tensor):
         """clean_frames(iters_tail=3) + get_frame_features(mask=d2, thr=3)."""
@@ -241,14 +260,14 @@ class GPUExtractor:
         raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
         prepped = self.prep(raw)
         inf = self.infer(prepped)
-        # clean is independent of the selection: queued before the host step
-        cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
-        nkeep = self.select_instances(inf) if self.cfg.select_instances else inf["nkeep"].cpu().numpy()
         d2 = inf["d2_mask"]
-        feats = proc.frame_moments(cleaned, d2, float(self.cfg.frame_threshold))
+        cleaned, feats = self.features(prepped, d2)
         host = {"centroid": feats["centroid"].cpu().numpy(), "orientation": feats["orientation"].cpu().numpy(),
                 "axis_length": feats["axis_length"].cpu().numpy(), "keypoints": inf["sel_keypoints"].cpu().numpy()}
-        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": nkeep}
+        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": inf["nkeep"].cpu().numpy()}
+        if self.cfg.select_instances:  # inputs of the host instance-selection step (select_instances)
+            state["inf"] = {k: inf[k] for k in ("masks", "keypoints", "keep_idx", "sel_keypoints")}
+            host["centers"] = inf["centers"].cpu().numpy()
         return state, host
 
     def finish_chunk(self, state: dict, centroid, keypoints, angles, flips, axis_length, frame_idxs=None,
@@ -301,6 +320,7 @@ class GPUExtractor:
         sequential over frames and chunks): the angle / tracking step
         (host_angles), scalar and keypoint tables."""
         state, host = self.features_pass(raw)
+        self.select_instances(state, host)
         cen, kp, angles, flips = self.host_angles(host)
         return self.finish_chunk(state, cen, kp, angles, flips, host["axis_length"], frame_idxs, offset, true_depth)
 

@@ -192,9 +192,14 @@ def test_extractor_select_instances_two_chunks():
         keep_h, nk_h, cen_h = inf["keep_idx"].cpu().numpy(), inf["nkeep"].cpu().numpy(), inf["centers"].cpu().numpy()
         for f in range(48):
             frames.append([((c0 + f, keep_h[f, s]), cen_h[f, s]) for s in range(nk_h[f])])
-        got_n.append(ex.select_instances(inf))
-        got_d2.append(inf["d2_mask"].cpu().numpy())
-        got_kp.append(inf["sel_keypoints"].cpu().numpy())
+        # what features_pass hands to the host step (moments of a blank frame)
+        state = {"d2": inf["d2_mask"], "cleaned": torch.zeros_like(inf["d2_mask"]), "nkeep": nk_h,
+                 "inf": {k: inf[k] for k in ("masks", "keypoints", "keep_idx", "sel_keypoints")}}
+        host = {"centers": cen_h, "keypoints": inf["sel_keypoints"].cpu().numpy()}
+        ex.select_instances(state, host)
+        got_n.append(state["nkeep"])
+        got_d2.append(state["d2"].cpu().numpy())
+        got_kp.append(host["keypoints"])
     got_d2, got_kp, got_n = np.concatenate(got_d2), np.concatenate(got_kp), np.concatenate(got_n)
     ref = R.select_instances(frames, 1)
     changed = 0
