@@ -24,7 +24,7 @@ import numpy as np
 from .pipeline import ExtractConfig, GPUExtractor
 from .results import KeypointsTSVWriter, create_extract_h5, open_results, write_extracted_chunk_to_h5
 from .session import RawDepthSource
-from .shard import tracking_exchange
+from .shard import instance_exchange, pass_tail_forward, tracking_exchange
 
 
 def shard_chunk_range(nchunks: int, world: int, rank: int):
@@ -51,14 +51,18 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         batches = batches[c0:c1]
     parts = []
     if exchange is None:  # two passes around the exchange step (needs torch.distributed initialised)
-        exchange = world > 1 and config.use_tracking
+        exchange = world > 1 and (config.use_tracking or config.select_instances)
     if exchange:
         states = []
         for idx, raw in src.iterate(device=True, batches=batches):
             st, host = ex.features_pass(raw)
-            ex.select_instances(st, host)
             states.append((np.asarray(idx), st, host))
-        tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
+        if config.select_instances:  # the instance tracker is sequential over the session too
+            _select_exchange(ex, states)
+        if config.use_tracking:
+            tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
+        else:  # per-chunk angle filtering: no sequential state across chunks
+            tracked = [ex.host_angles(h) for _, _, h in states]
         for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
             parts.append(_lighten(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)))
         states.clear()
@@ -108,6 +112,25 @@ def _write_outputs(output_dir, parts, src, bground_im, roi, true_depth, config, 
             tsv.write(d)
     finally:
         h5.close()
+
+
+def _select_exchange(ex, states):
+    """Instance selection of a sharded session: rank 0 runs the tracker over
+    every rank's frames in session order (shard.instance_exchange); each rank
+    gathers its picks, taking a pick at its shard's start from the preceding
+    rank's last frames (shard.pass_tail_forward)."""
+    import torch.distributed as dist
+    tracker = ex.instance_tracker if dist.get_rank() == 0 else None
+    off, changes = instance_exchange([h for _, _, h in states], [st["nkeep"] for _, st, _ in states], tracker)
+    f0s, f = [], off
+    for _, st, _ in states:
+        f0s.append(f)
+        f += len(st["nkeep"])
+    prev = pass_tail_forward(ex.chunk_tail(states[-1][1], f0s[-1]) if states else None)
+    for (_, st, host), ch, f0 in zip(states, changes, f0s):
+        tail = ex.chunk_tail(st, f0)
+        ex.apply_selection(st, host, ch, f0, prev)
+        prev = tail
 
 
 def _lighten(d: dict) -> dict:

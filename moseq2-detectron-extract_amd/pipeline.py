@@ -162,64 +162,77 @@ class GPUExtractor:
         """ProcessFeaturesStep.__select_instances (process_features_step.py:
         133-160) over a chunk, after the GPU mask NMS: the kept detections'
         centres go through the session's norfair-semantics tracker on the host
-        (instances.InstanceTracker).  Frames whose picked instance differs
-        from the NMS result (more than one tracked object) get the picked
-        detection's mask plane copied into the d2 masks on the device and its
-        keypoints, num_instances = the number picked, and the chunk's moments
-        are recomputed.  Part of the sequential host step (chunks in session
-        order); rewrites state / host in place."""
+        (instances.InstanceTracker), then apply_selection.  Part of the
+        sequential host step (chunks in session order); rewrites state / host
+        in place."""
+        if "inf" not in state:
+            return
+        f0 = self._frames_seen
+        changes = INS.select_chunk(self.instance_tracker, state["nkeep"], host["centers"], f0)
+        tail = self.chunk_tail(state, f0)
+        self.apply_selection(state, host, changes, f0, self._tail_dets)
+        self._tail_dets = tail
+        self._frames_seen = f0 + len(state["nkeep"])
+
+    def chunk_tail(self, state: dict, f0: int) -> dict:
+        """The chunk's last frames' kept detections {session frame: (mask
+        planes (D,h,w), keypoints (D,K,3), keep row (D,))}: the tracker's live
+        objects are at most pointwise_hit_counter_max frames old, so these are
+        all a later chunk's picks can refer to."""
+        inf = state["inf"]
+        masks = inf["masks"]
+        bs = masks[0].shape[0]
+        n = len(state["nkeep"])
+        a = max(0, n - INS.POINTWISE_HIT_COUNTER_MAX)
+        kp = inf["keypoints"][a:].cpu().numpy()
+        keep = inf["keep_idx"][a:].cpu().numpy()
+        return {f0 + f: (masks[f // bs][f % bs].clone(), kp[f - a], keep[f - a]) for f in range(a, n)}
+
+    def apply_selection(self, state: dict, host: dict, changes: dict, f0: int, prev_tail: dict):
+        """Frames whose picked instance differs from the NMS result get the
+        picked detection's mask plane gathered into the d2 masks on the
+        device (one mdx_gather_planes launch) and its keypoints;
+        num_instances = the number picked; the chunk's moments are then
+        recomputed.  `changes` = {chunk frame: [(session frame, kept slot)]},
+        `prev_tail` = chunk_tail of the preceding chunk (any rank)."""
         inf = state.pop("inf", None)
-        if inf is None:
+        if inf is None or not changes:
             return
         nkeep = state["nkeep"].astype(np.int64)
-        n = len(nkeep)
-        f0 = self._frames_seen
-        changes = INS.select_chunk(self.instance_tracker, nkeep, host["centers"], f0)
         masks = inf["masks"]
         bs = masks[0].shape[0]
         keep = inf["keep_idx"].cpu().numpy()
-        if changes:
-            d2 = state["d2"]
-            kph = host["keypoints"]
-            det_kp = inf["keypoints"].cpu().numpy()
-            hw = d2.shape[1] * d2.shape[2]
-            src, dst = [], []
-            for f, sel in changes.items():
-                nkeep[f] = len(sel)
-                dst.append(f)
-                if not sel:
-                    src.append(0)
-                    kph[f] = np.nan
-                    continue
-                g, slot = sel[0]
-                if g >= f0:
-                    j = int(keep[g - f0, slot])
-                    src.append(masks[(g - f0) // bs][(g - f0) % bs, j].data_ptr())
-                    kph[f] = det_kp[g - f0, j]
-                else:  # a detection of the previous chunk's last frames
-                    planes, kps, krow = self._tail_dets[g]
-                    src.append(planes[int(krow[slot])].data_ptr())
-                    kph[f] = kps[int(krow[slot])]
-            tab = torch.from_numpy(np.asarray(src, dtype=np.uint64).view(np.int64)).to(d2.device)
-            didx = torch.from_numpy(np.asarray(dst, dtype=np.int32)).to(d2.device)
-            for c in range(0, len(dst), 65535):
-                call("mdx_gather_planes", _p(tab[c:]), _p(didx[c:]), _p(d2), hw, min(65535, len(dst) - c), _stream())
-            feats = proc.frame_moments(state["cleaned"], d2, float(self.cfg.frame_threshold))
-            for k in ("centroid", "orientation", "axis_length"):
-                host[k] = feats[k].cpu().numpy()
-            state["nkeep"] = nkeep
-        # the tracker's live objects are at most pointwise_hit_counter_max
-        # frames old, so the last frames' detections are all a later chunk needs
-        tail = {}
-        kp_tail = None
-        for f in range(max(0, n - INS.POINTWISE_HIT_COUNTER_MAX), n):
-            if kp_tail is None:
-                kp_tail = inf["keypoints"][f:].cpu().numpy()
-                t0 = f
-            tail[f0 + f] = (masks[f // bs][f % bs].clone(), kp_tail[f - t0], keep[f])
-        self._tail_dets = tail
-        self._frames_seen = f0 + n
-        # the copies / clones above read the chunk's mask planes, freed on return
+        d2 = state["d2"]
+        kph = host["keypoints"]
+        det_kp = inf["keypoints"].cpu().numpy()
+        hw = d2.shape[1] * d2.shape[2]
+        src, dst = [], []
+        for f, sel in sorted(changes.items()):
+            nkeep[f] = len(sel)
+            dst.append(f)
+            if not sel:
+                src.append(0)
+                kph[f] = np.nan
+                continue
+            g, slot = sel[0]
+            if g >= f0:
+                j = int(keep[g - f0, slot])
+                src.append(masks[(g - f0) // bs][(g - f0) % bs, j].data_ptr())
+                kph[f] = det_kp[g - f0, j]
+            else:  # a detection of the preceding chunk's last frames
+                planes, kps, krow = prev_tail[g]
+                j = int(krow[slot])
+                src.append(planes[j].data_ptr())
+                kph[f] = kps[j]
+        tab = torch.from_numpy(np.asarray(src, dtype=np.uint64).view(np.int64)).to(d2.device)
+        didx = torch.from_numpy(np.asarray(dst, dtype=np.int32)).to(d2.device)
+        for c in range(0, len(dst), 65535):
+            call("mdx_gather_planes", _p(tab[c:]), _p(didx[c:]), _p(d2), hw, min(65535, len(dst) - c), _stream())
+        feats = proc.frame_moments(state["cleaned"], d2, float(self.cfg.frame_threshold))
+        for k in ("centroid", "orientation", "axis_length"):
+            host[k] = feats[k].cpu().numpy()
+        state["nkeep"] = nkeep
+        # the gathers read the chunk's mask planes, freed on return
         torch.cuda.current_stream().synchronize()
 
     def features(self, prepped: torch.Tensor, d2_mask: torch.Tensor):

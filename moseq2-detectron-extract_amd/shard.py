@@ -18,7 +18,7 @@ tensors (tests).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -162,3 +162,110 @@ def tracking_exchange(host_chunks: List[Dict[str, np.ndarray]], point_tracker=No
         o += ln
         res.append((x[:, 0:2].copy(), x[:, 4:].reshape(ln, K, 3).copy(), x[:, 2].copy(), x[:, 3] != 0))
     return res
+
+
+def instance_exchange(host_chunks: List[Dict[str, np.ndarray]], nkeeps: List[np.ndarray], tracker=None,
+                      group=None, device=None):
+    """§8(e) exchange step for the instance selection (A15): the norfair
+    tracker is sequential over the whole session, tracking on or off.  Every
+    rank sends its per-frame (nkeep, kept-detection centres) to rank 0, whose
+    tracker (instances.InstanceTracker) runs over every rank's chunks in
+    session order exactly as one process would; each rank gets back its
+    frames' picks.  Returns (this rank's session frame offset, per chunk
+    {chunk frame: [(session frame, kept slot), ...]} for the frames that
+    change) -- what GPUExtractor.apply_selection consumes."""
+    import torch
+    import torch.distributed as dist
+    from . import instances as INS
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    rank = dist.get_rank(group)
+    D = host_chunks[0]["centers"].shape[1] if host_chunks else 1
+    lens = np.array([len(k) for k in nkeeps], dtype=np.int64)
+    recs = (np.concatenate([np.concatenate([np.asarray(k, np.float64).reshape(-1, 1), h["centers"].reshape(len(k), 2 * D)],
+                                           axis=1) for k, h in zip(nkeeps, host_chunks)])
+            if host_chunks else np.zeros((0, 1 + 2 * D)))
+    sizes = _sizes(len(recs), device, group)
+    offset = int(sum(sizes[:rank]))
+    # per frame back: [npicked (-1 = unchanged), (session frame, slot) x expected]
+    E_ = tracker.expected_instances if tracker is not None else 1
+    E_t = torch.tensor([E_], dtype=torch.int64, device=device)
+    dist.broadcast(E_t, 0, group=group)
+    E_ = int(E_t.item())
+    wout = 1 + 2 * E_
+    all_rec = gather_ragged_to_rank0(torch.from_numpy(np.ascontiguousarray(recs)).to(device), group)
+    parts = None
+    if rank == 0:
+        if tracker is None:
+            raise ValueError("rank 0 needs the instance tracker")
+        parts, f0 = [], 0
+        for r_rec in all_rec:
+            x = r_rec.cpu().numpy()
+            n = len(x)
+            out = np.full((n, wout), -1.0)
+            ch = INS.select_chunk(tracker, x[:, 0].astype(np.int64), x[:, 1:].reshape(n, D, 2), f0)
+            for f, sel in ch.items():
+                out[f, 0] = len(sel)
+                for e, (g, s) in enumerate(sel[:E_]):
+                    out[f, 1 + 2 * e:3 + 2 * e] = (g, s)
+            f0 += n
+            parts.append(torch.from_numpy(out).to(device))
+    mine = scatter_ragged_from_rank0(parts, len(recs), sizes, wout, torch.float64, device, group).cpu().numpy()
+    res, o = [], 0
+    for ln in lens.tolist():
+        x = mine[o:o + ln]
+        o += ln
+        ch = {}
+        for f in np.nonzero(x[:, 0] >= 0)[0].tolist():
+            k = int(x[f, 0])
+            ch[f] = [(int(x[f, 1 + 2 * e]), int(x[f, 2 + 2 * e])) for e in range(k)]
+        res.append(ch)
+    return offset, res
+
+
+def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
+    """Chain rank r-1 -> rank r of the last frames' kept detections (mask
+    planes, keypoints, keep rows; instances.POINTWISE_HIT_COUNTER_MAX frames):
+    a pick at the start of rank r's shard can be a detection of the previous
+    shard's last frames.  `tail` is {session frame: (planes (D,h,w) uint8,
+    keypoints (D,K,3), keep row (D,))} or None for a rank without frames (it
+    forwards what it received).  Returns the previous shard's tail ({} on
+    rank 0)."""
+    import torch
+    import torch.distributed as dist
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    got: Dict = {}
+    if rank > 0:
+        hdr = torch.zeros(6, dtype=torch.int64, device=device)
+        dist.recv(hdr, rank - 1, group=group)
+        nf, D, h, w, K = (int(v) for v in hdr[:5].tolist())
+        if nf:
+            planes = torch.empty((nf, D, h, w), dtype=torch.uint8, device=device)
+            meta = torch.empty((nf, 1 + D + D * K * 3), dtype=torch.float64, device=device)
+            dist.recv(planes, rank - 1, group=group)
+            dist.recv(meta, rank - 1, group=group)
+            m = meta.cpu().numpy()
+            for i in range(nf):
+                got[int(m[i, 0])] = (planes[i], m[i, 1 + D:].reshape(D, K, 3).astype(np.float32),
+                                     m[i, 1:1 + D].astype(np.int64))
+    send = got if tail is None else tail
+    if rank < world - 1:
+        keys = sorted(send)
+        if keys:
+            p0, k0, _ = send[keys[0]]
+            D, h, w = (int(v) for v in p0.shape)
+            K = int(np.asarray(k0).shape[1])
+        else:
+            D = h = w = K = 0
+        hdr = torch.tensor([len(keys), D, h, w, K, 0], dtype=torch.int64, device=device)
+        dist.send(hdr, rank + 1, group=group)
+        if keys:
+            planes = torch.stack([send[g][0].to(device) for g in keys]).contiguous()
+            meta = np.concatenate([np.array([[g] for g in keys], np.float64),
+                                   np.stack([np.asarray(send[g][2], np.float64) for g in keys]),
+                                   np.stack([np.asarray(send[g][1], np.float64).reshape(-1) for g in keys])], axis=1)
+            dist.send(planes, rank + 1, group=group)
+            dist.send(torch.from_numpy(np.ascontiguousarray(meta)).to(device), rank + 1, group=group)
+    return got

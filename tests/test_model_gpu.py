@@ -603,7 +603,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
                                                                      true_depth=s.true_depth)
     np.testing.assert_array_equal(out_n["frames"][4:8], d["depth_frames"])
     halves = [extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
-                              world=2, rank=r) for r in (0, 1)]
+                              world=2, rank=r, exchange=False) for r in (0, 1)]
     np.testing.assert_array_equal(np.concatenate([h["frame_idxs"] for h in halves]), np.arange(10))
     # tracking on: the session equals process_chunk chunk after chunk on one
     # extractor (the trackers carry their state across chunks)
@@ -627,6 +627,9 @@ def test_extract_session_from_dat(mdx, tmp_path):
     try:
         out_x = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_t,
                                 true_depth=s.true_depth, exchange=True)
+        # tracking off: the exchange carries the instance selection only
+        out_xn = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg,
+                                 true_depth=s.true_depth, exchange=True)
     finally:
         dist.destroy_process_group()
     # writers: the h5 tree (npz without h5py) + keypoints TSV of the same run
@@ -639,3 +642,5 @@ def test_extract_session_from_dat(mdx, tmp_path):
     assert set(out_x) == set(out_t)
     for k in out_t:
         np.testing.assert_array_equal(out_x[k], out_t[k], err_msg=k)
+    for k in out:
+        np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)

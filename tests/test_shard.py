@@ -149,3 +149,85 @@ def test_tracking_exchange_equals_sequential(mdx, world, n_chunks):
     for g, w in zip(flat, want):
         for gx, wx in zip(g, w):
             np.testing.assert_array_equal(np.asarray(gx, dtype=np.asarray(wx).dtype), wx)
+
+
+def _sel_session(n_chunks, chunk, D=4, seed=4):
+    """Per-chunk (nkeep, centres (n,D,2)) of a multi-animal scenario."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_instances import _scenario
+    frames = _scenario(seed, n=n_chunks * chunk, max_det=D)
+    nk = np.array([len(d) for d in frames])
+    cen = np.full((len(frames), D, 2), np.nan)
+    for f, d in enumerate(frames):
+        for s, (_, c) in enumerate(d):
+            cen[f, s] = c
+    return [(nk[i:i + chunk], cen[i:i + chunk]) for i in range(0, len(frames), chunk)]
+
+
+def _select_worker(rank, world, port, q, n_chunks, chunk):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.extract import shard_chunk_range
+    from moseq2_detectron_extract_amd.instances import InstanceTracker
+    from moseq2_detectron_extract_amd.shard import instance_exchange, pass_tail_forward
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sess = _sel_session(n_chunks, chunk)
+    c0, c1 = shard_chunk_range(len(sess), world, rank)
+    mine = sess[c0:c1]
+    off, ch = instance_exchange([{"centers": c} for _, c in mine], [k for k, _ in mine],
+                                InstanceTracker(1) if rank == 0 else None)
+    # tail chain: a stand-in tail keyed by this shard's last session frame
+    tail = None
+    if mine:
+        last = off + sum(len(k) for k, _ in mine) - 1
+        tail = {last: (torch.full((2, 3, 5), rank, dtype=torch.uint8), np.full((2, 4, 3), float(last), np.float32),
+                       np.array([1, 0]))}
+    got = pass_tail_forward(tail)
+    got = {g: (int(p[0, 0, 0]), float(k[0, 0, 0]), list(r)) for g, (p, k, r) in got.items()}
+    q.put((rank, (off, c1 - c0, [{f: v for f, v in c.items()} for c in ch], got)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_chunks", [(2, 3), (3, 2)])
+def test_instance_exchange_equals_sequential(mdx, world, n_chunks):
+    """Rank 0 runs the instance tracker over every rank's frames in session
+    order: the scattered picks equal one process's select_chunk chunk by chunk
+    (incl. a rank without chunks), and each rank receives the preceding
+    shard's tail (forwarded through a rank without frames)."""
+    from moseq2_detectron_extract_amd.instances import InstanceTracker, select_chunk
+    chunk = 60
+    sess = _sel_session(n_chunks, chunk)
+    tr = InstanceTracker(1)
+    want, f0 = [], 0
+    for nk, cen in sess:
+        want.append(select_chunk(tr, nk, cen, f0))
+        f0 += len(nk)
+    assert sum(len(w) for w in want) > 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_select_worker, args=(r, world, port, q, n_chunks, chunk)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    flat = [c for r in sorted(got) for c in got[r][2]]
+    assert flat == want
+    last_tail = None
+    for r in sorted(got):
+        off, nch, _, tail = got[r]
+        if r == 0:
+            assert tail == {}
+        else:
+            assert tail == (last_tail or {})
+        if nch:
+            g = off + nch * chunk - 1
+            last_tail = {g: (r, float(g), [1, 0])}
