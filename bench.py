@@ -296,7 +296,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "extracted frames/sec, 512x424 depth video batch=32",
+            "metric": f"extracted frames/sec, 512x424 depth video batch={B}",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
