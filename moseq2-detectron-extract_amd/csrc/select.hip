@@ -151,8 +151,18 @@ __global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *
 // 116-130): scipy.ndimage.center_of_mass of each kept mask = (sum rows / area,
 // sum cols / area) -- integer sums, so the fp64 quotients are exact -- and the
 // box centre (x, y) when the mask is empty (the reference's fallback, in its
-// (x, y) order).  One workgroup per (frame, kept slot).
-constexpr int CEN_THREADS = 256;
+// (x, y) order).  One workgroup per (frame, kept slot).  Mask bytes are 0/1:
+// a 16-B word at plane offset p holds pixels p..p+15, i.e. row p / w from
+// column p % w, wrapping onto the next row at most once when w >= 16, so its
+// three sums come from per-dword popcounts and byte-index sums, without a
+// per-pixel division.
+constexpr int CEN_THREADS = 512, CEN_UNROLL = 4;
+
+__device__ __forceinline__ unsigned byte_index_sum(unsigned d, unsigned base) {
+    // sum over the 0/1 bytes of d of (base + byte index)
+    const unsigned b0 = d & 1u, b1 = (d >> 8) & 1u, b2 = (d >> 16) & 1u, b3 = d >> 24;
+    return base * (b0 + b1 + b2 + b3) + b1 + 2u * b2 + 3u * b3;
+}
 
 __global__ __launch_bounds__(CEN_THREADS) void k_mask_centers(const uint8_t *__restrict__ masks, long long plane,
                                                              const int *__restrict__ keep_idx,
@@ -168,21 +178,56 @@ __global__ __launch_bounds__(CEN_THREADS) void k_mask_centers(const uint8_t *__r
     }
     const int j = keep_idx[b * D + slot];
     const uint8_t *m = masks + ((long long)b * D + j) * plane;
+    const long long hw = (long long)h * w;
     unsigned long long area = 0, sy = 0, sx = 0;
-    // one image row per wave iteration; mask bytes are 0/1
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int y = wave; y < h; y += CEN_THREADS / 64) {
-        const uint8_t *row = m + (long long)y * w;
-        unsigned ra = 0, rx = 0;
-        for (int x = lane; x < w; x += 64) {
-            const unsigned v = row[x] != 0;
-            ra += v;
-            rx += v * (unsigned)x;
+    long long p0 = 0;
+    if (w >= 16 && (reinterpret_cast<uintptr_t>(m) & 15) == 0) {
+        const int nv = (int)(hw / 16);
+        const uint4 *mv = reinterpret_cast<const uint4 *>(m);
+        for (int v0 = threadIdx.x; v0 < nv; v0 += CEN_THREADS * CEN_UNROLL) {
+            uint4 q[CEN_UNROLL];
+#pragma unroll
+            for (int u = 0; u < CEN_UNROLL; ++u) {
+                const int v = v0 + u * CEN_THREADS;
+                q[u] = v < nv ? mv[v] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < CEN_UNROLL; ++u) {
+                const int v = v0 + u * CEN_THREADS;
+                const unsigned d[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+                unsigned cnt = 0, ks = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    cnt += __popc(d[t]);
+                    ks += byte_index_sum(d[t], 4u * t);
+                }
+                const long long pp = 16LL * v;
+                const unsigned y0 = (unsigned)(pp / w), x0 = (unsigned)(pp - (long long)y0 * w);
+                unsigned hi = 0;  // pixels of the word that wrapped onto row y0 + 1
+                if (x0 + 15u >= (unsigned)w) {
+                    const unsigned kk = (unsigned)w - x0;  // first wrapped byte, 1..15
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int sh = (int)kk - 4 * t;
+                        const unsigned msk = sh <= 0 ? 0xffffffffu : (sh >= 4 ? 0u : (0xffffffffu << (8 * sh)));
+                        hi += __popc(d[t] & msk);
+                    }
+                }
+                area += cnt;
+                sx += (unsigned long long)x0 * cnt + ks - (unsigned long long)w * hi;
+                sy += (unsigned long long)y0 * cnt + hi;
+            }
         }
-        area += ra;
-        sy += (unsigned long long)ra * (unsigned)y;
-        sx += rx;
+        p0 = (long long)nv * 16;
     }
+    for (long long p = p0 + threadIdx.x; p < hw; p += CEN_THREADS) {  // tail / unaligned
+        const unsigned v = m[p] != 0;
+        const long long y = p / w;
+        area += v;
+        sy += v * (unsigned long long)y;
+        sx += v * (unsigned long long)(p - y * w);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         area += __shfl_xor(area, off);
