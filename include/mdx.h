@@ -131,6 +131,20 @@ int mdx_bground_median(const int16_t *frames, int64_t n, int H, int W, int med_s
 int mdx_iterative_filter_angles(const double *angles, int64_t n, int window, double tolerance, int max_iters,
                                 double *out, uint8_t *flips);
 
+/* Host (CPU) functions: the instance tracker of
+ * ProcessFeaturesStep.__select_instances (M/pipeline/process_features_step.py:
+ * 35-38, 133-160; norfair 2.x Tracker semantics, see instances.py).  The
+ * tracker state carries from call to call (chunks in session order).
+ * select: per frame f < n, nkeep[f] kept detections with centres
+ * centers[f][0..nkeep[f])[2] (row, col; rows of D) -> out_n[f] = -1 when the
+ * frame's instances stay as they are, else the number picked (<=
+ * expected_instances) with out_ids[f][m] = (session frame, kept slot) of
+ * each pick, oldest object first.  frame0 = the session index of frame 0. */
+void *mdx_instance_tracker_create(int expected_instances);
+int mdx_instance_tracker_destroy(void *handle);
+int mdx_instance_tracker_select(void *handle, const int *nkeep, const double *centers, int64_t n, int D,
+                                int64_t frame0, int *out_n, int64_t *out_ids);
+
 /* ---------------------------------------------------------------------
  * Mask/Keypoint R-CNN forward (Predictor.__call__, M/model/predict.py:53-102,
  * Detectron2 GeneralizedRCNN built by M/model/config.py:21-94).  Tensors are

@@ -72,6 +72,9 @@ SIGNATURES = {
     "mdx_mask_nms_select": (I32, [P, I64, P, P, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P]),
     "mdx_mask_centers": (I32, [P, I64, P, P, P, I32, I32, I32, I32, P, P]),
     "mdx_gather_planes": (I32, [P, P, P, I64, I32, P]),
+    "mdx_instance_tracker_create": (P, [I32]),
+    "mdx_instance_tracker_destroy": (I32, [P]),
+    "mdx_instance_tracker_select": (I32, [P, P, P, I64, I32, I64, P, P]),
 }
 
 

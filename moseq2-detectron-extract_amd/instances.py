@@ -24,6 +24,11 @@ norfair >= 2.0, so this restates the published 2.x algorithm:
   coordinates of a 1-point detection share the same covariance, so it is kept
   as three scalars.
 
+`InstanceTracker` is the product: the native host tracker in libmdx
+(csrc/host_instances.hip, one call per chunk, no GIL).  `InstanceTrackerPy`
+below states the same algorithm frame by frame in Python (the two are
+checked against each other and against oracle/norfair_ref.py).
+
 `select` then does what __select_instances does with the tracked objects: if
 more than one is active, keep those with a live point, sort by age (stable)
 and take up to `expected_instances` from the oldest end, each object's LAST
@@ -86,9 +91,9 @@ class _Object:
         self.vv += KF_Q - (v_over * v_over) * added
 
 
-class InstanceTracker:
+class InstanceTrackerPy:
     """norfair Tracker as configured by ProcessFeaturesStep (one per session;
-    state carried from chunk to chunk)."""
+    state carried from chunk to chunk), frame by frame in Python."""
 
     def __init__(self, expected_instances: int = 1):
         self.expected_instances = int(expected_instances)
@@ -143,20 +148,59 @@ class InstanceTracker:
         return out
 
 
-def select_chunk(tracker: InstanceTracker, nkeep: np.ndarray, centers: np.ndarray, frame0: int):
+    def select_chunk(self, nkeep: np.ndarray, centers: np.ndarray, frame0: int):
+        """See select_chunk."""
+        changes = {}
+        nk = np.asarray(nkeep).tolist()
+        cen = np.asarray(centers, dtype=np.float64).tolist()
+        for f in range(len(nk)):
+            k = nk[f]
+            g = frame0 + f
+            sel = self.select(cen[f][:k], [(g, s) for s in range(k)])
+            if sel is not None:
+                if len(sel) == k and all(d == (g, s) for s, d in enumerate(sel)):
+                    continue  # same instances, same order
+                changes[f] = sel
+        return changes
+
+
+class InstanceTracker:
+    """The session's instance tracker: the native host implementation
+    (mdx_instance_tracker_*), state held behind a handle."""
+
+    def __init__(self, expected_instances: int = 1):
+        from ._lib import MdxError, lib
+        self.expected_instances = int(expected_instances)
+        self._lib = lib()
+        self._h = self._lib.mdx_instance_tracker_create(self.expected_instances)
+        if not self._h:
+            raise MdxError("mdx_instance_tracker_create failed (expected_instances >= 1)")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.mdx_instance_tracker_destroy(h)
+
+    def select_chunk(self, nkeep: np.ndarray, centers: np.ndarray, frame0: int):
+        """See select_chunk."""
+        import ctypes
+        from ._lib import call
+        nk = np.ascontiguousarray(nkeep, dtype=np.int32)
+        n = len(nk)
+        cen = np.ascontiguousarray(centers, dtype=np.float64)
+        D = cen.shape[1] if n else 1
+        out_n = np.empty(n, np.int32)
+        ids = np.empty((n, self.expected_instances, 2), np.int64)
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        call("mdx_instance_tracker_select", ctypes.c_void_p(self._h), vp(nk), vp(cen), n, D, int(frame0), vp(out_n),
+             vp(ids))
+        return {f: [(int(ids[f, m, 0]), int(ids[f, m, 1])) for m in range(out_n[f])]
+                for f in np.nonzero(out_n >= 0)[0].tolist()}
+
+
+def select_chunk(tracker, nkeep: np.ndarray, centers: np.ndarray, frame0: int):
     """Run the tracker over a chunk's frames.  nkeep (n,), centers (n,D,2)
     float64 (kept detections in pick order).  A detection id is (session frame,
     kept slot).  Returns {chunk frame: list of picked detection ids} for the
     frames whose instances change."""
-    changes = {}
-    nk = np.asarray(nkeep).tolist()
-    cen = np.asarray(centers, dtype=np.float64).tolist()
-    for f in range(len(nk)):
-        k = nk[f]
-        g = frame0 + f
-        sel = tracker.select(cen[f][:k], [(g, s) for s in range(k)])
-        if sel is not None:
-            if len(sel) == k and all(d == (g, s) for s, d in enumerate(sel)):
-                continue  # same instances, same order
-            changes[f] = sel
-    return changes
+    return tracker.select_chunk(nkeep, centers, frame0)

@@ -39,8 +39,9 @@ def _scenario(seed, n=400, max_det=4):
     return frames
 
 
-def _product(frames, expected=1, chunk=None):
-    tr = I.InstanceTracker(expected)
+def _product(frames, expected=1):
+    """The per-frame Python statement."""
+    tr = I.InstanceTrackerPy(expected)
     out = []
     for dets in frames:
         sel = tr.select([c for _, c in dets], [i for i, _ in dets])
@@ -48,11 +49,29 @@ def _product(frames, expected=1, chunk=None):
     return out
 
 
+def _native(frames, expected=1, chunk=97, D=4):
+    """The native tracker, chunk by chunk (state carried)."""
+    tr = I.InstanceTracker(expected)
+    out = []
+    for c0 in range(0, len(frames), chunk):
+        fr = frames[c0:c0 + chunk]
+        nk = np.array([len(d) for d in fr])
+        cen = np.full((len(fr), D, 2), np.nan)
+        for f, d in enumerate(fr):
+            for s, (_, c) in enumerate(d):
+                cen[f, s] = c
+        ch = I.select_chunk(tr, nk, cen, c0)
+        out.extend(ch.get(f, [(c0 + f, s) for s in range(nk[f])]) for f in range(len(fr)))
+    return out
+
+
 @pytest.mark.parametrize("seed", range(12))
 @pytest.mark.parametrize("expected", [1, 2])
 def test_tracker_matches_restatement(seed, expected):
     frames = _scenario(seed)
-    assert _product(frames, expected) == R.select_instances(frames, expected)
+    ref = R.select_instances(frames, expected)
+    assert _product(frames, expected) == ref
+    assert _native(frames, expected) == ref
 
 
 def test_selection_changes_something():
@@ -88,7 +107,7 @@ def test_select_chunk_carries_state():
     for f, d in enumerate(frames):
         for s, (_, c) in enumerate(d):
             cen[f, s] = c
-    tr = I.InstanceTracker(1)
+    tr = I.InstanceTrackerPy(1)
     ch = I.select_chunk(tr, nkeep[:150], cen[:150], 0)
     ch.update({f + 150: v for f, v in I.select_chunk(tr, nkeep[150:], cen[150:], 150).items()})
     ref = R.select_instances(frames, 1)
