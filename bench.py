@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--stream1x1", type=int, default=None, help="conv knob (mdx_conv_set_stream1x1)")
     ap.add_argument("--stream-min-m", type=int, default=65536, help="conv knob (mdx_conv_set_stream1x1 min_m)")
     ap.add_argument("--dma-after", type=int, default=None, help="conv knob (mdx_conv_set_dma_after)")
+    ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -215,6 +216,9 @@ def main():
     if args.dma_after is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_dma_after", args.dma_after)
+    if args.roi_mode is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_roi_align_set_mode", args.roi_mode)
     if args.prio256 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_mfma_prio256", args.prio256)

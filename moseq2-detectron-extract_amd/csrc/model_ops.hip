@@ -1077,9 +1077,16 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
 // path are what bound this kernel.  Rounding differs from the per-sample sum
 // (fp32, ~1 ulp); bins needing more than ROI_RMAX rows or columns (fixed
 // sampling ratios) take the per-sample path.
-constexpr int ROI_RMAX = 8, ROI_PMAX = 16;
+//
+// ROWS (mode 5): the same sum as sum_c B[c] (sum_r A[r] F[r][c]): per bin row,
+// the row-weighted values R[x] of every column x of the ROI's span are formed
+// once in LDS (fp32) and shared by all P bins of that row, so a row of bins
+// costs nr * (span) 16-B taps instead of P * nr * (nc)
+// ((7 gw + 1) vs 7 (gw + 1) columns; rounding again ~1 ulp).  Spans wider
+// than ROI_SPAN_FLOATS / C columns take the mode-4 loop.
+constexpr int ROI_RMAX = 8, ROI_PMAX = 16, ROI_SPAN_FLOATS = 8192;
 
-template <typename T>
+template <typename T, bool ROWS = false>
 __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float *__restrict__ rois,
                                                        const int *__restrict__ counts, T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;
@@ -1181,6 +1188,75 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
             st16(o + (long long)t * V, acc);
         }
         return;
+    }
+    if constexpr (ROWS) {
+        __shared__ int s_span[2];
+        __shared__ __attribute__((aligned(16))) float sR[ROI_SPAN_FLOATS];
+        if (threadIdx.x == 0) {
+            int lo = 1 << 30, hi = 0;
+            for (int pw = 0; pw < P; ++pw)
+                if (s_nc[pw] > 0) {
+                    lo = s_c0[pw] < lo ? s_c0[pw] : lo;
+                    hi = s_c0[pw] + s_nc[pw] > hi ? s_c0[pw] + s_nc[pw] : hi;
+                }
+            if (lo > hi) lo = hi = 0;
+            s_span[0] = lo;
+            s_span[1] = hi - lo;
+        }
+        __syncthreads();
+        const int cx0 = s_span[0], span = s_span[1];
+        if (span * C <= ROI_SPAN_FLOATS) {
+            const int n1 = span * G, n2 = P * G;
+            for (int ph = 0; ph < P; ++ph) {
+                const int nr = s_nr[ph];
+                const T *rowp = f + ((long long)s_r0[ph] * g.W + cx0) * C;
+                for (int it = threadIdx.x; it < n1; it += 256) {
+                    const int x = it / G, cg = it - x * G;
+                    const T *src = rowp + (long long)x * C + cg * V;
+                    float acc[V];
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+                    for (int j = 0; j < nr; j += 2) {
+                        const bool two = j + 1 < nr;
+                        float v0[V], v1[V];
+                        ld16(src + (long long)j * g.W * C, v0);
+                        ld16(src + (long long)(two ? j + 1 : j) * g.W * C, v1);
+                        const float a0 = s_A[ph][j], a1 = two ? s_A[ph][j + 1] : 0.f;
+#pragma unroll
+                        for (int i = 0; i < V; ++i) acc[i] += a0 * v0[i] + a1 * v1[i];
+                    }
+                    float *d = sR + x * C + cg * V;
+#pragma unroll
+                    for (int i = 0; i < V; i += 4)
+                        *reinterpret_cast<float4 *>(d + i) = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
+                }
+                __syncthreads();
+                for (int it = threadIdx.x; it < n2; it += 256) {
+                    const int pw = it / G, cg = it - pw * G;
+                    const int nc = s_nc[pw];
+                    const float *srow = sR + (s_c0[pw] - cx0) * C + cg * V;
+                    float acc[V];
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+                    for (int k = 0; k < nc; ++k) {
+                        const float bk = s_B[pw][k];
+#pragma unroll
+                        for (int i = 0; i < V; i += 4) {
+                            const float4 r4 = *reinterpret_cast<const float4 *>(srow + k * C + i);
+                            acc[i] += bk * r4.x;
+                            acc[i + 1] += bk * r4.y;
+                            acc[i + 2] += bk * r4.z;
+                            acc[i + 3] += bk * r4.w;
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+                    st16(o + ((long long)(ph * P + pw) * G + cg) * V, acc);
+                }
+                __syncthreads();
+            }
+            return;
+        }
     }
     for (int t = threadIdx.x; t < nitems; t += 256) {
         const int bin = t / G, cg = t - bin * G;
@@ -1692,7 +1768,14 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     }
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
-    if (g_roi_mode == 4 && P <= ROI_PMAX) {
+    if (g_roi_mode == 5 && P <= ROI_PMAX) {
+        if (dtype == 1)
+            hipLaunchKernelGGL((k_roi_align_sep<_Float16, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
+                               counts, (_Float16 *)out);
+        else
+            hipLaunchKernelGGL((k_roi_align_sep<float, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
+                               counts, (float *)out);
+    } else if (g_roi_mode == 4 && P <= ROI_PMAX) {
         if (dtype == 1)
             hipLaunchKernelGGL(k_roi_align_sep<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
                                (_Float16 *)out);

@@ -263,7 +263,7 @@ def test_rpn_proposals_from_identical_heads(mdx):
         torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True)])
 def test_roi_align_matches_oracle(mdx, rt, C, half, mode):
     import ctypes

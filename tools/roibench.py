@@ -46,7 +46,7 @@ def main():
     from moseq2_detectron_extract_amd._lib import call
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     outs = {}
-    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4"), (4, "separable")):
+    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4"), (4, "separable"), (5, "separable, row-shared")):
         old = call("mdx_roi_align_set_mode", mode)
         for _ in range(2):
             out = orig(feats, props, pcount, R, P, *a, **k)
