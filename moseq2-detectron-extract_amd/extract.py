@@ -22,7 +22,8 @@ from typing import Dict, Optional
 import numpy as np
 
 from .pipeline import ExtractConfig, GPUExtractor
-from .results import KeypointsTSVWriter, create_extract_h5, open_results, write_extracted_chunk_to_h5
+from .results import (KeypointsTSVWriter, check_completion_status, create_extract_h5, open_results, status_filename,
+                      write_extracted_chunk_to_h5, write_status)
 from .session import RawDepthSource
 from .shard import instance_exchange, pass_tail_forward, tracking_exchange
 
@@ -38,11 +39,23 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
                     config: ExtractConfig = ExtractConfig(), true_depth: float = 673.1,
                     frame_trim=(0, 0), world: int = 1, rank: int = 0, out_npz: Optional[str] = None,
                     exchange: Optional[bool] = None, output_dir: Optional[str] = None,
-                    first_frame: Optional[np.ndarray] = None, status: Optional[dict] = None) -> Dict:
+                    first_frame: Optional[np.ndarray] = None, status: Optional[dict] = None,
+                    skip_completed: bool = True) -> Dict:
     """Extract every chunk of the session (or of this rank's shard).  Returns
     {'frames': uint8 (n,80,80), 'frames_mask': uint8 (n,80,80),
     'scalars/<name>': (n,), 'keypoints/<name>': (n,), 'flips': bool (n,),
     'frame_idxs': (n,)} in frame order."""
+    status_path = None
+    if output_dir:  # status file first, as M/extract.py:47-62 (skip a completed session)
+        out_dir = output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}")
+        os.makedirs(out_dir, exist_ok=True)
+        status_path = status_filename(out_dir)
+        if skip_completed and check_completion_status(status_path):
+            return {}
+        status = status or {"complete": False, "skip": False, "uuid": str(uuid.uuid4()),
+                            "metadata": _load_metadata(path), "parameters": dict(vars(config))}
+        status["complete"] = False
+        write_status(status_path, status)
     src = RawDepthSource(path, frame_trim=frame_trim)
     ex = GPUExtractor(bground_im, roi, predictor, config)
     batches = src.batches(config.chunk_size, config.chunk_overlap)
@@ -76,6 +89,8 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     if output_dir:
         _write_outputs(output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}"), parts, src, bground_im,
                        roi, true_depth, config, first_frame, status)
+        status["complete"] = True  # M/extract.py:129-131
+        write_status(status_path, status)
     if not parts:
         return out
     out["frame_idxs"] = np.concatenate([p["frame_idxs"] for p in parts])
@@ -89,6 +104,16 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     if out_npz:
         np.savez_compressed(out_npz, **out)
     return out
+
+
+def _load_metadata(path: str) -> dict:
+    """Session metadata.json next to the depth file (Session.load_metadata)."""
+    import json
+    f = os.path.join(os.path.dirname(os.path.abspath(path)), "metadata.json")
+    if os.path.exists(f):
+        with open(f, "r", encoding="utf-8") as fh:
+            return json.load(fh)
+    return {}
 
 
 def _write_outputs(output_dir, parts, src, bground_im, roi, true_depth, config, first_frame, status):

@@ -213,3 +213,37 @@ class KeypointsTSVWriter:
         df = pd.DataFrame(cols)
         df.to_csv(self.path, sep="\t", index=False, mode="w" if self._header else "a", header=self._header)
         self._header = False
+
+
+def _plain(v):
+    """YAML-safe plain value (tuples -> lists, numpy scalars/arrays -> Python)."""
+    if isinstance(v, dict):
+        return {str(k): _plain(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def status_filename(output_dir: str, bg_roi_index: int = 0) -> str:
+    """results_XX.yaml next to the results (M/extract.py:48)."""
+    return os.path.join(output_dir, f"results_{bg_roi_index:02d}.yaml")
+
+
+def write_status(path: str, status: dict) -> None:
+    """write_yaml (M/io/util.py:99-109): safe YAML, block style."""
+    import yaml
+    with open(path, "w", encoding="utf-8") as fh:
+        yaml.safe_dump(_plain(status), fh, default_flow_style=False)
+
+
+def check_completion_status(path: str) -> bool:
+    """M/proc/util.py:63-77: True when the status file says complete."""
+    if os.path.exists(path):
+        import yaml
+        with open(path, "r", encoding="utf-8") as fh:
+            return bool(yaml.safe_load(fh)["complete"])
+    return False

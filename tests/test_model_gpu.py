@@ -639,6 +639,11 @@ def test_extract_session_from_dat(mdx, tmp_path):
     np.testing.assert_array_equal(res["frames"], out_t["frames"])
     np.testing.assert_array_equal(res["scalars/angle"], out_t["scalars/angle"].astype(np.float32))
     assert (tmp_path / "out" / "keypoints_00.tsv").read_text().count("\n") == 11
+    # status file: complete after the run, and a completed session is skipped (M/extract.py:47-51)
+    from moseq2_detectron_extract_amd.results import check_completion_status
+    assert check_completion_status(str(tmp_path / "out" / "results_00.yaml"))
+    assert extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg_t, true_depth=s.true_depth,
+                           output_dir=str(tmp_path / "out")) == {}
     assert set(out_x) == set(out_t)
     for k in out_t:
         np.testing.assert_array_equal(out_x[k], out_t[k], err_msg=k)

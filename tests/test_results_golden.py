@@ -83,3 +83,23 @@ def test_keypoints_tsv_bytes(g, RS, tmp_path):
     with open(w.path, "rb") as fh:
         got = fh.read()
     assert got == bytes(g["tsv"])
+
+
+def test_status_yaml_roundtrip(tmp_path, RS):
+    """Status file (M/extract.py:47-62,129-131; write_yaml M/io/util.py:99-109;
+    check_completion_status M/proc/util.py:63-77)."""
+    p = RS.status_filename(str(tmp_path))
+    assert p.endswith("results_00.yaml")
+    assert not RS.check_completion_status(p)  # missing file
+    st = {"complete": False, "skip": False, "uuid": "u", "metadata": {"DepthResolution": [512, 424]},
+          "parameters": {"crop_size": (80, 80), "chunk_size": np.int64(1000), "min_height": 0.0}}
+    RS.write_status(p, st)
+    assert not RS.check_completion_status(p)
+    st["complete"] = True
+    RS.write_status(p, st)
+    assert RS.check_completion_status(p)
+    import yaml
+    with open(p) as fh:
+        d = yaml.safe_load(fh)
+    assert d["parameters"]["crop_size"] == [80, 80] and d["parameters"]["chunk_size"] == 1000
+    assert d["metadata"]["DepthResolution"] == [512, 424]
