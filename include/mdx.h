@@ -265,6 +265,10 @@ int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const 
  * in lockstep; 4 (default) = one workgroup per ROI, separable form (per-bin row and
  * column weight sums, (gh+1)(gw+1) taps per output instead of 4 gh gw).
  * Returns the old mode. */
+/* Tuning knob: 1 (default) maps the ROIAlign workgroups to XCD-contiguous
+ * ROI ranges; 0 keeps dispatch order (ROIs of the same images in flight on
+ * every XCD).  Returns the previous value. */
+int mdx_roi_align_set_order(int xcd_remap);
 int mdx_roi_align_set_mode(int mode);
 
 /* fast_rcnn_inference_single_image + detector_postprocess for 1 class:

@@ -64,6 +64,7 @@ SIGNATURES = {
                                 P, P, P, P, P]),
     "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "mdx_roi_align_set_mode": (I32, [I32]),
+    "mdx_roi_align_set_order": (I32, [I32]),
     "mdx_box_postprocess": (I32, [P, I32, P, P, I32, I32, I32, F32, F32, I32, I32, P, F32, P, P, P, P, P]),
     "mdx_paste_masks": (I32, [P, P, P, I32, I32, I32, I32, I32, I64, F32, P, P]),
     "mdx_deconv_col2im": (I32, [P, P, I32, I32, I32, I32, P, P]),

@@ -670,6 +670,7 @@ struct RoiLevels {
     float scale[MAX_LEVELS];
     int L, min_level, C, P, sampling, aligned, per_image;
     float canonical_size, canonical_level;
+    int xcd_remap;  // 1: XCD-contiguous ROI ranges (default); 0: ROIs in dispatch order across XCDs
 };
 
 template <typename T>
@@ -779,8 +780,8 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
     __shared__ __attribute__((aligned(16))) char s_win[ROI_WIN_BYTES];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
-    int r;
-    {
+    int r = blockIdx.x;
+    if (rl.xcd_remap) {
         const int Lb = blockIdx.x, nwg = gridDim.x;
         const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
         r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
@@ -939,8 +940,8 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
     constexpr int V = Vec16<T>::N;
     __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
-    int r;
-    {
+    int r = blockIdx.x;
+    if (rl.xcd_remap) {
         const int Lb = blockIdx.x, nwg = gridDim.x;
         const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
         r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
@@ -1093,8 +1094,8 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     __shared__ int s_r0[ROI_PMAX], s_nr[ROI_PMAX], s_c0[ROI_PMAX], s_nc[ROI_PMAX];
     __shared__ float s_A[ROI_PMAX][ROI_RMAX], s_B[ROI_PMAX][ROI_RMAX];
     __shared__ int s_bad;
-    int r;
-    {
+    int r = blockIdx.x;
+    if (rl.xcd_remap) {
         const int Lb = blockIdx.x, nwg = gridDim.x;
         const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
         r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
@@ -1297,7 +1298,12 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     }
 }
 
-static int g_roi_mode = 4;
+static int g_roi_mode = 4, g_roi_xcd = 1;
+extern "C" int mdx_roi_align_set_order(int xcd_remap) {
+    const int old = g_roi_xcd;
+    g_roi_xcd = xcd_remap;
+    return old;
+}
 extern "C" int mdx_roi_align_set_mode(int mode) {
     const int old = g_roi_mode;
     g_roi_mode = mode;
@@ -1768,6 +1774,7 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     }
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
+    rl.xcd_remap = g_roi_xcd;
     if (g_roi_mode == 5 && P <= ROI_PMAX) {
         if (dtype == 1)
             hipLaunchKernelGGL((k_roi_align_sep<_Float16, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,

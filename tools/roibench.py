@@ -58,6 +58,17 @@ def main():
         call("mdx_roi_align_set_mode", old)
         outs[mode] = out.float()
         print(f"box ROIAlign [{name}]: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
+    for order in (0, 1):
+        oldo = call("mdx_roi_align_set_order", order)
+        for _ in range(2):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e0.record()
+        for _ in range(5):
+            out = orig(feats, props, pcount, R, P, *a, **k)
+        e1.record()
+        torch.cuda.synchronize()
+        call("mdx_roi_align_set_order", oldo)
+        print(f"box ROIAlign [separable, xcd_remap={order}]: {e0.elapsed_time(e1) / 5 * 1e3:8.1f} us", flush=True)
     print("max |diff| between kernels:", max((outs[0] - outs[m]).abs().max().item() for m in outs))
     # locality experiment: ROIs of each image ordered by level, then position
     pr = props.reshape(pcount.shape[0], -1, 4)
