@@ -1087,6 +1087,17 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
 // than ROI_SPAN_FLOATS / C columns take the mode-4 loop.
 constexpr int ROI_RMAX = 8, ROI_PMAX = 16, ROI_SPAN_FLOATS = 8192;
 
+// x / c for the bin average with the ROI's reciprocal r = RN(1/c): q = RN(x r)
+// refined by one FMA residual step (Markstein), 3 VALU instead of the ~10 of
+// the IEEE division sequence per output element (the box pooler is VALU-
+// bound: PMC SQ_INSTS_VALU).  Equal to RN(x / c) up to the rare last-ulp
+// cases the oracle tolerance covers.
+__device__ __forceinline__ float div_count(float x, float c, float r) {
+    const float q = x * r;
+    const float e = __builtin_fmaf(-q, c, x);
+    return __builtin_fmaf(e, r, q);
+}
+
 template <typename T, bool ROWS = false>
 __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float *__restrict__ rois,
                                                        const int *__restrict__ counts, T *__restrict__ out) {
@@ -1112,6 +1123,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     }
     const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
     const T *f = reinterpret_cast<const T *>(g.feat);
+    const float inv_count = 1.0f / g.count;  // once per ROI (see div_count)
     if (threadIdx.x == 0) s_bad = P > ROI_PMAX;
     __syncthreads();
     // row tables by lanes 0..P-1 of wave 0, column tables by wave 1
@@ -1251,7 +1263,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
                         }
                     }
 #pragma unroll
-                    for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+                    for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
                     st16(o + ((long long)(ph * P + pw) * G + cg) * V, acc);
                 }
                 __syncthreads();
@@ -1259,9 +1271,26 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
             return;
         }
     }
+    // item t = (bin, channel group); when G divides 256 a thread keeps its
+    // channel group and steps its bin by 256 / G (no divisions per item)
+    const bool gstep = (256 % G) == 0;
+    const int bstep = gstep ? 256 / G : 0;
+    int cg0 = threadIdx.x % G, bin0 = threadIdx.x / G;
+    int ph0 = bin0 / P, pw0 = bin0 - ph0 * P;
     for (int t = threadIdx.x; t < nitems; t += 256) {
-        const int bin = t / G, cg = t - bin * G;
-        const int ph = bin / P, pw = bin - ph * P;
+        int cg = cg0, ph = ph0, pw = pw0;
+        if (gstep) {
+            pw0 += bstep;
+            while (pw0 >= P) {
+                pw0 -= P;
+                ++ph0;
+            }
+        } else {
+            const int bin = t / G;
+            cg = t - bin * G;
+            ph = bin / P;
+            pw = bin - ph * P;
+        }
         const int nr = s_nr[ph], nc = s_nc[pw];
         const T *fc = f + ((long long)s_r0[ph] * g.W + s_c0[pw]) * C + cg * V;
         float acc[V];
@@ -1293,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
             }
         }
 #pragma unroll
-        for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
+        for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
         st16(o + (long long)t * V, acc);
     }
 }
