@@ -1305,19 +1305,24 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
             const T *rp0 = fc + (long long)j * g.W * C;
             const T *rp1 = two ? rp0 + (long long)g.W * C : rp0;
             for (int kc = 0; kc < nc; kc += 4) {
-                float v[8][V];
+                uint4 raw[8];  // raw 16-B taps, converted inside the FMAs
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int k = kc + u < nc ? kc + u : nc - 1;
-                    ld16(rp0 + (long long)k * C, v[u]);
-                    ld16(rp1 + (long long)k * C, v[4 + u]);
+                    raw[u] = *reinterpret_cast<const uint4 *>(rp0 + (long long)k * C);
+                    raw[4 + u] = *reinterpret_cast<const uint4 *>(rp1 + (long long)k * C);
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const float bk = kc + u < nc ? s_B[pw][kc + u] : 0.f;
                     const float w0 = a0 * bk, w1 = a1 * bk;
+                    const T *e0 = reinterpret_cast<const T *>(&raw[u]);
+                    const T *e1 = reinterpret_cast<const T *>(&raw[4 + u]);
+                    // fma(w, (float)half, acc): one mixed-precision FMA per tap
+                    // and channel (v_fma_mix_f32) instead of cvt + mul + fma + add
 #pragma unroll
-                    for (int i = 0; i < V; ++i) acc[i] += w0 * v[u][i] + w1 * v[4 + u][i];
+                    for (int i = 0; i < V; ++i)
+                        acc[i] = __builtin_fmaf(w1, (float)e1[i], __builtin_fmaf(w0, (float)e0[i], acc[i]));
                 }
             }
         }
