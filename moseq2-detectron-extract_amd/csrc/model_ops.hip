@@ -1116,9 +1116,12 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     const int G = C / V;
     T *o = out + (long long)r * P * P * C;
     const int nitems = P * P * G;
+    // gridDim.y workgroups share one ROI's items (small ROI counts: mask /
+    // keypoint poolers), each building the ROI's tables itself
+    const int tstart = threadIdx.x + 256 * blockIdx.y, tstep = 256 * gridDim.y;
     if (ri >= counts[b]) {
         const float z[V] = {};
-        for (int i = threadIdx.x; i < nitems; i += 256) st16(o + (long long)i * V, z);
+        for (int i = tstart; i < nitems; i += tstep) st16(o + (long long)i * V, z);
         return;
     }
     const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
@@ -1168,7 +1171,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     __syncthreads();
     if (s_bad) {
         // per-sample path (the reference formula), taps from global memory
-        for (int t = threadIdx.x; t < nitems; t += 256) {
+        for (int t = tstart; t < nitems; t += tstep) {
             const int bin = t / G, cg = t - bin * G;
             const int ph = bin / P, pw = bin - ph * P;
             const T *fc = f + cg * V;
@@ -1273,11 +1276,11 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     }
     // item t = (bin, channel group); when G divides 256 a thread keeps its
     // channel group and steps its bin by 256 / G (no divisions per item)
-    const bool gstep = (256 % G) == 0;
-    const int bstep = gstep ? 256 / G : 0;
-    int cg0 = threadIdx.x % G, bin0 = threadIdx.x / G;
+    const bool gstep = (tstep % G) == 0;
+    const int bstep = gstep ? tstep / G : 0;
+    int cg0 = tstart % G, bin0 = tstart / G;
     int ph0 = bin0 / P, pw0 = bin0 - ph0 * P;
-    for (int t = threadIdx.x; t < nitems; t += 256) {
+    for (int t = tstart; t < nitems; t += tstep) {
         int cg = cg0, ph = ph0, pw = pw0;
         if (gstep) {
             pw0 += bstep;
@@ -1817,12 +1820,15 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
             hipLaunchKernelGGL((k_roi_align_sep<float, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (float *)out);
     } else if (g_roi_mode == 4 && P <= ROI_PMAX) {
+        // few ROIs (mask / keypoint heads: B x D): split each ROI's items over
+        // up to 4 workgroups so the grid covers the CUs
+        const int split = R >= 1024 ? 1 : (R >= 512 ? 2 : 4);
         if (dtype == 1)
-            hipLaunchKernelGGL(k_roi_align_sep<_Float16>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                               (_Float16 *)out);
+            hipLaunchKernelGGL(k_roi_align_sep<_Float16>, dim3(R, split), dim3(256), 0, as_stream(stream), rl, rois,
+                               counts, (_Float16 *)out);
         else
-            hipLaunchKernelGGL(k_roi_align_sep<float>, dim3(R), dim3(256), 0, as_stream(stream), rl, rois, counts,
-                               (float *)out);
+            hipLaunchKernelGGL(k_roi_align_sep<float>, dim3(R, split), dim3(256), 0, as_stream(stream), rl, rois,
+                               counts, (float *)out);
     } else if (g_roi_mode >= 1 && g_roi_mode <= 4) {
 #define MDX_ROI_FULL(NI_)                                                                                     \
     do {                                                                                                      \
