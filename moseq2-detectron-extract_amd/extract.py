@@ -50,7 +50,10 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         out_dir = output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}")
         os.makedirs(out_dir, exist_ok=True)
         status_path = status_filename(out_dir)
-        if skip_completed and check_completion_status(status_path):
+        done = skip_completed and check_completion_status(status_path)
+        if world > 1:  # every rank must agree, or a skipping rank would leave the others in the exchange
+            done = _all_ranks(done)
+        if done:
             return {}
         status = status or {"complete": False, "skip": False, "uuid": str(uuid.uuid4()),
                             "metadata": _load_metadata(path), "parameters": dict(vars(config))}
@@ -106,6 +109,17 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     return out
 
 
+def _all_ranks(flag: bool) -> bool:
+    """True only if `flag` holds on every rank (MIN all-reduce; RCCL for the
+    nccl backend, gloo on the CPU)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
 def _load_metadata(path: str) -> dict:
     """Session metadata.json next to the depth file (Session.load_metadata)."""
     import json
@@ -151,9 +165,18 @@ def _select_exchange(ex, states):
     for _, st, _ in states:
         f0s.append(f)
         f += len(st["nkeep"])
-    prev = pass_tail_forward(ex.chunk_tail(states[-1][1], f0s[-1]) if states else None)
+    # this shard's tail for the next rank, chained from the preceding shard's
+    # through its own chunks: a shard shorter than POINTWISE_HIT_COUNTER_MAX
+    # frames still forwards the session's last frames
+    def own_tail(got):
+        t = got
+        for (_, st, _), f0 in zip(states, f0s):
+            t = ex.chunk_tail(st, f0, t)
+        return t
+
+    prev = pass_tail_forward(own_tail)
     for (_, st, host), ch, f0 in zip(states, changes, f0s):
-        tail = ex.chunk_tail(st, f0)
+        tail = ex.chunk_tail(st, f0, prev)
         ex.apply_selection(st, host, ch, f0, prev)
         prev = tail
 
@@ -182,15 +205,22 @@ def _run_overlapped(src, batches, ex, true_depth):
     dev = torch.cuda.current_device()
 
     def worker():
+        # The loop keeps draining the queue after an error (it only skips the
+        # work), so the producer's q.put() and the final sentinel never block
+        # on a dead consumer; the first error is raised by the caller.
+        ws = None
         try:
             torch.cuda.set_device(dev)
             ws = torch.cuda.Stream()
-            while True:
-                item = q.get()
-                if item is None:
-                    return
-                if err:
-                    continue
+        except BaseException as e:  # surfaced by the caller
+            err.append(e)
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            if err:
+                continue
+            try:
                 idx, st, host, ev = item
                 ws.wait_event(ev)
                 with torch.cuda.stream(ws):
@@ -200,8 +230,8 @@ def _run_overlapped(src, batches, ex, true_depth):
                     cen, kp, ang, fl = ex.host_angles(host)
                     d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
                 parts.append(_lighten(d))
-        except BaseException as e:  # surfaced by the caller
-            err.append(e)
+            except BaseException as e:  # surfaced by the caller
+                err.append(e)
 
     import sys
     # the worker's host step is many short numpy calls: a short GIL switch

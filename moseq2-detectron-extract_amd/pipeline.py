@@ -169,24 +169,29 @@ class GPUExtractor:
             return
         f0 = self._frames_seen
         changes = INS.select_chunk(self.instance_tracker, state["nkeep"], host["centers"], f0)
-        tail = self.chunk_tail(state, f0)
+        tail = self.chunk_tail(state, f0, self._tail_dets)
         self.apply_selection(state, host, changes, f0, self._tail_dets)
         self._tail_dets = tail
         self._frames_seen = f0 + len(state["nkeep"])
 
-    def chunk_tail(self, state: dict, f0: int) -> dict:
-        """The chunk's last frames' kept detections {session frame: (mask
-        planes (D,h,w), keypoints (D,K,3), keep row (D,))}: the tracker's live
-        objects are at most pointwise_hit_counter_max frames old, so these are
-        all a later chunk's picks can refer to."""
+    def chunk_tail(self, state: dict, f0: int, prev_tail: Optional[dict] = None) -> dict:
+        """The session's last POINTWISE_HIT_COUNTER_MAX frames' kept detections
+        up to the end of this chunk {session frame: (mask planes (D,h,w),
+        keypoints (D,K,3), keep row (D,))}: the tracker's live objects are at
+        most that many frames old, so these are all a later chunk's picks can
+        refer to.  A chunk shorter than that window keeps the frames of
+        `prev_tail` (the preceding chunk's tail, any rank) still inside it."""
         inf = state["inf"]
         masks = inf["masks"]
         bs = masks[0].shape[0]
         n = len(state["nkeep"])
+        lo = f0 + n - INS.POINTWISE_HIT_COUNTER_MAX  # first session frame of the window
         a = max(0, n - INS.POINTWISE_HIT_COUNTER_MAX)
         kp = inf["keypoints"][a:].cpu().numpy()
         keep = inf["keep_idx"][a:].cpu().numpy()
-        return {f0 + f: (masks[f // bs][f % bs].clone(), kp[f - a], keep[f - a]) for f in range(a, n)}
+        out = {g: v for g, v in (prev_tail or {}).items() if lo <= g < f0}
+        out.update({f0 + f: (masks[f // bs][f % bs].clone(), kp[f - a], keep[f - a]) for f in range(a, n)})
+        return out
 
     def apply_selection(self, state: dict, host: dict, changes: dict, f0: int, prev_tail: dict):
         """Frames whose picked instance differs from the NMS result get the
@@ -221,6 +226,10 @@ class GPUExtractor:
                 kph[f] = det_kp[g - f0, j]
             else:  # a detection of the preceding chunk's last frames
                 planes, kps, krow = prev_tail[g]
+                if not planes.is_cuda or planes.device != d2.device:
+                    # received over a CPU (gloo) group: the gather kernel reads device memory only
+                    planes = planes.to(d2.device)
+                    prev_tail[g] = (planes, kps, krow)
                 j = int(krow[slot])
                 src.append(planes[j].data_ptr())
                 kph[f] = kps[j]

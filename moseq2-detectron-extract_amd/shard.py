@@ -228,8 +228,9 @@ def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
     planes, keypoints, keep rows; instances.POINTWISE_HIT_COUNTER_MAX frames):
     a pick at the start of rank r's shard can be a detection of the previous
     shard's last frames.  `tail` is {session frame: (planes (D,h,w) uint8,
-    keypoints (D,K,3), keep row (D,))} or None for a rank without frames (it
-    forwards what it received).  Returns the previous shard's tail ({} on
+    keypoints (D,K,3), keep row (D,))}, a callable mapping the received tail
+    to the one to send, or None for a rank without frames (it forwards what
+    it received).  Returns the previous shard's tail ({} on
     rank 0)."""
     import torch
     import torch.distributed as dist
@@ -250,7 +251,7 @@ def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
             for i in range(nf):
                 got[int(m[i, 0])] = (planes[i], m[i, 1 + D:].reshape(D, K, 3).astype(np.float32),
                                      m[i, 1:1 + D].astype(np.int64))
-    send = got if tail is None else tail
+    send = got if tail is None else (tail(got) if callable(tail) else tail)
     if rank < world - 1:
         keys = sorted(send)
         if keys:

@@ -13,6 +13,8 @@ from their published code, with plain torch ops only:
 * RPN: StandardRPNHead, DefaultAnchorGenerator, find_top_rpn_proposals
   (per-level topk, decode, clip, nonempty, per-level NMS 0.7, top 1000)
 * ROIPooler(ROIAlignV2) = torchvision roi_align(aligned=True, sampling 0)
+  (roi_align / nms below restate torchvision's CPU kernels in torch; the
+  forward runs their C twins in model_ops.c, bit-identical and ~100x faster)
 * FastRCNNConvFCHead + fast_rcnn_inference_single_image
 * MaskRCNNConvUpsampleHead + mask_rcnn_inference + paste_masks_in_image
 * KRCNNConvDeconvUpsampleHead + heatmaps_to_keypoints
@@ -24,12 +26,64 @@ intermediates for stage-wise parity tests.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
+import subprocess
 from typing import Dict, List
 
 import numpy as np
 import torch
 import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_CLIB = None
+
+
+def _clib():
+    """model_ops.c (torchvision's CPU roi_align / nms kernels restated in C;
+    bit-identical to the torch restatements below, which stay as their
+    cross-check)."""
+    global _CLIB
+    if _CLIB is None:
+        so = os.path.join(_HERE, "liboracle_model.so")
+        src = os.path.join(_HERE, "model_ops.c")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        lib = ctypes.CDLL(so)
+        P, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        lib.orc_roi_align.argtypes = [P, i32, i32, i32, i32, P, i32, i32, f32, i32, i32, P]
+        lib.orc_nms.argtypes = [P, P, i32, f32, P]
+        lib.orc_nms.restype = i32
+        _CLIB = lib
+    return _CLIB
+
+
+def _ptr(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def roi_align_c(feat, rois, out_size, scale, sampling_ratio, aligned):
+    """roi_align through model_ops.c (same values as roi_align below)."""
+    feat = feat.detach().to(torch.float32).contiguous()
+    rois = rois.detach().to(torch.float32).contiguous()
+    N, C, H, W = feat.shape
+    out = torch.empty((rois.shape[0], C, out_size, out_size), dtype=torch.float32)
+    if rois.shape[0]:
+        _clib().orc_roi_align(_ptr(feat), N, C, H, W, _ptr(rois), rois.shape[0], out_size, float(scale),
+                              int(sampling_ratio), int(bool(aligned)), _ptr(out))
+    return out
+
+
+def nms_c(boxes, scores, thresh):
+    """nms through model_ops.c (same result as nms below)."""
+    if boxes.numel() == 0:
+        return torch.empty(0, dtype=torch.int64)
+    order = torch.sort(scores, descending=True, stable=True)[1].contiguous()
+    b = boxes.detach().to(torch.float32).contiguous()
+    keep = torch.empty(len(order), dtype=torch.int64)
+    n = _clib().orc_nms(_ptr(b), _ptr(order), len(order), float(thresh), _ptr(keep))
+    return keep[:n].clone()
 
 
 # ---------------------------------------------------------------- backbone
@@ -164,7 +218,7 @@ def batched_nms(boxes, scores, idxs, thresh):
     keep_mask = torch.zeros_like(scores, dtype=torch.bool)
     for c in torch.unique(idxs):
         ci = torch.where(idxs == c)[0]
-        keep_mask[ci[nms(boxes[ci], scores[ci], thresh)]] = True
+        keep_mask[ci[nms_c(boxes[ci], scores[ci], thresh)]] = True
     keep = torch.where(keep_mask)[0]
     return keep[scores[keep].sort(descending=True, stable=True)[1]]
 
@@ -276,6 +330,9 @@ def roi_align(feat, rois, out_size, scale, sampling_ratio, aligned, chunk=256):
         vx = torch.arange(G)[None, None, :] < gw[:, None, None]
 
         def prep(v, size):
+            # a zero-size ROI has grid 0 (no samples; masked by vy / vx below)
+            # and NaN positions: keep its gather indices in range
+            v = torch.where(torch.isfinite(v), v, torch.zeros_like(v))
             empty = (v < -1.0) | (v > size)
             v = torch.where(v <= 0, torch.zeros_like(v), v)
             lo = v.to(torch.int64)
@@ -328,8 +385,8 @@ def pooler(feats, boxes_per_image, out_size, cfg):
     for li, l in enumerate(lv):
         sel = torch.where(lvl == li)[0]
         if len(sel):
-            out[sel] = roi_align(feats[f"p{l}"], rois[sel], out_size, 1.0 / 2 ** l, cfg.pooler_sampling_ratio,
-                                 cfg.pooler_aligned)
+            out[sel] = roi_align_c(feats[f"p{l}"], rois[sel], out_size, 1.0 / 2 ** l, cfg.pooler_sampling_ratio,
+                                   cfg.pooler_aligned)
     return out
 
 
