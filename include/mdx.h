@@ -330,6 +330,135 @@ int mdx_gather_planes(const uint64_t *src_ptrs, const int *dst_idx, uint8_t *dst
 int mdx_heatmaps_to_keypoints(const float *maps, const float *boxes, const int *counts, int B, int D,
                               int K, int M, float *out, mdx_stream_t stream);
 
+/* ---------------------------------------------------------------------
+ * Model handle: the whole Mask/Keypoint R-CNN forward as one C call.
+ * Replaces Predictor.from_config (M/model/predict.py:31-44: build_model +
+ * DetectionCheckpointer.load) and Predictor.__call__'s model(inputs)
+ * (:53-102, eval-mode GeneralizedRCNN.inference + detector_postprocess).
+ * ------------------------------------------------------------------- */
+
+/* Inference hyper-parameters of the Detectron2 CfgNode the reference builds
+ * (get_base_config, M/model/config.py:21-94, add_dataset_cfg :113-150, the
+ * InferenceStep overrides M/pipeline/inference_step.py:48-51).  Only these
+ * architectures are supported: ResNet-50/101 (FrozenBN, num_groups 1), FPN
+ * with GN, avg or sum fuse, LastLevelMaxPool, StandardRPNHead, 1+ box FCs,
+ * MaskRCNNConvUpsampleHead, KRCNNConvDeconvUpsampleHead. */
+typedef struct mdx_model_cfg {
+    int depth;                     /* MODEL.RESNETS.DEPTH: 50 or 101 */
+    int dtype;                     /* arithmetic: 0 = float32, 1 = float16 (fp32 accumulation) */
+    int stem_out_channels;         /* 64 */
+    int res2_out_channels;         /* 256 */
+    int width_per_group;           /* 64 (NUM_GROUPS must be 1) */
+    int stride_in_1x1;             /* 1 */
+    int fpn_out_channels;          /* 256 */
+    int fpn_fuse_avg;              /* FPN.FUSE_TYPE: 1 = "avg", 0 = "sum" */
+    int gn_groups;                 /* 32 (FPN.NORM must be "GN") */
+    float gn_eps;                  /* 1e-5 */
+    int n_anchor_sizes;            /* 5, one per level p2..p6 */
+    float anchor_sizes[5];         /* 32 64 128 256 512 */
+    int n_aspect_ratios;           /* 3 */
+    float aspect_ratios[4];        /* 0.5 1 2 */
+    float anchor_offset;           /* 0 */
+    int rpn_pre_nms_topk;          /* PRE_NMS_TOPK_TEST 1000 */
+    int rpn_post_nms_topk;         /* POST_NMS_TOPK_TEST 1000 */
+    float rpn_nms_thresh;          /* 0.7 */
+    float rpn_min_box_size;        /* 0 */
+    int num_classes;               /* ROI_HEADS.NUM_CLASSES (must be 1) */
+    float score_thresh;            /* SCORE_THRESH_TEST (--instance-threshold) */
+    float nms_thresh;              /* NMS_THRESH_TEST 0.5 */
+    int detections_per_image;      /* TEST.DETECTIONS_PER_IMAGE (--allowed-detections) */
+    int box_pooler_resolution;     /* 7 */
+    int box_num_fc;                /* 2 */
+    int box_fc_dim;                /* 1024 */
+    float box_reg_weights[4];      /* 10 10 5 5 */
+    int mask_on;                   /* 1 */
+    int mask_pooler_resolution;    /* 14 */
+    int mask_num_conv;             /* 4 */
+    int mask_conv_dim;             /* 256 */
+    float mask_threshold;          /* 0.5 (paste_masks_in_image) */
+    int keypoint_on;               /* 1 */
+    int keypoint_pooler_resolution;/* 7 (M/model/config.py:84) */
+    int n_keypoint_convs;          /* 8 */
+    int keypoint_conv_dims[16];    /* 512 x 8 */
+    int num_keypoints;             /* 8 */
+    int pooler_sampling_ratio;     /* 0 (adaptive) */
+    int pooler_aligned;            /* 1 (ROIAlignV2) */
+    float canonical_box_size;      /* 224 */
+    float canonical_level;         /* 4 */
+    int in_channels;               /* 3 (INPUT.FORMAT RGB: the gray frame replicated) or 1 */
+    float pixel_mean[3];           /* 1.12 x3 (M/model/config.py:141-148) */
+    float pixel_std[3];            /* 5.79 x3 */
+    int size_divisibility;         /* 32 */
+} mdx_model_cfg;
+
+typedef void *mdx_model_t;
+
+/* Weights blob: Detectron2 state-dict layout (parameter / buffer names of
+ * GeneralizedRCNN, e.g. "backbone.bottom_up.res2.0.conv1.weight"), serialised
+ * as  "MDXW" | u32 version (1) | u32 count | count x { u32 name_len | name |
+ * u32 ndim | i64 shape[ndim] | float32 data[prod(shape)] }  (little endian).
+ * Create folds FrozenBN into the convs, packs every weight once into the
+ * kernels' layouts (NHWC/OHWI, fp16 when cfg->dtype == 1) and uploads them
+ * to `device`; it synchronises the host.  Missing or mis-shaped tensors fail
+ * with MDX_EINVAL naming the key. */
+int mdx_model_create(const void *weights_blob, int64_t blob_bytes, const mdx_model_cfg *cfg, int device,
+                     mdx_model_t *out);
+int mdx_model_destroy(mdx_model_t model);
+
+/* Caller-owned device outputs of one forward over B frames of h x w
+ * (D = detections_per_image, K = num_keypoints, S = 4 * keypoint pooler
+ * resolution).  Detections are score-ordered, rows >= ndet[b] are padding.
+ * masks: B*D planes at masks + (b*D+d)*mask_plane_stride (h x w bytes,
+ * 0/1), may be NULL; keypoints (B,D,K,3) [x, y, score] may be NULL;
+ * keypoint_heatmaps (B,D,K,S,S) may be NULL (then kept in the workspace). */
+typedef struct mdx_model_outputs {
+    float *boxes;               /* (B,D,4) XYXY, image pixels */
+    float *scores;              /* (B,D) */
+    int64_t *classes;           /* (B,D) */
+    int32_t *ndet;              /* (B) */
+    uint8_t *masks;
+    int64_t mask_plane_stride;  /* >= h*w; a multiple of 16 keeps planes 16-B aligned */
+    float *keypoints;
+    float *keypoint_heatmaps;
+} mdx_model_outputs;
+
+/* Reserve the workspace for forwards of up to B frames of h x w on `stream`
+ * (each stream has its own workspace, so forwards on different streams may
+ * run concurrently).  Allocates (device memory, synchronous): call it before
+ * capturing forwards into a HIP graph.  mdx_model_forward reserves on demand. */
+int mdx_model_reserve(mdx_model_t model, int B, int h, int w, mdx_stream_t stream);
+
+/* One forward: frames uint8 (B,h,w) device (the gray depth frame; replicated
+ * to in_channels as Predictor.__call__ does, M/model/predict.py:74-77); lut
+ * host uint8[256] applied first (scale_raw_frames fused; NULL = identity).
+ * Everything is enqueued on `stream` with no host synchronisation (fixed
+ * shapes: rpn_post_nms_topk proposals and D detections per image, counts on
+ * the device), so the call can be captured into a HIP graph once reserved. */
+int mdx_model_forward(mdx_model_t model, const uint8_t *frames, int B, int h, int w, const uint8_t *lut,
+                      const mdx_model_outputs *out, mdx_stream_t stream);
+
+/* Intermediates of the last forward on `stream` (valid until the next forward
+ * on it), for stage-wise parity tests: "input" (B,Hp,Wp,4 NHWC), "res2".."res5",
+ * "p2".."p6" (NHWC), "proposals" (B,P,4) f32, "proposal_scores" (B,P) f32,
+ * "proposal_count" (B) i32, "box_pooled" (B*P,R,R,C), "box_pred" (B*P,6) f32,
+ * "mask_logits" (B*D,2M,2M,1) f32.  shape[4] gets the dims (unused = 1),
+ * dtype: 0 f32, 1 f16, 2 i32.  copy: D2D copy of `bytes` into dst on `stream`. */
+int mdx_model_tensor_info(mdx_model_t model, mdx_stream_t stream, const char *name, int64_t shape[4], int *dtype);
+int mdx_model_tensor_copy(mdx_model_t model, mdx_stream_t stream, const char *name, void *dst, int64_t bytes);
+
+/* Per-convolution timing of later forwards (HIP events around every conv
+ * launch; host-only bookkeeping, off by default).  read: after the stream
+ * is synchronised, up to max records {kernel (MDX_CONV_KERNEL_*), ksplit, M,
+ * N, K, algorithmic FLOP, milliseconds} of the last profiled forward; returns
+ * the number written. */
+typedef struct mdx_conv_record {
+    int kernel, ksplit;
+    int64_t M, N, K;
+    double flop, ms;
+} mdx_conv_record;
+int mdx_model_profile(mdx_model_t model, int on);
+int mdx_model_profile_read(mdx_model_t model, mdx_conv_record *out, int max);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,6 +76,14 @@ SIGNATURES = {
     "mdx_instance_tracker_create": (P, [I32]),
     "mdx_instance_tracker_destroy": (I32, [P]),
     "mdx_instance_tracker_select": (I32, [P, P, P, I64, I32, I64, P, P]),
+    "mdx_model_create": (I32, [ctypes.c_char_p, I64, P, I32, P]),
+    "mdx_model_destroy": (I32, [P]),
+    "mdx_model_reserve": (I32, [P, I32, I32, I32, P]),
+    "mdx_model_forward": (I32, [P, P, I32, I32, I32, P, P, P]),
+    "mdx_model_tensor_info": (I32, [P, P, ctypes.c_char_p, P, P]),
+    "mdx_model_tensor_copy": (I32, [P, P, ctypes.c_char_p, P, I64]),
+    "mdx_model_profile": (I32, [P, I32]),
+    "mdx_model_profile_read": (I32, [P, P, I32]),
 }
 
 

@@ -7,12 +7,17 @@
 * ``load_state_dict(path)``: a Detectron2 ``model_final.pth`` (``{'model':
   state_dict}``), read with ``torch.load(weights_only=True)`` (no unpickling of
   arbitrary objects).
+* ``pack_blob(sd)``: the state dict as the weights blob of the C ABI
+  (``mdx_model_create``).
 """
 from __future__ import annotations
 
 import math
+import struct
 from collections import OrderedDict
+from typing import Mapping
 
+import numpy as np
 import torch
 
 from .config import ModelConfig
@@ -119,3 +124,19 @@ def load_state_dict(path: str) -> "OrderedDict[str, torch.Tensor]":
     obj = torch.load(path, map_location="cpu", weights_only=True)
     sd = obj.get("model", obj) if isinstance(obj, dict) else obj
     return OrderedDict((k, v if isinstance(v, torch.Tensor) else torch.as_tensor(v)) for k, v in sd.items())
+
+
+def pack_blob(sd: Mapping[str, torch.Tensor]) -> bytes:
+    """Serialise a state dict into the "MDXW" weights blob mdx_model_create
+    reads (include/mdx.h): "MDXW" | u32 version 1 | u32 count | per tensor
+    u32 name_len | name | u32 ndim | i64 shape[ndim] | float32 data."""
+    parts = [b"MDXW", struct.pack("<II", 1, len(sd))]
+    for k, v in sd.items():
+        a = np.ascontiguousarray(torch.as_tensor(v).detach().to("cpu", torch.float32).numpy(), dtype="<f4")
+        name = k.encode()
+        parts.append(struct.pack("<I", len(name)))
+        parts.append(name)
+        parts.append(struct.pack("<I", a.ndim))
+        parts.append(struct.pack(f"<{a.ndim}q", *a.shape))
+        parts.append(a.tobytes())
+    return b"".join(parts)

@@ -86,26 +86,32 @@ void orc_scale_lut(double vmin, double vmax, int int_vmin, uint8_t *lut)
 /* ------------------------------------------------------------------ */
 /* cv2.medianBlur(ksize=3), BORDER_REPLICATE                           */
 /* ------------------------------------------------------------------ */
-static int cmp_u8(const void *a, const void *b) { return (int)*(const uint8_t *)a - (int)*(const uint8_t *)b; }
+#define SORT2(a, b) do { if (a > b) { uint8_t t_ = a; a = b; b = t_; } } while (0)
+/* median of 9 by a fixed compare-exchange network (the middle order statistic) */
+static inline uint8_t median9(uint8_t p0, uint8_t p1, uint8_t p2, uint8_t p3, uint8_t p4, uint8_t p5,
+                              uint8_t p6, uint8_t p7, uint8_t p8)
+{
+    SORT2(p1, p2); SORT2(p4, p5); SORT2(p7, p8); SORT2(p0, p1); SORT2(p3, p4); SORT2(p6, p7);
+    SORT2(p1, p2); SORT2(p4, p5); SORT2(p7, p8); SORT2(p0, p3); SORT2(p5, p8); SORT2(p4, p7);
+    SORT2(p3, p6); SORT2(p1, p4); SORT2(p2, p5); SORT2(p4, p7); SORT2(p4, p2); SORT2(p6, p4);
+    SORT2(p4, p2);
+    return p4;
+}
 
 void orc_median3(const uint8_t *src, int64_t n, int H, int W, uint8_t *dst)
 {
+#pragma omp parallel for schedule(dynamic, 1)
     for (int64_t f = 0; f < n; ++f) {
         const uint8_t *s = src + f * (int64_t)H * W;
         uint8_t *d = dst + f * (int64_t)H * W;
-        for (int y = 0; y < H; ++y)
+        for (int y = 0; y < H; ++y) {
+            const uint8_t *r0 = s + (int64_t)(y > 0 ? y - 1 : 0) * W, *r1 = s + (int64_t)y * W;
+            const uint8_t *r2 = s + (int64_t)(y < H - 1 ? y + 1 : H - 1) * W;
             for (int x = 0; x < W; ++x) {
-                uint8_t win[9]; int c = 0;
-                for (int dy = -1; dy <= 1; ++dy)
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        int yy = y + dy, xx = x + dx;
-                        yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
-                        xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
-                        win[c++] = s[yy * W + xx];
-                    }
-                qsort(win, 9, 1, cmp_u8);
-                d[y * W + x] = win[4];
+                const int xl = x > 0 ? x - 1 : 0, xr = x < W - 1 ? x + 1 : W - 1;
+                d[(int64_t)y * W + x] = median9(r0[xl], r0[x], r0[xr], r1[xl], r1[x], r1[xr], r2[xl], r2[x], r2[xr]);
             }
+        }
     }
 }
 
@@ -114,9 +120,59 @@ void orc_median3(const uint8_t *src, int64_t n, int H, int W, uint8_t *dst)
 /* border (pixels outside the image never win the min / max).          */
 /* ------------------------------------------------------------------ */
 static void morph_once(const uint8_t *s, uint8_t *d, int H, int W,
-                       const uint8_t *strel, int kh, int kw, int is_dilate)
+                       const uint8_t *strel, int kh, int kw, int is_dilate, uint8_t *rows)
 {
     const int ay = kh / 2, ax = kw / 2;  /* default anchor = centre */
+    /* each strel row as one run [k0, k1] when it is contiguous: the min / max
+     * over the element is the min / max over its rows of the horizontal run
+     * extremum (clipped to the image, i.e. outside pixels ignored) */
+    int k0[32], k1[32], runs = kh <= 32;
+    for (int ky = 0; ky < kh && runs; ++ky) {
+        k0[ky] = -1; k1[ky] = -2;
+        for (int kx = 0; kx < kw; ++kx)
+            if (strel[ky * kw + kx]) { if (k0[ky] < 0) k0[ky] = kx; k1[ky] = kx; }
+        for (int kx = k0[ky] < 0 ? kw : k0[ky]; kx <= k1[ky]; ++kx)
+            if (!strel[ky * kw + kx]) runs = 0;
+    }
+    if (runs && rows) {
+        /* rows[slot][y][x] = horizontal extremum of row y over a distinct run
+         * (strel rows with the same run share a slot) */
+        int slot[32];
+        for (int ky = 0; ky < kh; ++ky) {
+            slot[ky] = ky;
+            for (int j = 0; j < ky; ++j)
+                if (k0[j] == k0[ky] && k1[j] == k1[ky]) { slot[ky] = slot[j]; break; }
+        }
+        for (int ky = 0; ky < kh; ++ky) {
+            if (k0[ky] < 0 || slot[ky] != ky) continue;
+            uint8_t *o = rows + (int64_t)ky * H * W;
+            for (int y = 0; y < H; ++y) {
+                const uint8_t *r = s + (int64_t)y * W;
+                for (int x = 0; x < W; ++x) {
+                    int a = x + k0[ky] - ax, b = x + k1[ky] - ax;
+                    a = a < 0 ? 0 : a; b = b >= W ? W - 1 : b;
+                    int acc = is_dilate ? 0 : 255;
+                    for (int xx = a; xx <= b; ++xx) {
+                        const int v = r[xx];
+                        if (is_dilate) { if (v > acc) acc = v; } else { if (v < acc) acc = v; }
+                    }
+                    o[(int64_t)y * W + x] = (uint8_t)acc;
+                }
+            }
+        }
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                int acc = is_dilate ? 0 : 255;
+                for (int ky = 0; ky < kh; ++ky) {
+                    const int yy = y + ky - ay;
+                    if (k0[ky] < 0 || yy < 0 || yy >= H) continue;
+                    const int v = rows[((int64_t)slot[ky] * H + yy) * W + x];
+                    if (is_dilate) { if (v > acc) acc = v; } else { if (v < acc) acc = v; }
+                }
+                d[(int64_t)y * W + x] = (uint8_t)acc;
+            }
+        return;
+    }
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             int acc = is_dilate ? 0 : 255;
@@ -137,8 +193,10 @@ static void morph_once(const uint8_t *s, uint8_t *d, int H, int W,
 void orc_morph(const uint8_t *src, int64_t n, int H, int W, int op,
                const uint8_t *strel, int kh, int kw, int iters, uint8_t *dst)
 {
-    uint8_t *a = (uint8_t *)malloc((size_t)H * W), *b = (uint8_t *)malloc((size_t)H * W);
+#pragma omp parallel for schedule(dynamic, 1)
     for (int64_t f = 0; f < n; ++f) {
+        uint8_t *a = (uint8_t *)malloc((size_t)H * W), *b = (uint8_t *)malloc((size_t)H * W);
+        uint8_t *rows = kh <= 32 ? (uint8_t *)malloc((size_t)kh * H * W) : NULL;
         memcpy(a, src + f * (int64_t)H * W, (size_t)H * W);
         int passes[2] = {0, 0}, nph = 1;
         if (op == 0) passes[0] = 0;
@@ -147,12 +205,12 @@ void orc_morph(const uint8_t *src, int64_t n, int H, int W, int op,
         else { passes[0] = 1; passes[1] = 0; nph = 2; }
         for (int p = 0; p < nph; ++p)
             for (int it = 0; it < iters; ++it) {
-                morph_once(a, b, H, W, strel, kh, kw, passes[p]);
+                morph_once(a, b, H, W, strel, kh, kw, passes[p], rows);
                 uint8_t *t = a; a = b; b = t;
             }
         memcpy(dst + f * (int64_t)H * W, a, (size_t)H * W);
+        free(a); free(b); free(rows);
     }
-    free(a); free(b);
 }
 
 /* ------------------------------------------------------------------ */
