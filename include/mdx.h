@@ -95,10 +95,14 @@ int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int
  * frame of src0 (and of src1 when not NULL, same centers/angles) --
  * M/proc/proc.py:305-340, called twice per frame at
  * M/pipeline/process_features_step.py:186-198.
- * center float64 [n][2] (x, y), angle_deg float64 [n]; out uint8 [n][ch][cw]. */
+ * center float64 [n][2] (x, y), angle_deg float64 [n]; out uint8 [n][ch][cw].
+ * window int32 [n][4] or NULL: the integer crop window (xmin, xmax, ymin,
+ * ymax) in the zero-bordered frame, computed as the reference does
+ * (int() truncation, proc.py:325-328); -1 x4 for frames the reference
+ * returns zeros for before computing one (NaN angle / centre, centre < 0). */
 int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, int W,
                     const double *center, const double *angle_deg, int cw, int ch,
-                    uint8_t *out0, uint8_t *out1, mdx_stream_t stream);
+                    uint8_t *out0, uint8_t *out1, int32_t *window, mdx_stream_t stream);
 
 
 /* Per-frame reductions of compute_scalars (M/proc/scalars.py:79-103) over
@@ -130,6 +134,23 @@ int mdx_bground_median(const int16_t *frames, int64_t n, int H, int W, int med_s
  * 180).  Bit-identical to the numpy code; runs without the GIL. */
 int mdx_iterative_filter_angles(const double *angles, int64_t n, int window, double tolerance, int max_iters,
                                 double *out, uint8_t *flips);
+
+/* Host (CPU) function: flips_from_keypoints (M/proc/proc.py:851-889): per
+ * frame, keypoints float64 [n][K][3] (K >= 7; 0-3 front, 4-6 rear) rotated
+ * by -angle_deg about centroid [n][2] vote for the end of the body axis
+ * (centroid x -+ length / 2) they are nearer to; flips[n] = front mean vote
+ * < rear mean vote, conf[n] = share of the 7 votes agreeing with it. */
+int mdx_flips_from_keypoints(const double *kp, int64_t n, int K, const double *centroid,
+                             const double *angle_deg, const double *length, uint8_t *flips, double *conf);
+
+/* Host (CPU) function: the no-tracking angle branch of instances_to_features
+ * (M/proc/proc.py:720-724, 827-839): angle = clamp_angles_deg(-rad2deg(
+ * orientation)); +180 where mdx_flips_from_keypoints (length = max axis)
+ * flips; iterative_filter_angles(window 3, tolerance 60, 1000 iterations);
+ * flips_out = keypoint flips xor filter flips.  float64 in, angles_out
+ * float64 [n], flips_out uint8 [n]. */
+int mdx_finalize_angles(const double *orientation, const double *axis_length, const double *centroid,
+                        const double *kp, int64_t n, int K, double *angles_out, uint8_t *flips_out);
 
 /* Host (CPU) functions: the instance tracker of
  * ProcessFeaturesStep.__select_instances (M/pipeline/process_features_step.py:

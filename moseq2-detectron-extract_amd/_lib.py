@@ -37,10 +37,12 @@ SIGNATURES = {
     "mdx_clean_workspace_bytes": (I64, [I64, I32, I32]),
     "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P, P]),
     "mdx_frame_moments": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P]),
-    "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P]),
+    "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P, P]),
     "mdx_frame_scalars": (I32, [P, P, I64, I32, I32, F64, F64, P, I32, P, P, P, P, P]),
     "mdx_bground_median": (I32, [P, I64, I32, I32, I32, P, P, P]),
     "mdx_iterative_filter_angles": (I32, [P, I64, I32, F64, I32, P, P]),
+    "mdx_flips_from_keypoints": (I32, [P, I64, I32, P, P, P, P, P]),
+    "mdx_finalize_angles": (I32, [P, P, P, P, I64, I32, P, P]),
     "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
     "mdx_conv_set_large_tiles": (I32, [I32]),
     "mdx_conv_set_narrow_kmax": (I32, [I32]),

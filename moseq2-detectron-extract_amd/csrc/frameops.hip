@@ -503,7 +503,8 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
 __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, const uint8_t *__restrict__ src1,
                                               int H, int W, const double *__restrict__ center,
                                               const double *__restrict__ angle, int cw, int ch,
-                                              uint8_t *__restrict__ out0, uint8_t *__restrict__ out1) {
+                                              uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,
+                                              int *__restrict__ window) {
     const int64_t f = blockIdx.x;
     const double cxc = center[2 * f], cyc = center[2 * f + 1], ang_deg = angle[f];
     uint8_t *o0 = out0 + f * (int64_t)cw * ch;
@@ -511,11 +512,20 @@ __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, 
     bool zero = isnan(ang_deg) || isnan(cxc) || isnan(cyc) || cxc < 0 || cyc < 0;
     int xmin = 0, ymin = 0, pw = 0, ph = 0;
     double M[6] = {0, 0, 0, 0, 0, 0};
+    if (window && threadIdx.x == 0) {  // -1 x4: the reference returns zeros before computing a window
+        window[4 * f] = window[4 * f + 1] = window[4 * f + 2] = window[4 * f + 3] = -1;
+    }
     if (!zero) {
         xmin = (int)(cxc - cw / 2) + cw;
         const int xmax = (int)(cxc + cw / 2) + cw;
         ymin = (int)(cyc - ch / 2) + ch;
         const int ymax = (int)(cyc + ch / 2) + ch;
+        if (window && threadIdx.x == 0) {
+            window[4 * f] = xmin;
+            window[4 * f + 1] = xmax;
+            window[4 * f + 2] = ymin;
+            window[4 * f + 3] = ymax;
+        }
         const int PWd = W + 2 * cw, PHd = H + 2 * ch;
         const int sx0 = xmin < 0 ? 0 : (xmin > PWd ? PWd : xmin);
         const int sx1 = xmax < 0 ? 0 : (xmax > PWd ? PWd : xmax);
@@ -802,13 +812,13 @@ extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int
 
 extern "C" int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, int W,
                                const double *center, const double *angle_deg, int cw, int ch, uint8_t *out0,
-                               uint8_t *out1, mdx_stream_t stream) {
+                               uint8_t *out1, int32_t *window, mdx_stream_t stream) {
     MDX_REQUIRE(src0 && out0 && center && angle_deg, "mdx_crop_rotate: null pointer");
     MDX_REQUIRE(!src1 == !out1, "mdx_crop_rotate: src1/out1 must both be set or both NULL");
     MDX_REQUIRE(cw > 0 && ch > 0 && H > 0 && W > 0, "mdx_crop_rotate: bad shape");
     if (n == 0) return MDX_OK;
     hipLaunchKernelGGL(k_crop, dim3((unsigned)n), dim3(256), 0, as_stream(stream), src0, src1, H, W, center,
-                       angle_deg, cw, ch, out0, out1);
+                       angle_deg, cw, ch, out0, out1, (int *)window);
     MDX_CHECK_LAUNCH("mdx_crop_rotate");
     return MDX_OK;
 }

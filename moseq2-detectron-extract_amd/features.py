@@ -11,12 +11,12 @@ convert_pxs_to_mm                  M/proc/util.py:29-60
 clamp_angles_deg / _rad            M/proc/proc.py:688-697
 angle_difference                   M/proc/kalman.py:93-98
 rotate_points / _batch             M/proc/keypoints.py:11-64
-flips_from_keypoints               M/proc/proc.py:851-889
+flips_from_keypoints               M/proc/proc.py:851-889 (libmdx host code)
 estimate_keypoint_rotation         M/proc/proc.py:892-907
 compute_keypoint_alignment_scores  M/proc/proc.py:936-985
 move_median                        bottleneck.move_median (min_count semantics)
 filter_angles / iterative_...      M/proc/proc.py:600-654
-finalize_angles (no tracking)      M/proc/proc.py:720-724, 827-839
+finalize_angles (no tracking)      M/proc/proc.py:720-724, 827-839 (libmdx host code)
 compute_scalars                    M/proc/scalars.py:36-120
 keypoints_to_dict                  M/proc/keypoints.py:93-165
 scalar_attributes / keypoint_...   M/proc/scalars.py:6-33, keypoints.py:67-90
@@ -45,17 +45,15 @@ default_keypoint_names = ['Nose', 'Left Ear', 'Right Ear', 'Neck', 'Left Hip', '
 # ---------------------------------------------------------------------------
 def convert_pxs_to_mm(coords: np.ndarray, resolution=(512, 424), field_of_view=(70.6, 60),
                       true_depth: float = 673.1) -> np.ndarray:
-    """Pixel -> mm (Kinect intrinsics from the field of view), M/proc/util.py:29-60."""
-    cx = resolution[0] // 2
-    cy = resolution[1] // 2
-    xhat = coords[:, 0] - cx
-    yhat = coords[:, 1] - cy
-    f_w = resolution[0] / (2 * np.deg2rad(field_of_view[0] / 2))
-    f_h = resolution[1] / (2 * np.deg2rad(field_of_view[1] / 2))
-    new_coords = np.zeros_like(coords)
-    new_coords[:, 0] = true_depth * xhat / f_w
-    new_coords[:, 1] = true_depth * yhat / f_h
-    return new_coords
+    """Pixel -> mm on the floor plane at `true_depth`: a pinhole camera whose
+    focal lengths follow from the Kinect field of view (M/proc/util.py:29-60).
+    Element-wise: mm = true_depth * (px - centre) / focal."""
+    centre = (resolution[0] // 2, resolution[1] // 2)
+    focal = [resolution[a] / (2 * np.deg2rad(field_of_view[a] / 2)) for a in (0, 1)]
+    out = np.zeros_like(coords)
+    for a in (0, 1):
+        out[:, a] = true_depth * (coords[:, a] - centre[a]) / focal[a]
+    return out
 
 
 def clamp_angles_deg(angles: np.ndarray) -> np.ndarray:
@@ -66,91 +64,70 @@ def clamp_angles_rad(angles: np.ndarray) -> np.ndarray:
     return np.where(angles < 0, (2 * np.pi) + angles, angles) % (2 * np.pi)
 
 
+def _wrap180(d: np.ndarray) -> np.ndarray:
+    """Degrees in [0, 360) -> (-180, 180]."""
+    return np.where(d > 180, d - 360, d)
+
+
 def angle_difference(angles1: np.ndarray, angles2: np.ndarray) -> np.ndarray:
     """Signed smaller difference angles2 - angles1 in degrees (M/proc/kalman.py:93-98)."""
-    diff = (angles2 - angles1) % 360
-    to_min = diff > 180
-    diff[to_min] = -(360 - diff[to_min])
-    return diff
+    return _wrap180((angles2 - angles1) % 360)
 
 
 # ---------------------------------------------------------------------------
 # keypoint geometry
 # ---------------------------------------------------------------------------
-def rotate_points(points: np.ndarray, center=(0, 0), angle: float = 0) -> np.ndarray:
-    """Rotate (K, 2|3) points about `center` by -angle degrees; column 2 (if
-    present) is carried as a weight (M/proc/keypoints.py:11-39)."""
-    if points.shape[1] == 3:
-        weights = points[:, 2]
-        points = points[:, :2]
-    elif points.shape[1] == 2:
-        weights = None
-    else:
-        raise ValueError(f'Expected axis 1 of `points` to have length 2 or 3, but got {points.shape[1]}')
-    a = np.deg2rad(-angle)
-    R = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]])
-    o = np.atleast_2d(center)
-    p = np.atleast_2d(points)
-    rotated = np.squeeze((R @ (p.T - o.T) + o.T).T)
-    if weights is not None:
-        rotated = np.append(rotated, weights[..., None], 1)
-    return rotated
-
-
 def rotate_points_batch(points: np.ndarray, centers: np.ndarray, angles: Union[np.ndarray, float]) -> np.ndarray:
-    """Per-frame rotate_points, in place on `points` (M/proc/keypoints.py:42-64).
-    Vectorised over frames: x' = c (x - ox) - s (y - oy) + ox,
-    y' = s (x - ox) + c (y - oy) + oy with c, s of deg2rad(-angle)."""
+    """Rotate every frame's points by -angle degrees about its centre, in
+    place on columns 0-1 of `points` (M/proc/keypoints.py:42-64):
+    x' = c (x - ox) - s (y - oy) + ox, y' = s (x - ox) + c (y - oy) + oy,
+    (c, s) = (cos, sin) of deg2rad(-angle)."""
     if isinstance(angles, (int, float)):
-        angles_array = np.array([angles] * points.shape[0])
-    elif isinstance(angles, np.ndarray):
-        angles_array = np.array(angles)
-    else:
+        angles = np.full(points.shape[0], float(angles))
+    elif not isinstance(angles, np.ndarray):
         raise TypeError(f'Expected angles to be of type numpy.ndarray or float, got {type(angles).__name__} instead!')
     if points.shape[-1] not in (2, 3):
         raise ValueError(f'Expected axis 2 of `points` to have length 2 or 3, but got {points.shape[-1]}')
-    a = np.deg2rad(-angles_array.astype(np.float64))
-    c, s = np.cos(a)[:, None], np.sin(a)[:, None]
+    theta = np.deg2rad(-np.asarray(angles, np.float64))
+    c, s = np.cos(theta)[:, None], np.sin(theta)[:, None]
     ox, oy = centers[:, 0:1], centers[:, 1:2]
     dx, dy = points[..., 0] - ox, points[..., 1] - oy
-    x = c * dx + (-s) * dy + ox
-    y = s * dx + c * dy + oy
-    points[..., 0] = x
-    points[..., 1] = y
+    points[..., 0], points[..., 1] = c * dx + (-s) * dy + ox, s * dx + c * dy + oy
     return points
+
+
+def rotate_points(points: np.ndarray, center=(0, 0), angle: float = 0) -> np.ndarray:
+    """One frame of rotate_points_batch on (K, 2|3) points (column 2 carried
+    through) (M/proc/keypoints.py:11-39)."""
+    if points.shape[1] not in (2, 3):
+        raise ValueError(f'Expected axis 1 of `points` to have length 2 or 3, but got {points.shape[1]}')
+    out = rotate_points_batch(np.array(points, np.float64)[None], np.asarray(center, np.float64).reshape(1, 2),
+                              np.array([float(angle)]))[0]
+    return np.squeeze(out)
 
 
 def flips_from_keypoints(keypoints: np.ndarray, centroids: np.ndarray, angles: np.ndarray,
                          length: Union[float, np.ndarray] = 80) -> Tuple[np.ndarray, np.ndarray]:
-    """Front (0-3) vs rear (4-6) keypoints vote on which end of the rotated
-    body they sit; returns (flips bool, confidence) (M/proc/proc.py:851-889)."""
-    front_keypoints = [0, 1, 2, 3]
-    rear_keypoints = [4, 5, 6]
-    rotated_keypoints = rotate_points_batch(np.copy(keypoints), centroids, angles)
-    extent_x_min = centroids[:, 0] - (length / 2)
-    extent_x_max = centroids[:, 0] + (length / 2)
-    left_dist = np.abs(extent_x_min[:, np.newaxis] - rotated_keypoints[:, :, 0])
-    right_dist = np.abs(extent_x_max[:, np.newaxis] - rotated_keypoints[:, :, 0])
-    rot_keypoint_scores = np.where(left_dist < right_dist, -1, 1)
-    front_votes = np.mean(rot_keypoint_scores[:, front_keypoints], axis=1)
-    rear_votes = np.mean(rot_keypoint_scores[:, rear_keypoints], axis=1)
-    flips = np.where(front_votes < rear_votes, True, False)
-    expected = np.where(flips[:, None], np.array([-1, 1]), np.array([1, -1]))
-    agree = np.count_nonzero(rot_keypoint_scores[:, front_keypoints] == expected[:, 0, None], axis=1) \
-        + np.count_nonzero(rot_keypoint_scores[:, rear_keypoints] == expected[:, 1, None], axis=1)
-    conf_scores = agree / (len(front_keypoints) + len(rear_keypoints))
-    return flips, conf_scores
+    """Head/tail vote of the keypoints along the body axis (M/proc/proc.py:
+    851-889): (flips bool (n,), confidence (n,)).  Runs in libmdx
+    (mdx_flips_from_keypoints, host code)."""
+    kp = np.ascontiguousarray(keypoints, np.float64)
+    n, K = kp.shape[0], kp.shape[1]
+    cen = np.ascontiguousarray(centroids, np.float64)
+    ang = np.ascontiguousarray(np.broadcast_to(np.asarray(angles, np.float64), (n,)))
+    ln = np.ascontiguousarray(np.broadcast_to(np.asarray(length, np.float64), (n,)))
+    flips = np.empty(n, np.uint8)
+    conf = np.empty(n, np.float64)
+    call("mdx_flips_from_keypoints", _np(kp), n, K, _np(cen), _np(ang), _np(ln), _np(flips), _np(conf))
+    return flips.astype(bool), conf
 
 
 def estimate_keypoint_rotation(keypoints: np.ndarray) -> np.ndarray:
-    """Median per-frame rotation of the keypoints between frames (M/proc/proc.py:892-907)."""
-    angles = np.arctan2(keypoints[..., 1], keypoints[..., 0])
-    angles = clamp_angles_deg(np.rad2deg(angles))
-    angles = np.diff(angles, axis=0, prepend=angles[0, None, ...])
-    angles = angles % 360
-    to_min = angles > 180
-    angles[to_min] = -(360 - angles[to_min])
-    return np.median(angles, axis=1)
+    """Per-frame median of the keypoints' polar-angle change since the
+    previous frame, wrapped to (-180, 180] (M/proc/proc.py:892-907)."""
+    theta = clamp_angles_deg(np.rad2deg(np.arctan2(keypoints[..., 1], keypoints[..., 0])))
+    step = np.diff(theta, axis=0, prepend=theta[:1])
+    return np.median(_wrap180(step % 360), axis=1)
 
 
 def get_expected_keypoint_alignment() -> np.ndarray:
@@ -167,17 +144,14 @@ def get_expected_keypoint_alignment() -> np.ndarray:
 
 
 def compute_keypoint_alignment_scores(keypoints: np.ndarray, expected_alignment: Optional[np.ndarray] = None):
-    """Share of keypoint pairs whose x-order matches the expectation (M/proc/proc.py:936-957)."""
-    if expected_alignment is None:
-        expected_alignment = get_expected_keypoint_alignment()
-    # pairwise x differences (calc_keypoint_keypoint_distance, metric 'x', :910-933)
-    distances = keypoints[..., :, None, 0] - keypoints[..., None, :, 0]
-    distance_signs = np.sign(distances)
-    masked_distance_signs = np.where(expected_alignment == 0, 0, distance_signs)
-    axis = (1, 2) if len(keypoints.shape) == 3 else None
-    num_expectations_met = np.count_nonzero(masked_distance_signs == expected_alignment, axis=axis) \
-        - np.count_nonzero(expected_alignment == 0)
-    return num_expectations_met / np.count_nonzero(expected_alignment)
+    """Fraction of the constrained keypoint pairs (non-zero entries of the
+    expectation) whose x order -- sign of x_i - x_j -- matches it
+    (M/proc/proc.py:910-957)."""
+    exp = get_expected_keypoint_alignment() if expected_alignment is None else expected_alignment
+    sign = np.sign(keypoints[..., :, None, 0] - keypoints[..., None, :, 0])
+    met = (sign == exp) & (exp != 0)
+    count = met.sum(axis=(-2, -1)) if keypoints.ndim == 3 else met.sum()
+    return count / np.count_nonzero(exp)
 
 
 # ---------------------------------------------------------------------------
@@ -242,65 +216,53 @@ def move_median(a: np.ndarray, window: int, min_count: Optional[int] = None, axi
 
 
 def filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60) -> np.ndarray:
-    """Undo ~180 degree jumps against a moving median (M/proc/proc.py:600-624)."""
-    out = np.copy(angles)
-    window = min(window, out.shape[0])
-    windows = move_median(angles, window=window, min_count=1)
-    diff = out - windows
-    absdiff = np.abs(diff)
-    flips = ((absdiff > (180 - tolerance)) & (absdiff < (180 + tolerance)))
-    signs = np.sign(diff[flips])
-    out[flips] = out[flips] + (-180 * signs)
+    """One pass of the 180-degree jump filter (M/proc/proc.py:600-624): an
+    angle within `tolerance` of 180 degrees away from its trailing moving
+    median is moved back by 180 towards it."""
+    out = np.array(angles, copy=True)
+    dev = out - move_median(angles, window=min(window, out.shape[0]), min_count=1)
+    jump = (np.abs(dev) > 180 - tolerance) & (np.abs(dev) < 180 + tolerance)
+    out[jump] -= 180 * np.sign(dev[jump])
     return out
 
 
 def iterative_filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60,
                             max_iters: int = 1000) -> Tuple[np.ndarray, np.ndarray]:
-    """filter_angles until it stops changing (M/proc/proc.py:627-654).  Runs
-    in libmdx (mdx_iterative_filter_angles, host code, bit-identical to
-    iterative_filter_angles_numpy) without holding the GIL: the reference
-    loops up to 1000 times whenever an angle is NaN."""
+    """filter_angles repeated until it stops changing (M/proc/proc.py:627-654);
+    returns (angles, flips).  Runs in libmdx (mdx_iterative_filter_angles, host
+    code) without holding the GIL: the reference loops up to 1000 times
+    whenever an angle is NaN."""
     a = np.ascontiguousarray(angles, dtype=np.float64)
-    if a.ndim != 1 or window > 8:
-        return iterative_filter_angles_numpy(angles, window, tolerance, max_iters)
+    if a.ndim != 1 or not 1 <= window <= 8:
+        raise NotImplementedError("iterative_filter_angles: 1-D angles and window <= 8")
     out = np.empty_like(a)
     flips = np.empty(a.shape, dtype=np.uint8)
-    call("mdx_iterative_filter_angles", a.ctypes.data_as(ctypes.c_void_p), a.shape[0], int(window), float(tolerance),
-         int(max_iters), out.ctypes.data_as(ctypes.c_void_p), flips.ctypes.data_as(ctypes.c_void_p))
+    call("mdx_iterative_filter_angles", _np(a), a.shape[0], int(window), float(tolerance), int(max_iters), _np(out),
+         _np(flips))
     return out, flips.astype(bool)
-
-
-def iterative_filter_angles_numpy(angles: np.ndarray, window: int = 3, tolerance: float = 60,
-                                  max_iters: int = 1000) -> Tuple[np.ndarray, np.ndarray]:
-    """The same loop in numpy (the reference's formulation)."""
-    last = np.copy(angles)
-    iterations = 0
-    while True:
-        if iterations > max_iters:
-            break
-        iterations += 1
-        curr = filter_angles(last, window=window, tolerance=tolerance)
-        if np.allclose(curr, last):
-            break
-        last = curr
-    flips = np.isclose(np.abs(curr - angles), 180)
-    return curr, flips
 
 
 def finalize_angles(orientation: np.ndarray, axis_length: np.ndarray, centroid: np.ndarray,
                     keypoints: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
     """The no-tracking branch of instances_to_features (M/proc/proc.py:720-724,
-    827-839): orientation (rad) -> degrees in [0, 360), keypoint flips,
-    iterative 180-degree filtering.  keypoints (n, K, 3) of instance 0.
-    Returns (angles deg, flips bool)."""
-    lengths = np.max(axis_length, axis=1)
-    angles = -np.rad2deg(orientation)
-    angles = clamp_angles_deg(angles)
-    flips, _ = flips_from_keypoints(keypoints, centroid, angles, lengths)
-    angles[flips] += 180
-    angles, filter_flips = iterative_filter_angles(angles)
-    flips = np.logical_xor(flips, filter_flips)
-    return angles, flips
+    827-839) in one libmdx host call (mdx_finalize_angles): orientation (rad)
+    -> degrees in [0, 360), keypoint flips (+180), iterative 180-degree
+    filtering.  keypoints (n, K, 3) of instance 0.  Returns (angles deg,
+    flips bool)."""
+    o = np.ascontiguousarray(orientation, np.float64)
+    n = o.shape[0]
+    ax = np.ascontiguousarray(axis_length, np.float64)
+    cen = np.ascontiguousarray(centroid, np.float64)
+    kp = np.ascontiguousarray(keypoints, np.float64)
+    ang = np.empty(n, np.float64)
+    flips = np.empty(n, np.uint8)
+    call("mdx_finalize_angles", _np(o), _np(ax), _np(cen), _np(kp), n, kp.shape[1] if kp.ndim == 3 else 8,
+         _np(ang), _np(flips))
+    return ang, flips.astype(bool)
+
+
+def _np(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
 
 
 # ---------------------------------------------------------------------------
@@ -380,102 +342,74 @@ def frame_scalars(frames, masks=None, min_height: float = 10, max_height: float 
 
 def compute_scalars(frames, track_features: dict, min_height: float = 10, max_height: float = 100,
                     true_depth: float = 673.1, reductions=None) -> Dict[str, np.ndarray]:
-    """Per-frame scalars (M/proc/scalars.py:36-120).  `frames` is the uint8
-    chunk already multiplied by the masks (or pass reductions=(area_px,
-    height_ave) from frame_scalars, computed on the device, and frames=None /
-    any object with shape[0] == nframes).  Dtypes follow the reference."""
-    centroid = np.asarray(track_features['centroid'])
-    nframes = centroid.shape[0]
+    """Per-frame scalars of the h5 schema (M/proc/scalars.py:36-120).
+    The frame reductions (pixels with min_height < v < max_height in
+    frames * masks, and their mean height) come from the device
+    (reductions=(area_px, height_ave) of frame_scalars; `frames` may then be
+    None); everything else is derived from the tracked centroid / axes /
+    orientation.  Dtypes are the reference's: float64 except height_ave_mm
+    (float32) and area_px (int64)."""
+    cen = np.asarray(track_features['centroid'])
+    axes = np.asarray(track_features['axis_length'])
     if reductions is None:
         area, hmean, _ = frame_scalars(frames, None, min_height, max_height)
         reductions = (area.cpu().numpy(), hmean.cpu().numpy())
-    area_px, height_mean = (np.asarray(r) for r in reductions)
-    features = {
-        'centroid_x_px': np.zeros((nframes,), 'float32'),
-        'centroid_y_px': np.zeros((nframes,), 'float32'),
-        'velocity_2d_px': np.zeros((nframes,), 'float32'),
-        'velocity_3d_px': np.zeros((nframes,), 'float32'),
-        'width_px': np.zeros((nframes,), 'float32'),
-        'length_px': np.zeros((nframes,), 'float32'),
-        'area_px': np.zeros((nframes,)),
-        'centroid_x_mm': np.zeros((nframes,), 'float32'),
-        'centroid_y_mm': np.zeros((nframes,), 'float32'),
-        'velocity_2d_mm': np.zeros((nframes,), 'float32'),
-        'velocity_3d_mm': np.zeros((nframes,), 'float32'),
-        'width_mm': np.zeros((nframes,), 'float32'),
-        'length_mm': np.zeros((nframes,), 'float32'),
-        'area_mm': np.zeros((nframes,)),
-        'height_ave_mm': np.zeros((nframes,), 'float32'),
-        'angle': np.zeros((nframes,), 'float32'),
-        'velocity_theta': np.zeros((nframes,)),
+    area_px, hmean = (np.asarray(r) for r in reductions)
+    cen_mm = convert_pxs_to_mm(cen, true_depth=true_depth)
+    mm_per_px = np.abs(convert_pxs_to_mm(cen + 1, true_depth=true_depth) - cen_mm)  # at the centroid
+    width, length = np.min(axes, axis=1), np.max(axes, axis=1)
+    area = area_px.astype(np.int64)
+    height = np.where(area > 0, hmean, 0).astype(np.float32)
+
+    def step(x):  # frame-to-frame change, 0 at the first frame
+        return np.diff(x, prepend=x[:1])
+
+    dz2 = np.square(step(height))  # float32, as the reference squares it
+    vx, vy = step(cen[:, 0]), step(cen[:, 1])
+    vx_mm, vy_mm = step(cen_mm[:, 0]), step(cen_mm[:, 1])
+    vals = {
+        'centroid_x_px': cen[:, 0], 'centroid_y_px': cen[:, 1],
+        'velocity_2d_px': np.hypot(vx, vy), 'velocity_3d_px': np.sqrt(np.square(vx) + np.square(vy) + dz2),
+        'width_px': width, 'length_px': length, 'area_px': area,
+        'centroid_x_mm': cen_mm[:, 0], 'centroid_y_mm': cen_mm[:, 1],
+        'velocity_2d_mm': np.hypot(vx_mm, vy_mm),
+        'velocity_3d_mm': np.sqrt(np.square(vx_mm) + np.square(vy_mm) + dz2),
+        'width_mm': width * mm_per_px[:, 1], 'length_mm': length * mm_per_px[:, 0],
+        'area_mm': area * mm_per_px.mean(axis=1), 'height_ave_mm': height,
+        'angle': np.deg2rad(track_features['orientation']), 'velocity_theta': np.arctan2(vy_mm, vx_mm),
     }
-    centroid_mm = convert_pxs_to_mm(centroid, true_depth=true_depth)
-    centroid_mm_shift = convert_pxs_to_mm(centroid + 1, true_depth=true_depth)
-    px_to_mm = np.abs(centroid_mm_shift - centroid_mm)
-    features['centroid_x_px'] = centroid[:, 0]
-    features['centroid_y_px'] = centroid[:, 1]
-    features['centroid_x_mm'] = centroid_mm[:, 0]
-    features['centroid_y_mm'] = centroid_mm[:, 1]
-    features['width_px'] = np.min(track_features['axis_length'], axis=1)
-    features['length_px'] = np.max(track_features['axis_length'], axis=1)
-    features['area_px'] = area_px.astype(np.int64)
-    features['width_mm'] = features['width_px'] * px_to_mm[:, 1]
-    features['length_mm'] = features['length_px'] * px_to_mm[:, 0]
-    features['area_mm'] = features['area_px'] * px_to_mm.mean(axis=1)
-    features['angle'] = np.deg2rad(track_features['orientation'])
-    nz = area_px > 0
-    features['height_ave_mm'][nz] = height_mean[nz]
-    vel_x = np.diff(np.concatenate((features['centroid_x_px'][:1], features['centroid_x_px'])))
-    vel_y = np.diff(np.concatenate((features['centroid_y_px'][:1], features['centroid_y_px'])))
-    vel_z = np.diff(np.concatenate((features['height_ave_mm'][:1], features['height_ave_mm'])))
-    features['velocity_2d_px'] = np.hypot(vel_x, vel_y)
-    features['velocity_3d_px'] = np.sqrt(np.square(vel_x) + np.square(vel_y) + np.square(vel_z))
-    vel_x = np.diff(np.concatenate((features['centroid_x_mm'][:1], features['centroid_x_mm'])))
-    vel_y = np.diff(np.concatenate((features['centroid_y_mm'][:1], features['centroid_y_mm'])))
-    features['velocity_2d_mm'] = np.hypot(vel_x, vel_y)
-    features['velocity_3d_mm'] = np.sqrt(np.square(vel_x) + np.square(vel_y) + np.square(vel_z))
-    features['velocity_theta'] = np.arctan2(vel_y, vel_x)
-    return features
+    return {k: vals[k] for k in scalar_attributes()}
 
 
 def keypoints_to_dict(keypoints: np.ndarray, frames, centers: np.ndarray, angles: np.ndarray,
                       true_depth: float = 673.1, keypoint_names: Optional[List[str]] = None,
                       z_data: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
-    """Keypoints in reference/rotated coordinates, px and mm, plus the z of
-    each keypoint read from `frames` (M/proc/keypoints.py:93-165).  Pass
-    z_data from frame_scalars (device lookup) to skip the frame gather."""
-    if keypoint_names is None:
-        keypoint_names = default_keypoint_names
-    old_error_settings = np.seterr(invalid='ignore')
-    try:
+    """The keypoint tables of the h5 schema (M/proc/keypoints.py:93-165):
+    every keypoint in the camera ('reference') frame and in the animal's
+    ('rotated': about the centroid by -angle, centroid at the origin) frame,
+    in px and mm, with its score and the depth under it (z, read from
+    `frames` on the device, or given as z_data)."""
+    n, K = keypoints.shape[0], keypoints.shape[1]
+    with np.errstate(invalid="ignore"):
         if z_data is None:  # device lookup (mdx_frame_scalars)
             _, _, z = frame_scalars(frames, None, 0, 0, keypoints=keypoints, z_frames=frames)
             z_data = z.cpu().numpy()
-        ref_kpts_px = np.copy(keypoints)
-        ref_kpts_mm = np.zeros_like(keypoints)
-        ref_kpts_mm[:, :, 2] = keypoints[:, :, 2]
-        for kpi in range(keypoints.shape[1]):
-            ref_kpts_mm[:, kpi, :2] = convert_pxs_to_mm(keypoints[:, kpi, :2], true_depth=true_depth)
-        rot_kpts_px = rotate_points_batch(np.copy(keypoints[:, :, :]), centers=centers, angles=angles)
-        rot_kpts_px[:, :, :2] -= np.expand_dims(centers, axis=1)
-        centroid_mm = convert_pxs_to_mm(centers, true_depth=true_depth)
-        rot_kpts_mm = rotate_points_batch(np.copy(ref_kpts_mm), centers=centroid_mm, angles=angles)
-        rot_kpts_mm[:, :, :2] -= np.expand_dims(centroid_mm, axis=1)
-        out = {}
-        # the reference iterates default_keypoint_names here whatever names it was given
-        for kpi, kpn in enumerate(default_keypoint_names):
-            out[f'reference/{kpn}_x_px'] = ref_kpts_px[:, kpi, 0]
-            out[f'reference/{kpn}_y_px'] = ref_kpts_px[:, kpi, 1]
-            out[f'reference/{kpn}_score'] = ref_kpts_px[:, kpi, 2]
-            out[f'reference/{kpn}_x_mm'] = ref_kpts_mm[:, kpi, 0]
-            out[f'reference/{kpn}_y_mm'] = ref_kpts_mm[:, kpi, 1]
-            out[f'reference/{kpn}_z_mm'] = z_data[:, kpi]
-            out[f'rotated/{kpn}_x_px'] = rot_kpts_px[:, kpi, 0]
-            out[f'rotated/{kpn}_y_px'] = rot_kpts_px[:, kpi, 1]
-            out[f'rotated/{kpn}_score'] = rot_kpts_px[:, kpi, 2]
-            out[f'rotated/{kpn}_x_mm'] = rot_kpts_mm[:, kpi, 0]
-            out[f'rotated/{kpn}_y_mm'] = rot_kpts_mm[:, kpi, 1]
-            out[f'rotated/{kpn}_z_mm'] = z_data[:, kpi]
-    finally:
-        np.seterr(**old_error_settings)
+        ref_px = np.copy(keypoints)
+        ref_mm = np.zeros_like(keypoints)
+        ref_mm[..., 2] = keypoints[..., 2]
+        ref_mm[..., :2] = convert_pxs_to_mm(keypoints[..., :2].reshape(n * K, 2),
+                                            true_depth=true_depth).reshape(n, K, 2)
+        cen_mm = convert_pxs_to_mm(centers, true_depth=true_depth)
+        rot_px = rotate_points_batch(np.copy(keypoints), centers=centers, angles=angles)
+        rot_px[..., :2] -= centers[:, None, :]
+        rot_mm = rotate_points_batch(np.copy(ref_mm), centers=cen_mm, angles=angles)
+        rot_mm[..., :2] -= cen_mm[:, None, :]
+    frames_by_system = (("reference", ref_px, ref_mm), ("rotated", rot_px, rot_mm))
+    out = {}
+    # the reference names the columns by default_keypoint_names whatever names it is given
+    for k, name in enumerate(default_keypoint_names):
+        for system, px, mm in frames_by_system:
+            out.update({f'{system}/{name}_x_px': px[:, k, 0], f'{system}/{name}_y_px': px[:, k, 1],
+                        f'{system}/{name}_score': px[:, k, 2], f'{system}/{name}_x_mm': mm[:, k, 0],
+                        f'{system}/{name}_y_mm': mm[:, k, 1], f'{system}/{name}_z_mm': z_data[:, k]})
     return out

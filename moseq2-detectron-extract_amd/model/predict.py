@@ -1,7 +1,8 @@
 """Predictor -- drop-in for the reference's DefaultPredictor-shaped wrapper
 (M/model/predict.py:12-102), backed by the MI355X-native runtime.
 
-Same constructors (``from_config``; ``from_torchscript`` raises, see below),
+Same constructors (``from_config``; ``from_torchscript`` reads an exported
+archive weights-only, see model/torchscript.py),
 same ``device`` property and the same call contract: uint8 ``(H,W,C)`` or
 ``(N,H,W,C)`` (numpy or torch) -> ``{'instances': Instances}`` or a list of
 them, with Detectron2's field names.
@@ -47,10 +48,22 @@ class Predictor:
         return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype))
 
     @classmethod
-    def from_torchscript(cls, path):
-        raise NotImplementedError(
-            "TorchScript models embed their own Detectron2 graph and cannot run on the native kernels; export the "
-            "checkpoint (model_final.pth + config.yaml) and use Predictor.from_config")
+    def from_torchscript(cls, path: str, cfg: Optional[ModelConfig] = None, dtype: str = "fp16", device="cuda",
+                         **overrides) -> "Predictor":
+        """An exported ``model.ts`` (M/model/predict.py:46-51, export
+        M/model/deploy.py:77-121): its parameters, buffers and thresholds are
+        read weights-only from the archive (model/torchscript.py; no
+        TorchScript is executed) and run on the native kernels.  The
+        architecture is inferred from the state dict unless `cfg` is given;
+        `overrides` set ModelConfig fields (e.g. score_thresh_test)."""
+        from .torchscript import infer_config, load_torchscript
+        sd, scalars = load_torchscript(path)
+        if cfg is None:
+            cfg = infer_config(sd, scalars, **overrides)
+        else:
+            for k, v in overrides.items():
+                setattr(cfg, k, v)
+        return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype), is_torchscript=True)
 
     def run(self, frames_u8: torch.Tensor, lut: Optional[np.ndarray] = None) -> dict:
         """Batched device-resident call: uint8 (B,h,w) GPU tensor -> dict of

@@ -310,9 +310,11 @@ def get_frame_features(frames, frame_threshold=10, mask=np.array([]), mask_thres
 # ---------------------------------------------------------------------------
 # crop and rotate
 # ---------------------------------------------------------------------------
-def crop_and_rotate_frames(frames, centers, angles, crop_size=(80, 80), frames2=None):
+def crop_and_rotate_frames(frames, centers, angles, crop_size=(80, 80), frames2=None, return_window=False):
     """Batched crop_and_rotate_frame for every frame (and frames2 with the same
-    centres/angles, e.g. the d2 masks).  Returns uint8 (n, crop_h, crop_w)."""
+    centres/angles, e.g. the d2 masks).  Returns uint8 (n, crop_h, crop_w)
+    (a tuple with frames2's crops; with return_window, also the int32 (n, 4)
+    crop windows (xmin, xmax, ymin, ymax), -1 where the crop is zeros)."""
     torch = _torch()
     as_np = _is_np(frames)
     src0 = _to_dev(frames, torch.uint8)
@@ -325,11 +327,12 @@ def crop_and_rotate_frames(frames, centers, angles, crop_size=(80, 80), frames2=
     cw, ch = int(crop_size[0]), int(crop_size[1])
     o0 = torch.empty((n, ch, cw), dtype=torch.uint8, device=src0.device)
     o1 = None if src1 is None else torch.empty_like(o0)
+    win = torch.empty((n, 4), dtype=torch.int32, device=src0.device) if return_window else None
     call("mdx_crop_rotate", _ptr(src0), _ptr(src1), n, H, W, _ptr(c), _ptr(a), cw, ch, _ptr(o0), _ptr(o1),
-         _stream())
-    if src1 is None:
-        return _ret(o0, as_np)
-    return _ret(o0, as_np), _ret(o1, as_np)
+         _ptr(win), _stream())
+    out = (_ret(o0, as_np),) + (() if src1 is None else (_ret(o1, as_np),)) + \
+        (() if win is None else (_ret(win, as_np),))
+    return out[0] if len(out) == 1 else out
 
 
 def crop_and_rotate_frame(frame, center, angle, crop_size=(80, 80)):

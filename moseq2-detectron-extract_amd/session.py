@@ -6,7 +6,7 @@ chunks and streamed to HBM.
 this module                    reference (M/ = moseq2_detectron_extract/)
 =============================  =============================================
 get_raw_info                   M/io/video.py:28-56
-collapse_consecutive_values    M/io/video.py:130-148
+frame_runs                     M/io/video.py:130-148 (collapse_consecutive_values)
 read_frames_raw                M/io/video.py:67-127
 gen_batch_sequence             M/io/util.py:24-35 (shard.gen_batch_sequence)
 RawDepthSource.iterate         Session.iterate / SessionFramesIterator
@@ -25,9 +25,7 @@ import os
 import queue
 import tarfile
 import threading
-from itertools import groupby
-from operator import itemgetter
-from typing import Callable, Iterable, List, Optional, Sequence, Tuple, Union
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -35,61 +33,66 @@ from .shard import gen_batch_sequence
 
 
 def get_raw_info(filename: Union[str, tarfile.TarInfo], bit_depth: int = 16, frame_dims: Tuple[int, int] = (512, 424)):
-    """bytes / nframes / dims / bytes_per_frame of a raw depth file (M/io/video.py:28-56)."""
-    bytes_per_frame = int((frame_dims[0] * frame_dims[1] * bit_depth) / 8)
-    size = os.stat(filename).st_size if isinstance(filename, str) else filename.size
-    return {"bytes": size, "nframes": int(size / bytes_per_frame), "dims": frame_dims,
-            "bytes_per_frame": bytes_per_frame}
+    """Size and frame count of a headerless raw depth file or tar member
+    (M/io/video.py:28-56): {bytes, nframes, dims, bytes_per_frame}."""
+    frame_bytes = frame_dims[0] * frame_dims[1] * bit_depth // 8
+    total = filename.size if isinstance(filename, tarfile.TarInfo) else os.path.getsize(filename)
+    return {"bytes": total, "nframes": total // frame_bytes, "dims": frame_dims, "bytes_per_frame": frame_bytes}
 
 
-def collapse_consecutive_values(values: Iterable) -> List[Tuple[int, int]]:
-    """[0,1,2,10,11] -> [(0, 3), (10, 2)] (M/io/video.py:130-148)."""
-    out = []
-    for _, group in groupby(enumerate(values), lambda ix: ix[0] - ix[1]):
-        g = list(map(itemgetter(1), group))
-        out.append((g[0], len(g)))
-    return out
+def frame_runs(frame_idxs: np.ndarray) -> List[Tuple[int, int, np.ndarray]]:
+    """Runs of consecutive frame numbers in the sorted request: (first frame,
+    length, positions in the request that receive the run's frames).  One
+    file read serves a run (the reference's collapse_consecutive_values,
+    M/io/video.py:130-148, plus the read-back positions in O(n log n))."""
+    idx = np.asarray(frame_idxs, np.int64).ravel()
+    if idx.size == 0:
+        return []
+    order = np.argsort(idx, kind="stable")
+    srt = idx[order]
+    cuts = np.flatnonzero(np.diff(srt) != 1) + 1
+    return [(int(srt[p[0]]), len(p), order[p]) for p in np.split(np.arange(srt.size), cuts)]
 
 
 def read_frames_raw(filename: Union[str, tarfile.TarInfo], frames=None, frame_dims: Tuple[int, int] = (512, 424),
                     bit_depth: int = 16, dtype="<i2", tar_object: Optional[tarfile.TarFile] = None,
                     out: Optional[np.ndarray] = None) -> np.ndarray:
-    """Frames (n, H, W) from a raw file, in the order of `frames` (None or []
-    = all), reading each run of consecutive indices with one seek + read
-    (M/io/video.py:67-127).  `out` (e.g. a pinned buffer view) receives the
-    frames when given."""
+    """Frames (n, H, W) of a raw depth file (or a member of `tar_object`) in
+    the order of `frames` (an index, a sequence, or None / [] for every
+    frame), one seek + read per run of consecutive frames (M/io/video.py:
+    67-127).  `out` (e.g. a pinned host buffer view) receives them when
+    given."""
     info = get_raw_info(filename, frame_dims=frame_dims, bit_depth=bit_depth)
-    if isinstance(frames, (int, np.integer)):
-        frames = [int(frames)]
-    elif frames is not None:
-        frames = [int(i) for i in frames]
-    if frames is None or len(frames) == 0:
-        frames = list(range(0, info["nframes"]))
-    blocks = []
-    for start, nfr in collapse_consecutive_values(sorted(frames)):
-        blocks.append({"seek_point": int(np.maximum(0, start * info["bytes_per_frame"])),
-                       "read_bytes": int(nfr * info["bytes_per_frame"]),
-                       "read_points": int(nfr * frame_dims[0] * frame_dims[1]),
-                       "dims": (nfr, frame_dims[1], frame_dims[0]),
-                       "idxs": [frames.index(start + i) for i in range(nfr)]})
+    if frames is None or (not np.isscalar(frames) and len(frames) == 0):
+        want = np.arange(info["nframes"], dtype=np.int64)
+    else:
+        want = np.atleast_1d(np.asarray(frames, np.int64))
+    W, H = frame_dims
+    dt = np.dtype(dtype)
     if out is None:
-        out = np.empty((len(frames), frame_dims[1], frame_dims[0]), dtype=np.dtype(dtype))
+        out = np.empty((want.size, H, W), dtype=dt)
+    runs = frame_runs(want)
     if isinstance(tar_object, tarfile.TarFile):
         fh = tar_object.extractfile(filename)
         if fh is None:
             raise FileNotFoundError(f"Could not open tar member: {getattr(filename, 'name', filename)}")
-        for blk in blocks:
-            fh.seek(blk["seek_point"])
-            out[blk["idxs"], ...] = np.frombuffer(fh.read(blk["read_bytes"]), dtype=np.dtype(dtype)).reshape(blk["dims"])
-        fh.close()
+
+        def fetch(first, count):
+            fh.seek(first * info["bytes_per_frame"])
+            return np.frombuffer(fh.read(count * info["bytes_per_frame"]), dtype=dt)
     elif isinstance(filename, str):
-        with open(filename, "rb") as fh:
-            for blk in blocks:
-                fh.seek(blk["seek_point"])
-                chunk = np.fromfile(file=fh, dtype=np.dtype(dtype), count=blk["read_points"]).reshape(blk["dims"])
-                out[blk["idxs"], ...] = chunk
+        fh = open(filename, "rb")
+
+        def fetch(first, count):
+            fh.seek(first * info["bytes_per_frame"])
+            return np.fromfile(fh, dtype=dt, count=count * H * W)
     else:
         raise ValueError("Could not read!")
+    try:
+        for first, count, dest in runs:
+            out[dest] = fetch(max(first, 0), count).reshape(count, H, W)
+    finally:
+        fh.close()
     return out
 
 

@@ -108,9 +108,11 @@ def test_attribute_tables(F):
 
 
 def test_iterative_filter_angles_native_matches_numpy(F):
-    """libmdx's host loop (mdx_iterative_filter_angles) vs the numpy
-    formulation, bit for bit: NaN (1000-iteration runs), constant series,
-    max_iters cut-offs, windows 1..5, empty and 1-element series."""
+    """libmdx's host loop (mdx_iterative_filter_angles) vs the numpy checker
+    (oracle/features_ref.py), bit for bit: NaN (1000-iteration runs),
+    constant series, max_iters cut-offs, windows 1..5, empty and 1-element
+    series."""
+    from oracle import features_ref as FR
     rng = np.random.default_rng(4)
     for trial in range(120):
         n = int(rng.integers(0, 200))
@@ -122,8 +124,28 @@ def test_iterative_filter_angles_native_matches_numpy(F):
         if trial % 7 == 0 and n:
             a[:] = a[0]
         for w in (1, 2, 3, 5):
-            mi = int(rng.integers(0, 20)) if trial % 2 else 1000
+            mi = int(rng.integers(0, 20)) if trial % 2 else (1000 if trial % 6 else 40)
             o1, f1 = F.iterative_filter_angles(a, w, 60, mi)
-            o2, f2 = F.iterative_filter_angles_numpy(a, w, 60, mi)
+            o2, f2 = FR.iterative_filter_angles_ref(a, w, 60, mi)
             np.testing.assert_array_equal(o1, o2)
             np.testing.assert_array_equal(f1, f2)
+
+
+def test_flips_native_matches_numpy(F):
+    """mdx_flips_from_keypoints vs the numpy checker on random frames incl.
+    NaN keypoints, NaN lengths and exact ties."""
+    from oracle import features_ref as FR
+    rng = np.random.default_rng(9)
+    n = 3000
+    kp = rng.uniform(0, 400, (n, 8, 3))
+    kp[rng.random((n, 8)) < 0.02, :2] = np.nan
+    cen = rng.uniform(50, 350, (n, 2))
+    ang = rng.uniform(0, 360, n)
+    ln = rng.uniform(20, 100, n)
+    ln[::97] = np.nan
+    kp[::31, :, 0] = cen[::31, 0, None]  # keypoints on the centroid: distance ties
+    ang[::31] = 0.0
+    f1, c1 = F.flips_from_keypoints(kp, cen, ang, ln)
+    f2, c2 = FR.flips_ref(kp, cen, ang, ln)
+    np.testing.assert_array_equal(f1, f2)
+    np.testing.assert_array_equal(c1, c2)

@@ -133,6 +133,15 @@ def test_crop_and_rotate(mdx, session, raw):
     np.testing.assert_array_equal(gotm, wantm)
     one = proc.crop_and_rotate_frame(prepped[7], centers[7], angles[7])
     np.testing.assert_array_equal(one, want[7])
+    # integer crop windows, exactly as M/proc/proc.py:325-328 computes them
+    # (python int() truncates toward zero); -1 where it returns zeros first
+    _, _, win = proc.crop_and_rotate_frames(prepped, centers, angles, frames2=masks, return_window=True)
+    for i in range(n):
+        cx, cy = centers[i]
+        if np.isnan(angles[i]) or np.isnan(cx) or np.isnan(cy) or cx < 0 or cy < 0:
+            assert list(win[i]) == [-1] * 4, i
+        else:
+            assert list(win[i]) == [int(cx - 40) + 80, int(cx + 40) + 80, int(cy - 40) + 80, int(cy + 40) + 80], i
 
 
 @pytest.mark.parametrize("p,seed", [(0.03, 1), (0.2, 2)])

@@ -170,7 +170,6 @@ def test_conv_mfma_layout_identity(mdx):
 
 
 def test_deconv2x2_pixel_shuffle(mdx, rt):
-    from moseq2_detectron_extract_amd.model.runtime import Conv
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     g = torch.Generator().manual_seed(3)

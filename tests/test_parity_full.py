@@ -11,14 +11,15 @@ Tolerances (written here, stated in DESIGN.md §4):
   features p2..p6, rel. max error:   fp32 <= 2e-4,  fp16 <= 3e-2
   detections: same count; every oracle box matched by a GPU box of IoU
     >= 0.98 (fp32) / 0.9 (fp16), |score diff| <= 1e-3 (fp32) / 2e-2 (fp16)
-  masks of matched detections: IoU >= 0.97 (fp32) / 0.9 (fp16)
+  masks of matched detections: differing pixels <= max(4, 3 % (fp32) /
+    10 % (fp16) of the union) -- seeded random weights give masks of a few
+    pixels up to blob size, where an IoU bound alone says little
   keypoints of matched detections: >= 90 % (fp32) / 75 % (fp16) within 1 px
   downstream (selected mask -> clean -> moments -> angle -> crop):
-    fp32: selected-mask IoU >= 0.97, centroid within 0.5 px, angle within
-          1 deg (mod 180), and the crop at the GPU centroid / angle equals the
-          oracle crop at the same centroid / angle bit for bit;
-    fp16: selected-mask IoU >= 0.9, centroid within 2 px, angle within
-          5 deg (mod 180).
+    selected mask: the mask bound above; centroid within 0.5 px (fp32) /
+    2 px (fp16), angle within 1 deg / 5 deg (mod 180), NaN (no contour)
+    on both sides or neither; the crop at the GPU centroid / angle equals
+    the oracle crop at the same centroid / angle bit for bit.
 The measured numbers are written to gpurun_out/parity_full_<case>.json when
 that directory exists (evidence for DESIGN.md)."""
 import json
@@ -32,8 +33,9 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_iou=0.97, kp=0.9, sel_iou=0.97, cen=0.5, ang=1.0),
-       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_iou=0.9, kp=0.75, sel_iou=0.9, cen=2.0, ang=5.0)}
+TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, cen=0.5, ang=1.0),
+       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0)}
+MASK_PX_FLOOR = 4  # pixels: the seeded-weight masks can be a handful of pixels
 
 
 def _iou_box(a, b):
@@ -47,6 +49,23 @@ def _iou_box(a, b):
 def _mask_iou(a, b):
     u = np.logical_or(a, b).sum()
     return 1.0 if u == 0 else np.logical_and(a, b).sum() / u
+
+
+def _mask_px(a, b):
+    """(differing pixels, union pixels)"""
+    return int(np.logical_xor(a, b).sum()), int(np.logical_or(a, b).sum())
+
+
+def _mask_ok(diff_union, frac):
+    d, u = diff_union
+    return d <= max(MASK_PX_FLOOR, frac * u)
+
+
+def _close_nan(a, b, tol):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    if np.isnan(a).any() or np.isnan(b).any():
+        return bool(np.array_equal(np.isnan(a), np.isnan(b)))
+    return bool(np.abs(a - b).max() <= tol)
 
 
 def _ang_diff(a, b):
@@ -110,7 +129,8 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         gs = inf["scores"][i, :n].cpu().numpy()
         rec["score_diff_max"] = float(np.abs(gs[match] - w["scores"].numpy()[:m]).max()) if m else 0.0
         gm = masks_all[i, :n].astype(bool)
-        rec["mask_iou_min"] = float(min([_mask_iou(gm[match[j]], w["pred_masks"][j].numpy()) for j in range(m)] or [1]))
+        rec["mask_iou"] = [float(_mask_iou(gm[match[j]], w["pred_masks"][j].numpy())) for j in range(m)]
+        rec["mask_px"] = [_mask_px(gm[match[j]], w["pred_masks"][j].numpy()) for j in range(m)]
         gk = inf["keypoints"][i, :n].cpu().numpy()
         wk = w["pred_keypoints"].numpy()[:m]
         d = np.abs(gk[match][..., :2] - wk[..., :2]).max(-1)
@@ -120,6 +140,7 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         d2w = w["pred_masks"][keep[0]].numpy().astype(np.uint8) if keep else np.zeros(prepped.shape[1:], np.uint8)
         d2g = inf["d2_mask"][i].cpu().numpy()
         rec["sel_mask_iou"] = float(_mask_iou(d2g.astype(bool), d2w.astype(bool)))
+        rec["sel_mask_px"] = _mask_px(d2g.astype(bool), d2w.astype(bool))
         cl = O.clean_frames(prepped[i:i + 1], iters_tail=3)
         rec["cleaned_bit_exact"] = bool(np.array_equal(cleaned_d[i].cpu().numpy(), cl[0]))
         fw = O.get_frame_features(cl, 3, mask=d2w[None])
@@ -127,6 +148,8 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         aw = np.mod(-np.rad2deg(fw["orientation"][0]), 360)
         cg = tail["centroid"][i].cpu().numpy()
         ag = float(tail["angle"][i])
+        rec["centroid"] = [cg.tolist(), cw.tolist()]
+        rec["angle"] = [ag, float(aw)]
         rec["centroid_px"] = float(np.abs(cg - cw).max())
         rec["angle_deg_mod180"] = float(_ang_diff(ag, aw))
         # crops: the GPU crop equals the oracle crop at the same centre / angle
@@ -139,10 +162,12 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         assert rec["ndet"][0] == rec["ndet"][1], rec
         assert rec["box_iou_min"] >= tol["box_iou"], rec
         assert rec["score_diff_max"] <= tol["score"], rec
-        assert rec["mask_iou_min"] >= tol["mask_iou"], rec
+        assert all(_mask_ok(x, tol["mask_px"]) for x in rec["mask_px"]), rec
         assert rec["kp_within_1px"] >= tol["kp"], rec
         assert rec["cleaned_bit_exact"], rec
-        assert rec["sel_mask_iou"] >= tol["sel_iou"], rec
-        assert rec["centroid_px"] <= tol["cen"], rec
-        assert rec["angle_deg_mod180"] <= tol["ang"], rec
+        assert _mask_ok(rec["sel_mask_px"], tol["mask_px"]), rec
+        assert _close_nan(rec["centroid"][0], rec["centroid"][1], tol["cen"]), rec
+        a, b = rec["angle"]
+        assert (np.isnan(a) and np.isnan(b)) or (not np.isnan(a) and not np.isnan(b) and
+                                                 _ang_diff(a, b) <= tol["ang"]), rec
         assert rec["crop_bit_exact_same_pose"], rec
