@@ -152,6 +152,25 @@ int mdx_flips_from_keypoints(const double *kp, int64_t n, int K, const double *c
 int mdx_finalize_angles(const double *orientation, const double *axis_length, const double *centroid,
                         const double *kp, int64_t n, int K, double *angles_out, uint8_t *flips_out);
 
+/* Host (CPU) functions: the tracking branch of instances_to_features
+ * (--use-tracking, the reference's default; M/proc/proc.py:720-800) with
+ * ProcessFeaturesStep's point tracker (centroid + K keypoints, order-3
+ * Kalman items) and angle tracker ((sin, cos), order 3)
+ * (M/pipeline/process_features_step.py:40-51, M/proc/kalman.py:101-418),
+ * pykalman semantics: EM (10 iterations on Q, R, P0) on the first chunk,
+ * RTS smoothing per chunk (state carried), keypoint flips, alignment
+ * scores and the per-frame sample / intervene / filter_update angle loop.
+ * track: centroid [n][2], keypoints [n][K][3], orientation [n] (rad),
+ * axis_length [n][2] (float64) -> smoothed centroid, keypoints (first 7
+ * smoothed), angles (deg), flips.  state: which 0 = point, 1 = angle
+ * tracker; *initialized, and its last state mean (returns its length). */
+void *mdx_tracking_create(int n_keypoints);
+int mdx_tracking_destroy(void *handle);
+int mdx_tracking_state(void *handle, int which, int *initialized, double *mean, int64_t mean_len);
+int mdx_tracking_track(void *handle, int64_t n, int K, const double *centroid, const double *keypoints,
+                       const double *orientation, const double *axis_length, double *centroid_out,
+                       double *keypoints_out, double *angles_out, uint8_t *flips_out);
+
 /* Host (CPU) functions: the instance tracker of
  * ProcessFeaturesStep.__select_instances (M/pipeline/process_features_step.py:
  * 35-38, 133-160; norfair 2.x Tracker semantics, see instances.py).  The
@@ -460,12 +479,26 @@ int mdx_model_forward(mdx_model_t model, const uint8_t *frames, int B, int h, in
 
 /* Intermediates of the last forward on `stream` (valid until the next forward
  * on it), for stage-wise parity tests: "input" (B,Hp,Wp,4 NHWC), "res2".."res5",
- * "p2".."p6" (NHWC), "proposals" (B,P,4) f32, "proposal_scores" (B,P) f32,
+ * "p2".."p6" (NHWC), per FPN level l "fpn_lateral<l>" (lateral conv),
+ * "fpn_inner<l>" (its GroupNorm + top-down fuse), "fpn_output<l>" (output conv
+ * before GroupNorm), "proposals" (B,P,4) f32, "proposal_scores" (B,P) f32,
  * "proposal_count" (B) i32, "box_pooled" (B*P,R,R,C), "box_pred" (B*P,6) f32,
  * "mask_logits" (B*D,2M,2M,1) f32.  shape[4] gets the dims (unused = 1),
  * dtype: 0 f32, 1 f16, 2 i32.  copy: D2D copy of `bytes` into dst on `stream`. */
 int mdx_model_tensor_info(mdx_model_t model, mdx_stream_t stream, const char *name, int64_t shape[4], int *dtype);
 int mdx_model_tensor_copy(mdx_model_t model, mdx_stream_t stream, const char *name, void *dst, int64_t bytes);
+
+/* Testing aid: reserve the workspace of `stream` for (B, h, w) and fill all of
+ * it with `byte` (asynchronously on `stream`), so a test can show that a
+ * forward's results do not depend on what the workspace held before. */
+int mdx_model_debug_fill(mdx_model_t model, int B, int h, int w, int byte, mdx_stream_t stream);
+
+/* Testing aid: the byte size of `stream`'s workspace, the offset of a named
+ * intermediate in it (-1 when it lives in a caller buffer), and a D2D copy of
+ * its first dst_bytes bytes into dst (each part skipped when its pointer is
+ * NULL). */
+int mdx_model_debug_arena(mdx_model_t model, mdx_stream_t stream, const char *name, int64_t *offset,
+                          int64_t *arena_bytes, void *dst, int64_t dst_bytes);
 
 /* Per-convolution timing of later forwards (HIP events around every conv
  * launch; host-only bookkeeping, off by default).  read: after the stream

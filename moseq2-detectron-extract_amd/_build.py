@@ -32,6 +32,11 @@ def _flags():
             "-munsafe-fp-atomics", f"-I{os.path.dirname(HERE)}"]
 
 
+# per-file host-code flags: the dense linear algebra of the Kalman recursions
+# vectorises with AVX2 / FMA (every x86-64 host of an MI355X has them)
+HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mfma"]}
+
+
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
@@ -58,7 +63,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
 
     def comp(so):
         s, o = so
-        cmd = [cc, *_flags(), "-c", s, "-o", o]
+        cmd = [cc, *_flags(), *HOST_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

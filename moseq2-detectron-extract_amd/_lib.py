@@ -11,7 +11,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmdx.so")
+# MDX_LIB_VARIANT=<name> loads libmdx_<name>.so (an instrumented build, debugging only)
+LIB_PATH = os.path.join(_HERE, "libmdx.so" if not os.environ.get("MDX_LIB_VARIANT") else
+                        f"libmdx_{os.environ['MDX_LIB_VARIANT']}.so")
 _LIB = None
 
 
@@ -78,6 +80,10 @@ SIGNATURES = {
     "mdx_instance_tracker_create": (P, [I32]),
     "mdx_instance_tracker_destroy": (I32, [P]),
     "mdx_instance_tracker_select": (I32, [P, P, P, I64, I32, I64, P, P]),
+    "mdx_tracking_create": (P, [I32]),
+    "mdx_tracking_destroy": (I32, [P]),
+    "mdx_tracking_state": (I32, [P, I32, P, P, I64]),
+    "mdx_tracking_track": (I32, [P, I64, I32, P, P, P, P, P, P, P, P]),
     "mdx_model_create": (I32, [ctypes.c_char_p, I64, P, I32, P]),
     "mdx_model_destroy": (I32, [P]),
     "mdx_model_reserve": (I32, [P, I32, I32, I32, P]),
@@ -85,6 +91,8 @@ SIGNATURES = {
     "mdx_model_tensor_info": (I32, [P, P, ctypes.c_char_p, P, P]),
     "mdx_model_tensor_copy": (I32, [P, P, ctypes.c_char_p, P, I64]),
     "mdx_model_profile": (I32, [P, I32]),
+    "mdx_model_debug_fill": (I32, [P, I32, I32, I32, I32, P]),
+    "mdx_model_debug_arena": (I32, [P, P, ctypes.c_char_p, P, P, P, I64]),
     "mdx_model_profile_read": (I32, [P, P, I32]),
 }
 

@@ -19,6 +19,7 @@
 // one allocation sized by a dry run of the same code, bump-allocated per
 // forward, so forwards on different streams run concurrently.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -64,6 +65,7 @@ struct TensorRec {
     void *p;
     int64_t shape[4];
     int dtype;
+    int64_t offset;  // bytes from the arena base (-1: caller-owned)
 };
 
 struct ProfEv {
@@ -460,7 +462,9 @@ struct Fwd {
     }
     void *alloc(size_t bytes) { return c.alloc(bytes); }
     void name(const char *n, void *p, int64_t a, int64_t b, int64_t cc, int64_t d, int dtype) {
-        if (!c.dry) c.named[n] = TensorRec{p, {a, b, cc, d}, dtype};
+        if (c.dry) return;
+        const int64_t off = (char *)p >= c.base && (char *)p < c.base + c.cap ? (char *)p - c.base : -1;
+        c.named[n] = TensorRec{p, {a, b, cc, d}, dtype, off};
     }
     // conv + bias (+ residual) (+ ReLU); out_mode 1 = 2x2 deconv pixel shuffle
     void *conv(const void *x, int N, int H, int W, const ConvW &cw, bool relu, int &OH, int &OW,
@@ -490,10 +494,14 @@ struct Fwd {
         }
         return out;
     }
+    void *last_gn_ws = nullptr;
+    size_t last_gn_ws_bytes = 0;
     void *groupnorm(const void *x, int N, int H, int W, const GnW &g, const void *up, int fuse) {
         const int C = m.cfg.fpn_out_channels, G = m.cfg.gn_groups;
         void *out = alloc((size_t)N * H * W * C * m.es);
-        void *ws = alloc((size_t)mdx_groupnorm_workspace_bytes(N, H, W, G));
+        last_gn_ws_bytes = (size_t)mdx_groupnorm_workspace_bytes(N, H, W, G);
+        void *ws = alloc(last_gn_ws_bytes);
+        last_gn_ws = ws;
         if (!c.dry && ok())
             chk(mdx_groupnorm(x, N, H, W, C, G, m.cfg.gn_eps, g.g, g.b, up, fuse, m.dt, out, (float *)ws, s));
         return out;
@@ -562,8 +570,34 @@ struct Fwd {
             void *lat = conv(res[i], B, rh[i], rw[i], m.fpn_lat[i], false, oh, ow);
             void *pv = groupnorm(lat, B, rh[i], rw[i], m.gn_lat[i], prev, prev ? fuse : 0);
             prev = pv;
+            static const bool shadow_ws = getenv("MDX_DEBUG_SHADOW") != nullptr;
+            if (shadow_ws && i == 3) {
+                void *a0 = alloc(last_gn_ws_bytes);
+                if (!c.dry && ok()) (void)hipMemcpyAsync(a0, last_gn_ws, last_gn_ws_bytes, hipMemcpyDeviceToDevice, s);
+                name("shadow_gnws5", a0, 1, 1, 1, (int64_t)last_gn_ws_bytes / 4, 0);
+                name("gnws5", last_gn_ws, 1, 1, 1, (int64_t)last_gn_ws_bytes / 4, 0);
+            }
             void *o = conv(pv, B, rh[i], rw[i], m.fpn_out[i], false, oh, ow);
             feat[i] = groupnorm(o, B, rh[i], rw[i], m.gn_out[i], nullptr, 0);
+            static const char *ln[4] = {"fpn_lateral2", "fpn_lateral3", "fpn_lateral4", "fpn_lateral5"};
+            static const char *gn[4] = {"fpn_inner2", "fpn_inner3", "fpn_inner4", "fpn_inner5"};
+            static const char *on[4] = {"fpn_output2", "fpn_output3", "fpn_output4", "fpn_output5"};
+            name(ln[i], lat, B, rh[i], rw[i], C, m.dt);
+            name(gn[i], pv, B, rh[i], rw[i], C, m.dt);
+            name(on[i], o, B, rh[i], rw[i], C, m.dt);
+            static const bool shadow = getenv("MDX_DEBUG_SHADOW") != nullptr;
+            if (shadow) {  // debugging aid: copies of the GN outputs taken right after they are written
+                static const char *sg[4] = {"shadow_inner2", "shadow_inner3", "shadow_inner4", "shadow_inner5"};
+                static const char *sp[4] = {"shadow_p2", "shadow_p3", "shadow_p4", "shadow_p5"};
+                const size_t nb = (size_t)B * rh[i] * rw[i] * C * m.es;
+                void *a1 = alloc(nb), *a2 = alloc(nb);
+                if (!c.dry && ok()) {
+                    (void)hipMemcpyAsync(a1, pv, nb, hipMemcpyDeviceToDevice, s);
+                    (void)hipMemcpyAsync(a2, feat[i], nb, hipMemcpyDeviceToDevice, s);
+                }
+                name(sg[i], a1, B, rh[i], rw[i], C, m.dt);
+                name(sp[i], a2, B, rh[i], rw[i], C, m.dt);
+            }
             fh[i] = rh[i];
             fw[i] = rw[i];
         }
@@ -769,6 +803,36 @@ extern "C" int mdx_model_tensor_copy(mdx_model_t model, mdx_stream_t stream, con
     MDX_REQUIRE(bytes <= have, "mdx_model_tensor_copy: %lld bytes requested, \"%s\" has %lld", (long long)bytes,
                 name, (long long)have);
     MDX_HIP(hipMemcpyAsync(dst, t.p, (size_t)bytes, hipMemcpyDeviceToDevice, s));
+    return MDX_OK;
+}
+
+extern "C" int mdx_model_debug_fill(mdx_model_t model, int B, int h, int w, int byte, mdx_stream_t stream) {
+    MDX_REQUIRE(model && byte >= 0 && byte <= 255, "mdx_model_debug_fill: bad arguments");
+    Model &m = *(Model *)model;
+    hipStream_t s = as_stream(stream);
+    Ctx &c = *get_ctx(m, s);
+    const int r = reserve(m, c, B, h, w, s);
+    if (r != MDX_OK) return r;
+    MDX_HIP(hipMemsetAsync(c.base, byte, c.cap, s));
+    return MDX_OK;
+}
+
+extern "C" int mdx_model_debug_arena(mdx_model_t model, mdx_stream_t stream, const char *name, int64_t *offset,
+                                     int64_t *arena_bytes, void *dst, int64_t dst_bytes) {
+    MDX_REQUIRE(model, "mdx_model_debug_arena: null model");
+    Model &m = *(Model *)model;
+    hipStream_t s = as_stream(stream);
+    Ctx &c = *get_ctx(m, s);
+    if (arena_bytes) *arena_bytes = (int64_t)c.cap;
+    if (name && offset) {
+        auto it = c.named.find(name);
+        MDX_REQUIRE(it != c.named.end(), "mdx_model_debug_arena: no intermediate \"%s\"", name);
+        *offset = it->second.offset;
+    }
+    if (dst) {
+        MDX_REQUIRE(dst_bytes >= 0 && (size_t)dst_bytes <= c.cap, "mdx_model_debug_arena: bad copy size");
+        MDX_HIP(hipMemcpyAsync(dst, c.base, (size_t)dst_bytes, hipMemcpyDeviceToDevice, s));
+    }
     return MDX_OK;
 }
 

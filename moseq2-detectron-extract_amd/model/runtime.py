@@ -171,6 +171,10 @@ class MaskRCNN:
         call("mdx_model_tensor_copy", self._h, _stream(), name.encode(), _p(t), t.numel() * t.element_size())
         return t
 
+    def debug_fill(self, B: int, h: int, w: int, byte: int):
+        """Fill the current stream's workspace with `byte` (testing aid)."""
+        call("mdx_model_debug_fill", self._h, B, h, w, int(byte), _stream())
+
     def profile(self, on: bool) -> bool:
         """Time every conv launch of later forwards (HIP events)."""
         return bool(call("mdx_model_profile", self._h, int(on)))

@@ -42,6 +42,7 @@ import numpy.ma as ma
 from scipy.linalg import block_diag
 
 from . import features as F
+from ._lib import call
 
 
 # ---------------------------------------------------------------------------
@@ -384,8 +385,70 @@ class KalmanTracker:
 # ---------------------------------------------------------------------------
 # the tracking branch of instances_to_features
 # ---------------------------------------------------------------------------
-def make_trackers(n_keypoints: int = 8) -> Tuple[KalmanTracker, KalmanTracker]:
-    """(point_tracker, angle_tracker) as ProcessFeaturesStep builds them."""
+class NativeTracking:
+    """The tracking branch's two trackers in libmdx host code
+    (mdx_tracking_*): the same model as the numpy KalmanTracker pair below,
+    without the per-step Python overhead.  ``point`` / ``angle`` expose the
+    trackers' ``is_initialized`` / ``last_mean`` like KalmanTracker does."""
+
+    class _View:
+        def __init__(self, owner, which):
+            self._o, self._w = owner, which
+
+        def _state(self):
+            import ctypes
+            ini = ctypes.c_int()
+            buf = np.empty(1024, np.float64)
+            n = call("mdx_tracking_state", self._o._h, self._w, ctypes.byref(ini),
+                     buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+            return bool(ini.value), buf[:n].copy()
+
+        @property
+        def is_initialized(self) -> bool:
+            return self._state()[0]
+
+        @property
+        def last_mean(self) -> np.ndarray:
+            return self._state()[1]
+
+    def __init__(self, n_keypoints: int = 8):
+        self.n_keypoints = n_keypoints
+        self._h = call("mdx_tracking_create", int(n_keypoints))
+        if not self._h:
+            raise ValueError("mdx_tracking_create failed")
+        self.point, self.angle = NativeTracking._View(self, 0), NativeTracking._View(self, 1)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                call("mdx_tracking_destroy", h)
+            except Exception:
+                pass
+            self._h = None
+
+    def track(self, centroid, keypoints, orientation, axis_length):
+        import ctypes
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        cen = np.ascontiguousarray(centroid, np.float64)
+        kp = np.ascontiguousarray(keypoints, np.float64)
+        ori = np.ascontiguousarray(orientation, np.float64)
+        ax = np.ascontiguousarray(axis_length, np.float64)
+        n, K = kp.shape[0], kp.shape[1]
+        c_out, k_out = np.empty_like(cen), np.empty_like(kp)
+        a_out, f_out = np.empty(n, np.float64), np.empty(n, np.uint8)
+        call("mdx_tracking_track", self._h, n, K, P(cen), P(kp), P(ori), P(ax), P(c_out), P(k_out), P(a_out),
+             P(f_out))
+        return c_out, k_out, a_out, f_out.astype(bool)
+
+
+def make_trackers(n_keypoints: int = 8, native: bool = True):
+    """(point_tracker, angle_tracker) as ProcessFeaturesStep builds them
+    (process_features_step.py:40-51): by default views of one NativeTracking
+    (libmdx host code); native=False gives the numpy KalmanTracker pair."""
+    if native:
+        t = NativeTracking(n_keypoints)
+        return t.point, t.angle
     point = KalmanTracker([KalmanTrackerPoint2D(order=3, delta_t=1.0),
                            KalmanTrackerNPoints2D(n_keypoints, order=3, delta_t=1.0)])
     angle = KalmanTracker([KalmanTrackerAngle(order=3, delta_t=1.0, degrees=True)])
@@ -431,6 +494,10 @@ def track_features(point_tracker: KalmanTracker, angle_tracker: KalmanTracker, c
     orientation (n,) radians, axis_length (n,2).  The trackers carry their
     state into the next chunk.  Returns (centroid, keypoints, angles deg,
     flips) with the keypoints' first 7 (x, y) replaced by the smoothed ones."""
+    if isinstance(point_tracker, NativeTracking._View):
+        if not isinstance(angle_tracker, NativeTracking._View) or angle_tracker._o is not point_tracker._o:
+            raise ValueError("native trackers come in pairs (make_trackers())")
+        return point_tracker._o.track(centroid, keypoints, orientation, axis_length)
     centroid = np.array(centroid, dtype=np.float64)
     keypoints = np.array(keypoints, dtype=np.float64)
     lengths = np.max(axis_length, axis=1)

@@ -67,7 +67,7 @@ def test_reference_documented_examples(T):
 
 
 def test_tracker_items(T, R):
-    p, a = T.make_trackers()
+    p, a = T.make_trackers(native=False)
     A1 = T.KalmanTrackerPoint1D(order=3).build_trans_mat()
     np.testing.assert_array_equal(A1, [[1, 1, 0.5], [0, 1, 1], [0, 0, 1]])
     assert [it.state_size for it in p.items] == [6, 48]
@@ -159,3 +159,24 @@ def test_track_features_nan_first_frame_propagates(T):
     p, a = T.make_trackers()
     c, k, ang, fl = T.track_features(p, a, cen, kp, ori, axl)
     assert np.isnan(c).all()
+
+
+def test_native_tracking_matches_numpy_statement(T):
+    """libmdx's tracking recursion (mdx_tracking_*) against the numpy
+    statement in tracking.py over a session of chunks incl. a one-frame
+    chunk (filter_update path) and NaN frames: smoothed centroid / keypoints
+    and angles to 1e-9, flips exactly, tracker states to 1e-9."""
+    cen, kp, ori, axl = _traj(900, seed=11, nan_frames=(5, 300, 301, 650), flip_every=17)
+    pn, an = T.make_trackers(native=False)
+    pc, ac = T.make_trackers()
+    assert not pc.is_initialized and not ac.is_initialized
+    for c0, c1 in ((0, 400), (400, 401), (401, 800), (800, 900)):
+        args = (cen[c0:c1], kp[c0:c1], ori[c0:c1], axl[c0:c1])
+        a = T.track_features(pn, an, *args)
+        b = T.track_features(pc, ac, *args)
+        for x, y in zip(a[:3], b[:3]):
+            np.testing.assert_allclose(y, x, rtol=1e-9, atol=1e-9)
+        np.testing.assert_array_equal(b[3], a[3])
+    assert pc.is_initialized and ac.is_initialized
+    np.testing.assert_allclose(pc.last_mean, pn.last_mean, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(ac.last_mean, an.last_mean, rtol=1e-9, atol=1e-12)

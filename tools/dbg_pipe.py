@@ -11,6 +11,14 @@ from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, O
 
 dt = sys.argv[1] if len(sys.argv) > 1 else "fp16"
 nms = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+knob = sys.argv[3] if len(sys.argv) > 3 else ""
+from moseq2_detectron_extract_amd._lib import call
+if knob == "nolarge":
+    call("mdx_conv_set_large_tiles", 0)
+elif knob == "nostream":
+    call("mdx_conv_set_stream1x1", 0, 65536)
+elif knob == "dma128":
+    call("mdx_conv_set_dma128", 2, 0)
 s = synth.SyntheticSession(12, seed=5)
 raw = torch.from_numpy(s.frames(0, 12)).cuda()
 pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt)
@@ -60,4 +68,4 @@ for i in range(3):
             out["inf:masks"] = sum(d(a, b) for a, b in zip(v, rec["inf"][i][k]))
     for k in ("depth_frames", "mask_frames", "centroid", "angle", "keypoints"):
         out[k] = d(want[i][k], got[i][k])
-    print(dt, nms, "batch", i, {k: v for k, v in out.items() if v} or "identical", flush=True)
+    print(dt, nms, knob, "batch", i, {k: v for k, v in out.items() if v} or "identical", flush=True)

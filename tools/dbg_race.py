@@ -1,0 +1,100 @@
+"""Debug: a forward on stream A while another forward runs on stream B,
+repeated; the earliest intermediate of A (forward order) that differs from a
+serial run of the same batch."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import mdx_pkg
+mdx_pkg.load()
+from moseq2_detectron_extract_amd import synth, proc
+from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+
+dt = sys.argv[1] if len(sys.argv) > 1 else "fp16"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+mode = sys.argv[3] if len(sys.argv) > 3 else "same"   # same | other (second handle) | conv (background conv)
+order = ["res2", "res3", "res4", "res5", "fpn_lateral5", "fpn_inner5", "fpn_output5", "p5",
+         "fpn_lateral4", "fpn_inner4", "fpn_output4", "p4", "p3", "p2", "p6", "proposals", "proposal_scores",
+         "proposal_count", "box_pooled", "box_pred", "mask_logits"]
+if os.environ.get("MDX_DEBUG_SHADOW"):
+    order = order[:4] + ["shadow_gnws5", "gnws5"] + [f"{k}{l}" for l in (5, 4, 3, 2) for k in ("fpn_lateral", "shadow_inner", "fpn_inner",
+                                                                     "fpn_output", "shadow_p", "p")]
+s = synth.SyntheticSession(8, seed=5)
+pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt)
+prep = proc.FramePrep(s.bground_im, s.roi, 0, 100)
+x = prep(torch.from_numpy(s.frames(0, 8)).cuda())
+xa, xb = x[:4].contiguous(), x[4:].contiguous()
+lut = proc.scale_lut(0, 100)
+m = pred.model
+mb = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt).model if mode == "other" else m
+import ctypes
+from moseq2_detectron_extract_amd._lib import call
+P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+tdt = torch.float16 if dt == "fp16" else torch.float32
+bx = torch.randn(8, 112, 128, 256).to(tdt).cuda()
+bw = (torch.randn(256, 2304) * 0.02).to(tdt).cuda()
+bo = torch.empty(8, 112, 128, 256, dtype=tdt, device="cuda")
+
+
+def background(n):
+    for _ in range(n):
+        if mode == "conv":
+            call("mdx_conv2d", P(bx), 8, 112, 128, 256, P(bw), None, 256, 3, 3, 1, 1, None, 0, 0, int(dt == "fp16"),
+                 int(dt == "fp16"), P(bo), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        else:
+            mb.forward(xb, lut)
+
+
+ref = m.forward(xa, lut)
+torch.cuda.synchronize()
+ref["intermediates"] = {k: m.tensor(k) for k in order}
+torch.cuda.synchronize()
+sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+with torch.cuda.stream(sa):
+    m.reserve(4, *xa.shape[1:])
+with torch.cuda.stream(sb):
+    mb.reserve(4, *xb.shape[1:])
+torch.cuda.synchronize()
+hist = {}
+for r in range(reps):
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    sa.wait_event(ev); sb.wait_event(ev)
+    # B first so that A's kernels overlap B's in varying phase
+    with torch.cuda.stream(sb):
+        background(r % 3 + (3 if mode == "conv" else 0))
+    with torch.cuda.stream(sa):
+        oa = m.forward(xa, lut)
+    with torch.cuda.stream(sb):
+        background(1 + (3 if mode == "conv" else 0))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        inter = {k: m.tensor(k) for k in order}
+    torch.cuda.synchronize()
+    first = None
+    for k in order:
+        a, b = ref["intermediates"][k], inter[k]
+        if k in ("proposals", "proposal_scores", "box_pred"):
+            b = b.reshape(a.shape) if b.numel() == a.numel() else b
+        if k == "proposal_count":
+            b = b.view(-1)
+        if k == "input":
+            continue
+        if a.shape != b.shape:
+            b = b.reshape(a.shape)
+        if not torch.equal(torch.nan_to_num(a.float(), nan=7e7), torch.nan_to_num(b.float(), nan=7e7)):
+            d = (a.float() - b.float()).abs()
+            first = (k, int((d != 0).sum()), float(d.max()))
+            break
+    print(dt, mode, "rep", r, first or "identical", "boxes_equal", bool(torch.equal(oa["boxes"], ref["boxes"])), flush=True)
+    hist[first[0] if first else None] = hist.get(first[0] if first else None, 0) + 1
+print("summary", dt, mode, hist, flush=True)
+if os.environ.get("MDX_DEBUG_SHADOW"):
+    # where in the level-5 GN workspace: [stats 2*N*G][partials 3*N*G*nch]
+    N, G = 4, 32
+    a = ref["intermediates"]["shadow_gnws5"].flatten()
+    with torch.cuda.stream(sa):
+        b = m.tensor("shadow_gnws5").flatten()
+    torch.cuda.synchronize()
+    d = (a != b).nonzero().flatten().cpu().numpy()
+    print("last rep gnws5 differing floats:", d.size, "stats part" if d.size and d[0] < 2 * N * G else "",
+          d[:20].tolist(), flush=True)
