@@ -56,6 +56,9 @@ with torch.cuda.stream(sb):
 torch.cuda.synchronize()
 hist = {}
 for r in range(reps):
+    if os.environ.get("DBG_FILL"):
+        with torch.cuda.stream(sa):
+            m.debug_fill(4, *xa.shape[1:], int(os.environ["DBG_FILL"], 0))
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
     sa.wait_event(ev); sb.wait_event(ev)
