@@ -36,6 +36,16 @@ def _flags():
 # vectorises with AVX2 / FMA (every x86-64 host of an MI355X has them)
 HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mfma"]}
 
+# per-file device-code flags.  model_ops.hip is compiled without the packed
+# FP32 VALU instructions (v_pk_add/mul/fma_f32): in its kernels the compiler
+# forms them with op_sel / neg source modifiers (broadcast-and-subtract), and
+# with those the GroupNorm statistics came out nondeterministic on MI355X
+# whenever two model forwards ran concurrently on different hardware queues
+# (~1e-3 relative errors in whole channel halves; 0 of 24 runs without them
+# against ~60 % with, tools/dbg_race.py).  The target-feature switch reaches
+# the host compile too, where clang ignores it with a warning.
+DEVICE_FLAGS = {"model_ops.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]}
+
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
@@ -63,7 +73,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
 
     def comp(so):
         s, o = so
-        cmd = [cc, *_flags(), *HOST_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o]
+        base = os.path.basename(s)
+        cmd = [cc, *_flags(), *HOST_FLAGS.get(base, []), *DEVICE_FLAGS.get(base, []), "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

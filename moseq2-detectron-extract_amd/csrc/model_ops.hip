@@ -180,9 +180,6 @@ constexpr int GN_CHUNK_PIX = 64;
 template <typename T>
 __global__ __launch_bounds__(256) void k_gn_partial(const T *__restrict__ x, int HW, int C, int G,
                                                     float *__restrict__ part) {
-#ifdef MDX_GN_ACQUIRE
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     __shared__ float s_n[256], s_m[256], s_q[256];
     const int n = blockIdx.y, chunk = blockIdx.x;
     const int nchunks = gridDim.x;

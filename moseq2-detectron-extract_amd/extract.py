@@ -196,24 +196,55 @@ def _run_overlapped(src, batches, ex, true_depth):
     to a worker thread, which runs the sequential host step (angles / Kalman
     tracking, in chunk order) and the small device tail (scalars, keypoint z,
     crops) on its own stream while the next chunk's device pass runs."""
-    import queue
-    import threading
-
     import torch
-    q: "queue.Queue" = queue.Queue(maxsize=2)
-    parts, err = [], []
     dev = torch.cuda.current_device()
+    ctx = {}
+
+    def setup():
+        torch.cuda.set_device(dev)
+        ctx["ws"] = torch.cuda.Stream()
+
+    def produce():
+        for idx, raw in src.iterate(device=True, batches=batches):
+            st, host = ex.features_pass(raw)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            yield np.asarray(idx), st, host, ev
+
+    def consume(item):
+        idx, st, host, ev = item
+        ws = ctx["ws"]
+        ws.wait_event(ev)
+        with torch.cuda.stream(ws):
+            for t in (st["prepped"], st["d2"], st["cleaned"]):
+                t.record_stream(ws)
+            ex.select_instances(st, host)
+            cen, kp, ang, fl = ex.host_angles(host)
+            d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
+        return _lighten(d)
+
+    return host_pipeline(produce(), consume, setup)
+
+
+def host_pipeline(items, consume, setup=None, depth: int = 2):
+    """Run consume(item) for every item of the iterator `items` on one worker
+    thread, in order, while the calling thread produces the next ones (at most
+    `depth` queued).  Returns the results in order.  The first error of either
+    side stops production and is raised here; the worker keeps draining the
+    queue after an error (it only skips the work), so neither the producer's
+    put() nor the final sentinel can block on a dead consumer."""
+    import queue
+    import sys
+    import threading
+    q: "queue.Queue" = queue.Queue(maxsize=depth)
+    out, err = [], []
 
     def worker():
-        # The loop keeps draining the queue after an error (it only skips the
-        # work), so the producer's q.put() and the final sentinel never block
-        # on a dead consumer; the first error is raised by the caller.
-        ws = None
-        try:
-            torch.cuda.set_device(dev)
-            ws = torch.cuda.Stream()
-        except BaseException as e:  # surfaced by the caller
-            err.append(e)
+        if setup is not None:
+            try:
+                setup()
+            except BaseException as e:  # surfaced by the caller
+                err.append(e)
         while True:
             item = q.get()
             if item is None:
@@ -221,37 +252,25 @@ def _run_overlapped(src, batches, ex, true_depth):
             if err:
                 continue
             try:
-                idx, st, host, ev = item
-                ws.wait_event(ev)
-                with torch.cuda.stream(ws):
-                    for t in (st["prepped"], st["d2"], st["cleaned"]):
-                        t.record_stream(ws)
-                    ex.select_instances(st, host)
-                    cen, kp, ang, fl = ex.host_angles(host)
-                    d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
-                parts.append(_lighten(d))
+                out.append(consume(item))
             except BaseException as e:  # surfaced by the caller
                 err.append(e)
 
-    import sys
     # the worker's host step is many short numpy calls: a short GIL switch
-    # interval keeps the launching thread from waiting out the default 5 ms
+    # interval keeps the producing thread from waiting out the default 5 ms
     old_si = sys.getswitchinterval()
     sys.setswitchinterval(1e-4)
     t = threading.Thread(target=worker, daemon=True)
     t.start()
     try:
-        for idx, raw in src.iterate(device=True, batches=batches):
+        for item in items:
             if err:
                 break
-            st, host = ex.features_pass(raw)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            q.put((np.asarray(idx), st, host, ev))
+            q.put(item)
     finally:
         q.put(None)
         t.join()
         sys.setswitchinterval(old_si)
     if err:
         raise err[0]
-    return parts
+    return out

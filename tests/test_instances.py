@@ -187,14 +187,19 @@ def test_mask_centers_kernel(h, w):
 
 
 @pytest.mark.gpu
-def test_extractor_select_instances_two_chunks():
-    """GPUExtractor.select_instances over two chunks (tracker state and the
-    previous chunk's last detections carried) == the oracle's selection."""
+@pytest.mark.parametrize("chunk,bs,host_tail", [(48, 16, False), (2, 2, False), (3, 1, True), (48, 16, True)])
+def test_extractor_select_instances_two_chunks(chunk, bs, host_tail):
+    """GPUExtractor.select_instances over a session of chunks (tracker state
+    and the preceding chunks' last detections carried) == the oracle's
+    selection.  chunk < POINTWISE_HIT_COUNTER_MAX: a pick can refer to a frame
+    two chunks back (the merged tail).  host_tail: the carried planes live in
+    host memory, as pass_tail_forward receives them over a gloo group -- a
+    cross-chunk pick must still reach the device gather."""
     import torch
     from moseq2_detectron_extract_amd.pipeline import (ExtractConfig, GPUExtractor, mask_centers,
                                                          mask_nms_select)
     rng = np.random.default_rng(2)
-    B, D, h, w, K, bs = 96, 4, 64, 96, 8, 16
+    B, D, h, w, K = 96, 4, 64, 96, 8
     masks, scores, boxes, ndet = _disc_masks(rng, B, D, h, w)
     kps = rng.normal(0, 10, (B, D, K, 3)).astype(np.float32)
     ex = GPUExtractor.__new__(GPUExtractor)
@@ -202,9 +207,11 @@ def test_extractor_select_instances_two_chunks():
     ex.instance_tracker = I.InstanceTracker(1)
     ex._frames_seen, ex._tail_dets = 0, {}
     frames, got_d2, got_kp, got_n = [], [], [], []
-    for c0 in (0, 48):
+    for c0 in range(0, B, chunk):
+        if host_tail:
+            ex._tail_dets = {g: (p.cpu(), k, r) for g, (p, k, r) in ex._tail_dets.items()}
         outs = []
-        for i in range(c0, c0 + 48, bs):
+        for i in range(c0, c0 + chunk, bs):
             o = {"masks": torch.from_numpy(masks[i:i + bs]).cuda(), "scores": torch.from_numpy(scores[i:i + bs]).cuda(),
                  "ndet": torch.from_numpy(ndet[i:i + bs]).cuda(), "boxes": torch.from_numpy(boxes[i:i + bs]).cuda(),
                  "keypoints": torch.from_numpy(kps[i:i + bs]).cuda()}
@@ -214,7 +221,7 @@ def test_extractor_select_instances_two_chunks():
         keys = ("keypoints", "d2_mask", "sel_keypoints", "nkeep", "keep_idx", "centers")
         inf = {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
         keep_h, nk_h, cen_h = inf["keep_idx"].cpu().numpy(), inf["nkeep"].cpu().numpy(), inf["centers"].cpu().numpy()
-        for f in range(48):
+        for f in range(chunk):
             frames.append([((c0 + f, keep_h[f, s]), cen_h[f, s]) for s in range(nk_h[f])])
         # what features_pass hands to the host step (moments of a blank frame)
         state = {"d2": inf["d2_mask"], "cleaned": torch.zeros_like(inf["d2_mask"]), "nkeep": nk_h,

@@ -231,3 +231,42 @@ def test_instance_exchange_equals_sequential(mdx, world, n_chunks):
         if nch:
             g = off + nch * chunk - 1
             last_tail = {g: (r, float(g), [1, 0])}
+
+
+# ---------------------------------------------------------------- host pipeline
+def test_host_pipeline_order_and_errors(mdx):
+    """extract.host_pipeline (the overlapped chunk loop's worker hand-off):
+    results in order; a consumer error part-way through a session of more
+    than 3 chunks is raised without hanging (the queue holds 2), and so is a
+    producer error and a setup error."""
+    from moseq2_detectron_extract_amd.extract import host_pipeline
+    assert host_pipeline(iter(range(7)), lambda i: i * i) == [i * i for i in range(7)]
+    produced = []
+
+    def gen(n):
+        for i in range(n):
+            produced.append(i)
+            yield i
+
+    def bad(i):
+        if i == 2:
+            raise RuntimeError("finish_chunk failed")
+        return i
+
+    with pytest.raises(RuntimeError, match="finish_chunk failed"):
+        host_pipeline(gen(10), bad)
+    assert len(produced) < 10  # production stopped early
+
+    def bad_gen():
+        yield 0
+        yield 1
+        raise ValueError("frame source failed")
+
+    with pytest.raises(ValueError, match="frame source failed"):
+        host_pipeline(bad_gen(), lambda i: i)
+
+    def bad_setup():
+        raise OSError("no stream")
+
+    with pytest.raises(OSError, match="no stream"):
+        host_pipeline(gen(6), lambda i: i, setup=bad_setup)

@@ -1,6 +1,8 @@
-"""Debug: a forward on stream A while another forward runs on stream B,
-repeated; the earliest intermediate of A (forward order) that differs from a
-serial run of the same batch."""
+"""Debug: a forward on stream A while another forward (or a background
+kernel loop: modes conv / gn / torch) runs on stream B, repeated; the earliest
+intermediate of A (forward order) that differs from a serial run of the same
+batch.  This located the packed-FP32 GroupNorm nondeterminism (see
+_build.DEVICE_FLAGS): python tools/dbg_race.py fp16 24 same."""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -13,7 +15,7 @@ dt = sys.argv[1] if len(sys.argv) > 1 else "fp16"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 mode = sys.argv[3] if len(sys.argv) > 3 else "same"   # same | other (second handle) | conv (background conv)
 order = ["res2", "res3", "res4", "res5", "fpn_lateral5", "fpn_inner5", "fpn_output5", "p5",
-         "fpn_lateral4", "fpn_inner4", "fpn_output4", "p4", "p3", "p2", "p6", "proposals", "proposal_scores",
+         "fpn_lateral4", "fpn_inner4", "fpn_output4", "p4", "fpn_inner3", "p3", "fpn_inner2", "p2", "p6", "proposals", "proposal_scores",
          "proposal_count", "box_pooled", "box_pred", "mask_logits"]
 if os.environ.get("MDX_DEBUG_SHADOW"):
     order = order[:4] + ["shadow_gnws5", "gnws5"] + [f"{k}{l}" for l in (5, 4, 3, 2) for k in ("fpn_lateral", "shadow_inner", "fpn_inner",
@@ -33,6 +35,8 @@ tdt = torch.float16 if dt == "fp16" else torch.float32
 bx = torch.randn(8, 112, 128, 256).to(tdt).cuda()
 bw = (torch.randn(256, 2304) * 0.02).to(tdt).cuda()
 bo = torch.empty(8, 112, 128, 256, dtype=tdt, device="cuda")
+gg, gb = torch.ones(256, device="cuda"), torch.zeros(256, device="cuda")
+gws = torch.empty(1 << 22, dtype=torch.float32, device="cuda")
 
 
 def background(n):
@@ -40,10 +44,20 @@ def background(n):
         if mode == "conv":
             call("mdx_conv2d", P(bx), 8, 112, 128, 256, P(bw), None, 256, 3, 3, 1, 1, None, 0, 0, int(dt == "fp16"),
                  int(dt == "fp16"), P(bo), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        elif mode == "gn":
+            call("mdx_groupnorm", P(bx), 8, 112, 128, 256, 32, 1e-5, P(gg), P(gb), None, 0,
+                 int(dt == "fp16"), P(bo), P(gws), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        elif mode == "torch":
+            bo.copy_(bx)
+            bo.mul_(1.5)
         else:
             mb.forward(xb, lut)
 
 
+# DBG_SET="fn:arg[:arg],fn:arg": planner knobs set before the runs (bisecting the kernels involved)
+for spec in filter(None, os.environ.get("DBG_SET", "").split(",")):
+    fn, *args = spec.split(":")
+    print("set", fn, args, "->", call(fn, *[int(v) for v in args]))
 ref = m.forward(xa, lut)
 torch.cuda.synchronize()
 ref["intermediates"] = {k: m.tensor(k) for k in order}
@@ -64,11 +78,11 @@ for r in range(reps):
     sa.wait_event(ev); sb.wait_event(ev)
     # B first so that A's kernels overlap B's in varying phase
     with torch.cuda.stream(sb):
-        background(r % 3 + (3 if mode == "conv" else 0))
+        background(r % 3 + (int(os.environ.get("DBG_BG", "3")) if mode in ("conv", "gn", "torch") else 0))
     with torch.cuda.stream(sa):
         oa = m.forward(xa, lut)
     with torch.cuda.stream(sb):
-        background(1 + (3 if mode == "conv" else 0))
+        background(1 + (int(os.environ.get("DBG_BG", "3")) if mode in ("conv", "gn", "torch") else 0))
     torch.cuda.synchronize()
     with torch.cuda.stream(sa):
         inter = {k: m.tensor(k) for k in order}
@@ -87,6 +101,14 @@ for r in range(reps):
         if not torch.equal(torch.nan_to_num(a.float(), nan=7e7), torch.nan_to_num(b.float(), nan=7e7)):
             d = (a.float() - b.float()).abs()
             first = (k, int((d != 0).sum()), float(d.max()))
+            if os.environ.get("DBG_DETAIL") and d.dim() == 4:
+                Bn, Hh, Ww, Cc = d.shape
+                grp = (d != 0).reshape(Bn, Hh * Ww, 32, Cc // 32)  # GN groups of C/32 channels
+                per = grp.float().mean(dim=(1, 3))                # fraction differing per (image, group)
+                bad = (per > 0).nonzero().tolist()
+                pix = (d != 0).any(dim=3).reshape(Bn, -1).sum(1).tolist()
+                print("   detail", k, "img/grp with diffs:", len(bad), bad[:12], "frac", [round(float(per[i, j]), 3) for i, j in bad[:12]],
+                      "pixels differing per image", pix, "ref max", float(a.float().abs().max()), flush=True)
             break
     print(dt, mode, "rep", r, first or "identical", "boxes_equal", bool(torch.equal(oa["boxes"], ref["boxes"])), flush=True)
     hist[first[0] if first else None] = hist.get(first[0] if first else None, 0) + 1
