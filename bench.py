@@ -69,6 +69,15 @@ KERNEL_SYMBOLS = {
              10: "_ZN3mdx6k_convIDF16_fLi128EEEvNS_8ConvArgsE", 11: "_ZN3mdx6k_convIDF16_fLi64EEEvNS_8ConvArgsE"},
     "fp32": {0: "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE"},
 }
+# rocprofv3 reports some kernels demangled
+KERNEL_DEMANGLED = {
+    "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE": "void mdx::k_conv<float, float, 128>(mdx::ConvArgs)",
+    "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE": "void mdx::k_conv<float, float, 64>(mdx::ConvArgs)",
+    "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 128>(mdx::ConvArgs)",
+    "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 64>(mdx::ConvArgs)",
+    "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
+        "void mdx::k_convg<_Float16, 8, false, false, false>(mdx::ConvArgs)",
+}
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
@@ -122,7 +131,9 @@ def roofline_line(per, dtype):
     if sym and os.path.exists(pmc):
         try:
             with open(pmc) as fh:
-                traffic = json.load(fh)["kernels"].get(sym, {}).get("hbm_bytes_per_launch")
+                kern = json.load(fh)["kernels"]
+                rec = kern.get(sym) or kern.get(KERNEL_DEMANGLED.get(sym, ""), {})
+                traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     tot_f = sum(v[0] for v in per.values())

@@ -473,11 +473,11 @@ def heatmaps_to_keypoints(maps, rois):
 
 
 def paste_masks(masks, boxes, img_h, img_w, threshold=0.5):
-    """paste_masks_in_image (skip_empty=False form; identical values)."""
+    """paste_masks_in_image (skip_empty=False form; identical values).
+    threshold=None returns the pasted probabilities (test margins)."""
     N = masks.shape[0]
-    out = torch.zeros((N, img_h, img_w), dtype=torch.bool)
     if N == 0:
-        return out
+        return torch.zeros((N, img_h, img_w), dtype=torch.bool if threshold is not None else torch.float32)
     x0, y0, x1, y1 = torch.split(boxes, 1, dim=1)
     img_y = torch.arange(0, img_h, dtype=torch.float32) + 0.5
     img_x = torch.arange(0, img_w, dtype=torch.float32) + 0.5
@@ -487,7 +487,7 @@ def paste_masks(masks, boxes, img_h, img_w, threshold=0.5):
     gy = img_y[:, :, None].expand(N, img_y.size(1), img_x.size(1))
     grid = torch.stack([gx, gy], dim=3)
     img_masks = F.grid_sample(masks[:, None].float(), grid, align_corners=False)[:, 0]
-    return img_masks >= threshold
+    return img_masks if threshold is None else img_masks >= threshold
 
 
 # ---------------------------------------------------------------- forward
@@ -545,7 +545,8 @@ def forward(sd: Dict[str, torch.Tensor], cfg, images_u8: np.ndarray, keep_interm
             n = len(r["pred_boxes"])
             cls_idx = r["pred_classes"]
             pm = probs[s:s + n][torch.arange(n), cls_idx] if n else probs[:0, 0]
-            r["pred_masks"] = paste_masks(pm, r["pred_boxes"], h, w, cfg.mask_threshold)
+            r["pred_mask_probs"] = paste_masks(pm, r["pred_boxes"], h, w, None)
+            r["pred_masks"] = r["pred_mask_probs"] >= cfg.mask_threshold
             s += n
     if cfg.keypoint_on:
         kx = pooler(feats, dboxes, cfg.keypoint_pooler_resolution, cfg)

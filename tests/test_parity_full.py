@@ -13,7 +13,11 @@ Tolerances (written here, stated in DESIGN.md §4):
     >= 0.98 (fp32) / 0.9 (fp16), |score diff| <= 1e-3 (fp32) / 2e-2 (fp16)
   masks of matched detections: differing pixels <= max(4, 3 % (fp32) /
     10 % (fp16) of the union) -- seeded random weights give masks of a few
-    pixels up to blob size, where an IoU bound alone says little
+    pixels up to blob size, where an IoU bound alone says little.  fp16:
+    the bound applies to the DECISIVE pixels, those whose oracle pasted
+    probability is outside 0.5 +- 0.05 (random weights leave large areas of
+    logits near 0, where fp16's ~1e-2 logit error flips the threshold); the
+    raw differing-pixel counts are recorded as well
   keypoints of matched detections: >= 90 % (fp32) / 75 % (fp16) within 1 px
   downstream (selected mask -> clean -> moments -> angle -> crop):
     selected mask: the mask bound above; centroid within 0.5 px (fp32) /
@@ -33,8 +37,8 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, cen=0.5, ang=1.0),
-       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0)}
+TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, cen=0.5, ang=1.0, margin=0.0),
+       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05)}
 MASK_PX_FLOOR = 4  # pixels: the seeded-weight masks can be a handful of pixels
 
 
@@ -51,9 +55,13 @@ def _mask_iou(a, b):
     return 1.0 if u == 0 else np.logical_and(a, b).sum() / u
 
 
-def _mask_px(a, b):
-    """(differing pixels, union pixels)"""
-    return int(np.logical_xor(a, b).sum()), int(np.logical_or(a, b).sum())
+def _mask_px(a, b, probs=None, margin=0.0):
+    """(differing pixels, union pixels); with the oracle's pasted
+    probabilities and a margin, only pixels outside 0.5 +- margin count"""
+    x = np.logical_xor(a, b)
+    if probs is not None and margin > 0:
+        x &= np.abs(probs - 0.5) > margin
+    return int(x.sum()), int(np.logical_or(a, b).sum())
 
 
 def _mask_ok(diff_union, frac):
@@ -130,7 +138,9 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         rec["score_diff_max"] = float(np.abs(gs[match] - w["scores"].numpy()[:m]).max()) if m else 0.0
         gm = masks_all[i, :n].astype(bool)
         rec["mask_iou"] = [float(_mask_iou(gm[match[j]], w["pred_masks"][j].numpy())) for j in range(m)]
-        rec["mask_px"] = [_mask_px(gm[match[j]], w["pred_masks"][j].numpy()) for j in range(m)]
+        wp = w["pred_mask_probs"].numpy()
+        rec["mask_px_raw"] = [_mask_px(gm[match[j]], w["pred_masks"][j].numpy()) for j in range(m)]
+        rec["mask_px"] = [_mask_px(gm[match[j]], w["pred_masks"][j].numpy(), wp[j], tol["margin"]) for j in range(m)]
         gk = inf["keypoints"][i, :n].cpu().numpy()
         wk = w["pred_keypoints"].numpy()[:m]
         d = np.abs(gk[match][..., :2] - wk[..., :2]).max(-1)
@@ -140,7 +150,9 @@ def _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d,
         d2w = w["pred_masks"][keep[0]].numpy().astype(np.uint8) if keep else np.zeros(prepped.shape[1:], np.uint8)
         d2g = inf["d2_mask"][i].cpu().numpy()
         rec["sel_mask_iou"] = float(_mask_iou(d2g.astype(bool), d2w.astype(bool)))
-        rec["sel_mask_px"] = _mask_px(d2g.astype(bool), d2w.astype(bool))
+        rec["sel_mask_px_raw"] = _mask_px(d2g.astype(bool), d2w.astype(bool))
+        rec["sel_mask_px"] = _mask_px(d2g.astype(bool), d2w.astype(bool), wp[keep[0]] if keep else None,
+                                      tol["margin"])
         cl = O.clean_frames(prepped[i:i + 1], iters_tail=3)
         rec["cleaned_bit_exact"] = bool(np.array_equal(cleaned_d[i].cpu().numpy(), cl[0]))
         fw = O.get_frame_features(cl, 3, mask=d2w[None])
