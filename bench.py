@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="run batches back to back on one stream instead of the multi-stream pipeline")
     ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
+    ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -287,6 +288,9 @@ def main():
     from moseq2_detectron_extract_amd.model import ModelConfig
     from moseq2_detectron_extract_amd.model.runtime import flops_per_image
 
+    if args.dma_f32 is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_dma_f32", args.dma_f32)
     if args.roi_mode is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_roi_align_set_mode", args.roi_mode)

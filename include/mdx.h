@@ -219,6 +219,11 @@ int mdx_conv_set_dma128(int mode, int min_tiles);
 int mdx_conv_set_mfma_prio(int on);
 /* s_setprio(1) around the MFMA bursts of the 256x256 LDS-DMA kernel (0/1). */
 int mdx_conv_set_mfma_prio256(int on);
+/* fp32 layers (Cin % 32 == 0, fp32 output) on the LDS-DMA kernels (16x16x4
+ * f32 MFMAs): 0 never, 1 the 128x128 tile (>= 512 tiles), 2 the 256x256 tile
+ * for layers with >= 500 such tiles and K >= 2048 (default), 3 the 256x256
+ * tile under the fp16 policy.  Returns the old value. */
+int mdx_conv_set_dma_f32(int on);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */

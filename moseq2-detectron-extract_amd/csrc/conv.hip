@@ -18,6 +18,8 @@
 // Output modes: NHWC, or the ConvTranspose(k=2,s=2) pixel shuffle (N = 4*Co).
 // Blocks are remapped XCD-contiguously so the tiles that share an input row
 // panel run on one XCD's L2.
+#include <type_traits>
+
 #include "common.h"
 
 namespace mdx {
@@ -679,10 +681,21 @@ __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 #define MDX_WAIT_LGKM0() \
     do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_waitcnt(0xC07F); asm volatile("" ::: "memory"); } while (0)
 
-template <typename TO, int NW, bool ILV, bool PRIO = false, bool DMA_AFTER = false>
-__global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
+// TIN: operand type.  fp16: a 64-B LDS row is 32 halves (one 16x16x32 f16
+// MFMA per fragment pair); fp32: 16 floats, and each 16-B fragment feeds four
+// 16x16x4 f32 MFMAs (element e of lane (row, piece) is k = 4 piece + e, the
+// same permutation on both operands, so the dot products are unchanged).
+// A K "chunk" is one 128-B run of input channels (64 halves / 32 floats),
+// split into two 64-B substeps.
+template <typename TIN, typename TO, int NW, bool ILV, bool PRIO = false, bool DMA_AFTER = false>
+__global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
+    constexpr bool F32 = sizeof(TIN) == 4;
+    constexpr int VEC = 16 / (int)sizeof(TIN);  // elements per 16-B piece
+    constexpr int SUBK = 4 * VEC;               // K elements per substep (one 64-B row)
+    constexpr int CHK = 2 * SUBK;               // channels per chunk
+    static_assert(!(F32 && ILV), "the interleaved DMA schedule is fp16-only");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int tile;
     {
@@ -696,13 +709,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     const int wm = wid / GT::WN, wn = wid - wm * GT::WN;
 
     // DMA descriptors: instruction j of wave w fills LDS rows 32w + 16j .. +16
-    const _Float16 *X = reinterpret_cast<const _Float16 *>(a.x);
-    const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
+    const TIN *X = reinterpret_cast<const TIN *>(a.x);
+    const TIN *Wt = reinterpret_cast<const TIN *>(a.w);
     const int ohw = a.OH * a.OW;
     int a_iy0[2], a_ix0[2];
     long long a_base[2];
     bool a_ok[2];
-    const _Float16 *b_src[2];
+    const TIN *b_src[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int r = 32 * wid + 16 * j + (lane >> 2);
@@ -714,9 +727,9 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         const int oy = rem / a.OW, ox = rem - oy * a.OW;
         a_iy0[j] = oy * a.stride - a.pad;
         a_ix0[j] = ox * a.stride - a.pad;
-        a_base[j] = (long long)b * a.H * a.W * a.Cin + c * 8;
+        a_base[j] = (long long)b * a.H * a.W * a.Cin + c * VEC;
         const int gn = n0 + r;
-        b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * 8 : nullptr;
+        b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * VEC : nullptr;
     }
     // issue state (uniform): the 64-chunk being issued and its tap
     // split-K: slice z = blockIdx.y multiplies substeps [s0, s0 + T) of the
@@ -727,14 +740,14 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         const int q = s0 >> 1, taps = a.KH * a.KW;
         i_half = s0 & 1;
         const int tap = q % taps;
-        i_kci = (q / taps) * 64;
+        i_kci = (q / taps) * CHK;
         i_kky = tap / a.KW;
         i_kkx = tap - i_kky * a.KW;
     }
     // DMA piece p of the substep being issued into buffer buf: p = 0, 1 the A
     // rows of instruction j = p, p = 2, 3 the B rows of j = p - 2
     auto issue_piece = [&](int buf, int p) {
-        const int kofs = i_kci + 32 * i_half;
+        const int kofs = i_kci + SUBK * i_half;
         if (p < 2) {
             const int j = p;
             const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
@@ -759,7 +772,7 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
                 i_kkx = 0;
                 if (++i_kky == a.KH) {
                     i_kky = 0;
-                    i_kci += 64;
+                    i_kci += CHK;
                 }
             }
         }
@@ -771,29 +784,45 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    const int T = min(a.K / 32 - s0, a.ksteps);  // substeps of this slice
+    const int T = min(a.K / SUBK - s0, a.ksteps);  // substeps of this slice
     // fragment rows of this lane: r = 16 i + (lane & 15) (+ multiples of 64)
     const int off = ((lane >> 4) ^ g_swz(lane & 15)) * 16;
     const char *Abase = smem + (wm * GT::WROWS + (lane & 15)) * 64 + off;
     const char *Bbase = smem + BM * 64 + (wn * GT::WCOLS + (lane & 15)) * 64 + off;
     // fragments are register double-buffered: the LDS reads of substep t+1
     // are in flight while the MFMAs of substep t run from registers
-    half8 fa[2][TI], fb[2][TJ];
+    using frag_t = typename std::conditional<F32, float4v, half8>::type;
+    // fp16: register double-buffered fragments; fp32: one set (its MFMA burst
+    // per substep is 8x longer, the other wave of the SIMD covers the reads,
+    // and two sets would spill at the 256-VGPR budget)
+    constexpr int NSET = (F32 && NW == 8) ? 1 : 2;
+    frag_t fa[NSET][TI], fb[NSET][TJ];
     auto read_frags = [&](int t, int set) {
         const char *Ab = Abase + (t & 3) * SUB;
         const char *Bb = Bbase + (t & 3) * SUB;
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) fb[set][j] = *reinterpret_cast<const half8 *>(Bb + j * 16 * 64);
+        for (int j = 0; j < TJ; ++j) fb[set][j] = *reinterpret_cast<const frag_t *>(Bb + j * 16 * 64);
 #pragma unroll
-        for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const half8 *>(Ab + i * 16 * 64);
+        for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const frag_t *>(Ab + i * 16 * 64);
     };
     auto mma = [&](int set) {
         if (PRIO) __builtin_amdgcn_s_setprio(1);  // the wave in its MFMA burst keeps the issue slots
+        if constexpr (F32) {
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int j = 0; j < TJ; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[set][i][e], fb[set][j][e], acc[i][j], 0,
+                                                                          0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+        }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
     };
     // wait until substep u has landed (4 DMAs per thread per substep)
@@ -810,17 +839,36 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
     if (T > 1) issue(1);
     if (T > 2) issue(2);
     int issued = T < 3 ? T - 1 : 2;
+    if constexpr (NSET == 1) {
+        // substep t: [wait t, barrier, read frags t, DMA t+3] then its MFMAs
+        // (buffer (t+3)&3 == (t-1)&3: every wave drained its reads of t-1
+        // before the barrier)
+        for (int t = 0; t < T; ++t) {
+            wait_landed(t, issued);
+            MDX_WAIT_LGKM0();
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            read_frags(t, 0);
+            if (t + 3 < T) {
+                issue((t + 3) & 3);
+                issued = t + 3;
+            }
+            mma(0);
+        }
+    } else {
     wait_landed(0, issued);
     __builtin_amdgcn_s_barrier();
     read_frags(0, 0);
     // iteration t: [wait t+1, barrier, DMA t+3, read frags t+1] then MFMAs of t
     // MFMAs q0 .. q1 - 1 of the wave's TI x TJ tile loop
     auto mma_range = [&](int set, int q0, int q1) {
+        if constexpr (!F32) {
 #pragma unroll
-        for (int q = 0; q < TI * TJ; ++q) {
-            if (q < q0 || q >= q1) continue;
-            const int i = q / TJ, j = q - i * TJ;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+            for (int q = 0; q < TI * TJ; ++q) {
+                if (q < q0 || q >= q1) continue;
+                const int i = q / TJ, j = q - i * TJ;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
+            }
         }
     };
     // Every step -- the last one too -- waits, crosses the barrier and reads
@@ -839,7 +887,7 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
             asm volatile("" ::: "memory");
             read_frags(t + 1, cur ^ 1);
             if (t + 3 < T) {
-                if (ILV) {
+                if constexpr (ILV) {
                     // the four DMA pieces ride in the MFMA issue gaps instead of
                     // stalling every wave right after the barrier
                     constexpr int QP = TI * TJ / 4;
@@ -886,6 +934,7 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, 1) void k_convg(ConvArgs a) {
         step(t + 1, 1);
     }
     if (t < T) step(t, 0);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
@@ -967,6 +1016,17 @@ static int g_dma_after = 0;
 extern "C" int mdx_conv_set_dma_after(int on) {
     const int old = g_dma_after;
     g_dma_after = on;
+    return old;
+}
+// fp32 layers on the LDS-DMA kernels: 0 never, 1 the 128x128 tile for layers
+// with >= 512 tiles, 2 the 256x256 tile for the big deep-K layers (default:
+// measured +1-2 % on the FPN/RPN p2 3x3 and box fc1 layers; the 128x128 tile
+// and the 256x256 tile on smaller layers lose to k_conv<128>), 3 the 256x256
+// tile under the fp16 policy
+static int g_dma_f32 = 2;
+extern "C" int mdx_conv_set_dma_f32(int on) {
+    const int old = g_dma_f32;
+    g_dma_f32 = on;
     return old;
 }
 // s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
@@ -1104,33 +1164,54 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     // 128x128 tile (DMA pieces interleaved with the MFMAs) for layers with
     // many tiles, the 256x256 tile by policy, else the register-staged kernel
     // (with split-K) below, which serves the small grids better
-    if (in_dtype == 1 && Cin % 64 == 0 && (ksplit == 1 || ksplit == 0) && KH * KW * Cin > g_narrow_kmax) {
+    // fp32 operands (Cin % 32 == 0, fp32 out): the 256x256 kernel on 16x16x4 f32
+    // MFMAs, same LDS image (64-B rows of 16 floats)
+    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32;
+    if (((in_dtype == 1 && Cin % 64 == 0) || dma_f32) && (ksplit == 1 || ksplit == 0) &&
+        KH * KW * Cin > g_narrow_kmax) {
+        const int subk = in_dtype == 1 ? 32 : 16;  // K elements per 64-B substep
         const long long t128 = ceil_div(M, 128) * ceil_div(Cout, 128);
-        if (g_dma128 == 2 || (g_dma128 == 1 && Cout > 64 && t128 >= g_dma128_min_tiles)) {
+        if (in_dtype == 0 && g_dma_f32 == 1 && Cout > 64 && (g_large_tiles == 2 || t128 >= 512)) {
+            // fp32: the 128x128 LDS-DMA tile, two workgroups per CU (their
+            // barriers interleave, so one wave's fragment reads overlap the
+            // other's MFMA bursts)
+            using G4 = GTile<4>;
+            a.tiles_n = (int)ceil_div(Cout, G4::BN);
+            a.tiles_total = (int)t128;
+            a.ksplit = 1;
+            a.ksteps = a.K / subk;
+            hipLaunchKernelGGL((k_convg<float, float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s,
+                               a);
+            t_plan_kernel = MDX_CONV_KERNEL_DMA128;
+            t_plan_ksplit = 1;
+            MDX_CHECK_LAUNCH("mdx_conv2d");
+            return MDX_OK;
+        }
+        if (in_dtype == 1 && (g_dma128 == 2 || (g_dma128 == 1 && Cout > 64 && t128 >= g_dma128_min_tiles))) {
             using G4 = GTile<4>;
             a.tiles_n = (int)ceil_div(Cout, G4::BN);
             a.tiles_total = (int)t128;
             a.ksplit = 1;
             a.ksteps = a.K / 32;
             if (out_dtype == 1 && g_prio)
-                hipLaunchKernelGGL((k_convg<_Float16, 4, true>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 4, true>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
             else if (out_dtype == 1)
-                hipLaunchKernelGGL((k_convg<_Float16, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s,
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s,
                                    a);
             else
-                hipLaunchKernelGGL((k_convg<float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, float, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
             t_plan_kernel = MDX_CONV_KERNEL_DMA128;
             t_plan_ksplit = 1;
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && t256 >= 384;
+        const bool big = Cout >= 192 && (in_dtype == 1 || g_dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 2048);
         // split-K on the 256x256 kernel for layers with few tiles but a deep
         // K (res4/res5 and head 3x3 convs): enough slices to fill the chip
         int ks256 = 1;
         if (!big && g_split256 && workspace && Cout % 256 == 0 && ksplit <= 1) {
-            const int nsub = a.K / 32;
+            const int nsub = a.K / subk;
             for (int k = 2; k <= 8; ++k) {
                 if (nsub / k < g_split256_min_sub || (long long)k * M * Cout * 4 > workspace_bytes) break;
                 ks256 = k;
@@ -1142,19 +1223,21 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
             a.ksplit = ks256;
-            a.ksteps = (a.K / 32 + ks256 - 1) / ks256;
-            a.ksplit = (a.K / 32 + a.ksteps - 1) / a.ksteps;
+            a.ksteps = (a.K / subk + ks256 - 1) / ks256;
+            a.ksplit = (a.K / subk + a.ksteps - 1) / a.ksteps;
             a.part = reinterpret_cast<float *>(workspace);
             const dim3 grid256((unsigned)a.tiles_total, (unsigned)a.ksplit);
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
-            if (out_dtype == 1 && g_dma_after)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
+            if (in_dtype == 0)
+                hipLaunchKernelGGL((k_convg<float, float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
+            else if (out_dtype == 1 && g_dma_after)
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else if (out_dtype == 1 && g_prio8)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else if (out_dtype == 1)
-                hipLaunchKernelGGL((k_convg<_Float16, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else
-                hipLaunchKernelGGL((k_convg<float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
+                hipLaunchKernelGGL((k_convg<_Float16, float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
             if (a.ksplit > 1) {
                 if (out_dtype == 1)
                     hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)),

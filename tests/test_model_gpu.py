@@ -42,6 +42,7 @@ CONV_CASES = [
     (2, 20, 30, 128, 192, 1, 1, 0, True, True),
     (1, 17, 19, 256, 64, 1, 1, 0, False, False),
     (1, 12, 10, 128, 512, 3, 1, 1, True, True),
+    (2, 11, 13, 96, 256, 3, 1, 1, False, True),   # Cin % 32 == 0, % 64 != 0 (fp32 LDS-DMA kernel)
 ]
 
 
@@ -104,12 +105,13 @@ def test_conv2d(mdx, dtype, case, ksplit):
         finally:
             call("mdx_conv_set_stream1x1", old, 65536)
     elif ksplit == "split256":
-        if dtype != "fp16" or Cin % 64 or Cout % 256:
-            pytest.skip("256x256 split-K: fp16, Cin % 64 == 0, Cout % 256 == 0")
+        if Cin % (64 if dtype == "fp16" else 32) or Cout % 256:
+            pytest.skip("256x256 split-K: Cin % 64 (fp16) / 32 (fp32) == 0, Cout % 256 == 0")
         nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
         ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
         old_nk = call("mdx_conv_set_narrow_kmax", 0)
         old = call("mdx_conv_set_split256", 2, 1)
+        old_f = call("mdx_conv_set_dma_f32", 2)
         try:
             call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu),
                  0, dc, dc, P(out), 0, P(ws), nb, None)
@@ -117,20 +119,30 @@ def test_conv2d(mdx, dtype, case, ksplit):
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
             assert kid.value == 2 and (ks_.value > 1 or Cin * k * k <= 32)
         finally:
+            call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_split256", old, 18)
             call("mdx_conv_set_narrow_kmax", old_nk)
     elif ksplit in ("large", "dma128"):
-        if dtype != "fp16" or Cin % 64:
-            pytest.skip("LDS-DMA kernels: fp16, Cin % 64 == 0")
+        if (dtype != "fp16" and ksplit == "dma128") or Cin % (64 if dtype == "fp16" else 32):
+            pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 one fp16 only")
         old_nk = call("mdx_conv_set_narrow_kmax", 0)
         old = call("mdx_conv_set_large_tiles", 2 if ksplit == "large" else 0)
         old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
         old_i = call("mdx_conv_set_mfma_prio", int(case[0] % 2 == 0))  # both DMA schedules across the cases
         old_da = call("mdx_conv_set_dma_after", int(case[1] % 2 == 0))
+        f32_mode = 1 + CONV_CASES.index(case) % 2  # fp32: the 128x128 (1) and 256x256 (2) variants across the cases
+        old_f = call("mdx_conv_set_dma_f32", f32_mode)
         try:
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            if dtype == "fp32" and Cout > 64:
+                assert kid.value == (3 if f32_mode == 1 else 2)
+            elif dtype == "fp16":
+                assert kid.value == (2 if ksplit == "large" else 3)
         finally:
+            call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_large_tiles", old)
             call("mdx_conv_set_narrow_kmax", old_nk)
             call("mdx_conv_set_dma128", old_d, 1536)
