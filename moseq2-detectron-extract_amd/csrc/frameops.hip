@@ -264,7 +264,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict_
 // the reference's first blob in scan order).  Traces started inside a hole
 // produce hole borders whose area never exceeds their blob's outer border.
 // ---------------------------------------------------------------------------
-constexpr int MOM_THREADS = 256;
+constexpr int MOM_THREADS = 1024;
 
 struct Green {
     long long a00, a10, a01, a20, a11, a02;
@@ -292,12 +292,13 @@ __device__ __forceinline__ int getbit(const uint32_t *bits, int pww, int px, int
     return (bits[py * pww + (px >> 5)] >> (px & 31)) & 1;
 }
 
-// bits (x-1 .. x+1) of padded row y as a 3-bit value
+// bits (x-1 .. x+1) of padded row y as a 3-bit value.  Both words are read
+// unconditionally (one ds_read2_b32, no branch on the trace's critical path;
+// the LDS image has a slack word after its last row)
 __device__ __forceinline__ uint32_t row3(const uint32_t *bits, int pww, int x, int y) {
     const int xm = x - 1, w = xm >> 5, b = xm & 31;
     const uint32_t *r = bits + y * pww + w;
-    uint64_t v = r[0];
-    if (b > 29) v |= (uint64_t)r[1] << 32;
+    const uint64_t v = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
     return (uint32_t)(v >> b) & 7u;
 }
 
@@ -308,6 +309,23 @@ __device__ __forceinline__ uint32_t nbmask(const uint32_t *bits, int pww, int x,
            ((d & 1u) << 5) | (((d >> 1) & 1u) << 6) | (((d >> 2) & 1u) << 7);
 }
 
+// One edge of green_edge between 8-neighbouring contour points (|dx|, |dy| <=
+// 1) of a frame with both sides <= 512: every per-edge product fits in int32
+// (|dxy| <= 1024, the largest term 1024 * 1.58e6 < 2^31), only the sums need
+// int64 -- the same integers as green_edge with a fraction of the 64-bit
+// multiplies.
+__device__ __forceinline__ void green_edge_small(Green &g, int xi_1, int yi_1, int xi, int yi) {
+    const int dxy = xi_1 * yi - xi * yi_1;
+    const int xii_1 = xi_1 + xi, yii_1 = yi_1 + yi;
+    g.a00 += dxy;
+    g.a10 += dxy * xii_1;
+    g.a01 += dxy * yii_1;
+    g.a20 += dxy * (xi_1 * xii_1 + xi * xi);
+    g.a11 += dxy * (xi_1 * (yii_1 + yi_1) + xi * (yii_1 + yi));
+    g.a02 += dxy * (yi_1 * yii_1 + yi * yi);
+}
+
+template <bool SMALL>
 __device__ Green trace_outer(const uint32_t *bits, int pww, int x0, int y0, long long max_steps) {
     Green g = {0, 0, 0, 0, 0, 0};
     // first fg neighbour clockwise from W: directions 3, 2, 1, 0, 7, 6, 5 (4 = none)
@@ -337,7 +355,10 @@ __device__ Green trace_outer(const uint32_t *bits, int pww, int x0, int y0, long
         s = (r + __builtin_ctz(rot)) & 7;
         const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
         if (!first) {
-            green_edge(g, px, py, x3 - 1, y3 - 1);
+            if constexpr (SMALL)
+                green_edge_small(g, (int)px, (int)py, x3 - 1, y3 - 1);
+            else
+                green_edge(g, px, py, x3 - 1, y3 - 1);
             px = x3 - 1;
             py = y3 - 1;
         }
@@ -347,7 +368,10 @@ __device__ Green trace_outer(const uint32_t *bits, int pww, int x0, int y0, long
         y3 = y4;
         s = (s + 4) & 7;
     }
-    green_edge(g, px, py, sx, sy);
+    if constexpr (SMALL)
+        green_edge_small(g, (int)px, (int)py, (int)sx, (int)sy);
+    else
+        green_edge(g, px, py, sx, sy);
     return g;
 }
 
@@ -394,9 +418,11 @@ __device__ void moments_to_features(const Green &g, double *cen, double *ori, do
     ax[1] = k * sqrt((mu20 + mu02 - common) / m00);
 }
 
+// ithr: the threshold as an integer, v > thr <=> (int)v > ithr for uint8 v
+template <bool SMALL>
 __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restrict__ frames,
                                                          const uint8_t *__restrict__ mask, int H, int W,
-                                                         double thr, double *__restrict__ cen,
+                                                         int ithr, double *__restrict__ cen,
                                                          double *__restrict__ ori, double *__restrict__ axl,
                                                          double *__restrict__ area, int pww) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
@@ -433,18 +459,19 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
                     const uint8_t *me = reinterpret_cast<const uint8_t *>(mv);
                     uint32_t u = 0;
 #pragma unroll
-                    for (int k = 0; k < 31; ++k) u |= (uint32_t)((double)fe[k] > thr && (!my || me[k])) << (k + 1);
-                    if (xb > 0) u |= (uint32_t)((double)fy[xb - 1] > thr && (!my || my[xb - 1]));
+                    for (int k = 0; k < 31; ++k) u |= (uint32_t)((int)fe[k] > ithr && (!my || me[k])) << (k + 1);
+                    if (xb > 0) u |= (uint32_t)((int)fy[xb - 1] > ithr && (!my || my[xb - 1]));
                     word = u;
                 } else {
                     for (int k = 0; k < 32; ++k) {
                         const int x = xb + k - 1;
-                        if (x >= 0 && x < W) word |= (uint32_t)((double)fy[x] > thr && (!my || my[x])) << k;
+                        if (x >= 0 && x < W) word |= (uint32_t)((int)fy[x] > ithr && (!my || my[x])) << k;
                     }
                 }
             }
             bits[w] = word;
         }
+        if (threadIdx.x == 0) bits[nwords] = 0u;  // slack word read by row3
     }
     __syncthreads();
     unsigned long long best = 0ull;
@@ -466,7 +493,7 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
             const int b = __builtin_ctz(cand);
             cand &= cand - 1;
             const int px = wx * 32 + b;
-            const Green g = trace_outer(bits, pww, px, py, max_steps);
+            const Green g = trace_outer<SMALL>(bits, pww, px, py, max_steps);
             const unsigned long long a = (unsigned long long)(g.a00 < 0 ? -g.a00 : g.a00);
             const unsigned long long start = (unsigned long long)py * PW + px;
             const unsigned long long key = (a << 32) | (0xFFFFFFFFull - start);
@@ -801,11 +828,17 @@ extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int
     MDX_REQUIRE(H > 0 && W > 0, "mdx_frame_moments: bad shape");
     if (n == 0) return MDX_OK;
     const int pww = (int)ceil_div(W + 2, 32);
-    const size_t lds = (size_t)(H + 2) * pww * 4;
+    const size_t lds = ((size_t)(H + 2) * pww + 4) * 4;  // + slack words
     MDX_REQUIRE(lds <= 120 * 1024, "mdx_frame_moments: frame %dx%d too large for LDS", H, W);
     MDX_REQUIRE(n <= 0x7fffffff, "mdx_frame_moments: n too large");
-    hipLaunchKernelGGL(k_moments, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask, H, W,
-                       thr, centroid, orientation, axis_length, area, pww);
+    // v > thr for uint8 v <=> v > floor(thr) (NaN: never)
+    const int ithr = thr != thr ? 255 : thr < 0 ? -1 : thr >= 255 ? 255 : (int)floor(thr);
+    if (H <= 512 && W <= 512)
+        hipLaunchKernelGGL(k_moments<true>, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask,
+                           H, W, ithr, centroid, orientation, axis_length, area, pww);
+    else
+        hipLaunchKernelGGL(k_moments<false>, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask,
+                           H, W, ithr, centroid, orientation, axis_length, area, pww);
     MDX_CHECK_LAUNCH("mdx_frame_moments");
     return MDX_OK;
 }

@@ -196,3 +196,25 @@ def test_compute_scalars_and_keypoints_on_device_match_reference(mdx):
                              true_depth=660.0)
     for i, k in enumerate(list(gf["kd_keys"])):
         np.testing.assert_allclose(kd[k], gf[f"kd_{i}"], rtol=1e-12, atol=1e-9, equal_nan=True, err_msg=k)
+
+
+@pytest.mark.parametrize("shape,thr", [((3, 64, 600), 3.0), ((3, 530, 80), 2.5), ((2, 423, 511), -1.0),
+                                       ((2, 423, 511), 254.5), ((2, 40, 50), 7.0)])
+def test_frame_moments_sizes_and_thresholds(mdx, shape, thr):
+    """Both contour-sum paths (sides <= 512: int32 per-edge products; larger
+    frames: int64) and the integer form of the threshold (fractional,
+    negative, near 255) against the oracle, bit for bit."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    rng = np.random.default_rng(sum(shape))
+    n, h, w = shape
+    f = np.zeros(shape, np.uint8)
+    for i in range(n):
+        y0, x0 = rng.integers(0, h // 3), rng.integers(0, w // 3)
+        f[i, y0:y0 + h // 2, x0:x0 + w // 2] = rng.integers(0, 256, (h // 2, w // 2))
+    f[0, : h // 4, : w // 4] = 255
+    got = proc.frame_moments(f, None, thr)
+    want = O.get_frame_features(f, thr)
+    for k in ("centroid", "axis_length", "area"):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), want[k], err_msg=k)
+    np.testing.assert_allclose(got["orientation"].cpu().numpy(), want["orientation"], atol=1e-14)
