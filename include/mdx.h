@@ -286,6 +286,11 @@ int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, c
                   const float *beta, const void *up, int fuse, int dtype, void *out, float *workspace,
                   mdx_stream_t stream);
 
+/* RPN top-k policy (testing / timing): 1 (default) splits every (image,
+ * level) over several workgroups (per-slice top-k, then a merge), 0 one
+ * workgroup per (image, level).  Returns the old value. */
+int mdx_rpn_set_sliced(int on);
+
 /* RPN find_top_rpn_proposals: per level head tensor float32 (B,H_l,W_l,A*5)
  * = [objectness(A), deltas(A*4)]; cell_anchors float32 [L][A][4].
  * out_boxes (B,post_topk,4), out_scores (B,post_topk) (logits, -inf pad),

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mdx_conv_set_mfma_prio": (I32, [I32]),
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
     "mdx_conv_set_dma_f32": (I32, [I32]),
+    "mdx_rpn_set_sliced": (I32, [I32]),
     "mdx_conv2d_last_plan": (I32, [P, P]),
     "mdx_conv_set_stream1x1": (I32, [I32, I32]),
     "mdx_conv_set_split256": (I32, [I32, I32]),

@@ -378,108 +378,20 @@ struct RpnLevels {
     float offset, img_h, img_w, min_size, clampv;
 };
 
-constexpr int TOPK_THREADS = 1024, TOPK_MAX = 1024;
-
-__global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *__restrict__ ws_boxes,
-                                                           float *__restrict__ ws_scores, int *__restrict__ ws_valid,
-                                                           int *__restrict__ ws_k) {
-    __shared__ unsigned hist[256];
-    __shared__ unsigned s_key[TOPK_MAX], s_val[TOPK_MAX];
-    __shared__ unsigned s_prefix, s_kk, s_cnt_gt, s_cnt_eq;
-    const int seg = blockIdx.x;  // b * L + l
+// decode the k score-sorted anchors s_val[0..k) of segment seg (image b,
+// level l) into boxes (apply_deltas, clip, nonempty), scores, valid flags
+__device__ void rpn_decode(const RpnLevels &rl, int seg, int k, const unsigned *s_val, float *__restrict__ ws_boxes,
+                           float *__restrict__ ws_scores, int *__restrict__ ws_valid, int *__restrict__ ws_k) {
     const int b = seg / rl.L, l = seg - b * rl.L;
     const int A = rl.A, CH = A * 5;
     const int HW = rl.H[l] * rl.W[l];
-    const int n = HW * A;
-    const int k = n < rl.pre_topk ? n : rl.pre_topk;
     const float *hd = rl.head[l] + (long long)b * HW * CH;
-    auto keyat = [&](int i) {
-        const int pix = i / A, a = i - pix * A;
-        return fkey(hd[(long long)pix * CH + a]);
-    };
-    // radix select of the k-th largest key
-    unsigned prefix = 0, mask = 0, kk = (unsigned)k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int i = threadIdx.x; i < 256; i += TOPK_THREADS) hist[i] = 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
-            const unsigned key = keyat(i);
-            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned above = 0;
-            int d = 255;
-            for (; d > 0; --d) {
-                if (above + hist[d] >= kk) break;
-                above += hist[d];
-            }
-            s_prefix = prefix | ((unsigned)d << shift);
-            s_kk = kk - above;
-        }
-        __syncthreads();
-        prefix = s_prefix;
-        kk = s_kk;
-        mask |= 255u << shift;
-        __syncthreads();
-    }
-    const unsigned T = prefix;  // k-th largest key; take kk of the ties (lowest indices)
-    if (threadIdx.x == 0) {
-        s_cnt_gt = 0;
-        s_cnt_eq = 0;
-    }
-    for (int i = threadIdx.x; i < TOPK_MAX; i += TOPK_THREADS) {
-        s_key[i] = 0;
-        s_val[i] = 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    const unsigned n_gt = (unsigned)k - kk;
-    // keys > T (any order, sorted later); keys == T in index order (ordered scan)
-    for (int base = 0; base < n; base += TOPK_THREADS) {
-        const int i = base + threadIdx.x;
-        unsigned key = 0;
-        bool gt = false, eq = false;
-        if (i < n) {
-            key = keyat(i);
-            gt = key > T;
-            eq = key == T;
-        }
-        if (gt) {
-            const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
-            s_key[pos] = key;
-            s_val[pos] = (unsigned)i;
-        }
-        // ordered compaction of ties: prefix count within the chunk
-        const unsigned long long bal = __ballot(eq);
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        __shared__ unsigned wcnt[TOPK_THREADS / 64];
-        if (lane == 0) wcnt[wid] = (unsigned)__popcll(bal);
-        __syncthreads();
-        if (eq) {
-            unsigned before = s_cnt_eq;
-            for (int w2 = 0; w2 < wid; ++w2) before += wcnt[w2];
-            before += (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-            if (before < kk) {
-                s_key[n_gt + before] = key;
-                s_val[n_gt + before] = (unsigned)i;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned tot = 0;
-            for (int w2 = 0; w2 < TOPK_THREADS / 64; ++w2) tot += wcnt[w2];
-            s_cnt_eq += tot;
-        }
-        __syncthreads();
-    }
-    bitonic_desc(s_key, s_val, TOPK_MAX);
-    // decode the k sorted entries
     const int st = rl.stride[l];
     float *ob = ws_boxes + (long long)seg * rl.pre_topk * 4;
     float *os = ws_scores + (long long)seg * rl.pre_topk;
     int *ov = ws_valid + (long long)seg * rl.pre_topk;
     const float wts[4] = {1.f, 1.f, 1.f, 1.f};
-    for (int r = threadIdx.x; r < k; r += TOPK_THREADS) {
+    for (int r = threadIdx.x; r < k; r += blockDim.x) {
         const int i = (int)s_val[r];
         const int pix = i / A, a = i - pix * A;
         const int y = pix / rl.W[l], x = pix - y * rl.W[l];
@@ -505,6 +417,363 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *
         ov[r] = (fin && ne) ? 1 : 0;
     }
     if (threadIdx.x == 0) ws_k[seg] = k;
+}
+
+// Wave 0 of the block: the radix digit of a descending select.  d = the
+// largest d >= 1 with S(d) = sum_{d' >= d} hist[d'] >= kk, else 0; returns
+// through *s_d, *s_above (= S(d + 1)) and *s_cnt (= hist[d]).
+__device__ void pick_digit(const unsigned *hist, unsigned kk, unsigned *s_d, unsigned *s_above, unsigned *s_cnt) {
+    const int lane = threadIdx.x & 63;
+    unsigned h[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = hist[4 * lane + q];
+    const unsigned lsum = h[0] + h[1] + h[2] + h[3];
+    unsigned suf = lsum;
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned t = __shfl_down(suf, off);
+        if (lane + off < 64) suf += t;
+    }
+    unsigned S[4];
+    S[3] = suf - lsum + h[3];
+    S[2] = S[3] + h[2];
+    S[1] = S[2] + h[1];
+    S[0] = S[1] + h[0];
+    int qbest = -1;
+#pragma unroll
+    for (int q = 3; q >= 0; --q)
+        if (qbest < 0 && 4 * lane + q >= 1 && S[q] >= kk) qbest = q;
+    const unsigned long long any = __ballot(qbest >= 0);
+    const int lb = any ? 63 - __builtin_clzll(any) : 0;
+    const int qb = any ? __shfl(qbest, lb) : 0;
+    const int Sd = __shfl((int)(qb == 3 ? S[3] : qb == 2 ? S[2] : qb == 1 ? S[1] : S[0]), lb);
+    const int hd = __shfl((int)(qb == 3 ? h[3] : qb == 2 ? h[2] : qb == 1 ? h[1] : h[0]), lb);
+    if (lane == 0) {
+        *s_d = (unsigned)(4 * lb + qb);
+        *s_above = (unsigned)Sd - (unsigned)hd;
+        *s_cnt = (unsigned)hd;
+    }
+}
+
+// Exact top-kk of the block's register-held unique 64-bit keys (descending):
+// returns (mask, prefix) such that the selected keys are exactly those with
+// (key & mask) >= prefix -- 8-bit radix passes from the top, stopping early
+// once a digit's whole bin is taken.
+template <int KPT, int NT>
+__device__ void select_top64(const unsigned long long (&kr)[KPT], const bool (&ok)[KPT], unsigned kk, unsigned *hist,
+                             unsigned *s_sel, unsigned long long &mask_out, unsigned long long &prefix_out) {
+    unsigned long long prefix = 0, mask = 0;
+    const int wid = threadIdx.x >> 6;
+    for (int shift = 56; shift >= 0 && kk > 0; shift -= 8) {
+        for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+            if (ok[j] && (kr[j] & mask) == prefix) atomicAdd(&hist[(unsigned)(kr[j] >> shift) & 255u], 1u);
+        __syncthreads();
+        if (wid == 0) pick_digit(hist, kk, &s_sel[0], &s_sel[1], &s_sel[2]);
+        __syncthreads();
+        const unsigned d = s_sel[0], above = s_sel[1], cnt = s_sel[2];
+        __syncthreads();
+        prefix |= (unsigned long long)d << shift;
+        mask |= 255ull << shift;
+        kk -= above;
+        if (cnt == kk) break;  // the whole bin is taken
+    }
+    mask_out = mask;
+    prefix_out = prefix;
+}
+
+constexpr int TOPK_THREADS = 1024, TOPK_MAX = 1024;
+constexpr int TOPK_KPT = 44;  // keys per thread held in registers (segments of <= 45056 anchors: p2 of a 448x512 input has 43008)
+
+// INREG: every key of the segment is loaded once into registers (all loads in
+// flight together) and the radix passes and the tie scan run from there;
+// otherwise each pass re-reads the head tensor.
+template <bool INREG>
+__global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *__restrict__ ws_boxes,
+                                                           float *__restrict__ ws_scores, int *__restrict__ ws_valid,
+                                                           int *__restrict__ ws_k) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_key[TOPK_MAX], s_val[TOPK_MAX];
+    __shared__ unsigned s_prefix, s_kk, s_cnt_gt, s_cnt_eq, s_eq;
+    __shared__ unsigned wcnt[TOPK_THREADS / 64];
+    const int seg = blockIdx.x;  // b * L + l
+    const int b = seg / rl.L, l = seg - b * rl.L;
+    const int A = rl.A, CH = A * 5;
+    const int HW = rl.H[l] * rl.W[l];
+    const int n = HW * A;
+    const int k = n < rl.pre_topk ? n : rl.pre_topk;
+    const float *hd = rl.head[l] + (long long)b * HW * CH;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    auto keyat = [&](int i) {
+        const int pix = i / A, a = i - pix * A;
+        return fkey(hd[(long long)pix * CH + a]);
+    };
+    constexpr int NJ = INREG ? TOPK_KPT : 1;
+    unsigned kreg[NJ];
+    if constexpr (INREG) {
+#pragma unroll
+        for (int j = 0; j < TOPK_KPT; ++j) {
+            const int i = j * TOPK_THREADS + threadIdx.x;
+            kreg[j] = i < n ? keyat(i) : 0u;
+        }
+    }
+    // chunk c (elements c * 1024 + tid): key of this thread, valid flag
+    const int nchunks = (n + TOPK_THREADS - 1) / TOPK_THREADS;
+    auto chunk_key = [&](int c, unsigned &key) -> bool {
+        const int i = c * TOPK_THREADS + threadIdx.x;
+        if (i >= n) return false;
+        if constexpr (INREG) {
+            key = 0u;
+#pragma unroll
+            for (int j = 0; j < TOPK_KPT; ++j)
+                if (j == c) key = kreg[j];
+        } else {
+            key = keyat(i);
+        }
+        return true;
+    };
+    // radix select of the k-th largest key
+    unsigned prefix = 0, mask = 0, kk = (unsigned)k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = threadIdx.x; i < 256; i += TOPK_THREADS) hist[i] = 0;
+        __syncthreads();
+        if constexpr (INREG) {
+#pragma unroll
+            for (int j = 0; j < TOPK_KPT; ++j) {
+                if (j >= nchunks) continue;  // (uniform; no break: keeps the loop unrolled, kreg in registers)
+                const int i = j * TOPK_THREADS + threadIdx.x;
+                const unsigned key = kreg[j];
+                const bool ok = i < n && (key & mask) == prefix;
+                if (shift == 24) {
+                    // the top byte is sign + exponent: a wave's keys share a
+                    // handful of bins -- one atomic per distinct bin
+                    const unsigned bin = key >> 24;
+                    unsigned long long rem = __ballot(ok);
+                    while (rem) {
+                        const int leader = __builtin_ctzll(rem);
+                        const unsigned b0 = __builtin_amdgcn_readlane(bin, leader);
+                        const unsigned long long m = __ballot(ok && bin == b0);
+                        if (lane == leader) atomicAdd(&hist[b0], (unsigned)__popcll(m));
+                        rem &= ~m;
+                    }
+                } else if (ok) {
+                    atomicAdd(&hist[(key >> shift) & 255], 1u);
+                }
+            }
+        } else {
+            for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
+                const unsigned key = keyat(i);
+                if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            // digit d = the largest d >= 1 with S(d) = sum_{d' >= d} hist[d'] >= kk,
+            // else 0 (a descending scan from 255); one wave, 4 bins per lane
+            unsigned h[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) h[q] = hist[4 * lane + q];
+            const unsigned lsum = h[0] + h[1] + h[2] + h[3];
+            unsigned suf = lsum;  // sum over lanes >= lane
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned t = __shfl_down(suf, off);
+                if (lane + off < 64) suf += t;
+            }
+            unsigned S[4];
+            S[3] = suf - lsum + h[3];
+            S[2] = S[3] + h[2];
+            S[1] = S[2] + h[1];
+            S[0] = S[1] + h[0];
+            int qbest = -1;
+#pragma unroll
+            for (int q = 3; q >= 0; --q)
+                if (qbest < 0 && 4 * lane + q >= 1 && S[q] >= kk) qbest = q;
+            const unsigned long long any = __ballot(qbest >= 0);
+            const int lbest = any ? 63 - __builtin_clzll(any) : 0;
+            const int qb = __shfl(qbest, lbest);
+            int d = 0;
+            unsigned Sd = 0, hd_ = 0;
+            if (any) {
+                d = 4 * lbest + qb;
+                Sd = __shfl((int)(qb == 3 ? S[3] : qb == 2 ? S[2] : qb == 1 ? S[1] : S[0]), lbest);
+                hd_ = __shfl((int)(qb == 3 ? h[3] : qb == 2 ? h[2] : qb == 1 ? h[1] : h[0]), lbest);
+            } else {
+                Sd = __shfl((int)S[0], 0);  // d = 0: everything
+                hd_ = __shfl((int)h[0], 0);
+            }
+            if (lane == 0) {
+                s_prefix = prefix | ((unsigned)d << shift);
+                s_kk = kk - (Sd - hd_);
+                s_eq = hd_;
+            }
+        }
+        __syncthreads();
+        prefix = s_prefix;
+        kk = s_kk;
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    const unsigned T = prefix;  // k-th largest key; take kk of the ties (lowest indices)
+    const bool all_ties = s_eq == kk;  // every key == T is taken: no ordered scan needed
+    if (threadIdx.x == 0) {
+        s_cnt_gt = 0;
+        s_cnt_eq = 0;
+    }
+    for (int i = threadIdx.x; i < TOPK_MAX; i += TOPK_THREADS) {
+        s_key[i] = 0;
+        s_val[i] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const unsigned n_gt = (unsigned)k - kk;
+    // keys > T (any order, sorted later); keys == T in index order (ordered scan)
+    auto scan_chunk = [&](int c, unsigned key, bool ok) {
+        const int i = c * TOPK_THREADS + threadIdx.x;
+        const bool gt = ok && key > T;
+        const bool eq = ok && key == T;
+        if (gt) {
+            const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
+            s_key[pos] = key;
+            s_val[pos] = (unsigned)i;
+        }
+        // ordered compaction of ties: prefix count within the chunk
+        const unsigned long long bal = __ballot(eq);
+        if (lane == 0) wcnt[wid] = (unsigned)__popcll(bal);
+        __syncthreads();
+        if (eq) {
+            unsigned before = s_cnt_eq;
+            for (int w2 = 0; w2 < wid; ++w2) before += wcnt[w2];
+            before += (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+            if (before < kk) {
+                s_key[n_gt + before] = key;
+                s_val[n_gt + before] = (unsigned)i;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned tot = 0;
+            for (int w2 = 0; w2 < TOPK_THREADS / 64; ++w2) tot += wcnt[w2];
+            s_cnt_eq += tot;
+        }
+        __syncthreads();
+    };
+    if (INREG && all_ties) {
+        // one unordered pass: the kept set is exact, the sort orders it
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            if (j >= nchunks) continue;
+            const int i = j * TOPK_THREADS + threadIdx.x;
+            const unsigned key = kreg[j];
+            if (i < n && key >= T) {
+                const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
+                s_key[pos] = key;
+                s_val[pos] = (unsigned)i;
+            }
+        }
+        __syncthreads();
+    } else if constexpr (INREG) {
+#pragma unroll
+        for (int j = 0; j < TOPK_KPT; ++j)
+            if (j < nchunks) scan_chunk(j, kreg[j], j * TOPK_THREADS + (int)threadIdx.x < n);
+    } else {
+        for (int c = 0; c < nchunks; ++c) {
+            unsigned key = 0;
+            const bool ok = chunk_key(c, key);
+            scan_chunk(c, key, ok);
+        }
+    }
+    bitonic_desc(s_key, s_val, TOPK_MAX);
+    rpn_decode(rl, seg, k, s_val, ws_boxes, ws_scores, ws_valid, ws_k);
+}
+
+// ---------------------------------------------------------------------------
+// RPN top-k over several workgroups per (image, level): the anchors are split
+// into RPN_SLICES slices, each workgroup keeps its slice's top-k by a 64-bit
+// key (score key << 32 | ~index: unique, and larger = earlier in Detectron2's
+// topk order, ties to the lower index), then one workgroup per segment merges
+// the <= RPN_SLICES * k candidates, sorts and decodes them.
+// ---------------------------------------------------------------------------
+constexpr int RPN_SLICES = 8, PART_KPT = 6, MERGE_KPT = 8;
+
+__device__ __forceinline__ unsigned long long rpn_ckey(unsigned key, int i) {
+    return ((unsigned long long)key << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)i);
+}
+
+__global__ __launch_bounds__(TOPK_THREADS) void k_rpn_part(RpnLevels rl, unsigned long long *__restrict__ cand,
+                                                           int *__restrict__ ccount) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_sel[3], s_pos;
+    const int sl = blockIdx.x, seg = blockIdx.y;
+    const int b = seg / rl.L, l = seg - b * rl.L;
+    const int A = rl.A, CH = A * 5;
+    const int HW = rl.H[l] * rl.W[l];
+    const int n = HW * A;
+    const int k = n < rl.pre_topk ? n : rl.pre_topk;
+    const int len = (n + RPN_SLICES - 1) / RPN_SLICES;
+    const int i0 = sl * len, i1 = min(n, i0 + len);
+    const int m = i1 > i0 ? i1 - i0 : 0;
+    const unsigned kk = (unsigned)min(k, m);
+    const float *hd = rl.head[l] + (long long)b * HW * CH;
+    unsigned long long kr[PART_KPT];
+    bool ok[PART_KPT];
+#pragma unroll
+    for (int j = 0; j < PART_KPT; ++j) {
+        const int i = i0 + j * TOPK_THREADS + threadIdx.x;
+        ok[j] = i < i1;
+        const int pix = i / A, a = i - pix * A;
+        kr[j] = ok[j] ? rpn_ckey(fkey(hd[(long long)pix * CH + a]), i) : 0ull;
+    }
+    unsigned long long mask, prefix;
+    select_top64<PART_KPT, TOPK_THREADS>(kr, ok, kk, hist, s_sel, mask, prefix);
+    if (threadIdx.x == 0) s_pos = 0;
+    __syncthreads();
+    unsigned long long *out = cand + ((long long)seg * RPN_SLICES + sl) * rl.pre_topk;
+#pragma unroll
+    for (int j = 0; j < PART_KPT; ++j)
+        if (kk > 0 && ok[j] && (kr[j] & mask) >= prefix) out[atomicAdd(&s_pos, 1u)] = kr[j];
+    if (threadIdx.x == 0) ccount[seg * RPN_SLICES + sl] = (int)kk;
+}
+
+__global__ __launch_bounds__(TOPK_THREADS) void k_rpn_merge_topk(RpnLevels rl,
+                                                                 const unsigned long long *__restrict__ cand,
+                                                                 const int *__restrict__ ccount,
+                                                                 float *__restrict__ ws_boxes,
+                                                                 float *__restrict__ ws_scores,
+                                                                 int *__restrict__ ws_valid, int *__restrict__ ws_k) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_key[TOPK_MAX], s_val[TOPK_MAX];
+    __shared__ unsigned s_sel[3], s_pos;
+    const int seg = blockIdx.x;
+    const int l = seg % rl.L;
+    const int n = rl.H[l] * rl.W[l] * rl.A;
+    const int k = n < rl.pre_topk ? n : rl.pre_topk;
+    const int P = rl.pre_topk;
+    unsigned long long kr[MERGE_KPT];
+    bool ok[MERGE_KPT];
+#pragma unroll
+    for (int j = 0; j < MERGE_KPT; ++j) {
+        const int c = j * TOPK_THREADS + threadIdx.x;  // candidate c: slice c / P, position c % P
+        const int sl = c / P, pos = c - sl * P;
+        ok[j] = sl < RPN_SLICES && pos < ccount[seg * RPN_SLICES + (sl < RPN_SLICES ? sl : 0)];
+        kr[j] = ok[j] ? cand[(long long)seg * RPN_SLICES * P + c] : 0ull;
+    }
+    unsigned long long mask, prefix;
+    select_top64<MERGE_KPT, TOPK_THREADS>(kr, ok, (unsigned)k, hist, s_sel, mask, prefix);
+    for (int i = threadIdx.x; i < TOPK_MAX; i += TOPK_THREADS) {
+        s_key[i] = 0;
+        s_val[i] = 0xFFFFFFFFu;
+    }
+    if (threadIdx.x == 0) s_pos = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MERGE_KPT; ++j)
+        if (ok[j] && (kr[j] & mask) >= prefix) {
+            const unsigned p = atomicAdd(&s_pos, 1u);
+            s_key[p] = (unsigned)(kr[j] >> 32);
+            s_val[p] = 0xFFFFFFFFu - (unsigned)kr[j];
+        }
+    bitonic_desc(s_key, s_val, TOPK_MAX);
+    rpn_decode(rl, seg, k, s_val, ws_boxes, ws_scores, ws_valid, ws_k);
 }
 
 // ---------------------------------------------------------------------------
@@ -549,60 +818,91 @@ __global__ __launch_bounds__(256) void k_nms_mask(const float *__restrict__ boxe
     mask[((long long)seg * cap + i) * words + w] = bits;
 }
 
-// one wave per segment: greedy sweep in score order; invalid boxes never keep
-// nor suppress (Detectron2 removes them before NMS).  Per 64-row chunk the
-// sweep is scalar: the chunk's own removed word and every row's word for the
-// chunk are read with v_readlane, so the serial dependency never waits on
-// memory; the kept rows' full masks are OR-ed into `removed` afterwards.
+// One workgroup per segment: the segment's whole IoU bitmask (k rows x words
+// 64-bit words, <= 128 KB) is first staged into LDS by all 256 threads with
+// every load in flight at once, then wave 0 sweeps it in score order from LDS;
+// invalid boxes never keep nor suppress (Detectron2 removes them before
+// NMS).  Per 64-row chunk the sweep is scalar over the rows still standing:
+// the chunk's removed word and each kept row's word for the chunk are
+// v_readlane'd, and the kept rows' full masks are OR-ed into `removed`
+// afterwards (lane w holds word w).
 constexpr int NMS_MAXW = 16;  // pre_topk <= 1024
-__global__ __launch_bounds__(64) void k_nms_scan(const int *__restrict__ valid, const int *__restrict__ kseg, int cap,
-                                                 int words, const unsigned long long *__restrict__ mask,
-                                                 int *__restrict__ keep) {
-    __shared__ unsigned long long rows[64][NMS_MAXW + 1];
-    const int seg = blockIdx.x, lane = threadIdx.x;
+constexpr int NMS_THREADS = 256;
+__global__ __launch_bounds__(NMS_THREADS) void k_nms_scan(const int *__restrict__ valid, const int *__restrict__ kseg,
+                                                          int cap, int words,
+                                                          const unsigned long long *__restrict__ mask,
+                                                          int *__restrict__ keep) {
+    extern __shared__ unsigned long long rows[];  // [k][words]
+    __shared__ unsigned long long vbits[NMS_MAXW];
+    const int seg = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int k = kseg[seg];
     const int *vl = valid + (long long)seg * cap;
     const unsigned long long *mk = mask + (long long)seg * cap * words;
     int *kp = keep + (long long)seg * cap;
-    unsigned long long removed = 0ull;  // lane w < words holds word w
-    for (int i0 = 0; i0 < k; i0 += 64) {
-        // unconditional loads from a clamped row (a "load or zero" select
-        // compiles to a branch + vmcnt(0) per load), then the select
-        for (int t = lane; t < 64 * words; t += 64) {
-            const int r = t / words, w = t - r * words;
-            const int rc = i0 + r < k ? i0 + r : k - 1;
-            const unsigned long long v = mk[(long long)rc * words + w];
-            rows[r][w] = (i0 + r < k) ? v : 0ull;
-        }
-        const int vraw = vl[i0 + lane < k ? i0 + lane : k - 1];
-        const int vf = (i0 + lane < k) ? vraw : 0;
-        __syncthreads();
-        const int cwi = i0 >> 6;
-        const unsigned long long own = rows[lane][cwi];  // row lane's bits inside this chunk
-        const unsigned long long vmask = __ballot(vf != 0);
-        unsigned long long cw = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(removed >> 32), cwi) << 32) |
-                                (unsigned)__builtin_amdgcn_readlane((unsigned)removed, cwi);
-        const unsigned own_lo = (unsigned)own, own_hi = (unsigned)(own >> 32);
-        const int nr = k - i0 < 64 ? k - i0 : 64;
-        unsigned long long kept = 0ull;
-        for (int r = 0; r < nr; ++r) {
-            if (((cw >> r) & 1ull) || !((vmask >> r) & 1ull)) continue;
-            kept |= 1ull << r;
-            cw |= ((unsigned long long)__builtin_amdgcn_readlane(own_hi, r) << 32) |
-                  (unsigned)__builtin_amdgcn_readlane(own_lo, r);
-        }
-        if (lane < words) {
-            unsigned long long kk = kept;
-            while (kk) {
-                const int r = __builtin_ctzll(kk);
-                kk &= kk - 1;
-                removed |= rows[r][lane];
+    const int total = k * words;
+    if ((((long long)cap * words) & 1) || (reinterpret_cast<uintptr_t>(mask) & 15)) {
+        for (int t = threadIdx.x; t < total; t += NMS_THREADS) rows[t] = mk[t];  // unaligned rows: 8-B pieces
+    } else {
+        // 16-B pieces, 8 loads in flight per thread before their LDS stores
+        // (a load -> store loop waits out the memory latency every iteration)
+        const int npc = total >> 1;
+        const uint4 *src = reinterpret_cast<const uint4 *>(mk);
+        uint4 *dst = reinterpret_cast<uint4 *>(rows);
+        for (int t0 = 0; t0 < npc; t0 += 8 * NMS_THREADS) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + u * NMS_THREADS + threadIdx.x;
+                v[u] = t < npc ? src[t] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + u * NMS_THREADS + threadIdx.x;
+                if (t < npc) dst[t] = v[u];
             }
         }
-        if (lane < nr) kp[i0 + lane] = (int)((kept >> lane) & 1ull);
-        __syncthreads();
+        if ((total & 1) && threadIdx.x == 0) rows[total - 1] = mk[total - 1];
     }
-    for (int i = k + lane; i < cap; i += 64) kp[i] = 0;
+    // valid flags as bits, one 64-row word per wave iteration
+    for (int c = wid; c * 64 < k; c += NMS_THREADS / 64) {
+        const int i = c * 64 + lane;
+        const unsigned long long b = __ballot(i < k && vl[i] != 0);
+        if (lane == 0) vbits[c] = b;
+    }
+    __syncthreads();
+    if (wid == 0) {
+        unsigned long long removed = 0ull;  // lane w < words holds word w
+        for (int i0 = 0; i0 < k; i0 += 64) {
+            const int cwi = i0 >> 6;
+            const int nr = k - i0 < 64 ? k - i0 : 64;
+            const unsigned long long own = lane < nr ? rows[(i0 + lane) * words + cwi] : 0ull;
+            const unsigned own_lo = (unsigned)own, own_hi = (unsigned)(own >> 32);
+            const unsigned long long vmask = vbits[cwi];
+            unsigned long long cw =
+                ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(removed >> 32), cwi) << 32) |
+                (unsigned)__builtin_amdgcn_readlane((unsigned)removed, cwi);
+            unsigned long long kept = 0ull;
+            const unsigned long long live = nr == 64 ? ~0ull : ((1ull << nr) - 1ull);
+            unsigned long long cand = ~cw & vmask & live;
+            while (cand) {
+                const int r = __builtin_ctzll(cand);
+                kept |= 1ull << r;
+                cw |= ((unsigned long long)__builtin_amdgcn_readlane(own_hi, r) << 32) |
+                      (unsigned)__builtin_amdgcn_readlane(own_lo, r);
+                cand = ~cw & vmask & live & ~((2ull << r) - 1ull);
+            }
+            if (lane < words) {
+                unsigned long long kk = kept;
+                while (kk) {
+                    const int r = __builtin_ctzll(kk);
+                    kk &= kk - 1;
+                    removed |= rows[(i0 + r) * words + lane];
+                }
+            }
+            if (lane < nr) kp[i0 + lane] = (int)((kept >> lane) & 1ull);
+        }
+    }
+    for (int i = k + threadIdx.x; i < cap; i += NMS_THREADS) kp[i] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1744,7 +2044,16 @@ extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, f
 extern "C" int64_t mdx_rpn_workspace_bytes(int B, int L, int pre_topk) {
     const long long segs = (long long)B * L;
     const long long words = (pre_topk + 63) / 64;
-    return segs * pre_topk * (16 + 4 + 4 + 4) + segs * 4 + segs * pre_topk * words * 8 + 256;
+    return segs * pre_topk * (16 + 4 + 4 + 4) + segs * 4 + segs * pre_topk * words * 8 + 256 +
+           segs * RPN_SLICES * pre_topk * 8 + segs * RPN_SLICES * 4 + 64;  // sliced top-k candidates
+}
+
+// RPN top-k: several workgroups per (image, level) (1, default) or one (0)
+static int g_rpn_sliced = 1;
+extern "C" int mdx_rpn_set_sliced(int on) {
+    const int old = g_rpn_sliced;
+    g_rpn_sliced = on;
+    return old;
 }
 
 extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
@@ -1779,11 +2088,26 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     int *wk = (int *)ws; ws += segs * 4;
     ws = (char *)(((uintptr_t)ws + 15) & ~(uintptr_t)15);
     unsigned long long *wmask = (unsigned long long *)ws;
+    ws += segs * pre_topk * words * 8;
+    ws = (char *)(((uintptr_t)ws + 15) & ~(uintptr_t)15);
+    unsigned long long *wcand = (unsigned long long *)ws;
+    ws += segs * RPN_SLICES * pre_topk * 8;
+    int *wccount = (int *)ws;
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(k_rpn_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
+    int nmax = 0;
+    for (int l = 0; l < L; ++l) nmax = std::max(nmax, lvl_h[l] * lvl_w[l] * A);
+    if (g_rpn_sliced && nmax <= RPN_SLICES * PART_KPT * TOPK_THREADS) {
+        hipLaunchKernelGGL(k_rpn_part, dim3(RPN_SLICES, (unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount);
+        hipLaunchKernelGGL(k_rpn_merge_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount, wb, wsc,
+                           wv, wk);
+    } else if (nmax <= TOPK_KPT * TOPK_THREADS)
+        hipLaunchKernelGGL(k_rpn_topk<true>, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
+    else
+        hipLaunchKernelGGL(k_rpn_topk<false>, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
     hipLaunchKernelGGL(k_nms_mask, dim3(words, (pre_topk + 255) / 256, (unsigned)segs), dim3(256), 0, s, wb, wk,
                        pre_topk, words, nms_thresh, wmask);
-    hipLaunchKernelGGL(k_nms_scan, dim3((unsigned)segs), dim3(64), 0, s, wv, wk, pre_topk, words, wmask, wkeep);
+    hipLaunchKernelGGL(k_nms_scan, dim3((unsigned)segs), dim3(NMS_THREADS), (size_t)pre_topk * words * 8, s, wv, wk,
+                       pre_topk, words, wmask, wkeep);
     hipLaunchKernelGGL(k_rpn_merge, dim3(B), dim3(1024), 2 * MERGE_MAX * sizeof(unsigned), s, wb, wsc, wkeep, wk, L,
                        pre_topk, post_topk, out_boxes, out_scores, out_count);
     MDX_CHECK_LAUNCH("mdx_rpn_proposals");

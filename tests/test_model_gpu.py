@@ -229,8 +229,10 @@ def test_backbone_fpn_fp32(small_case):
         assert err < 2e-4, f"{k}: rel err {err:.2e}"
 
 
-def test_rpn_proposals_from_identical_heads(mdx):
-    """Same head tensors into the GPU and the oracle proposal selection."""
+@pytest.mark.parametrize("sliced", [1, 0])
+def test_rpn_proposals_from_identical_heads(mdx, sliced):
+    """Same head tensors into the GPU and the oracle proposal selection, with
+    the top-k split over several workgroups per (image, level) and not."""
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
@@ -262,9 +264,13 @@ def test_rpn_proposals_from_identical_heads(mdx):
     ptrs = (ctypes.c_void_p * 5)(*[h.data_ptr() for h in heads])
     ia = lambda v: (ctypes.c_int * len(v))(*v)  # noqa: E731
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]), 5,
-         B, A, cells.ctypes.data_as(ctypes.c_void_p), 0.0, 423, 511, 1000, post, 0.7, 0.0, cfg.bbox_reg_clamp,
-         P(boxes), P(scores), P(cnt), P(ws), None)
+    old = call("mdx_rpn_set_sliced", sliced)
+    try:
+        call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]),
+             5, B, A, cells.ctypes.data_as(ctypes.c_void_p), 0.0, 423, 511, 1000, post, 0.7, 0.0,
+             cfg.bbox_reg_clamp, P(boxes), P(scores), P(cnt), P(ws), None)
+    finally:
+        call("mdx_rpn_set_sliced", old)
     for b in range(B):
         wb, wsc = want[b]
         n = int(cnt[b])
