@@ -2,7 +2,7 @@
 written as depth.dat, then extract.extract_session chunk by chunk (frame
 source -> device hot path -> host angle / tracking step -> crops, scalars,
 keypoints).  Prints frames/s with tracking off and on.
-Usage: python tools/extract_bench.py [nframes] [chunk]"""
+Usage: python tools/extract_bench.py [nframes] [chunk] [fp32|fp16]"""
 import json
 import os
 import sys
@@ -16,6 +16,7 @@ sys.path.insert(0, ROOT)
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
     chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+    dtype = sys.argv[3] if len(sys.argv) > 3 else "fp32"
     import numpy as np
     import torch
     import mdx_pkg
@@ -25,8 +26,8 @@ def main():
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig
     s = synth.SyntheticSession(n, seed=9)
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
-    res = {"nframes": n, "chunk": chunk}
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype)
+    res = {"nframes": n, "chunk": chunk, "dtype": dtype}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         t0 = time.perf_counter()
         s.write(td)
@@ -35,8 +36,8 @@ def main():
         # warm-up on a short prefix (model plans, allocator)
         extract_session(path, s.bground_im, s.roi, pred, ExtractConfig(chunk_size=64, use_tracking=False),
                         true_depth=s.true_depth, frame_trim=(0, n - 64))
-        for rep in range(2):
-            for overlap in (False, True):
+        for rep in range(int(os.environ.get("EXTRACT_REPS", "2"))):
+            for overlap in (True,) if os.environ.get("EXTRACT_OVERLAP_ONLY") else (False, True):
                 for tracking in (False, True):
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
