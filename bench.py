@@ -56,6 +56,7 @@ def parse():
                     help="run batches back to back on one stream instead of the multi-stream pipeline")
     ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
+    ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -82,6 +83,7 @@ KERNEL_DEMANGLED = {
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
+                6: "Winograd F(2x2,3x3) (input transform + 16 batched k_conv GEMMs + output transform)",
                 10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance"}
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 PMC_FILE = {"fp16": "r01_pmc_kernels.json", "fp32": "r02_pmc_kernels_fp32.json"}
@@ -123,7 +125,9 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
 def roofline_line(per, dtype):
     """Roofline object for the dominant conv kernel (most time per step)."""
     peak = PEAK[dtype]
-    key = max(per, key=lambda k: per[k][1])
+    # a single kernel: the Winograd records (6) bracket three kernels and count
+    # direct-convolution FLOPs, so they are reported separately below
+    key = max((k for k in per if k != 6), key=lambda k: per[k][1])
     fl, sec, n, ks = per[key]
     ach = fl / sec / 1e12
     traffic = None
@@ -145,7 +149,11 @@ def roofline_line(per, dtype):
                       f"{fl / n / 1e9:.1f} GFLOP and {sec / n * 1e6:.1f} us per launch (HIP events on the launch "
                       f"stream, serial steps; traffic = PMC HBM bytes per launch, profiles/{PMC_FILE[dtype]})",
             "all_conv": {"launches": round(sum(v[2] for v in per.values())), "tflop_per_step": round(tot_f / 1e12, 3),
-                         "ms_per_step": round(tot_s * 1e3, 3), "achieved": round(tot_f / tot_s / 1e12, 1)}}
+                         "ms_per_step": round(tot_s * 1e3, 3), "achieved": round(tot_f / tot_s / 1e12, 1),
+                         "note": "direct-convolution FLOPs; layers on Winograd F(2x2,3x3) execute 1/2.25 of them"},
+            **({"winograd": {"layers_per_step": round(per[6][2]), "ms_per_step": round(per[6][1] * 1e3, 3),
+                             "direct_tflop_per_step": round(per[6][0] / 1e12, 3),
+                             "mfma_tflop_per_step_approx": round(per[6][0] / 2.25 / 1e12, 3)}} if 6 in per else {})}
 
 
 def cpu_baseline(nframes: int, dtype_cfg, chunk: int = 16):
@@ -291,6 +299,9 @@ def main():
     if args.dma_f32 is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_dma_f32", args.dma_f32)
+    if args.winograd is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_winograd", args.winograd)
     if args.roi_mode is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_roi_align_set_mode", args.roi_mode)

@@ -49,6 +49,7 @@ struct ConvW {
     void *w = nullptr;
     float *b = nullptr;
     int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, kalg = 0;
+    float *wino = nullptr;  // Winograd F(2x2,3x3) weights [16][Cout][Cin] (fp32 3x3/s1/p1 layers, Cin >= 256)
 };
 
 struct GnW {
@@ -79,6 +80,10 @@ struct Ctx {
     bool dry = false;
     std::map<std::string, TensorRec> named;
     std::vector<ProfEv> prof;
+    // Winograd scratch (V and M of one layer at a time, stream-ordered):
+    // sized by the dry run's largest layer, allocated by reserve()
+    char *wino_base = nullptr;
+    size_t wino_cap = 0, wino_need = 0;
     void *alloc(size_t bytes) {
         off = (off + 255) & ~(size_t)255;
         void *p = base + off;
@@ -113,6 +118,7 @@ struct Model {
     ~Model() {
         for (auto &kv : ctx) {
             if (kv.second->base) (void)hipFree(kv.second->base);
+            if (kv.second->wino_base) (void)hipFree(kv.second->wino_base);
             for (auto &p : kv.second->prof) {
                 (void)hipEventDestroy(p.e0);
                 (void)hipEventDestroy(p.e1);
@@ -249,6 +255,15 @@ struct Packer {
         c.k = kh;
         c.stride = stride;
         c.pad = pad;
+        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 256 && ci % 4 == 0 && co % 8 == 0 &&
+            err.empty()) {
+            std::vector<float> oihw((size_t)co * ci * 9), u((size_t)16 * co * ci);
+            for (int o = 0; o < co; ++o)
+                for (size_t q = 0; q < (size_t)ci * 9; ++q)
+                    oihw[(size_t)o * ci * 9 + q] = w->v[(size_t)o * ci * 9 + q] * (scale ? scale[o] : 1.f);
+            mdx_winograd_weights(oihw.data(), co, ci, u.data());
+            c.wino = upload_f32(u);
+        }
         return c;
     }
     // FrozenBatchNorm2d folded: scale = w * rsqrt(var + eps), bias = b - mean * scale
@@ -473,6 +488,11 @@ struct Fwd {
         OW = (W + 2 * cw.pad - cw.k) / cw.stride + 1;
         const size_t oes = out_f32 ? 4 : m.es;
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
+        const bool wino = cw.wino && mdx_conv_winograd_enabled() && !residual && out_mode == 0;
+        if (wino) {
+            const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout);
+            if (c.dry) c.wino_need = need > c.wino_need ? need : c.wino_need;
+        }
         if (c.dry || !ok()) return out;
         ProfEv *pe = nullptr;
         if (m.profile) {
@@ -482,8 +502,12 @@ struct Fwd {
             (void)hipEventCreate(&pe->e1);
             (void)hipEventRecord(pe->e0, s);
         }
-        chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,
-                              relu ? 1 : 0, out_mode, m.dt, out_f32 ? 0 : m.dt, out, 0, splitk, SPLITK_WS, s));
+        if (wino)
+            chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, cw.wino, cw.b, cw.cout, relu ? 1 : 0,
+                                     (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
+        else
+            chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,
+                                  relu ? 1 : 0, out_mode, m.dt, out_f32 ? 0 : m.dt, out, 0, splitk, SPLITK_WS, s));
         if (pe) {
             (void)hipEventRecord(pe->e1, s);
             int kid = -1, ks = 0;
@@ -682,9 +706,24 @@ Ctx *get_ctx(Model &m, hipStream_t s) {
 int reserve(Model &m, Ctx &c, int B, int h, int w, hipStream_t s) {
     c.dry = true;
     c.off = 0;
+    c.wino_need = 0;
     Fwd f{m, c, s};
     f.run(nullptr, B, h, w, nullptr, nullptr);
     c.dry = false;
+    if (c.wino_need > c.wino_cap) {
+        if (c.wino_base) {
+            MDX_HIP(hipStreamSynchronize(s));
+            MDX_HIP(hipFree(c.wino_base));
+            c.wino_base = nullptr;
+            c.wino_cap = 0;
+        }
+        if (hipMalloc((void **)&c.wino_base, c.wino_need) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("mdx_model_reserve: cannot allocate a %.1f GB Winograd workspace", c.wino_need / 1e9);
+            return MDX_ENOMEM;
+        }
+        c.wino_cap = c.wino_need;
+    }
     const size_t need = c.off + 4096;
     if (need <= c.cap) return MDX_OK;
     if (c.base) {

@@ -666,3 +666,37 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_x[k], out_t[k], err_msg=k)
     for k in out:
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
+                                                 (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
+def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu):
+    """F(2x2,3x3) Winograd (fp32: input transform, 16 batched GEMMs, output
+    transform + bias + ReLU) against the fp64 direct convolution: within the
+    fp32 direct kernels' tolerance (1e-4 relative to the output scale; the
+    transform error is ~1e-6), odd sizes exercise the partial edge tiles."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(N * 1000 + H)
+    x = torch.randn(N, H, W, Cin, generator=g).clamp_min(0)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    want = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1)
+    if relu:
+        want = want.clamp_min(0)
+    want = want.permute(0, 2, 3, 1)
+    U = np.empty((16, Cout, Cin), np.float32)
+    wn = np.ascontiguousarray(w.numpy())
+    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, U.ctypes.data_as(ctypes.c_void_p))
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    xd, Ud, bd = x.cuda(), torch.from_numpy(U).cuda(), b.cuda()
+    out = torch.empty(N, H, W, Cout, device="cuda")
+    nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout)
+    ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
+    call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), P(out), P(ws), nb, None)
+    kid, ks_ = ctypes.c_int(), ctypes.c_int()
+    call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+    assert kid.value == 6
+    got = out.cpu().double()
+    err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+    assert err < 1e-4, err
