@@ -141,6 +141,8 @@ def roofline_line(per, dtype):
                 traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    from moseq2_detectron_extract_amd._lib import call
+    wino_m = call("mdx_conv_winograd_enabled")
     tot_f = sum(v[0] for v in per.values())
     tot_s = sum(v[1] for v in per.values())
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -150,10 +152,11 @@ def roofline_line(per, dtype):
                       f"stream, serial steps; traffic = PMC HBM bytes per launch, profiles/{PMC_FILE[dtype]})",
             "all_conv": {"launches": round(sum(v[2] for v in per.values())), "tflop_per_step": round(tot_f / 1e12, 3),
                          "ms_per_step": round(tot_s * 1e3, 3), "achieved": round(tot_f / tot_s / 1e12, 1),
-                         "note": "direct-convolution FLOPs; layers on Winograd F(2x2,3x3) execute 1/2.25 of them"},
-            **({"winograd": {"layers_per_step": round(per[6][2]), "ms_per_step": round(per[6][1] * 1e3, 3),
+                         "note": "direct-convolution FLOPs; the Winograd layers' GEMMs execute 1/2.25 (F(2x2,3x3)) or 1/4 (F(4x4,3x3)) of them"},
+            **({"winograd": {"tile": wino_m, "layers_per_step": round(per[6][2]), "ms_per_step": round(per[6][1] * 1e3, 3),
                              "direct_tflop_per_step": round(per[6][0] / 1e12, 3),
-                             "mfma_tflop_per_step_approx": round(per[6][0] / 2.25 / 1e12, 3)}} if 6 in per else {})}
+                             "gemm_tflop_per_step_approx": round(per[6][0] / (2.25 if wino_m == 2 else 4.0) / 1e12, 3)}}
+               if 6 in per else {})}
 
 
 def cpu_baseline(nframes: int, dtype_cfg, chunk: int = 16):

@@ -224,18 +224,19 @@ int mdx_conv_set_mfma_prio256(int on);
  * for layers with >= 500 such tiles and K >= 2048 (default), 3 the 256x256
  * tile under the fp16 policy.  Returns the old value. */
 int mdx_conv_set_dma_f32(int on);
-/* Winograd F(2x2, 3x3) for fp32 3x3 / stride-1 / pad-1 convolutions (NHWC),
- * the transform used by the model handle for layers with Cin >= 256 (cuDNN's
- * WINOGRAD algorithm family, which PyTorch selects for such fp32 convs):
- * weights: w float32 OIHW [Cout][Cin][3][3] -> U float32 [16][Cout][Cin]
- * (host function).  conv: x float32 (N,H,W,Cin), U as above, bias [Cout] or
- * NULL, optional ReLU -> out (N,H,W,Cout); workspace (16-B aligned) >=
- * mdx_winograd_workspace_bytes.  Cin % 4 == 0, Cout % 8 == 0.
- * set_winograd: the model handle's policy (0 off, 1 on, default 1). */
-int mdx_winograd_weights(const float *w, int Cout, int Cin, float *U);
-int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout);
+/* Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride-1 / pad-1
+ * convolutions (NHWC): the algorithm the model handle uses for such layers
+ * with Cin >= 256 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
+ * 3x3 convs).  weights: w float32 OIHW [Cout][Cin][3][3] -> U float32
+ * [(m+2)^2][Cout][Cin] (host function).  conv: x float32 (N,H,W,Cin), U as
+ * above, bias [Cout] or NULL, optional ReLU -> out (N,H,W,Cout); workspace
+ * (16-B aligned) >= mdx_winograd_workspace_bytes.  Cin % 4 == 0, Cout % 8 == 0.
+ * set_winograd: the model handle's policy (0 off (direct), 2 F(2x2,3x3),
+ * 4 F(4x4,3x3) default); returns the old one. */
+int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U);
+int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m);
 int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias, int Cout,
-                         int relu, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
+                         int relu, int m, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call

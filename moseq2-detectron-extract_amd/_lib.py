@@ -53,9 +53,9 @@ SIGNATURES = {
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
     "mdx_conv_set_dma_f32": (I32, [I32]),
     "mdx_rpn_set_sliced": (I32, [I32]),
-    "mdx_winograd_weights": (I32, [P, I32, I32, P]),
-    "mdx_winograd_workspace_bytes": (I64, [I32, I32, I32, I32, I32]),
-    "mdx_conv3x3_winograd": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, P, P, I64, P]),
+    "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),
+    "mdx_winograd_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32]),
+    "mdx_conv3x3_winograd": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_conv_set_winograd": (I32, [I32]),
     "mdx_conv_winograd_enabled": (I32, []),
     "mdx_conv2d_last_plan": (I32, [P, P]),

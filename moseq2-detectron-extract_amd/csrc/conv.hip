@@ -992,111 +992,144 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
 
 
 // ---------------------------------------------------------------------------
-// Winograd F(2x2, 3x3) for fp32 3x3 / stride 1 / pad 1 convolutions (NHWC):
-//   V[xi][t][c]  = (B^T d B)  of the 4x4 input patch of output tile t
-//   M[xi][t][k]  = sum_c V[xi][t][c] U[xi][k][c]       (16 batched GEMMs)
-//   Y(t)         = A^T M A  (+ bias, ReLU)              (2x2 outputs)
-// with U = G g G^T packed once per layer.  2.25x fewer multiplies; the
-// transforms add only additions/subtractions (exact in the constants), so the
-// error stays at the direct convolution's level (~7e-7 relative measured in
-// fp32 on 256-channel layers vs ~4e-7 direct).
+// Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride 1 / pad 1
+// convolutions (NHWC), a = m + 2:
+//   V[xi][t][c] = (B^T d B)[xi] of the a x a input patch of output tile t
+//   M[xi][t][k] = sum_c V[xi][t][c] U[xi][k][c]   (a*a batched GEMMs)
+//   Y(t)        = A^T M A (+ bias, ReLU)           (m x m outputs)
+// with U = G g G^T packed once per layer.  F(2,3): 2.25x fewer multiplies,
+// transforms of 0/+-1 coefficients (error ~7e-7 relative in fp32 on
+// 256-channel layers vs ~4e-7 direct); F(4,3): 4x fewer, coefficients up to
+// 8 (Lavin's points 0, +-1, +-2; error ~1e-5).
 // ---------------------------------------------------------------------------
+template <int M>
+struct WinoT;
+template <>
+struct WinoT<2> {
+    static constexpr int A = 4;
+    __device__ static constexpr float BT(int i, int j) {
+        constexpr float t[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
+        return t[i][j];
+    }
+    __device__ static constexpr float AT(int i, int j) {
+        constexpr float t[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
+        return t[i][j];
+    }
+};
+template <>
+struct WinoT<4> {
+    static constexpr int A = 6;
+    __device__ static constexpr float BT(int i, int j) {
+        constexpr float t[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0}, {0, 4, -4, -1, 1, 0},
+                                   {0, -2, -1, 2, 1, 0}, {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
+        return t[i][j];
+    }
+    __device__ static constexpr float AT(int i, int j) {
+        constexpr float t[4][6] = {{1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+        return t[i][j];
+    }
+};
+
+// one thread per (tile, channel); sums over nonzero coefficients only
+template <int M>
 __global__ __launch_bounds__(256) void k_wino_in(const float *__restrict__ x, int N, int H, int W, int C, int TH,
                                                  int TW, float *__restrict__ V) {
-    const int C4 = C >> 2;
+    constexpr int A = WinoT<M>::A;
     const long long T = (long long)N * TH * TW;
-    const long long total = T * C4;
+    const long long total = T * C;
+    const long long xs = T * C;  // stride between xi planes
     for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / C4;
-        const int c4 = (int)(idx - t * C4);
+        const long long t = idx / C;
+        const int c = (int)(idx - t * C);
         const int tx = (int)(t % TW);
         const long long r = t / TW;
         const int ty = (int)(r % TH), n = (int)(r / TH);
-        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-        float4 d[4][4];
+        const int y0 = M * ty - 1, x0 = M * tx - 1;
+        float d[A][A];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < A; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < A; ++j) {
                 const int yy = y0 + i, xx = x0 + j;
-                d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W)
-                              ? *reinterpret_cast<const float4 *>(x + (((long long)n * H + yy) * W + xx) * C + 4 * c4)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+                d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? x[(((long long)n * H + yy) * W + xx) * C + c] : 0.f;
             }
-        // columns: t = B^T d   (rows 0..3: d0 - d2, d1 + d2, d2 - d1, d1 - d3)
-        float4 tt[4][4];
+        float tt[A][A];  // B^T d
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            tt[0][j] = make_float4(d[0][j].x - d[2][j].x, d[0][j].y - d[2][j].y, d[0][j].z - d[2][j].z, d[0][j].w - d[2][j].w);
-            tt[1][j] = make_float4(d[1][j].x + d[2][j].x, d[1][j].y + d[2][j].y, d[1][j].z + d[2][j].z, d[1][j].w + d[2][j].w);
-            tt[2][j] = make_float4(d[2][j].x - d[1][j].x, d[2][j].y - d[1][j].y, d[2][j].z - d[1][j].z, d[2][j].w - d[1][j].w);
-            tt[3][j] = make_float4(d[1][j].x - d[3][j].x, d[1][j].y - d[3][j].y, d[1][j].z - d[3][j].z, d[1][j].w - d[3][j].w);
-        }
-        float *vo = V + t * C + 4 * c4;
-        const long long xs = T * C;  // stride between xi planes
+        for (int i = 0; i < A; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float4 a = tt[i][0], b = tt[i][1], c = tt[i][2], e = tt[i][3];
-            *reinterpret_cast<float4 *>(vo + (4 * i + 0) * xs) = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
-            *reinterpret_cast<float4 *>(vo + (4 * i + 1) * xs) = make_float4(b.x + c.x, b.y + c.y, b.z + c.z, b.w + c.w);
-            *reinterpret_cast<float4 *>(vo + (4 * i + 2) * xs) = make_float4(c.x - b.x, c.y - b.y, c.z - b.z, c.w - b.w);
-            *reinterpret_cast<float4 *>(vo + (4 * i + 3) * xs) = make_float4(b.x - e.x, b.y - e.y, b.z - e.z, b.w - e.w);
+            for (int j = 0; j < A; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(i, k) != 0.f) acc = acc + WinoT<M>::BT(i, k) * d[k][j];
+                tt[i][j] = acc;
+            }
+        float *vo = V + t * C + c;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {  // (B^T d) B
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(j, k) != 0.f) acc = acc + tt[i][k] * WinoT<M>::BT(j, k);
+                vo[(A * i + j) * xs] = acc;
+            }
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
+                                                  int TW, const float *__restrict__ bias, int relu,
+                                                  float *__restrict__ out) {
+    constexpr int A = WinoT<M>::A;
+    const long long T = (long long)N * TH * TW;
+    const long long total = T * K;
+    const long long xs = T * K;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const long long t = idx / K;
+        const int k = (int)(idx - t * K);
+        const int tx = (int)(t % TW);
+        const long long r = t / TW;
+        const int ty = (int)(r % TH), n = (int)(r / TH);
+        const float *mi = Mx + t * K + k;
+        float m[A][A];
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) m[i][j] = mi[(A * i + j) * xs];
+        float sa[M][A];  // A^T m
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < A; ++q)
+                    if (WinoT<M>::AT(i, q) != 0.f) acc = acc + WinoT<M>::AT(i, q) * m[q][j];
+                sa[i][j] = acc;
+            }
+        const float bv = bias ? bias[k] : 0.f;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int oy = M * ty + i;
+            if (oy >= OH) continue;
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                const int ox = M * tx + j;
+                if (ox >= OW) continue;
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < A; ++q)
+                    if (WinoT<M>::AT(j, q) != 0.f) acc = acc + sa[i][q] * WinoT<M>::AT(j, q);
+                float v = acc + bv;
+                if (relu) v = v > 0.f ? v : 0.f;
+                out[(((long long)n * OH + oy) * OW + ox) * K + k] = v;
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
-                                                  int TW, const float *__restrict__ bias, int relu,
-                                                  float *__restrict__ out) {
-    const int K4 = K >> 2;
-    const long long T = (long long)N * TH * TW;
-    const long long total = T * K4;
-    const long long xs = T * K;
-    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / K4;
-        const int k4 = (int)(idx - t * K4);
-        const int tx = (int)(t % TW);
-        const long long r = t / TW;
-        const int ty = (int)(r % TH), n = (int)(r / TH);
-        const float *mi = Mx + t * K + 4 * k4;
-        float4 m[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) m[i][j] = *reinterpret_cast<const float4 *>(mi + (4 * i + j) * xs);
-        // s = A^T m (2 x 4): s0 = m0 + m1 + m2, s1 = m1 - m2 - m3
-        float4 sa[2][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            sa[0][j] = make_float4(m[0][j].x + m[1][j].x + m[2][j].x, m[0][j].y + m[1][j].y + m[2][j].y,
-                                   m[0][j].z + m[1][j].z + m[2][j].z, m[0][j].w + m[1][j].w + m[2][j].w);
-            sa[1][j] = make_float4(m[1][j].x - m[2][j].x - m[3][j].x, m[1][j].y - m[2][j].y - m[3][j].y,
-                                   m[1][j].z - m[2][j].z - m[3][j].z, m[1][j].w - m[2][j].w - m[3][j].w);
-        }
-        const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int oy = 2 * ty + i;
-            if (oy >= OH) continue;
-            const float4 a = sa[i][0], b = sa[i][1], c = sa[i][2], e = sa[i][3];
-            float4 y[2] = {make_float4(a.x + b.x + c.x, a.y + b.y + c.y, a.z + b.z + c.z, a.w + b.w + c.w),
-                           make_float4(b.x - c.x - e.x, b.y - c.y - e.y, b.z - c.z - e.z, b.w - c.w - e.w)};
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int ox = 2 * tx + j;
-                if (ox >= OW) continue;
-                float4 v = make_float4(y[j].x + bv.x, y[j].y + bv.y, y[j].z + bv.z, y[j].w + bv.w);
-                if (relu) {
-                    v.x = v.x > 0.f ? v.x : 0.f;
-                    v.y = v.y > 0.f ? v.y : 0.f;
-                    v.z = v.z > 0.f ? v.z : 0.f;
-                    v.w = v.w > 0.f ? v.w : 0.f;
-                }
-                *reinterpret_cast<float4 *>(out + (((long long)n * OH + oy) * OW + ox) * K + 4 * k4) = v;
-            }
-        }
-    }
-}
 }  // namespace mdx
 
 using namespace mdx;
@@ -1421,9 +1454,9 @@ extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
 }
 
 // ---------------------------------------------------------------------------
-// Winograd F(2x2, 3x3) host side
+// Winograd F(m x m, 3x3) host side
 // ---------------------------------------------------------------------------
-static int g_winograd = 1;
+static int g_winograd = 4;
 extern "C" int mdx_conv_set_winograd(int mode) {
     const int old = g_winograd;
     g_winograd = mode;
@@ -1431,54 +1464,67 @@ extern "C" int mdx_conv_set_winograd(int mode) {
 }
 extern "C" int mdx_conv_winograd_enabled(void) { return g_winograd; }
 
-extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, float *U) {
-    MDX_REQUIRE(w && U && Cout > 0 && Cin > 0, "mdx_winograd_weights: bad args");
-    // U = G g G^T, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]] (in double, rounded once)
-    static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U) {
+    MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4), "mdx_winograd_weights: bad args");
+    // U = G g G^T (in double, rounded once)
+    static const double G2[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    static const double G4[6][3] = {{1.0 / 4, 0, 0},
+                                    {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                    {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                    {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                    {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                    {0, 0, 1}};
+    const int A = m + 2;
+    auto G = [&](int i, int j) { return m == 2 ? G2[i][j] : G4[i][j]; };
     const long long plane = (long long)Cout * Cin;
     for (int o = 0; o < Cout; ++o)
         for (int i = 0; i < Cin; ++i) {
             const float *g = w + ((long long)o * Cin + i) * 9;
-            double tg[4][3];
-            for (int a = 0; a < 4; ++a)
-                for (int c = 0; c < 3; ++c) tg[a][c] = G[a][0] * g[0 * 3 + c] + G[a][1] * g[1 * 3 + c] + G[a][2] * g[2 * 3 + c];
-            for (int a = 0; a < 4; ++a)
-                for (int b = 0; b < 4; ++b)
-                    U[(long long)(4 * a + b) * plane + (long long)o * Cin + i] =
-                        (float)(tg[a][0] * G[b][0] + tg[a][1] * G[b][1] + tg[a][2] * G[b][2]);
+            double tg[6][3];
+            for (int a = 0; a < A; ++a)
+                for (int c = 0; c < 3; ++c) tg[a][c] = G(a, 0) * g[0 * 3 + c] + G(a, 1) * g[1 * 3 + c] + G(a, 2) * g[2 * 3 + c];
+            for (int a = 0; a < A; ++a)
+                for (int b = 0; b < A; ++b)
+                    U[(long long)(A * a + b) * plane + (long long)o * Cin + i] =
+                        (float)(tg[a][0] * G(b, 0) + tg[a][1] * G(b, 1) + tg[a][2] * G(b, 2));
         }
     return MDX_OK;
 }
 
-extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout) {
-    const long long T = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
-    return 16ll * T * (Cin + Cout) * 4 + 256;
+extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m) {
+    if (m != 2 && m != 4) return -1;
+    const long long T = (long long)N * ((H + m - 1) / m) * ((W + m - 1) / m);
+    return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
 }
 
 extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias,
-                                    int Cout, int relu, float *out, void *workspace, int64_t workspace_bytes,
+                                    int Cout, int relu, int m, float *out, void *workspace, int64_t workspace_bytes,
                                     mdx_stream_t stream) {
     MDX_REQUIRE(x && U && out && workspace, "mdx_conv3x3_winograd: null pointer");
+    MDX_REQUIRE(m == 2 || m == 4, "mdx_conv3x3_winograd: tile m must be 2 or 4");
     MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cin % 4 == 0 && Cout % 8 == 0,
                 "mdx_conv3x3_winograd: Cin %% 4 == 0 and Cout %% 8 == 0 required");
-    MDX_REQUIRE(workspace_bytes >= mdx_winograd_workspace_bytes(N, H, W, Cin, Cout),
+    MDX_REQUIRE(workspace_bytes >= mdx_winograd_workspace_bytes(N, H, W, Cin, Cout, m),
                 "mdx_conv3x3_winograd: workspace too small");
-    MDX_REQUIRE((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
-                 reinterpret_cast<uintptr_t>(workspace)) % 16 == 0,
-                "mdx_conv3x3_winograd: 16-B aligned buffers required");
-    const int TH = (H + 1) / 2, TW = (W + 1) / 2;
+    MDX_REQUIRE((reinterpret_cast<uintptr_t>(workspace) % 16) == 0, "mdx_conv3x3_winograd: 16-B aligned workspace");
+    const int A = m + 2, NB = A * A;
+    const int TH = (H + m - 1) / m, TW = (W + m - 1) / m;
     const long long T = (long long)N * TH * TW;
-    MDX_REQUIRE(T < (1ll << 31) && T * Cin * 4 < (1ll << 31) && (long long)Cout * Cin * 4 < (1ll << 31),
+    MDX_REQUIRE(T < (1ll << 31) && T * Cin * 4 < (1ll << 31) && T * Cout * 4 < (1ll << 31) &&
+                    (long long)Cout * Cin * 4 < (1ll << 31),
                 "mdx_conv3x3_winograd: layer too large");
     hipStream_t s = as_stream(stream);
     float *V = reinterpret_cast<float *>(workspace);
-    float *Mx = V + 16 * T * Cin;
+    float *Mx = V + NB * T * Cin;
     {
-        const long long items = T * (Cin / 4);
+        const long long items = T * Cin;
         const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
-        hipLaunchKernelGGL(k_wino_in, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+        if (m == 2)
+            hipLaunchKernelGGL(k_wino_in<2>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+        else
+            hipLaunchKernelGGL(k_wino_in<4>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
     }
-    // 16 GEMMs M[xi] (T x Cout) = V[xi] (T x Cin) U[xi]^T in one launch (grid.z)
+    // NB GEMMs M[xi] (T x Cout) = V[xi] (T x Cin) U[xi]^T in one launch (grid.z)
     ConvArgs a{};
     a.x = V; a.w = U; a.bias = nullptr; a.res = nullptr; a.out = Mx;
     a.H = (int)T; a.W = 1; a.Cin = Cin; a.Cout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
@@ -1498,15 +1544,18 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     const size_t lds_main = (nk == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-    const dim3 grid((unsigned)a.tiles_total, 1, 16);
+    const dim3 grid((unsigned)a.tiles_total, 1, (unsigned)NB);
     if (bn == 64)
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
     else
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
     {
-        const long long items = T * (Cout / 4);
+        const long long items = T * Cout;
         const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
-        hipLaunchKernelGGL(k_wino_out, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
+        if (m == 2)
+            hipLaunchKernelGGL(k_wino_out<2>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
+        else
+            hipLaunchKernelGGL(k_wino_out<4>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
     }
     t_plan_kernel = MDX_CONV_KERNEL_WINOGRAD;
     t_plan_ksplit = 1;

@@ -49,7 +49,9 @@ struct ConvW {
     void *w = nullptr;
     float *b = nullptr;
     int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, kalg = 0;
-    float *wino = nullptr;  // Winograd F(2x2,3x3) weights [16][Cout][Cin] (fp32 3x3/s1/p1 layers, Cin >= 256)
+    // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
+    // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 256)
+    float *wino2 = nullptr, *wino4 = nullptr;
 };
 
 struct GnW {
@@ -261,8 +263,11 @@ struct Packer {
             for (int o = 0; o < co; ++o)
                 for (size_t q = 0; q < (size_t)ci * 9; ++q)
                     oihw[(size_t)o * ci * 9 + q] = w->v[(size_t)o * ci * 9 + q] * (scale ? scale[o] : 1.f);
-            mdx_winograd_weights(oihw.data(), co, ci, u.data());
-            c.wino = upload_f32(u);
+            mdx_winograd_weights(oihw.data(), co, ci, 2, u.data());
+            c.wino2 = upload_f32(u);
+            u.resize((size_t)36 * co * ci);
+            mdx_winograd_weights(oihw.data(), co, ci, 4, u.data());
+            c.wino4 = upload_f32(u);
         }
         return c;
     }
@@ -488,9 +493,11 @@ struct Fwd {
         OW = (W + 2 * cw.pad - cw.k) / cw.stride + 1;
         const size_t oes = out_f32 ? 4 : m.es;
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
-        const bool wino = cw.wino && mdx_conv_winograd_enabled() && !residual && out_mode == 0;
+        const int wm = mdx_conv_winograd_enabled();
+        const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : nullptr;
+        const bool wino = wu && !residual && out_mode == 0;
         if (wino) {
-            const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout);
+            const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout, wm);
             if (c.dry) c.wino_need = need > c.wino_need ? need : c.wino_need;
         }
         if (c.dry || !ok()) return out;
@@ -503,7 +510,7 @@ struct Fwd {
             (void)hipEventRecord(pe->e0, s);
         }
         if (wino)
-            chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, cw.wino, cw.b, cw.cout, relu ? 1 : 0,
+            chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
                                      (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
         else
             chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,

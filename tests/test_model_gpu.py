@@ -668,13 +668,14 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
+@pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
-def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu):
-    """F(2x2,3x3) Winograd (fp32: input transform, 16 batched GEMMs, output
-    transform + bias + ReLU) against the fp64 direct convolution: within the
-    fp32 direct kernels' tolerance (1e-4 relative to the output scale; the
-    transform error is ~1e-6), odd sizes exercise the partial edge tiles."""
+def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m):
+    """Winograd F(m x m, 3x3) (fp32: input transform, (m+2)^2 batched GEMMs,
+    output transform + bias + ReLU) against the fp64 direct convolution:
+    within the fp32 direct kernels' tolerance (1e-4 relative to the output
+    scale; F(2,3) ~1e-6, F(4,3) ~1e-5), ragged sizes exercise partial tiles."""
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
     g = torch.Generator().manual_seed(N * 1000 + H)
@@ -685,15 +686,15 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu):
     if relu:
         want = want.clamp_min(0)
     want = want.permute(0, 2, 3, 1)
-    U = np.empty((16, Cout, Cin), np.float32)
+    U = np.empty(((m + 2) ** 2, Cout, Cin), np.float32)
     wn = np.ascontiguousarray(w.numpy())
-    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, U.ctypes.data_as(ctypes.c_void_p))
+    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, m, U.ctypes.data_as(ctypes.c_void_p))
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     xd, Ud, bd = x.cuda(), torch.from_numpy(U).cuda(), b.cuda()
     out = torch.empty(N, H, W, Cout, device="cuda")
-    nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout)
+    nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout, m)
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
-    call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), P(out), P(ws), nb, None)
+    call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6

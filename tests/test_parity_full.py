@@ -81,8 +81,20 @@ def _ang_diff(a, b):
     return np.minimum(d, 180.0 - d)
 
 
-@pytest.mark.parametrize("depth,B,dtype", [(50, 32, "fp32"), (50, 32, "fp16"), (101, 64, "fp16")])
-def test_forward_full_frame(mdx, depth, B, dtype):
+@pytest.mark.parametrize("depth,B,dtype,wino", [(50, 32, "fp32", 4), (50, 32, "fp32", 2), (50, 32, "fp32", 0),
+                                                (50, 32, "fp16", 0), (101, 64, "fp16", 0)])
+def test_forward_full_frame(mdx, depth, B, dtype, wino):
+    """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
+    2 = F(2x2,3x3), 0 = direct); the same fp32 tolerances hold for all."""
+    from moseq2_detectron_extract_amd._lib import call
+    old = call("mdx_conv_set_winograd", wino)
+    try:
+        _forward_full_frame(depth, B, dtype, wino)
+    finally:
+        call("mdx_conv_set_winograd", old)
+
+
+def _forward_full_frame(depth, B, dtype, wino):
     from moseq2_detectron_extract_amd import synth
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor, synthetic_state_dict
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
@@ -104,13 +116,13 @@ def test_forward_full_frame(mdx, depth, B, dtype):
     np.testing.assert_array_equal(prepped_d.cpu().numpy(), prepped)  # bit-exact frame ops feed both sides
     scaled = O.scale_raw_frames(prepped, 0, 100)
     masks_all = torch.cat([m for m in inf["masks"]]).cpu().numpy()
-    stats = {"case": f"R{depth} B={B} {dtype}", "frames": []}
+    stats = {"case": f"R{depth} B={B} {dtype}" + (f" winograd F({wino}x{wino},3x3)" if wino else ""), "frames": []}
     try:
         _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d, tail, stats)
     finally:
         out = os.path.join(ROOT, "gpurun_out")
         if os.path.isdir(out):
-            with open(os.path.join(out, f"parity_full_R{depth}_B{B}_{dtype}.json"), "w") as fh:
+            with open(os.path.join(out, f"parity_full_R{depth}_B{B}_{dtype}" + (f"_wino{wino}" if wino else "") + ".json"), "w") as fh:
                 json.dump(stats, fh, indent=1)
 
 
