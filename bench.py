@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
+    ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_conv_set_winograd_min_cin")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -305,6 +306,9 @@ def main():
     if args.winograd is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_conv_set_winograd", args.winograd)
+    if args.winograd_min_cin is not None:
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_winograd_min_cin", args.winograd_min_cin)
     if args.roi_mode is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_roi_align_set_mode", args.roi_mode)

@@ -239,6 +239,10 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
                          int relu, int m, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
+/* Minimum Cin of the layers the model handle runs on Winograd (default 128;
+ * handles pack the transformed weights of the fp32 3x3 layers with Cin >= 128). */
+int mdx_conv_set_winograd_min_cin(int cin);
+int mdx_conv_winograd_min_cin(void);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */

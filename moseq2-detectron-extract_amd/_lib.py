@@ -58,6 +58,8 @@ SIGNATURES = {
     "mdx_conv3x3_winograd": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_conv_set_winograd": (I32, [I32]),
     "mdx_conv_winograd_enabled": (I32, []),
+    "mdx_conv_set_winograd_min_cin": (I32, [I32]),
+    "mdx_conv_winograd_min_cin": (I32, []),
     "mdx_conv2d_last_plan": (I32, [P, P]),
     "mdx_conv_set_stream1x1": (I32, [I32, I32]),
     "mdx_conv_set_split256": (I32, [I32, I32]),

@@ -1463,6 +1463,15 @@ extern "C" int mdx_conv_set_winograd(int mode) {
     return old;
 }
 extern "C" int mdx_conv_winograd_enabled(void) { return g_winograd; }
+// the model handle uses Winograd for layers with Cin >= this (the transforms'
+// traffic outweighs the saved multiplies on thinner layers)
+static int g_wino_min_cin = 128;
+extern "C" int mdx_conv_set_winograd_min_cin(int c) {
+    const int old = g_wino_min_cin;
+    g_wino_min_cin = c;
+    return old;
+}
+extern "C" int mdx_conv_winograd_min_cin(void) { return g_wino_min_cin; }
 
 extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U) {
     MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4), "mdx_winograd_weights: bad args");

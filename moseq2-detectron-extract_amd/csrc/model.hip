@@ -50,7 +50,7 @@ struct ConvW {
     float *b = nullptr;
     int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, kalg = 0;
     // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
-    // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 256)
+    // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 128)
     float *wino2 = nullptr, *wino4 = nullptr;
 };
 
@@ -257,7 +257,7 @@ struct Packer {
         c.k = kh;
         c.stride = stride;
         c.pad = pad;
-        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 256 && ci % 4 == 0 && co % 8 == 0 &&
+        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 128 && ci % 4 == 0 && co % 8 == 0 &&
             err.empty()) {
             std::vector<float> oihw((size_t)co * ci * 9), u((size_t)16 * co * ci);
             for (int o = 0; o < co; ++o)
@@ -495,7 +495,7 @@ struct Fwd {
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
         const int wm = mdx_conv_winograd_enabled();
         const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : nullptr;
-        const bool wino = wu && !residual && out_mode == 0;
+        const bool wino = wu && !residual && out_mode == 0 && cw.cin >= mdx_conv_winograd_min_cin();
         if (wino) {
             const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout, wm);
             if (c.dry) c.wino_need = need > c.wino_need ? need : c.wino_need;
