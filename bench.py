@@ -66,11 +66,12 @@ def parse():
 # MDX_CONV_KERNEL_* (+10: fp32-output instance of an fp16 model) -> rocprofv3 symbol, per dtype
 KERNEL_SYMBOLS = {
     "fp16": {0: "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE",
-             2: "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
-             3: "_ZN3mdx7k_convgIDF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
+             2: "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
+             3: "_ZN3mdx7k_convgIDF16_DF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
              4: "k_conv1x1_stream<KC> (three instances by K)", 5: "k_conv1x1_head<KC> (three instances by K)",
              10: "_ZN3mdx6k_convIDF16_fLi128EEEvNS_8ConvArgsE", 11: "_ZN3mdx6k_convIDF16_fLi64EEEvNS_8ConvArgsE"},
-    "fp32": {0: "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE"},
+    "fp32": {0: "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE",
+             2: "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE"},
 }
 # rocprofv3 reports some kernels demangled
 KERNEL_DEMANGLED = {
@@ -78,8 +79,10 @@ KERNEL_DEMANGLED = {
     "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE": "void mdx::k_conv<float, float, 64>(mdx::ConvArgs)",
     "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 128>(mdx::ConvArgs)",
     "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 64>(mdx::ConvArgs)",
-    "_ZN3mdx7k_convgIDF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
-        "void mdx::k_convg<_Float16, 8, false, false, false>(mdx::ConvArgs)",
+    "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
+        "void mdx::k_convg<_Float16, _Float16, 8, false, false, false>(mdx::ConvArgs)",
+    "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
+        "void mdx::k_convg<float, float, 8, false, false, false>(mdx::ConvArgs)",
 }
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
@@ -237,6 +240,8 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
                 if "ready" in r:
                     gstream.wait_event(r["ready"])
                 payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
+                if gather_bufs is not None and gather_bufs[0].device.type == "cpu":
+                    payload = payload.cpu()
                 dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
 
     def upload(i):
@@ -275,7 +280,8 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt, ex, cfg
@@ -289,10 +295,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MDX_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
+    # the one GPU of a test box (the driver's runs use nccl = RCCL, one GPU each)
+    backend = os.environ.get("MDX_BENCH_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(dev)
 
     import mdx_pkg
     mdx_pkg.load()
@@ -318,7 +331,8 @@ def main():
     raw_host = [torch.from_numpy(frames[i * B:(i + 1) * B]).pin_memory() for i in range(2)]
     gather_bufs = None
     if world > 1:
-        gather_bufs = [torch.empty((B, 2, 80, 80), dtype=torch.uint8, device="cuda") for _ in range(world)]
+        gdev = "cpu" if backend == "gloo" else "cuda"
+        gather_bufs = [torch.empty((B, 2, 80, 80), dtype=torch.uint8, device=gdev) for _ in range(world)]
 
     dt, ex, cfg = measure(args, args.dtype, B, world, rank, raw_host, sess, dist, gather_bufs)
     frames_done = world * args.steps * B
@@ -338,7 +352,7 @@ def main():
         secondary = {"fp16": {"value": round(frames_done / dt16, 2), "unit": "frames/s",
                               "ms_per_step": round(dt16 / args.steps * 1e3, 3), "dtype": "fp16",
                               "note": "fp16 MFMA forward (fp32 accumulation), same loop; tolerance vs the fp32 "
-                                      "oracle: tests/test_model_gpu.py::test_forward_full_frame_b32[fp16]"}}
+                                      "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0]"}}
         del ex16
 
     cpu = None
