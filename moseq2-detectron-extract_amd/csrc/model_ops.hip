@@ -484,18 +484,19 @@ __device__ void select_top64(const unsigned long long (&kr)[KPT], const bool (&o
 }
 
 constexpr int TOPK_THREADS = 1024, TOPK_MAX = 1024;
-constexpr int TOPK_KPT = 44;  // keys per thread held in registers (segments of <= 45056 anchors: p2 of a 448x512 input has 43008)
 
-// INREG: every key of the segment is loaded once into registers (all loads in
-// flight together) and the radix passes and the tie scan run from there;
-// otherwise each pass re-reads the head tensor.
-template <bool INREG>
+// One workgroup per (image, level): radix select of the k-th largest key over
+// the head tensor (every pass re-reads it), the ties taken in index order,
+// bitonic sort, decode.  The default path splits the segment over RPN_SLICES
+// workgroups (k_rpn_part / k_rpn_merge_topk below); this one serves
+// mdx_rpn_set_sliced(0) and segments above RPN_SLICES * PART_KPT *
+// TOPK_THREADS anchors.
 __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *__restrict__ ws_boxes,
                                                            float *__restrict__ ws_scores, int *__restrict__ ws_valid,
                                                            int *__restrict__ ws_k) {
     __shared__ unsigned hist[256];
     __shared__ unsigned s_key[TOPK_MAX], s_val[TOPK_MAX];
-    __shared__ unsigned s_prefix, s_kk, s_cnt_gt, s_cnt_eq, s_eq;
+    __shared__ unsigned s_sel[3], s_cnt_gt, s_cnt_eq;
     __shared__ unsigned wcnt[TOPK_THREADS / 64];
     const int seg = blockIdx.x;  // b * L + l
     const int b = seg / rl.L, l = seg - b * rl.L;
@@ -509,113 +510,25 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *
         const int pix = i / A, a = i - pix * A;
         return fkey(hd[(long long)pix * CH + a]);
     };
-    constexpr int NJ = INREG ? TOPK_KPT : 1;
-    unsigned kreg[NJ];
-    if constexpr (INREG) {
-#pragma unroll
-        for (int j = 0; j < TOPK_KPT; ++j) {
-            const int i = j * TOPK_THREADS + threadIdx.x;
-            kreg[j] = i < n ? keyat(i) : 0u;
-        }
-    }
-    // chunk c (elements c * 1024 + tid): key of this thread, valid flag
-    const int nchunks = (n + TOPK_THREADS - 1) / TOPK_THREADS;
-    auto chunk_key = [&](int c, unsigned &key) -> bool {
-        const int i = c * TOPK_THREADS + threadIdx.x;
-        if (i >= n) return false;
-        if constexpr (INREG) {
-            key = 0u;
-#pragma unroll
-            for (int j = 0; j < TOPK_KPT; ++j)
-                if (j == c) key = kreg[j];
-        } else {
-            key = keyat(i);
-        }
-        return true;
-    };
     // radix select of the k-th largest key
-    unsigned prefix = 0, mask = 0, kk = (unsigned)k;
+    unsigned prefix = 0, mask = 0, kk = (unsigned)k, eq_total = 0;
     for (int shift = 24; shift >= 0; shift -= 8) {
         for (int i = threadIdx.x; i < 256; i += TOPK_THREADS) hist[i] = 0;
         __syncthreads();
-        if constexpr (INREG) {
-#pragma unroll
-            for (int j = 0; j < TOPK_KPT; ++j) {
-                if (j >= nchunks) continue;  // (uniform; no break: keeps the loop unrolled, kreg in registers)
-                const int i = j * TOPK_THREADS + threadIdx.x;
-                const unsigned key = kreg[j];
-                const bool ok = i < n && (key & mask) == prefix;
-                if (shift == 24) {
-                    // the top byte is sign + exponent: a wave's keys share a
-                    // handful of bins -- one atomic per distinct bin
-                    const unsigned bin = key >> 24;
-                    unsigned long long rem = __ballot(ok);
-                    while (rem) {
-                        const int leader = __builtin_ctzll(rem);
-                        const unsigned b0 = __builtin_amdgcn_readlane(bin, leader);
-                        const unsigned long long m = __ballot(ok && bin == b0);
-                        if (lane == leader) atomicAdd(&hist[b0], (unsigned)__popcll(m));
-                        rem &= ~m;
-                    }
-                } else if (ok) {
-                    atomicAdd(&hist[(key >> shift) & 255], 1u);
-                }
-            }
-        } else {
-            for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
-                const unsigned key = keyat(i);
-                if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-            }
+        for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
+            const unsigned key = keyat(i);
+            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
         }
         __syncthreads();
-        if (wid == 0) {
-            // digit d = the largest d >= 1 with S(d) = sum_{d' >= d} hist[d'] >= kk,
-            // else 0 (a descending scan from 255); one wave, 4 bins per lane
-            unsigned h[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) h[q] = hist[4 * lane + q];
-            const unsigned lsum = h[0] + h[1] + h[2] + h[3];
-            unsigned suf = lsum;  // sum over lanes >= lane
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned t = __shfl_down(suf, off);
-                if (lane + off < 64) suf += t;
-            }
-            unsigned S[4];
-            S[3] = suf - lsum + h[3];
-            S[2] = S[3] + h[2];
-            S[1] = S[2] + h[1];
-            S[0] = S[1] + h[0];
-            int qbest = -1;
-#pragma unroll
-            for (int q = 3; q >= 0; --q)
-                if (qbest < 0 && 4 * lane + q >= 1 && S[q] >= kk) qbest = q;
-            const unsigned long long any = __ballot(qbest >= 0);
-            const int lbest = any ? 63 - __builtin_clzll(any) : 0;
-            const int qb = __shfl(qbest, lbest);
-            int d = 0;
-            unsigned Sd = 0, hd_ = 0;
-            if (any) {
-                d = 4 * lbest + qb;
-                Sd = __shfl((int)(qb == 3 ? S[3] : qb == 2 ? S[2] : qb == 1 ? S[1] : S[0]), lbest);
-                hd_ = __shfl((int)(qb == 3 ? h[3] : qb == 2 ? h[2] : qb == 1 ? h[1] : h[0]), lbest);
-            } else {
-                Sd = __shfl((int)S[0], 0);  // d = 0: everything
-                hd_ = __shfl((int)h[0], 0);
-            }
-            if (lane == 0) {
-                s_prefix = prefix | ((unsigned)d << shift);
-                s_kk = kk - (Sd - hd_);
-                s_eq = hd_;
-            }
-        }
+        if (wid == 0) pick_digit(hist, kk, &s_sel[0], &s_sel[1], &s_sel[2]);
         __syncthreads();
-        prefix = s_prefix;
-        kk = s_kk;
+        prefix |= s_sel[0] << shift;
+        kk -= s_sel[1];
+        eq_total = s_sel[2];
         mask |= 255u << shift;
         __syncthreads();
     }
-    const unsigned T = prefix;  // k-th largest key; take kk of the ties (lowest indices)
-    const bool all_ties = s_eq == kk;  // every key == T is taken: no ordered scan needed
+    const unsigned T = prefix;  // k-th largest key; take kk of the eq_total ties (lowest indices)
     if (threadIdx.x == 0) {
         s_cnt_gt = 0;
         s_cnt_eq = 0;
@@ -625,61 +538,47 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *
         s_val[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    const unsigned n_gt = (unsigned)k - kk;
-    // keys > T (any order, sorted later); keys == T in index order (ordered scan)
-    auto scan_chunk = [&](int c, unsigned key, bool ok) {
-        const int i = c * TOPK_THREADS + threadIdx.x;
-        const bool gt = ok && key > T;
-        const bool eq = ok && key == T;
-        if (gt) {
-            const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
-            s_key[pos] = key;
-            s_val[pos] = (unsigned)i;
-        }
-        // ordered compaction of ties: prefix count within the chunk
-        const unsigned long long bal = __ballot(eq);
-        if (lane == 0) wcnt[wid] = (unsigned)__popcll(bal);
-        __syncthreads();
-        if (eq) {
-            unsigned before = s_cnt_eq;
-            for (int w2 = 0; w2 < wid; ++w2) before += wcnt[w2];
-            before += (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-            if (before < kk) {
-                s_key[n_gt + before] = key;
-                s_val[n_gt + before] = (unsigned)i;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned tot = 0;
-            for (int w2 = 0; w2 < TOPK_THREADS / 64; ++w2) tot += wcnt[w2];
-            s_cnt_eq += tot;
-        }
-        __syncthreads();
-    };
-    if (INREG && all_ties) {
-        // one unordered pass: the kept set is exact, the sort orders it
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            if (j >= nchunks) continue;
-            const int i = j * TOPK_THREADS + threadIdx.x;
-            const unsigned key = kreg[j];
-            if (i < n && key >= T) {
+    if (eq_total == kk) {
+        // every key == T is taken: one unordered pass, the sort orders it
+        for (int i = threadIdx.x; i < n; i += TOPK_THREADS) {
+            const unsigned key = keyat(i);
+            if (key >= T) {
                 const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
                 s_key[pos] = key;
                 s_val[pos] = (unsigned)i;
             }
         }
-        __syncthreads();
-    } else if constexpr (INREG) {
-#pragma unroll
-        for (int j = 0; j < TOPK_KPT; ++j)
-            if (j < nchunks) scan_chunk(j, kreg[j], j * TOPK_THREADS + (int)threadIdx.x < n);
     } else {
-        for (int c = 0; c < nchunks; ++c) {
-            unsigned key = 0;
-            const bool ok = chunk_key(c, key);
-            scan_chunk(c, key, ok);
+        // keys > T (any order); keys == T in index order (ordered scan)
+        const unsigned n_gt = (unsigned)k - kk;
+        for (int base = 0; base < n; base += TOPK_THREADS) {
+            const int i = base + threadIdx.x;
+            const unsigned key = i < n ? keyat(i) : 0u;
+            const bool gt = i < n && key > T, eq = i < n && key == T;
+            if (gt) {
+                const unsigned pos = atomicAdd(&s_cnt_gt, 1u);
+                s_key[pos] = key;
+                s_val[pos] = (unsigned)i;
+            }
+            const unsigned long long bal = __ballot(eq);
+            if (lane == 0) wcnt[wid] = (unsigned)__popcll(bal);
+            __syncthreads();
+            if (eq) {
+                unsigned before = s_cnt_eq;
+                for (int w2 = 0; w2 < wid; ++w2) before += wcnt[w2];
+                before += (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+                if (before < kk) {
+                    s_key[n_gt + before] = key;
+                    s_val[n_gt + before] = (unsigned)i;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned tot = 0;
+                for (int w2 = 0; w2 < TOPK_THREADS / 64; ++w2) tot += wcnt[w2];
+                s_cnt_eq += tot;
+            }
+            __syncthreads();
         }
     }
     bitonic_desc(s_key, s_val, TOPK_MAX);
@@ -2100,10 +1999,9 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
         hipLaunchKernelGGL(k_rpn_part, dim3(RPN_SLICES, (unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount);
         hipLaunchKernelGGL(k_rpn_merge_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount, wb, wsc,
                            wv, wk);
-    } else if (nmax <= TOPK_KPT * TOPK_THREADS)
-        hipLaunchKernelGGL(k_rpn_topk<true>, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
-    else
-        hipLaunchKernelGGL(k_rpn_topk<false>, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
+    } else {
+        hipLaunchKernelGGL(k_rpn_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wb, wsc, wv, wk);
+    }
     hipLaunchKernelGGL(k_nms_mask, dim3(words, (pre_topk + 255) / 256, (unsigned)segs), dim3(256), 0, s, wb, wk,
                        pre_topk, words, nms_thresh, wmask);
     hipLaunchKernelGGL(k_nms_scan, dim3((unsigned)segs), dim3(NMS_THREADS), (size_t)pre_topk * words * 8, s, wv, wk,

@@ -77,19 +77,20 @@ __global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *
             }
     }
     __syncthreads();
+    // the serial decision of thread 0 keeps its run-time indexed arrays in LDS
+    // (as private arrays they would live in scratch memory)
+    __shared__ int pick[SEL_MAXD], cand[SEL_MAXD], idxs[SEL_MAXD];
+    __shared__ bool del[SEL_MAXD];
     if (threadIdx.x == 0) {
-        int pick[SEL_MAXD];
         int np = 0;
         if (n <= 1) {
             for (int i = 0; i < n; ++i) pick[np++] = i;
         } else {
             // drop instances with an empty mask
-            int cand[SEL_MAXD];
             int nc = 0;
             for (int i = 0; i < n; ++i)
                 if (s_cnt[i * SEL_MAXD + i] > 0) cand[nc++] = i;
             // idxs = argsort(scores) ascending (stable for these sizes)
-            int idxs[SEL_MAXD];
             for (int i = 0; i < nc; ++i) idxs[i] = cand[i];
             for (int i = 1; i < nc; ++i) {
                 const int v = idxs[i];
@@ -104,7 +105,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *
             while (len > 0) {
                 const int last = len - 1;
                 pick[np++] = idxs[last];
-                bool del[SEL_MAXD];
                 for (int r = 0; r < len; ++r) del[r] = (r == last);
                 for (int r = 0; r < len; ++r) {
                     for (int c = r + 1; c < len; ++c) {
