@@ -36,15 +36,19 @@ def _flags():
 # vectorises with AVX2 / FMA (every x86-64 host of an MI355X has them)
 HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mfma"]}
 
-# per-file device-code flags.  model_ops.hip is compiled without the packed
-# FP32 VALU instructions (v_pk_add/mul/fma_f32): in its kernels the compiler
-# forms them with op_sel / neg source modifiers (broadcast-and-subtract), and
-# with those the GroupNorm statistics came out nondeterministic on MI355X
-# whenever two model forwards ran concurrently on different hardware queues
-# (~1e-3 relative errors in whole channel halves; 0 of 24 runs without them
-# against ~60 % with, tools/dbg_race.py).  The target-feature switch reaches
-# the host compile too, where clang ignores it with a warning.
-DEVICE_FLAGS = {"model_ops.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]}
+# Device code is compiled without the packed FP32 VALU instructions
+# (v_pk_add/mul/fma_f32): the compiler forms them with op_sel / neg source
+# modifiers (broadcast operands), and with those (1) the GroupNorm statistics
+# came out nondeterministic on MI355X whenever two model forwards ran
+# concurrently on different hardware queues (~1e-3 relative errors in whole
+# channel halves; 0 of 24 runs without them against ~60 % with,
+# tools/dbg_race.py), and (2) once the Winograd output transform (the only
+# other kernel with such forms) was added, runs with more concurrency (three
+# forwards on eight hardware queues, or two processes on one GPU) ended in
+# illegal-address faults.  The target-feature switch reaches the host compile
+# too, where clang ignores it with a warning.
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32, "conv.hip": NO_PACKED_FP32, "inpaint.hip": NO_PACKED_FP32}
 
 
 def sources():
