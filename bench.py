@@ -30,12 +30,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# One HIP hardware queue per stream of the overlapped pipeline (H2D, front,
-# two model forwards, tail): with HIP's default of 4 the tail shares a queue
-# with a model stream, and its wait for one forward blocks the next forward
-# queued behind it (measured +2.7 % with 8 at fp16).  Read at HIP
-# initialisation; a value set by the launcher wins and is recorded in the line.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP hardware queues: HIP's default (4) unless the launcher sets one (recorded
+# in the line).  8 measured +2.7 % at fp16 and +0.6 % at fp32 with two model
+# streams, but 8 queues with three model streams ended in an illegal-address
+# fault that is not root-caused, so the bench does not
+# raise the count itself.
 
 
 def parse():
@@ -58,6 +57,8 @@ def parse():
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
     ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_conv_set_winograd_min_cin")
+    ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT",
+                    help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
     return ap.parse_args()
@@ -325,6 +326,12 @@ def main():
     if args.roi_mode is not None:
         from moseq2_detectron_extract_amd._lib import call
         call("mdx_roi_align_set_mode", args.roi_mode)
+    for kv in args.set:
+        from moseq2_detectron_extract_amd._lib import call
+        fn, val = kv.split("=")
+        if not (fn.startswith("mdx_") and "_set_" in fn):
+            raise SystemExit(f"--set: {fn} is not a libmdx tuning knob")
+        call(fn, int(val))
     B = args.batch
     sess = synth.SyntheticSession(2 * B, seed=1000 + rank)
     frames = sess.frames(0, 2 * B)

@@ -329,6 +329,18 @@ int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const 
                   int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
                   void *out, mdx_stream_t stream);
 
+/* Same, with an optional int32 scratch of R entries: when order_ws is not
+ * NULL (and mdx_roi_align_set_sorted(1), the default) the ROIs of each image
+ * are first permuted by pyramid level and map band (k_roi_order) so the
+ * workgroups in flight share one band of one level map; outputs are
+ * identical to the unordered call.  order_ws == NULL is mdx_roi_align. */
+int mdx_roi_align_ex(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
+                     int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
+                     int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
+                     int *order_ws, void *out, mdx_stream_t stream);
+/* Tuning knob for the permutation above (1 on, 0 off); returns the old value. */
+int mdx_roi_align_set_sorted(int on);
+
 /* ROIAlign kernel choice: 0 = one workgroup per (ROI, 128-B channel slice)
  * with the sample window staged in LDS; 1, 2, 3 = one workgroup per
  * ROI over all channels, taps gathered from the map, 1/2/4 items per thread

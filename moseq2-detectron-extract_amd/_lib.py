@@ -76,6 +76,8 @@ SIGNATURES = {
     "mdx_rpn_proposals": (I32, [P, P, P, P, I32, I32, I32, P, F32, I32, I32, I32, I32, F32, F32, F32,
                                 P, P, P, P, P]),
     "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
+    "mdx_roi_align_ex": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P, P]),
+    "mdx_roi_align_set_sorted": (I32, [I32]),
     "mdx_roi_align_set_mode": (I32, [I32]),
     "mdx_roi_align_set_order": (I32, [I32]),
     "mdx_box_postprocess": (I32, [P, I32, P, P, I32, I32, I32, F32, F32, I32, I32, P, F32, P, P, P, P, P]),

@@ -541,11 +541,13 @@ struct Fwd {
                     int per_image, int P) {
         const int C = m.cfg.fpn_out_channels;
         void *out = alloc((size_t)R * P * P * C * m.es);
+        // the box pooler (per_image = post-NMS proposals) runs in level/band order
+        int *order = per_image >= 256 ? (int *)alloc((size_t)R * sizeof(int)) : nullptr;
         const float sc[4] = {1.f / 4, 1.f / 8, 1.f / 16, 1.f / 32};
         if (!c.dry && ok())
-            chk(mdx_roi_align((const void *const *)feats, fh, fw, sc, 4, 2, C, rois, counts, R, per_image, P,
-                              m.cfg.pooler_sampling_ratio, m.cfg.pooler_aligned, m.cfg.canonical_box_size,
-                              m.cfg.canonical_level, m.dt, out, s));
+            chk(mdx_roi_align_ex((const void *const *)feats, fh, fw, sc, 4, 2, C, rois, counts, R, per_image, P,
+                                 m.cfg.pooler_sampling_ratio, m.cfg.pooler_aligned, m.cfg.canonical_box_size,
+                                 m.cfg.canonical_level, m.dt, order, out, s));
         return out;
     }
 

@@ -870,7 +870,20 @@ struct RoiLevels {
     int L, min_level, C, P, sampling, aligned, per_image;
     float canonical_size, canonical_level;
     int xcd_remap;  // 1: XCD-contiguous ROI ranges (default); 0: ROIs in dispatch order across XCDs
+    const int *order;  // optional ROI permutation (k_roi_order), applied after the XCD remap
 };
+
+// the ROI a workgroup pools: XCD-contiguous ranges of the dispatch order (the
+// ROIs of one image share its maps), then the optional locality permutation
+__device__ __forceinline__ int roi_of_block(const RoiLevels &rl) {
+    int r = blockIdx.x;
+    if (rl.xcd_remap) {
+        const int Lb = blockIdx.x, nwg = gridDim.x;
+        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
+        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
+    }
+    return rl.order ? rl.order[r] : r;
+}
 
 template <typename T>
 struct Vec16;
@@ -902,7 +915,7 @@ __device__ __forceinline__ void st16(T *p, const float *v) {
 // ROIAlign sample geometry of one ROI (ROIAlignV2 / ROIPooler semantics)
 struct RoiGeom {
     const void *feat;  // level map of this ROI's image
-    int H, W, gh, gw;
+    int li, H, W, gh, gw;
     float rsw, rsh, bh, bw, count;
 };
 
@@ -913,9 +926,11 @@ __device__ __forceinline__ RoiGeom roi_geom(const RoiLevels &rl, const float *ro
     const float bs = sqrtf(area);
     float lv = floorf(rl.canonical_level + log2f(bs / rl.canonical_size + 1e-8f));
     const float maxl = (float)(rl.min_level + rl.L - 1);
-    lv = lv < (float)rl.min_level ? (float)rl.min_level : (lv > maxl ? maxl : lv);
+    // (a non-finite box maps to the lowest level, never to an index outside the table)
+    lv = !(lv >= (float)rl.min_level) ? (float)rl.min_level : (lv > maxl ? maxl : lv);
     const int li = (int)lv - rl.min_level;
     RoiGeom g;
+    g.li = li;
     g.H = rl.H[li];
     g.W = rl.W[li];
     g.feat = reinterpret_cast<const char *>(rl.feat[li]) + (size_t)b * g.H * g.W * rl.C * esize;
@@ -979,12 +994,7 @@ __global__ __launch_bounds__(256) void k_roi_align(RoiLevels rl, const float *__
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
     __shared__ __attribute__((aligned(16))) char s_win[ROI_WIN_BYTES];
     // XCD-contiguous ROI ranges: the ROIs of one image share its feature maps
-    int r = blockIdx.x;
-    if (rl.xcd_remap) {
-        const int Lb = blockIdx.x, nwg = gridDim.x;
-        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
-        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
-    }
+    const int r = roi_of_block(rl);
     const int G = gslice, PXB = G * 16;  // 16-B groups per slice, LDS bytes per pixel
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
@@ -1139,12 +1149,7 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
     constexpr int V = Vec16<T>::N;
     __shared__ int s_y0[ROI_TAB], s_y1[ROI_TAB], s_x0[ROI_TAB], s_x1[ROI_TAB];
     __shared__ float s_ly[ROI_TAB], s_lx[ROI_TAB];
-    int r = blockIdx.x;
-    if (rl.xcd_remap) {
-        const int Lb = blockIdx.x, nwg = gridDim.x;
-        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
-        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
-    }
+    const int r = roi_of_block(rl);
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
     const int G = C / V;  // 16-B groups per pixel
@@ -1304,12 +1309,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     __shared__ int s_r0[ROI_PMAX], s_nr[ROI_PMAX], s_c0[ROI_PMAX], s_nc[ROI_PMAX];
     __shared__ float s_A[ROI_PMAX][ROI_RMAX], s_B[ROI_PMAX][ROI_RMAX];
     __shared__ int s_bad;
-    int r = blockIdx.x;
-    if (rl.xcd_remap) {
-        const int Lb = blockIdx.x, nwg = gridDim.x;
-        const int q = nwg / 8, rr = nwg % 8, xcd = Lb % 8;
-        r = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + Lb / 8;
-    }
+    const int r = roi_of_block(rl);
     const int b = r / rl.per_image, ri = r - b * rl.per_image;
     const int C = rl.C, P = rl.P;
     const int G = C / V;
@@ -1534,7 +1534,57 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     }
 }
 
-static int g_roi_mode = 4, g_roi_xcd = 1;
+// Per image, a permutation of its ROIs grouped by pyramid level and, within a
+// level, by horizontal band of the sample window's centre row, valid ROIs
+// first.  The pooler's workgroups in flight on one XCD then read one band of
+// one level map (L2 reuse) instead of all four maps of the image (the box
+// pooler fetched ~6x the map bytes in ROI order).  Positions come from LDS
+// atomics, so the permutation varies from run to run; the pooled rows do
+// not (every ROI writes its own rows with the same arithmetic).
+__global__ __launch_bounds__(256) void k_roi_order(RoiLevels rl, const float *__restrict__ rois,
+                                                   const int *__restrict__ counts, int *__restrict__ order) {
+    __shared__ int s_off[256];
+    const int b = blockIdx.x, n = rl.per_image, t = threadIdx.x;
+    const int valid = min(counts[b], n);
+    const int bands = 255 / rl.L, NK = rl.L * bands + 1;  // last key: empty slots
+    auto key = [&](int k) -> int {
+        if (k >= valid) return NK - 1;
+        const RoiGeom g = roi_geom(rl, rois, b * n + k, b, 4);
+        const float cy = g.rsh + 0.5f * g.bh * (float)rl.P;
+        int band = (int)(cy * (float)bands / (float)g.H);
+        band = band < 0 ? 0 : (band >= bands ? bands - 1 : band);
+        return g.li * bands + band;
+    };
+    s_off[t] = 0;
+    __syncthreads();
+    for (int k = t; k < n; k += 256) atomicAdd(&s_off[key(k)], 1);
+    __syncthreads();
+    // exclusive scan of the 256 counts (Hillis-Steele, inclusive then shift)
+    int v = s_off[t];
+    for (int d = 1; d < 256; d <<= 1) {
+        __syncthreads();
+        const int u = t >= d ? s_off[t - d] : 0;
+        __syncthreads();
+        v += u;
+        s_off[t] = v;
+    }
+    __syncthreads();
+    const int excl = t ? s_off[t - 1] : 0;
+    __syncthreads();
+    s_off[t] = excl;
+    __syncthreads();
+    for (int k = t; k < n; k += 256) {
+        const int pos = atomicAdd(&s_off[key(k)], 1);
+        order[b * n + pos] = b * n + k;
+    }
+}
+
+static int g_roi_mode = 4, g_roi_xcd = 1, g_roi_sorted = 1;
+extern "C" int mdx_roi_align_set_sorted(int on) {
+    const int old = g_roi_sorted;
+    g_roi_sorted = on;
+    return old;
+}
 extern "C" int mdx_roi_align_set_order(int xcd_remap) {
     const int old = g_roi_xcd;
     g_roi_xcd = xcd_remap;
@@ -2016,6 +2066,14 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
                              int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
                              int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
                              void *out, mdx_stream_t stream) {
+    return mdx_roi_align_ex(feats, fh, fw, scales, L, min_level, C, rois, counts, R, per_image, P, sampling, aligned,
+                            canonical_size, canonical_level, dtype, nullptr, out, stream);
+}
+
+extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
+                                int min_level, int C, const float *rois, const int *counts, int R, int per_image,
+                                int P, int sampling, int aligned, float canonical_size, float canonical_level,
+                                int dtype, int *order_ws, void *out, mdx_stream_t stream) {
     MDX_REQUIRE(feats && fh && fw && scales && rois && counts && out, "mdx_roi_align: null pointer");
     MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && per_image > 0 && R % per_image == 0, "mdx_roi_align: bad args");
     const int vch = dtype == 1 ? 8 : 4;  // channels per 16 B
@@ -2034,6 +2092,12 @@ extern "C" int mdx_roi_align(const void *const *feats, const int *fh, const int 
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     rl.xcd_remap = g_roi_xcd;
+    rl.order = nullptr;
+    if (order_ws && g_roi_sorted) {
+        hipLaunchKernelGGL(k_roi_order, dim3(R / per_image), dim3(256), 0, as_stream(stream), rl, rois, counts,
+                           order_ws);
+        rl.order = order_ws;
+    }
     if (g_roi_mode == 5 && P <= ROI_PMAX) {
         if (dtype == 1)
             hipLaunchKernelGGL((k_roi_align_sep<_Float16, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,

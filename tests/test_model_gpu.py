@@ -280,9 +280,10 @@ def test_rpn_proposals_from_identical_heads(mdx, sliced):
         torch.testing.assert_close(boxes[b, :n].cpu(), wb, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("ordered", [False, True], ids=["roi-order", "level-band-order"])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True)])
-def test_roi_align_matches_oracle(mdx, rt, C, half, mode):
+def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
@@ -308,10 +309,21 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode):
     sc = (ctypes.c_float * 4)(*[0.25, 0.125, 0.0625, 0.03125])
     bd, cd = boxes.contiguous().cuda(), counts.cuda()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    order = torch.full((B * per,), -1, dtype=torch.int32, device="cuda")
     old = call("mdx_roi_align_set_mode", mode)
     try:
-        call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4, 2,
-             C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(out), None)
+        # the level/band permutation (k_roi_order) changes which workgroup pools
+        # which ROI, never the pooled values
+        call("mdx_roi_align_ex", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
+             2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(order) if ordered else None, P(out),
+             None)
+        if ordered:
+            perm = order.cpu().view(B, per).sort(1).values
+            assert torch.equal(perm, torch.arange(B * per, dtype=torch.int32).view(B, per))  # a permutation per image
+            ref = torch.empty_like(out)
+            call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
+                 2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(ref), None)
+            assert torch.equal(out, ref)
     finally:
         call("mdx_roi_align_set_mode", old)
     got = out.cpu().float().permute(0, 3, 1, 2)
