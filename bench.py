@@ -89,6 +89,7 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
                 6: "Winograd F(2x2,3x3) (input transform + 16 batched k_conv GEMMs + output transform)",
+                7: "k_conv_x3<128> fp32 as bf16 plane products", 8: "k_conv_x3<64> fp32 as bf16 plane products",
                 10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance"}
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 PMC_FILE = {"fp16": "r01_pmc_kernels.json", "fp32": "r02_pmc_kernels_fp32.json"}
@@ -359,8 +360,23 @@ def main():
         secondary = {"fp16": {"value": round(frames_done / dt16, 2), "unit": "frames/s",
                               "ms_per_step": round(dt16 / args.steps * 1e3, 3), "dtype": "fp16",
                               "note": "fp16 MFMA forward (fp32 accumulation), same loop; tolerance vs the fp32 "
-                                      "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0]"}}
+                                      "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0-0]"}}
         del ex16
+        torch.cuda.synchronize()
+        from moseq2_detectron_extract_amd._lib import call
+        old = call("mdx_conv_set_fp32_split", 6)
+        try:
+            dtx, exx, _ = measure(args, "fp32", B, world, rank, raw_host, sess, dist, gather_bufs)
+        finally:
+            call("mdx_conv_set_fp32_split", old)
+        secondary["fp32_bf16x6"] = {
+            "value": round(frames_done / dtx, 2), "unit": "frames/s", "ms_per_step": round(dtx / args.steps * 1e3, 3),
+            "dtype": "fp32 operands split exactly into 3 bf16 planes, 6 plane products on the bf16 matrix cores, "
+                     "fp32 accumulation",
+            "note": "mdx_conv_set_fp32_split(6); per product the dropped terms are below one fp32 rounding; "
+                    "full-frame parity vs the fp32 oracle at least as close as the f32-MFMA kernels' "
+                    "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6], DESIGN.md section 3)"}
+        del exx
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

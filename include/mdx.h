@@ -224,6 +224,16 @@ int mdx_conv_set_mfma_prio256(int on);
  * for layers with >= 500 such tiles and K >= 2048 (default), 3 the 256x256
  * tile under the fp16 policy.  Returns the old value. */
 int mdx_conv_set_dma_f32(int on);
+/* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
+ * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
+ * the products accumulate in fp32.  9: all nine plane products (the exact
+ * products, fp32 accumulation); 6: without the three smallest (each below one
+ * fp32 rounding of the product); 0 (default): the f32 MFMA kernels.  Also
+ * used for the Winograd GEMMs.  Returns the old value. */
+int mdx_conv_set_fp32_split(int mode);
+/* Tuning knob: 1 (default) runs every split-plane launch on the 64-wide N
+ * tile (two workgroups per CU), 0 the 128-wide tile where Cout > 64. */
+int mdx_conv_set_x3_narrow(int on);
 /* Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride-1 / pad-1
  * convolutions (NHWC): the algorithm the model handle uses for such layers
  * with Cin >= 256 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
@@ -253,7 +263,9 @@ enum {
     MDX_CONV_KERNEL_DMA128 = 3,
     MDX_CONV_KERNEL_STREAM1X1 = 4,
     MDX_CONV_KERNEL_HEAD1X1 = 5,
-    MDX_CONV_KERNEL_WINOGRAD = 6
+    MDX_CONV_KERNEL_WINOGRAD = 6,
+    MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
+    MDX_CONV_KERNEL_X3_64 = 8
 };
 /* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256

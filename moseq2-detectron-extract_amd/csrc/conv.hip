@@ -447,6 +447,248 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores (the fp32 model's layers when
+// mdx_conv_set_fp32_split(6 | 9)).  Every fp32 operand is split into three
+// bf16 values x = hi + mid + lo (hi = RN(x), mid = RN(x - hi), lo = x - hi -
+// mid): each subtraction is exact (Sterbenz) and the last residual has at most
+// 8 significant bits, so the three parts represent x EXACTLY (normal range).
+// A bf16 x bf16 product (8 x 8 significant bits) is exact in fp32, so
+// sum_k a_k b_k = sum of the nine plane products, accumulated in fp32 by
+// v_mfma_f32_16x16x32_bf16 at 16x the f32 MFMA rate.  NP = 9 forms all nine;
+// NP = 6 drops mid*lo, lo*mid, lo*lo (each <= 2^-24 |a b|, the size of one
+// fp32 rounding).  The hi*hi products accumulate in their own registers, the
+// smaller cross products in a second set, added once at the end.
+//
+// Same tile, loads and epilogue as k_conv<float, float, BN_>: 128 x BN_ per
+// 256-thread workgroup, K-steps of 32 fp32 loaded 16 B per lane through the
+// range-checked descriptors one step ahead; the split happens between the
+// register stage and LDS, which holds 3 planes per operand of 64-B rows (32
+// bf16 of one K-step: a wave's 16-row x 4-piece fragment read is 1 KB
+// contiguous, no swizzle needed).  96 KB of LDS: one workgroup per CU.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int X3_ROWB = 64;
+
+__device__ __forceinline__ void split3_store(const uint4 &v, char *p0, int plane_bytes) {
+    const float f[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+    bf16x4 h, m, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const __bf16 hb = (__bf16)f[e];
+        const float r1 = f[e] - (float)hb;
+        const __bf16 mb = (__bf16)r1;
+        h[e] = hb;
+        m[e] = mb;
+        l[e] = (__bf16)(r1 - (float)mb);
+    }
+    *reinterpret_cast<bf16x4 *>(p0) = h;
+    *reinterpret_cast<bf16x4 *>(p0 + plane_bytes) = m;
+    *reinterpret_cast<bf16x4 *>(p0 + 2 * plane_bytes) = l;
+}
+
+template <typename TO, int BN_, int NP>
+__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(ConvArgs a) {
+    static_assert(NP == 6 || NP == 9, "x6 or x9 plane products");
+    constexpr int BK = 32, VEC = 4;
+    constexpr int TI = BM / 32, TJ = BN_ / 32;
+    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
+    constexpr int APL = BM * X3_ROWB, BPL = BN_ * X3_ROWB;  // bytes of one plane
+    constexpr int STAGE = 3 * (APL + BPL);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (gridDim.z > 1) {  // batch entry z of a batched GEMM
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN_;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // ---- global loads: as k_conv (rows tid/8 + 32 i, 16-byte chunk tid % 8)
+    const int kc = tid & 7;
+    const int lrow = tid >> 3;
+    int a_iy0[4], a_ix0[4];
+    long long a_base[4];
+    bool a_ok[4];
+    const int ohw = a.OH * a.OW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int gm = m0 + lrow + 32 * i;
+        a_ok[i] = gm < a.M;
+        const int gmc = a_ok[i] ? gm : 0;
+        const int b = gmc / ohw, rem = gmc - b * ohw;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_iy0[i] = oy * a.stride - a.pad;
+        a_ix0[i] = ox * a.stride - a.pad;
+        a_base[i] = (long long)b * a.H * a.W * a.Cin;
+    }
+    const int kz = blockIdx.y;
+    int kglob = kz * a.ksteps * BK + kc * VEC;
+    int kci = kglob % a.Cin;
+    int kr = kglob / a.Cin;
+    int kkx = kr % a.KW, kky = kr / a.KW;
+    uint4 ra[2][4], rb[2][BLOADS];
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
+        const bool kok = kglob < a.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
+            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
+            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i) {
+            const int gn = n0 + lrow + 32 * i;
+            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * 4ll);
+            Bv[i] = __builtin_bit_cast(uint4,
+                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
+        }
+    };
+    auto advance_k = [&]() {
+        kglob += BK;
+        kci += BK;
+        while (kci >= a.Cin) {
+            kci -= a.Cin;
+            if (++kkx == a.KW) {
+                kkx = 0;
+                ++kky;
+            }
+        }
+    };
+    // the 4 fp32 of chunk kc become 8 B at byte 8 kc of the row in each plane
+    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
+        char *st = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) split3_store(A[i], st + (lrow + 32 * i) * X3_ROWB + kc * 8, APL);
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i) split3_store(Bv[i], st + 3 * APL + (lrow + 32 * i) * X3_ROWB + kc * 8, BPL);
+    };
+
+    float4v acc_h[TI][TJ], acc_x[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            acc_h[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+            acc_x[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+        }
+
+    const int nk_all = (a.K + BK - 1) / BK;
+    const int nk = min(a.ksteps, nk_all - kz * a.ksteps);
+    load_global(ra[0], rb[0]);
+    advance_k();
+    store_lds(0, ra[0], rb[0]);
+    if (nk > 1) {
+        load_global(ra[1], rb[1]);
+        advance_k();
+    }
+    __syncthreads();
+    // cross products (plane of A, plane of B; 0 hi, 1 mid, 2 lo), smallest
+    // first, into acc_x: lo*lo, mid*lo, lo*mid (x9 only), mid*mid, hi*lo,
+    // lo*hi, hi*mid, mid*hi; hi*hi into acc_h
+    constexpr int PA[8] = {2, 1, 2, 1, 0, 2, 0, 1}, PB[8] = {2, 2, 1, 1, 2, 0, 1, 0};
+    constexpr int P0 = NP == 9 ? 0 : 3;
+    auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
+                     const uint4 (&Bs_)[BLOADS]) {
+        const int cur = kt & 1;
+        if (kt + 2 < nk) {
+            load_global(Ai, Bi);
+            advance_k();
+        }
+        const char *Ab = smem + cur * STAGE + (wm * (BM / 2) + (lane & 15)) * X3_ROWB + (lane >> 4) * 16;
+        const char *Bb = smem + cur * STAGE + 3 * APL + (wn * (BN_ / 2) + (lane & 15)) * X3_ROWB + (lane >> 4) * 16;
+        bf16x8 af[3][TI], bf[3][TJ];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i) af[p][i] = *reinterpret_cast<const bf16x8 *>(Ab + p * APL + i * 16 * X3_ROWB);
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) bf[p][j] = *reinterpret_cast<const bf16x8 *>(Bb + p * BPL + j * 16 * X3_ROWB);
+        }
+#pragma unroll
+        for (int q = P0; q < 8; ++q)
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+                    acc_x[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[PA[q]][i], bf[PB[q]][j], acc_x[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bf[0][j], acc_h[i][j], 0, 0, 0);
+        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
+        __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+        kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+        kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
+    }
+    if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+
+    // ---- epilogue: as k_conv, in two halves of BM/2 rows
+    constexpr int CP = BN_ + 4;
+    constexpr int HM = BM / 2;
+    float *Cs = reinterpret_cast<float *>(smem);
+    constexpr int CPR = BN_ / 8;
+    constexpr int NQ = HM * CPR / CONV_THREADS;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (wm == h) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = i * 16 + (lane >> 4) * 4 + r;
+                        const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
+                        Cs[row * CP + col] = acc_h[i][j][r] + acc_x[i][j][r];
+                    }
+        }
+        __syncthreads();
+        const int mh = m0 + h * HM;
+        if (a.ksplit > 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                const int gm = mh + row, gn0 = n0 + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) continue;
+                const float *src = Cs + row * CP + ch * 8;
+                float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
+                *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
+                *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
+            }
+        } else {
+            finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                gm = mh + row;
+                gn0 = n0 + ch * 8;
+                src = Cs + row * CP + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+            });
+        }
+        if (h == 0) __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Large-layer kernel (fp16, Cin % 64 == 0): 256x256 tile, 512 threads = 8
 // waves as 2(M) x 4(N), each wave 128x64 = 8x4 MFMA 16x16x32 tiles.  Both
 // operands are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
@@ -1177,6 +1419,41 @@ extern "C" int mdx_conv_set_dma_f32(int on) {
     g_dma_f32 = on;
     return old;
 }
+// fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
+static int g_fp32_split = 0;
+extern "C" int mdx_conv_set_fp32_split(int mode) {
+    const int old = g_fp32_split;
+    if (mode == 0 || mode == 6 || mode == 9) g_fp32_split = mode;
+    return old;
+}
+// 64-wide N tile for every split-plane launch (72 KB of LDS and <= 256
+// registers: two workgroups per CU, measured 6-25 % faster per layer than the
+// 128-wide tile's one workgroup per CU, whose single wave per SIMD serialises
+// the split/LDS work with the MFMAs) -- default; 0: the 128-wide tile where Cout > 64
+static int g_x3_narrow = 1;
+extern "C" int mdx_conv_set_x3_narrow(int on) {
+    const int old = g_x3_narrow;
+    g_x3_narrow = on;
+    return old;
+}
+// launch of the split-plane fp32 kernel (LDS: double-buffered planes or the epilogue image)
+static void launch_x3(const ConvArgs &a, int bn, dim3 grid, hipStream_t s) {
+    const size_t stage = 3 * ((size_t)BM * X3_ROWB + (size_t)bn * X3_ROWB);
+    const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * stage;
+    const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
+    const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+    if (bn == 64) {
+        if (g_fp32_split == 9)
+            hipLaunchKernelGGL((k_conv_x3<float, 64, 9>), grid, dim3(CONV_THREADS), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_conv_x3<float, 64, 6>), grid, dim3(CONV_THREADS), lds, s, a);
+    } else {
+        if (g_fp32_split == 9)
+            hipLaunchKernelGGL((k_conv_x3<float, 128, 9>), grid, dim3(CONV_THREADS), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_conv_x3<float, 128, 6>), grid, dim3(CONV_THREADS), lds, s, a);
+    }
+}
 // s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
 static int g_prio8 = 0;
 extern "C" int mdx_conv_set_mfma_prio256(int on) {
@@ -1207,9 +1484,8 @@ extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
 
 // split-K slice count for a launch of `tiles` output tiles and nk K-steps:
 // minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
-// with 2 resident workgroups on each of the 256 CUs
-static int choose_ksplit(long long tiles, int nk, long long M, int Cout, long long ws_bytes) {
-    const long long slots = 512;
+// with `slots` resident workgroups (2 on each of the 256 CUs; 1 for k_conv_x3)
+static int choose_ksplit(long long tiles, int nk, long long M, int Cout, long long ws_bytes, long long slots = 512) {
     int best = 1;
     double best_cost = 1e30;
     for (int ks = 1; ks <= 8; ++ks) {
@@ -1314,7 +1590,8 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     // (with split-K) below, which serves the small grids better
     // fp32 operands (Cin % 32 == 0, fp32 out): the 256x256 kernel on 16x16x4 f32
     // MFMAs, same LDS image (64-B rows of 16 floats)
-    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32;
+    const bool x3 = in_dtype == 0 && out_dtype == 0 && g_fp32_split;
+    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32 && !x3;
     if (((in_dtype == 1 && Cin % 64 == 0) || dma_f32) && (ksplit == 1 || ksplit == 0) &&
         KH * KW * Cin > g_narrow_kmax) {
         const int subk = in_dtype == 1 ? 32 : 16;  // K elements per 64-B substep
@@ -1402,13 +1679,15 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     }
     // 64-wide N tile: no wasted MFMA columns for 64-channel layers; more
     // workgroups per CU for the small-K layers
-    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax;
+    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax || (x3 && g_x3_narrow);
     const int bn = narrow ? 64 : BN;
     const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_n = tiles_n;
     a.tiles_total = tiles_m * tiles_n;
     const int nk = (a.K + (in_dtype == 1 ? 64 : 32) - 1) / (in_dtype == 1 ? 64 : 32);
-    if (ksplit <= 0) ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes) : 1;
+    if (ksplit <= 0)
+        ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes, x3 ? 256 : 512)
+                                              : 1;
     MDX_REQUIRE(ksplit == 1 || (workspace && Cout % 8 == 0 && (long long)ksplit * M * Cout * 4 <= workspace_bytes),
                 "mdx_conv2d: split-K needs Cout %% 8 == 0 and a workspace of ksplit*M*Cout*4 bytes");
     ksplit = ksplit > nk ? nk : ksplit;
@@ -1420,6 +1699,15 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+    if (x3) {
+        launch_x3(a, bn, dim3(a.tiles_total, a.ksplit), s);
+        if (a.ksplit > 1)
+            hipLaunchKernelGGL((k_conv_reduce<float>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0, s, a);
+        t_plan_kernel = narrow ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
+        t_plan_ksplit = a.ksplit;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
@@ -1544,7 +1832,7 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     a.bsx = T * Cin * 4;
     a.bsw = (long long)Cout * Cin * 4;
     a.bso = T * Cout * 4;
-    const int bn = Cout <= 64 ? 64 : BN;
+    const int bn = Cout <= 64 || (g_fp32_split && g_x3_narrow) ? 64 : BN;
     a.tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_total = (int)(ceil_div(T, BM) * a.tiles_n);
     const int nk = (Cin + 31) / 32;
@@ -1554,7 +1842,9 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     const dim3 grid((unsigned)a.tiles_total, 1, (unsigned)NB);
-    if (bn == 64)
+    if (g_fp32_split)
+        launch_x3(a, bn, grid, s);
+    else if (bn == 64)
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
     else
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);

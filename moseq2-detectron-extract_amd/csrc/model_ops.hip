@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256) void k_nms_mask(const float *__restrict__ boxe
                                                   unsigned long long *__restrict__ mask) {
     __shared__ float4 jb[64];
     const int seg = blockIdx.z, w = blockIdx.x;
-    const int k = kseg[seg];
+    const int k = min(max(kseg[seg], 0), cap);  // (counts never address past the segment)
     const int j0 = w * 64;
     const int i = blockIdx.y * 256 + threadIdx.x;
     if (j0 >= k || blockIdx.y * 256 >= k) return;  // uniform per block
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(NMS_THREADS) void k_nms_scan(const int *__restrict_
     extern __shared__ unsigned long long rows[];  // [k][words]
     __shared__ unsigned long long vbits[NMS_MAXW];
     const int seg = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int k = kseg[seg];
+    const int k = min(max(kseg[seg], 0), cap);
     const int *vl = valid + (long long)seg * cap;
     const unsigned long long *mk = mask + (long long)seg * cap * words;
     int *kp = keep + (long long)seg * cap;
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(1024) void k_rpn_merge(const float *__restrict__ ws
     __syncthreads();
     for (int l = 0; l < L; ++l) {
         const int seg = b * L + l;
-        const int k = kseg[seg];
+        const int k = min(max(kseg[seg], 0), cap);
         for (int r = threadIdx.x; r < k; r += blockDim.x) {
             if (keep[(long long)seg * cap + r]) {
                 const unsigned pos = atomicAdd(&s_n, 1u);

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_mask_nms_select(const uint8_t *
     __shared__ unsigned long long s_cnt[SEL_MAXD * SEL_MAXD];
     __shared__ int s_sel;
     const int b = blockIdx.x;
-    const int n = ndet[b];
+    const int n = min(max(ndet[b], 0), min(D, DM));  // (a count never addresses past the planes)
     const uint8_t *mb = masks + (long long)b * D * plane;
     for (int i = threadIdx.x; i < SEL_MAXD * SEL_MAXD; i += SEL_THREADS) s_cnt[i] = 0;
     __syncthreads();
@@ -172,11 +172,11 @@ __global__ __launch_bounds__(CEN_THREADS) void k_mask_centers(const uint8_t *__r
     __shared__ unsigned long long s_acc[3][CEN_THREADS / 64];
     const int b = blockIdx.x / D, slot = blockIdx.x % D;
     double *out = centers + ((long long)b * D + slot) * 2;
-    if (slot >= nkeep[b]) {
+    const int j = keep_idx[b * D + slot];
+    if (slot >= nkeep[b] || j < 0 || j >= D) {
         if (threadIdx.x == 0) out[0] = out[1] = __builtin_nan("");
         return;
     }
-    const int j = keep_idx[b * D + slot];
     const uint8_t *m = masks + ((long long)b * D + j) * plane;
     const long long hw = (long long)h * w;
     unsigned long long area = 0, sy = 0, sx = 0;

@@ -165,6 +165,56 @@ def test_conv2d(mdx, dtype, case, ksplit):
     assert err < tol, f"max rel err {err:.2e}"
 
 
+@pytest.mark.parametrize("narrow", [1, 0], ids=["n64", "n128"])
+@pytest.mark.parametrize("ksplit", [1, 3])
+@pytest.mark.parametrize("split", [6, 9])
+@pytest.mark.parametrize("case", CONV_CASES + [(192, 1, 1, 12544, 136, 1, 1, 0, False, True)])
+def test_conv2d_fp32_split(mdx, case, split, ksplit, narrow):
+    """fp32 layers as bf16 plane products (k_conv_x3): the exact three-way
+    split makes every product exact (x9) or drops terms below one fp32
+    rounding (x6), so the error against fp64 stays at the f32-MFMA kernel's:
+    measured side by side here, bounded at 4x it (and 1e-5 of the output
+    scale, the fp32 tolerance being 1e-4)."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    N, H, W, Cin, Cout, k, s, p, use_res, relu = case
+    if Cin % 4 or (ksplit > 1 and Cout % 8):
+        pytest.skip()
+    g = torch.Generator().manual_seed(hash(case) % 997)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = torch.randn(N, OH, OW, Cout, generator=g) if use_res else None
+    want = _conv_ref(x, w, b, s, p, res, relu)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    xd, bd = x.cuda(), b.cuda()
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
+    rd = res.cuda() if res is not None else None
+    nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
+    ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
+    errs = {}
+    for mode in (0, split):
+        out = torch.empty(N, OH, OW, Cout, device="cuda")
+        old = call("mdx_conv_set_fp32_split", mode)
+        old_f = call("mdx_conv_set_dma_f32", 0)
+        old_n = call("mdx_conv_set_x3_narrow", narrow)
+        try:
+            call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 0, 0,
+                 P(out), ksplit, P(ws), nb, None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+        finally:
+            call("mdx_conv_set_fp32_split", old)
+            call("mdx_conv_set_dma_f32", old_f)
+            call("mdx_conv_set_x3_narrow", old_n)
+        assert (kid.value in (7, 8)) == (mode != 0)
+        if mode and narrow:
+            assert kid.value == 8
+        errs[mode] = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+    assert errs[split] < max(4 * errs[0], 5e-7) and errs[split] < 1e-5, errs
+
+
 def test_conv_mfma_layout_identity(mdx):
     """A = I (as a 1x1 conv over an identity input) with an asymmetric B catches a
     transposed C write."""
@@ -680,10 +730,11 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
+@pytest.mark.parametrize("split", [0, 6], ids=["f32-mfma", "bf16x6"])
 @pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
-def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m):
+def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     """Winograd F(m x m, 3x3) (fp32: input transform, (m+2)^2 batched GEMMs,
     output transform + bias + ReLU) against the fp64 direct convolution:
     within the fp32 direct kernels' tolerance (1e-4 relative to the output
@@ -706,7 +757,11 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m):
     out = torch.empty(N, H, W, Cout, device="cuda")
     nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout, m)
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
-    call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
+    old = call("mdx_conv_set_fp32_split", split)
+    try:
+        call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
+    finally:
+        call("mdx_conv_set_fp32_split", old)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6

@@ -81,20 +81,25 @@ def _ang_diff(a, b):
     return np.minimum(d, 180.0 - d)
 
 
-@pytest.mark.parametrize("depth,B,dtype,wino", [(50, 32, "fp32", 4), (50, 32, "fp32", 2), (50, 32, "fp32", 0),
-                                                (50, 32, "fp16", 0), (101, 64, "fp16", 0)])
-def test_forward_full_frame(mdx, depth, B, dtype, wino):
+@pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 2, 0),
+                                                      (50, 32, "fp32", 0, 0), (50, 32, "fp32", 4, 6),
+                                                      (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0)])
+def test_forward_full_frame(mdx, depth, B, dtype, wino, split):
     """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
-    2 = F(2x2,3x3), 0 = direct); the same fp32 tolerances hold for all."""
+    2 = F(2x2,3x3), 0 = direct); split: the fp32 layers as exact bf16 plane
+    products (mdx_conv_set_fp32_split, 0 = the f32 MFMA kernels); the same
+    fp32 tolerances hold for all."""
     from moseq2_detectron_extract_amd._lib import call
     old = call("mdx_conv_set_winograd", wino)
+    old_s = call("mdx_conv_set_fp32_split", split)
     try:
-        _forward_full_frame(depth, B, dtype, wino)
+        _forward_full_frame(depth, B, dtype, wino, split)
     finally:
         call("mdx_conv_set_winograd", old)
+        call("mdx_conv_set_fp32_split", old_s)
 
 
-def _forward_full_frame(depth, B, dtype, wino):
+def _forward_full_frame(depth, B, dtype, wino, split=0):
     from moseq2_detectron_extract_amd import synth
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor, synthetic_state_dict
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
@@ -116,13 +121,15 @@ def _forward_full_frame(depth, B, dtype, wino):
     np.testing.assert_array_equal(prepped_d.cpu().numpy(), prepped)  # bit-exact frame ops feed both sides
     scaled = O.scale_raw_frames(prepped, 0, 100)
     masks_all = torch.cat([m for m in inf["masks"]]).cpu().numpy()
-    stats = {"case": f"R{depth} B={B} {dtype}" + (f" winograd F({wino}x{wino},3x3)" if wino else ""), "frames": []}
+    stats = {"case": f"R{depth} B={B} {dtype}" + (f" winograd F({wino}x{wino},3x3)" if wino else "") +
+             (f" bf16x{split} plane products" if split else ""), "frames": []}
     try:
         _compare(sd, cfg, tol, B, prepped, scaled, inf, gfeat, masks_all, cleaned_d, tail, stats)
     finally:
         out = os.path.join(ROOT, "gpurun_out")
         if os.path.isdir(out):
-            with open(os.path.join(out, f"parity_full_R{depth}_B{B}_{dtype}" + (f"_wino{wino}" if wino else "") + ".json"), "w") as fh:
+            name = f"parity_full_R{depth}_B{B}_{dtype}" + (f"_wino{wino}" if wino else "") + (f"_x{split}" if split else "")
+            with open(os.path.join(out, name + ".json"), "w") as fh:
                 json.dump(stats, fh, indent=1)
 
 
