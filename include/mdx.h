@@ -231,10 +231,6 @@ int mdx_conv_set_dma_f32(int on);
  * fp32 rounding of the product); 0 (default): the f32 MFMA kernels.  Also
  * used for the Winograd GEMMs.  Returns the old value. */
 int mdx_conv_set_fp32_split(int mode);
-/* fp32 streaming 1x1 kernel (K = 64 / 128, or 256 into 64 channels, stride 1,
- * M >= the mdx_conv_set_stream1x1 row threshold): 0 never, 1 (default),
- * 2 also K = 256 into more than 64 channels.  Returns the old value. */
-int mdx_conv_set_stream1x1_f32(int mode);
 /* Tuning knob: 1 (default) runs every split-plane launch on the 64-wide N
  * tile (two workgroups per CU), 0 the 128-wide tile where Cout > 64. */
 int mdx_conv_set_x3_narrow(int on);

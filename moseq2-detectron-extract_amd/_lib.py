@@ -53,7 +53,6 @@ SIGNATURES = {
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
     "mdx_conv_set_dma_f32": (I32, [I32]),
     "mdx_conv_set_fp32_split": (I32, [I32]),
-    "mdx_conv_set_stream1x1_f32": (I32, [I32]),
     "mdx_conv_set_x3_narrow": (I32, [I32]),
     "mdx_rpn_set_sliced": (I32, [I32]),
     "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),

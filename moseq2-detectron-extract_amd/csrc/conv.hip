@@ -832,109 +832,6 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
     }
 }
 
-// fp32 form of the streaming 1x1 kernel (K = Cin in {64, 128, 256}, Cout %
-// 64 == 0, stride 1): same workgroup shape (128 pixels x 64 channels, 4 waves
-// of 32 pixels), weights in LDS, activations straight into registers, D = W
-// X^T on v_mfma_f32_16x16x4_f32.  Lane group g = lane >> 4 holds the 16-B
-// piece k = 16 c + 4 g .. +4 of its row for every 16-wide K chunk c, and MFMA
-// e of chunk c takes component e of both operands (the K order k_conv uses).
-// Each lane ends with 4 consecutive fp32 channels of one pixel per (ms, ns):
-// 16-B residual loads and stores, no exchange, no LDS epilogue.
-//   lane l:  W operand = W[n0 + 16 ns + (l & 15)][16 c + 4 (l >> 4) + e]
-//            X operand = X[m0 + 16 ms + (l & 15)][16 c + 4 (l >> 4) + e]
-//            D[ms][ns][r] = out[m0 + 16 ms + (l & 15)][n0 + 16 ns + 4 (l >> 4) + r]
-template <int KC>
-__global__ __launch_bounds__(256) void k_conv1x1_stream_f32(ConvArgs a) {
-    constexpr int K = 16 * KC, WPITCH = 4 * K + 16;  // LDS row pitch (bytes): +16 spreads rows over banks
-    __shared__ __attribute__((aligned(16))) char sw[64 * WPITCH];
-    int tile;
-    {
-        const int L = blockIdx.x, nwg = a.tiles_total;
-        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
-        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-    }
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int n0 = tn * 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int g = lane >> 4;
-    const float *Wt = reinterpret_cast<const float *>(a.w);
-    const int m0 = tm * 128 + wid * 32;
-    // residual first: the longest stream, depends on nothing
-    float4v rr[2][4];
-    if (a.res) {
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
-                                                                            0x00020000);
-#pragma unroll
-        for (int ms = 0; ms < 2; ++ms) {
-            const int m = m0 + 16 * ms + (lane & 15);
-#pragma unroll
-            for (int ns = 0; ns < 4; ++ns) {
-                const unsigned off =
-                    m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 16 * ns + 4 * g) * 4) : 0xFFFFFFF0u;
-                rr[ms][ns] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
-            }
-        }
-    }
-    // stage the 64 x K weight slice
-    for (int i = tid; i < 64 * K / 4; i += 256) {
-        const int r = i / (K / 4), c = i - r * (K / 4);
-        *reinterpret_cast<uint4 *>(sw + r * WPITCH + c * 16) =
-            *reinterpret_cast<const uint4 *>(Wt + (long long)(n0 + r) * K + c * 4);
-    }
-    // this wave's 32 pixels: K floats per row, 16 B per lane and chunk
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
-    float4v xf[2][KC];
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-        const int m = m0 + 16 * ms + (lane & 15);
-        const unsigned base = (unsigned)((long long)m * K * 4) + 16u * g;
-#pragma unroll
-        for (int c = 0; c < KC; ++c)
-            xf[ms][c] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        rx, m < a.M ? base + 64u * c : 0xFFFFFFF0u, 0, 0));
-    }
-    __syncthreads();
-    float4v acc[2][4];
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = float4v{0.f, 0.f, 0.f, 0.f};
-    const char *wl = sw + (lane & 15) * WPITCH + 16 * g;
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-        float4v wf[4];
-#pragma unroll
-        for (int ns = 0; ns < 4; ++ns) wf[ns] = *reinterpret_cast<const float4v *>(wl + 16 * ns * WPITCH + 64 * c);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-                for (int ns = 0; ns < 4; ++ns)
-                    acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[ns][e], xf[ms][c][e], acc[ms][ns], 0, 0, 0);
-    }
-    float *O = reinterpret_cast<float *>(a.out);
-#pragma unroll
-    for (int ns = 0; ns < 4; ++ns) {
-        const int c0 = n0 + 16 * ns + 4 * g;
-        const float4 b4 = a.bias ? *reinterpret_cast<const float4 *>(a.bias + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int ms = 0; ms < 2; ++ms) {
-            const int m = m0 + 16 * ms + (lane & 15);
-            if (m >= a.M) continue;
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float x = acc[ms][ns][r] + bv[r];
-                if (a.res) x += rr[ms][ns][r];
-                v[r] = a.relu ? (x > 0.f ? x : 0.f) : x;
-            }
-            *reinterpret_cast<float4 *>(O + (long long)m * a.Cout + c0) = make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
-}
-
 // Narrow-output streaming 1x1 kernel (RPN head: 256 -> 15 logits/deltas,
 // fp32 out): one 16-row MFMA block of output channels (rows >= Cout read as
 // zero weights), no LDS and no barrier -- each wave loads its 16 x K weight
@@ -994,13 +891,6 @@ extern "C" int mdx_conv_set_stream1x1(int mode, int min_m) {
     const int old = g_stream1x1;
     g_stream1x1 = mode;
     g_stream_min_m = min_m;
-    return old;
-}
-// fp32 streaming 1x1 kernel policy (same modes; M >= g_stream_min_m)
-static int g_stream1x1_f32 = 1;
-extern "C" int mdx_conv_set_stream1x1_f32(int mode) {
-    const int old = g_stream1x1_f32;
-    g_stream1x1_f32 = mode;
     return old;
 }
 
@@ -1672,24 +1562,6 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
         else
             hipLaunchKernelGGL(k_conv1x1_head<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
         t_plan_kernel = MDX_CONV_KERNEL_HEAD1X1;
-        t_plan_ksplit = 1;
-        MDX_CHECK_LAUNCH("mdx_conv2d");
-        return MDX_OK;
-    }
-    // fp32 HBM-bound 1x1 layers (K = 64 / 128, or 256 into 64 channels): the fp32 streaming kernel
-    if (g_stream1x1_f32 && in_dtype == 0 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
-        pad == 0 && (Cin == 64 || Cin == 128 || (Cin == 256 && (Cout == 64 || g_stream1x1_f32 == 2))) &&
-        Cout % 64 == 0 && (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m && !g_fp32_split) {
-        a.tiles_n = Cout / 64;
-        a.tiles_total = (int)(ceil_div(M, 128) * a.tiles_n);
-        a.ksplit = 1;
-        if (Cin == 64)
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        else if (Cin == 128)
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<16>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        t_plan_kernel = MDX_CONV_KERNEL_STREAM1X1;
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
