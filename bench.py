@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp16 secondary measurement")
+    ap.add_argument("--x6", action="store_true",
+                    help="also measure the fp32 loop with the split-plane kernels (mdx_conv_set_fp32_split(6))")
     ap.add_argument("--no-h2d", action="store_true", help="raw batches already resident in HBM (no H2D in the loop)")
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
@@ -57,7 +59,7 @@ def parse():
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
     ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_conv_set_winograd_min_cin")
-    ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT",
+    ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT[,INT]",
                     help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
     ap.add_argument("--model-streams", type=int, default=2,
                     help="forwards of consecutive batches in flight at once (one HIP stream each)")
@@ -332,7 +334,7 @@ def main():
         fn, val = kv.split("=")
         if not (fn.startswith("mdx_") and "_set_" in fn):
             raise SystemExit(f"--set: {fn} is not a libmdx tuning knob")
-        call(fn, int(val))
+        call(fn, *[int(v) for v in val.split(",")])
     B = args.batch
     sess = synth.SyntheticSession(2 * B, seed=1000 + rank)
     frames = sess.frames(0, 2 * B)
@@ -362,6 +364,7 @@ def main():
                               "note": "fp16 MFMA forward (fp32 accumulation), same loop; tolerance vs the fp32 "
                                       "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0-0]"}}
         del ex16
+    if not args.no_secondary and args.dtype == "fp32" and args.x6:
         torch.cuda.synchronize()
         from moseq2_detectron_extract_amd._lib import call
         old = call("mdx_conv_set_fp32_split", 6)
