@@ -92,6 +92,7 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
                 6: "Winograd F(2x2,3x3) (input transform + 16 batched k_conv GEMMs + output transform)",
                 7: "k_conv_x3<128> fp32 as bf16 plane products", 8: "k_conv_x3<64> fp32 as bf16 plane products",
+                9: "k_gemm_x6 256x256 LDS-DMA GEMM over bf16 planes (fp32 split, two plane products per MFMA)",
                 10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance"}
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 PMC_FILE = {"fp16": "r01_pmc_kernels.json", "fp32": "r02_pmc_kernels_fp32.json"}

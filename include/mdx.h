@@ -231,6 +231,7 @@ int mdx_conv_set_dma_f32(int on);
  * fp32 rounding of the product); 0 (default): the f32 MFMA kernels.  Also
  * used for the Winograd GEMMs.  Returns the old value. */
 int mdx_conv_set_fp32_split(int mode);
+int mdx_conv_fp32_split(void);
 /* Tuning knob: 1 (default) runs every split-plane launch on the 64-wide N
  * tile (two workgroups per CU), 0 the 128-wide tile where Cout > 64. */
 int mdx_conv_set_x3_narrow(int on);
@@ -253,6 +254,25 @@ int mdx_conv_winograd_enabled(void);
  * handles pack the transformed weights of the fp32 3x3 layers with Cin >= 128). */
 int mdx_conv_set_winograd_min_cin(int cin);
 int mdx_conv_winograd_min_cin(void);
+/* Winograd GEMMs with Cout % 256 == 0 and Cin % 32 == 0 on the 256x256
+ * LDS-DMA fp32 kernel: mode 0 never, 1 when the batched launch has at least
+ * min_wgs workgroups (default, min_wgs 384), 2 whenever eligible; returns the
+ * old mode. */
+int mdx_conv_set_winograd_dma(int mode, int min_wgs);
+/* fp32 GEMM on the bf16 matrix cores over operands split once into bf16
+ * planes (replaces the fp32 Linear layers of Detectron2's FastRCNNConvFCHead,
+ * M/model/config.py:21-94 box head, when the model handle's x6 mode is on).
+ * split_x6: x float32 [rows][ldx] (first K columns, K % 16 == 0) -> planes
+ * (mdx_x6_plane_bytes(rows, K) bytes): per row K/16 groups of 96 B = hi, mid,
+ * lo bf16 of 16 values, x = hi + mid + lo exactly.  gemm_x6: out[m][n] =
+ * act(sum_k A[m][k] B[n][k] + bias[n] (+ residual[m][n])) for A [M][K], B
+ * [N][K] in plane layout, fp32 out [M][N]; six of the nine plane products
+ * (the dropped ones are below one fp32 rounding of each product), fp32
+ * accumulation. */
+int64_t mdx_x6_plane_bytes(int64_t rows, int K);
+int mdx_split_x6(const float *x, int64_t rows, int K, int64_t ldx, void *out, mdx_stream_t stream);
+int mdx_gemm_x6(const void *a_planes, const void *b_planes, const float *bias, int M, int N, int K,
+                const float *residual, int relu, float *out, mdx_stream_t stream);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */
@@ -265,7 +285,8 @@ enum {
     MDX_CONV_KERNEL_HEAD1X1 = 5,
     MDX_CONV_KERNEL_WINOGRAD = 6,
     MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
-    MDX_CONV_KERNEL_X3_64 = 8
+    MDX_CONV_KERNEL_X3_64 = 8,
+    MDX_CONV_KERNEL_X6DMA = 9   /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
 };
 /* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256

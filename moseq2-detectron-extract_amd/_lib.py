@@ -53,6 +53,7 @@ SIGNATURES = {
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
     "mdx_conv_set_dma_f32": (I32, [I32]),
     "mdx_conv_set_fp32_split": (I32, [I32]),
+    "mdx_conv_fp32_split": (I32, []),
     "mdx_conv_set_x3_narrow": (I32, [I32]),
     "mdx_rpn_set_sliced": (I32, [I32]),
     "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),
@@ -62,6 +63,10 @@ SIGNATURES = {
     "mdx_conv_winograd_enabled": (I32, []),
     "mdx_conv_set_winograd_min_cin": (I32, [I32]),
     "mdx_conv_winograd_min_cin": (I32, []),
+    "mdx_conv_set_winograd_dma": (I32, [I32, I32]),
+    "mdx_x6_plane_bytes": (I64, [I64, I32]),
+    "mdx_split_x6": (I32, [P, I64, I32, I64, P, P]),
+    "mdx_gemm_x6": (I32, [P, P, P, I32, I32, I32, P, I32, P, P]),
     "mdx_conv2d_last_plan": (I32, [P, P]),
     "mdx_conv_set_stream1x1": (I32, [I32, I32]),
     "mdx_conv_set_split256": (I32, [I32, I32]),

@@ -947,6 +947,12 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     constexpr int CHK = 2 * SUBK;               // channels per chunk
     static_assert(!(F32 && ILV), "the interleaved DMA schedule is fp16-only");
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (gridDim.z > 1) {  // batch entry z of a batched GEMM (the Winograd GEMMs)
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
     int tile;
     {
         const int L = blockIdx.x, nwg = a.tiles_total;
@@ -1232,6 +1238,199 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMM over operands split ONCE into bf16 planes in HBM ("x6 planes"),
+// on the bf16 matrix cores through the LDS-DMA pipeline.
+//
+// Plane layout of an fp32 matrix X [rows][K] (K % 16 == 0): per row, K/16
+// groups of 96 B = [hi k0-7 | hi k8-15 | mid k0-7 | mid k8-15 | lo k0-7 |
+// lo k8-15] (bf16), x = hi + mid + lo exactly (the split3 of k_conv_x3).
+//
+// One 16x16x32 bf16 MFMA sums 32 K slots; lane group g = lane >> 4 supplies
+// slots 8g..8g+7.  Feeding the two operands different planes per slot group
+// (k = 8 (g & 1) + e of the 16-deep group in both) gives two plane products
+// per MFMA, so three MFMAs per 16 K form the six products of k_conv_x3:
+//   MFMA 1: A [hi  | hi ]  B [hi | mid]   -> hi*hi  + hi*mid
+//   MFMA 2: A [mid | lo ]  B [hi | hi ]   -> mid*hi + lo*hi
+//   MFMA 3: A [hi  | mid]  B [lo | mid]   -> hi*lo  + mid*mid
+// (g < 2 | g >= 2), all into one fp32 accumulator per output element.
+//
+// Tile 256 x 256 per 512-thread workgroup (8 waves as 2 x 4, wave tile 128 x
+// 64), substeps of 16 K = 96-B rows: A 24 KiB + B 24 KiB per substep staged by
+// LDS-DMA (6 global_load_lds_dwordx4 per wave), three substep buffers, two in
+// flight ahead of the one multiplied.  With 96-B rows the fragment reads of
+// every ds_read_b128 lane group hit 16 distinct 16-B bank slots (6 r + piece
+// mod 16 is a permutation over the group's rows), so no swizzle is needed.
+// LDS bytes per FLOP are half the fp16 kernel's (three planes per operand
+// serve six products).
+// ---------------------------------------------------------------------------
+constexpr int X6_ROWB = 96;             // bytes of one 16-deep K group of one row (3 planes)
+constexpr int X6_BM = 256, X6_BN = 256, X6_THREADS = 512;
+constexpr int X6_ASUB = X6_BM * X6_ROWB;  // 24 KiB
+constexpr int X6_SUB = 2 * X6_ASUB;       // A + B of one substep
+constexpr int X6_NBUF = 3;
+constexpr int X6_LDS = X6_NBUF * X6_SUB > G_LDS ? X6_NBUF * X6_SUB : G_LDS;
+
+// x [rows][ldx] fp32 (the first K columns) -> planes [rows][K/16][96 B]; one
+// thread per 8 consecutive values (half a group)
+__global__ __launch_bounds__(256) void k_split_x6(const float *__restrict__ x, long long rows, int K, long long ldx,
+                                                  char *__restrict__ out) {
+    const long long per_row = K / 8;
+    const long long total = rows * per_row;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const long long r = i / per_row;
+        const int c8 = (int)(i - r * per_row);
+        const float *src = x + r * ldx + 8 * c8;
+        const float4 u = *reinterpret_cast<const float4 *>(src), v = *reinterpret_cast<const float4 *>(src + 4);
+        const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        bf16x8 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const __bf16 hb = (__bf16)f[e];
+            const float r1 = f[e] - (float)hb;
+            const __bf16 mb = (__bf16)r1;
+            h[e] = hb;
+            m[e] = mb;
+            l[e] = (__bf16)(r1 - (float)mb);
+        }
+        char *o = out + r * (long long)K * 6 + (long long)(c8 >> 1) * X6_ROWB + (c8 & 1) * 16;
+        *reinterpret_cast<bf16x8 *>(o) = h;
+        *reinterpret_cast<bf16x8 *>(o + 32) = m;
+        *reinterpret_cast<bf16x8 *>(o + 64) = l;
+    }
+}
+
+// out[m][n] = act(sum_k A[m][k] B[n][k] + bias[n] (+ res)) with A = a.x, B =
+// a.w in plane layout (K = a.K), M = a.M rows, N = a.Cout; batched over
+// grid.z with byte strides bsx / bsw / bso.
+__global__ __launch_bounds__(X6_THREADS, 1) void k_gemm_x6(ConvArgs a) {
+    constexpr int WN = 4, WROWS = 128, WCOLS = 64, TI = WROWS / 16, TJ = WCOLS / 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (gridDim.z > 1) {
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * X6_BM, n0 = tn * X6_BN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid - wm * WN;
+    const long long rowbytes = (long long)a.K * 6;
+
+    // DMA instruction j (0..2) of wave w fills bytes [1 KiB (3 w + j), +1 KiB)
+    // of the A (and the B) image of a substep: piece P = 64 (3 w + j) + lane
+    // = row P / 6, 16-B piece P % 6 of that row's 96-B group
+    const char *a_src[3], *b_src[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int P = 64 * (3 * wid + j) + lane;
+        const int row = P / 6, pc = P - row * 6;
+        const int gm = m0 + row, gn = n0 + row;
+        a_src[j] = gm < a.M ? reinterpret_cast<const char *>(a.x) + gm * rowbytes + pc * 16 : nullptr;
+        b_src[j] = gn < a.Cout ? reinterpret_cast<const char *>(a.w) + gn * rowbytes + pc * 16 : nullptr;
+    }
+    auto issue = [&](int buf, int kg) {
+        char *dst = smem + buf * X6_SUB + 3 * wid * 1024;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            glds16(a_src[j] ? (const void *)(a_src[j] + (long long)kg * X6_ROWB) : (const void *)g_zero16,
+                   dst + j * 1024);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            glds16(b_src[j] ? (const void *)(b_src[j] + (long long)kg * X6_ROWB) : (const void *)g_zero16,
+                   dst + X6_ASUB + j * 1024);
+    };
+
+    float4v acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+    // fragment addresses: row (lane & 15) of each 16-row tile, piece g & 1,
+    // plane per operand / MFMA / lane half (see above)
+    const int g = lane >> 4, hp = (g & 1) * 16;
+    const bool lo_half = g < 2;
+    const char *Ab = smem + (wm * WROWS + (lane & 15)) * X6_ROWB + hp;
+    const char *Bb = smem + X6_ASUB + (wn * WCOLS + (lane & 15)) * X6_ROWB + hp;
+    const int a1 = 0, a2 = lo_half ? 32 : 64, a3 = lo_half ? 0 : 32;
+    const int b1 = lo_half ? 0 : 32, b2 = 0, b3 = lo_half ? 64 : 32;
+
+    const int T = a.K / 16;
+    issue(0, 0);
+    if (T > 1) issue(1, 1);
+    int issued = T > 1 ? 1 : 0;
+    for (int t = 0; t < T; ++t) {
+        // substep t landed (6 DMA instructions per substep per wave)
+        if (issued - t >= 1)
+            MDX_WAIT_VM(6);
+        else
+            MDX_WAIT_VM(0);
+        MDX_WAIT_LGKM0();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // buffer (t + 2) % 3 == (t - 1) % 3: every wave is past its reads of t - 1
+        if (t + 2 < T) {
+            issue((t + 2) % 3, t + 2);
+            issued = t + 2;
+        }
+        const int boff = (t % 3) * X6_SUB;
+        bf16x8 fb[3][TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+            const char *p = Bb + boff + j * 16 * X6_ROWB;
+            fb[0][j] = *reinterpret_cast<const bf16x8 *>(p + b1);
+            fb[1][j] = *reinterpret_cast<const bf16x8 *>(p + b2);
+            fb[2][j] = *reinterpret_cast<const bf16x8 *>(p + b3);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const char *p = Ab + boff + i * 16 * X6_ROWB;
+            const bf16x8 f1 = *reinterpret_cast<const bf16x8 *>(p + a1);
+            const bf16x8 f2 = *reinterpret_cast<const bf16x8 *>(p + a2);
+            const bf16x8 f3 = *reinterpret_cast<const bf16x8 *>(p + a3);
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, fb[0][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2, fb[1][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f3, fb[2][j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // epilogue: as k_convg, per wave passes of 64 rows x 64 columns
+    constexpr int EPI_ROWS = 64, EPI_PITCH = 68, NPASS = WROWS / EPI_ROWS, IPP = EPI_ROWS / 16;
+    float *Cs = reinterpret_cast<float *>(smem) + wid * EPI_ROWS * EPI_PITCH;
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+#pragma unroll
+        for (int i = 0; i < IPP; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    Cs[(i * 16 + (lane >> 4) * 4 + r) * EPI_PITCH + j * 16 + (lane & 15)] = acc[IPP * h + i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        finish_batch<float, 8>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+            const int item = lane + 64 * q;
+            const int row = item >> 3, ch = item & 7;
+            gm = m0 + wm * WROWS + EPI_ROWS * h + row;
+            gn0 = n0 + wn * WCOLS + ch * 8;
+            src = Cs + row * EPI_PITCH + ch * 8;
+            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+        });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride 1 / pad 1
@@ -1426,6 +1625,7 @@ extern "C" int mdx_conv_set_fp32_split(int mode) {
     if (mode == 0 || mode == 6 || mode == 9) g_fp32_split = mode;
     return old;
 }
+extern "C" int mdx_conv_fp32_split(void) { return g_fp32_split; }
 // 64-wide N tile for every split-plane launch (72 KB of LDS and <= 256
 // registers: two workgroups per CU, measured 6-25 % faster per layer than the
 // 128-wide tile's one workgroup per CU, whose single wave per SIMD serialises
@@ -1734,6 +1934,48 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     return MDX_OK;
 }
 
+extern "C" int64_t mdx_x6_plane_bytes(int64_t rows, int K) {
+    if (rows < 0 || K <= 0 || K % 16) return -1;
+    return rows * (int64_t)K * 6;
+}
+
+extern "C" int mdx_split_x6(const float *x, int64_t rows, int K, int64_t ldx, void *out, mdx_stream_t stream) {
+    MDX_REQUIRE(x && out, "mdx_split_x6: null pointer");
+    MDX_REQUIRE(rows >= 0 && K > 0 && K % 16 == 0 && ldx >= K && ldx % 4 == 0,
+                "mdx_split_x6: K %% 16 == 0, ldx >= K and ldx %% 4 == 0 required");
+    MDX_REQUIRE((reinterpret_cast<uintptr_t>(x) % 16) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0,
+                "mdx_split_x6: 16-B aligned buffers required");
+    if (rows == 0) return MDX_OK;
+    const long long items = rows * (long long)(K / 8);
+    const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(k_split_x6, dim3(grid), dim3(256), 0, as_stream(stream), x, (long long)rows, K, (long long)ldx,
+                       reinterpret_cast<char *>(out));
+    MDX_CHECK_LAUNCH("mdx_split_x6");
+    return MDX_OK;
+}
+
+extern "C" int mdx_gemm_x6(const void *a_planes, const void *b_planes, const float *bias, int M, int N, int K,
+                           const float *residual, int relu, float *out, mdx_stream_t stream) {
+    MDX_REQUIRE(a_planes && b_planes && out, "mdx_gemm_x6: null pointer");
+    MDX_REQUIRE(M > 0 && N > 0 && K > 0 && K % 16 == 0, "mdx_gemm_x6: M, N > 0 and K %% 16 == 0 required");
+    MDX_REQUIRE(!residual || (long long)M * N * 4 < (1ll << 31), "mdx_gemm_x6: residual above 2 GiB");
+    ConvArgs a{};
+    a.x = a_planes; a.w = b_planes; a.bias = bias; a.res = residual; a.out = out;
+    a.H = M; a.W = 1; a.Cin = K; a.Cout = N; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+    a.OH = M; a.OW = 1; a.M = M; a.K = K;
+    a.relu = relu; a.out_mode = 0;
+    a.rbytes = residual ? (int)((long long)M * N * 4) : 0;
+    a.tiles_n = (int)ceil_div(N, X6_BN);
+    a.tiles_total = (int)(ceil_div(M, X6_BM) * a.tiles_n);
+    a.ksplit = 1;
+    a.ksteps = K / 16;
+    hipLaunchKernelGGL(k_gemm_x6, dim3((unsigned)a.tiles_total), dim3(X6_THREADS), X6_LDS, as_stream(stream), a);
+    t_plan_kernel = MDX_CONV_KERNEL_X6DMA;
+    t_plan_ksplit = 1;
+    MDX_CHECK_LAUNCH("mdx_gemm_x6");
+    return MDX_OK;
+}
+
 extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
     MDX_REQUIRE(kernel && ksplit, "mdx_conv2d_last_plan: null pointer");
     *kernel = t_plan_kernel;
@@ -1760,6 +2002,15 @@ extern "C" int mdx_conv_set_winograd_min_cin(int c) {
     return old;
 }
 extern "C" int mdx_conv_winograd_min_cin(void) { return g_wino_min_cin; }
+// Winograd GEMMs on the 256x256 LDS-DMA fp32 kernel: 0 never, 1 when the
+// batched launch has at least min_wgs workgroups (default), 2 whenever eligible
+static int g_wino_dma = 1, g_wino_dma_min_wgs = 384;
+extern "C" int mdx_conv_set_winograd_dma(int mode, int min_wgs) {
+    const int old = g_wino_dma;
+    g_wino_dma = mode;
+    g_wino_dma_min_wgs = min_wgs;
+    return old;
+}
 
 extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U) {
     MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4), "mdx_winograd_weights: bad args");
@@ -1842,7 +2093,18 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     const dim3 grid((unsigned)a.tiles_total, 1, (unsigned)NB);
-    if (g_fp32_split)
+    // the wide GEMMs (Cout a multiple of 256) on the 256x256 LDS-DMA kernel
+    // when the NB batch entries give it enough workgroups
+    const long long t256 = ceil_div(T, G_BM) * (Cout / G_BN);
+    const bool dma = !g_fp32_split && Cin % 32 == 0 && Cout % G_BN == 0 &&
+                     (g_wino_dma == 2 || (g_wino_dma == 1 && t256 * NB >= g_wino_dma_min_wgs));
+    if (dma) {
+        a.tiles_n = Cout / G_BN;
+        a.tiles_total = (int)t256;
+        a.ksteps = Cin / 16;  // 16-float substeps
+        hipLaunchKernelGGL((k_convg<float, float, 8, false>), dim3((unsigned)t256, 1, (unsigned)NB), dim3(G_THREADS),
+                           G_LDS, s, a);
+    } else if (g_fp32_split)
         launch_x3(a, bn, grid, s);
     else if (bn == 64)
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);

@@ -52,6 +52,9 @@ struct ConvW {
     // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
     // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 128)
     float *wino2 = nullptr, *wino4 = nullptr;
+    // fp32 Linear layers: the weights split once into bf16 planes for
+    // mdx_gemm_x6 (used while mdx_conv_fp32_split() != 0)
+    void *x6 = nullptr;
 };
 
 struct GnW {
@@ -328,12 +331,24 @@ struct Packer {
         return c;
     }
     // (out, in) linear as a 1x1 conv
-    ConvW linear(const std::vector<float> &w, int out, int in, const std::vector<float> &b) {
+    ConvW linear(const std::vector<float> &w, int out, int in, const std::vector<float> &b, bool x6 = false) {
         ConvW c;
         c.w = upload(w, true);
         c.b = upload_f32(b);
         c.cin = in;
         c.cout = out;
+        if (x6 && m.dt == 0 && in % 16 == 0 && err.empty()) {
+            void *d = nullptr;
+            if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes(out, in)) != hipSuccess) {
+                err = "device allocation of weight planes failed";
+                return c;
+            }
+            m.allocs.push_back(d);
+            if (mdx_split_x6((const float *)c.w, out, in, in, d, nullptr) != MDX_OK ||
+                hipDeviceSynchronize() != hipSuccess)
+                err = "weight plane split failed";
+            c.x6 = d;
+        }
         return c;
     }
 };
@@ -412,7 +427,7 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
                     for (int c = 0; c < C; ++c)
                         for (int q = 0; q < R * R; ++q)
                             pw[(size_t)o * fin + (size_t)q * C + c] = w->v[(size_t)o * fin + (size_t)c * R * R + q];
-            m.fc.push_back(P.linear(pw, F, fin, b->v));
+            m.fc.push_back(P.linear(pw, F, fin, b->v, true));
             fin = F;
         }
         const int nc = cfg.num_classes;
@@ -500,6 +515,11 @@ struct Fwd {
             const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout, wm);
             if (c.dry) c.wino_need = need > c.wino_need ? need : c.wino_need;
         }
+        // fp32 Linear layers in split-plane mode: activations split into bf16
+        // planes, GEMM on the bf16 matrix cores (mdx_gemm_x6)
+        const bool x6 = cw.x6 && m.dt == 0 && !out_f32 && out_mode == 0 && cw.k == 1 && cw.stride == 1 &&
+                        mdx_conv_fp32_split() == 6;
+        void *planes = x6 ? alloc((size_t)mdx_x6_plane_bytes((int64_t)N * H * W, cw.cin)) : nullptr;
         if (c.dry || !ok()) return out;
         ProfEv *pe = nullptr;
         if (m.profile) {
@@ -509,7 +529,12 @@ struct Fwd {
             (void)hipEventCreate(&pe->e1);
             (void)hipEventRecord(pe->e0, s);
         }
-        if (wino)
+        if (x6) {
+            const int64_t rows = (int64_t)N * H * W;
+            chk(mdx_split_x6((const float *)x, rows, cw.cin, cw.cin, planes, s));
+            chk(mdx_gemm_x6(planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
+                            (float *)out, s));
+        } else if (wino)
             chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
                                      (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
         else

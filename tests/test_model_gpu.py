@@ -730,7 +730,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6], ids=["f32-mfma", "bf16x6"])
+@pytest.mark.parametrize("split", [0, 6, -1], ids=["f32-mfma", "bf16x6", "f32-dma256"])
 @pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
@@ -757,14 +757,59 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     out = torch.empty(N, H, W, Cout, device="cuda")
     nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout, m)
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
-    old = call("mdx_conv_set_fp32_split", split)
+    if split == -1 and (Cout % 256 or Cin % 32):
+        pytest.skip("the 256x256 LDS-DMA GEMM needs Cout % 256 == 0 and Cin % 32 == 0")
+    old = call("mdx_conv_set_fp32_split", max(split, 0))
+    # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it
+    old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
     finally:
         call("mdx_conv_set_fp32_split", old)
+        call("mdx_conv_set_winograd_dma", old_dma, 384)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
     got = out.cpu().double()
     err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("M,N,K,relu,res", [(37, 24, 16, False, False), (300, 200, 48, True, False),
+                                            (1000, 1024, 1024, True, True), (513, 256, 12544, True, False)])
+def test_gemm_x6_planes(mdx, M, N, K, relu, res):
+    """fp32 GEMM over bf16 planes (mdx_split_x6 + mdx_gemm_x6, the 256x256
+    LDS-DMA kernel with two plane products per MFMA) against fp64: within the
+    f32-MFMA conv kernel's error on the same operands (1.5x + 1e-7), and
+    below 1e-5 of the output scale; ragged M / N exercise partial tiles."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) / K ** 0.5
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g) if res else None
+    want = A.double() @ B.double().T + bias.double()
+    if res:
+        want = want + R.double()
+    if relu:
+        want = want.clamp_min(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    Ad, Bd, bd = A.cuda(), B.cuda(), bias.cuda()
+    Rd = R.cuda() if res else None
+    pa = torch.empty(call("mdx_x6_plane_bytes", M, K), dtype=torch.uint8, device="cuda")
+    pb = torch.empty(call("mdx_x6_plane_bytes", N, K), dtype=torch.uint8, device="cuda")
+    call("mdx_split_x6", P(Ad), M, K, K, P(pa), None)
+    call("mdx_split_x6", P(Bd), N, K, K, P(pb), None)
+    out = torch.full((M, N), float("nan"), device="cuda")
+    call("mdx_gemm_x6", P(pa), P(pb), P(bd), M, N, K, P(Rd), int(relu), P(out), None)
+    kid, ks_ = ctypes.c_int(), ctypes.c_int()
+    call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+    assert kid.value == 9
+    ref = torch.empty((M, N), device="cuda")
+    call("mdx_conv2d", P(Ad), M, 1, 1, K, P(Bd), P(bd), N, 1, 1, 1, 0, P(Rd), int(relu), 0, 0, 0, P(ref), None)
+    torch.cuda.synchronize()
+    scale = want.abs().max().item()
+    err = (out.cpu().double() - want).abs().max().item() / scale
+    err_f32 = (ref.cpu().double() - want).abs().max().item() / scale
+    assert err < 1e-5 and err <= 1.5 * err_f32 + 1e-7, (err, err_f32)
