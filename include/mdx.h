@@ -255,9 +255,9 @@ int mdx_conv_winograd_enabled(void);
 int mdx_conv_set_winograd_min_cin(int cin);
 int mdx_conv_winograd_min_cin(void);
 /* Winograd GEMMs with Cout % 256 == 0 and Cin % 32 == 0 on the 256x256
- * LDS-DMA fp32 kernel: mode 0 never, 1 when the batched launch has at least
- * min_wgs workgroups (default, min_wgs 384), 2 whenever eligible; returns the
- * old mode. */
+ * LDS-DMA fp32 kernel: mode 0 never (default: measured no faster), 1 when the
+ * batched launch has at least min_wgs workgroups, 2 whenever eligible; returns
+ * the old mode. */
 int mdx_conv_set_winograd_dma(int mode, int min_wgs);
 /* fp32 GEMM on the bf16 matrix cores over operands split once into bf16
  * planes (replaces the fp32 Linear layers of Detectron2's FastRCNNConvFCHead,
@@ -356,7 +356,10 @@ int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl
                       mdx_stream_t stream);
 
 /* ROIPooler(ROIAlignV2): rois float32 (R,4) XYXY, R = B*per_image, rows with
- * index >= counts[b] produce zeros.  out (R,P,P,C). */
+ * index >= counts[b] produce zeros.  out (R,P,P,C).  dtype 0 fp32, 1 fp16
+ * (features and out); 2: fp32 features, each out row of P*P*C values written
+ * as bf16 planes in the mdx_split_x6 layout (mdx_x6_plane_bytes(R, P*P*C)
+ * bytes; the A operand of mdx_gemm_x6), separable kernel only. */
 int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const float *scales, int L,
                   int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
                   int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
@@ -373,6 +376,8 @@ int mdx_roi_align_ex(const void *const *feats, const int *fh, const int *fw, con
                      int *order_ws, void *out, mdx_stream_t stream);
 /* Tuning knob for the permutation above (1 on, 0 off); returns the old value. */
 int mdx_roi_align_set_sorted(int on);
+/* Current ROIAlign kernel choice (mdx_roi_align_set_mode). */
+int mdx_roi_align_get_mode(void);
 
 /* ROIAlign kernel choice: 0 = one workgroup per (ROI, 128-B channel slice)
  * with the sample window staged in LDS; 1, 2, 3 = one workgroup per

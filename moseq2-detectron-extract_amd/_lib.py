@@ -54,6 +54,7 @@ SIGNATURES = {
     "mdx_conv_set_dma_f32": (I32, [I32]),
     "mdx_conv_set_fp32_split": (I32, [I32]),
     "mdx_conv_fp32_split": (I32, []),
+    "mdx_roi_align_get_mode": (I32, []),
     "mdx_conv_set_x3_narrow": (I32, [I32]),
     "mdx_rpn_set_sliced": (I32, [I32]),
     "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),

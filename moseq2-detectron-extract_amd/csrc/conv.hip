@@ -2003,8 +2003,9 @@ extern "C" int mdx_conv_set_winograd_min_cin(int c) {
 }
 extern "C" int mdx_conv_winograd_min_cin(void) { return g_wino_min_cin; }
 // Winograd GEMMs on the 256x256 LDS-DMA fp32 kernel: 0 never, 1 when the
-// batched launch has at least min_wgs workgroups (default), 2 whenever eligible
-static int g_wino_dma = 1, g_wino_dma_min_wgs = 384;
+// batched launch has at least min_wgs workgroups, 2 whenever eligible; off by
+// default (measured no faster than k_conv<128> on the p2 / p3 layers)
+static int g_wino_dma = 0, g_wino_dma_min_wgs = 384;
 extern "C" int mdx_conv_set_winograd_dma(int mode, int min_wgs) {
     const int old = g_wino_dma;
     g_wino_dma = mode;

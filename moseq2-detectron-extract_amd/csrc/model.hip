@@ -502,8 +502,10 @@ struct Fwd {
         c.named[n] = TensorRec{p, {a, b, cc, d}, dtype, off};
     }
     // conv + bias (+ residual) (+ ReLU); out_mode 1 = 2x2 deconv pixel shuffle
+    // in_planes: x is already in the bf16 plane layout (the box pooler's plane output)
     void *conv(const void *x, int N, int H, int W, const ConvW &cw, bool relu, int &OH, int &OW,
-               const void *residual = nullptr, bool out_f32 = false, int out_mode = 0, void *out = nullptr) {
+               const void *residual = nullptr, bool out_f32 = false, int out_mode = 0, void *out = nullptr,
+               bool in_planes = false) {
         OH = (H + 2 * cw.pad - cw.k) / cw.stride + 1;
         OW = (W + 2 * cw.pad - cw.k) / cw.stride + 1;
         const size_t oes = out_f32 ? 4 : m.es;
@@ -519,7 +521,11 @@ struct Fwd {
         // planes, GEMM on the bf16 matrix cores (mdx_gemm_x6)
         const bool x6 = cw.x6 && m.dt == 0 && !out_f32 && out_mode == 0 && cw.k == 1 && cw.stride == 1 &&
                         mdx_conv_fp32_split() == 6;
-        void *planes = x6 ? alloc((size_t)mdx_x6_plane_bytes((int64_t)N * H * W, cw.cin)) : nullptr;
+        if (in_planes && !x6 && rc == MDX_OK) {
+            set_error("model forward: plane input for a layer not in split-plane mode");
+            rc = MDX_EINVAL;
+        }
+        void *planes = x6 && !in_planes ? alloc((size_t)mdx_x6_plane_bytes((int64_t)N * H * W, cw.cin)) : nullptr;
         if (c.dry || !ok()) return out;
         ProfEv *pe = nullptr;
         if (m.profile) {
@@ -531,8 +537,8 @@ struct Fwd {
         }
         if (x6) {
             const int64_t rows = (int64_t)N * H * W;
-            chk(mdx_split_x6((const float *)x, rows, cw.cin, cw.cin, planes, s));
-            chk(mdx_gemm_x6(planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
+            if (!in_planes) chk(mdx_split_x6((const float *)x, rows, cw.cin, cw.cin, planes, s));
+            chk(mdx_gemm_x6(in_planes ? x : planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
                             (float *)out, s));
         } else if (wino)
             chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
@@ -562,17 +568,18 @@ struct Fwd {
             chk(mdx_groupnorm(x, N, H, W, C, G, m.cfg.gn_eps, g.g, g.b, up, fuse, m.dt, out, (float *)ws, s));
         return out;
     }
+    // planes: fp32 pooled rows written as bf16 planes (mdx_roi_align dtype 2)
     void *roi_align(void *const *feats, const int *fh, const int *fw, const float *rois, const int *counts, int R,
-                    int per_image, int P) {
+                    int per_image, int P, bool planes = false) {
         const int C = m.cfg.fpn_out_channels;
-        void *out = alloc((size_t)R * P * P * C * m.es);
+        void *out = alloc(planes ? (size_t)mdx_x6_plane_bytes(R, P * P * C) : (size_t)R * P * P * C * m.es);
         // the box pooler (per_image = post-NMS proposals) runs in level/band order
         int *order = per_image >= 256 ? (int *)alloc((size_t)R * sizeof(int)) : nullptr;
         const float sc[4] = {1.f / 4, 1.f / 8, 1.f / 16, 1.f / 32};
         if (!c.dry && ok())
             chk(mdx_roi_align_ex((const void *const *)feats, fh, fw, sc, 4, 2, C, rois, counts, R, per_image, P,
                                  m.cfg.pooler_sampling_ratio, m.cfg.pooler_aligned, m.cfg.canonical_box_size,
-                                 m.cfg.canonical_level, m.dt, order, out, s));
+                                 m.cfg.canonical_level, planes ? 2 : m.dt, order, out, s));
         return out;
     }
 
@@ -688,11 +695,18 @@ struct Fwd {
         name("proposal_count", pcount, B, 1, 1, 1, 2);
         // box head + fast_rcnn_inference
         const int R = cfg.box_pooler_resolution;
-        void *pooled = roi_align(feat, fh, fw, props, pcount, B * post, post, R);
-        name("box_pooled", pooled, (int64_t)B * post, R, R, C, m.dt);
+        // split-plane mode: the pooler writes fc1's A operand as bf16 planes
+        const bool pl = m.dt == 0 && !m.fc.empty() && m.fc[0].x6 && mdx_conv_fp32_split() == 6 &&
+                        (mdx_roi_align_get_mode() == 4 || mdx_roi_align_get_mode() == 5) && (R * R * C) % 16 == 0;
+        void *pooled = roi_align(feat, fh, fw, props, pcount, B * post, post, R, pl);
+        if (pl)
+            name("box_pooled", pooled, (int64_t)B * post, R * R * C / 16, 3, 16, 3);
+        else
+            name("box_pooled", pooled, (int64_t)B * post, R, R, C, m.dt);
         const void *yv = pooled;
         int oh, ow;
-        for (const ConvW &f : m.fc) yv = conv(yv, B * post, 1, 1, f, true, oh, ow);
+        for (size_t i = 0; i < m.fc.size(); ++i)
+            yv = conv(yv, B * post, 1, 1, m.fc[i], true, oh, ow, nullptr, false, 0, nullptr, pl && i == 0);
         float *pred = (float *)conv(yv, B * post, 1, 1, m.box_pred, false, oh, ow, nullptr, true);
         name("box_pred", pred, (int64_t)B * post, m.box_pred.cout, 1, 1, 0);
         if (!c.dry && ok())
@@ -872,7 +886,7 @@ extern "C" int mdx_model_tensor_copy(mdx_model_t model, mdx_stream_t stream, con
     auto it = c.named.find(name);
     MDX_REQUIRE(it != c.named.end(), "mdx_model_tensor_copy: no intermediate \"%s\" on this stream", name);
     const TensorRec &t = it->second;
-    const int64_t have = t.shape[0] * t.shape[1] * t.shape[2] * t.shape[3] * (t.dtype == 1 ? 2 : 4);
+    const int64_t have = t.shape[0] * t.shape[1] * t.shape[2] * t.shape[3] * (t.dtype == 1 || t.dtype == 3 ? 2 : 4);
     MDX_REQUIRE(bytes <= have, "mdx_model_tensor_copy: %lld bytes requested, \"%s\" has %lld", (long long)bytes,
                 name, (long long)have);
     MDX_HIP(hipMemcpyAsync(dst, t.p, (size_t)bytes, hipMemcpyDeviceToDevice, s));

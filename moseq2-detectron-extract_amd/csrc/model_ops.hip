@@ -871,6 +871,7 @@ struct RoiLevels {
     float canonical_size, canonical_level;
     int xcd_remap;  // 1: XCD-contiguous ROI ranges (default); 0: ROIs in dispatch order across XCDs
     const int *order;  // optional ROI permutation (k_roi_order), applied after the XCD remap
+    int planes;        // fp32 only: write each ROI row as bf16 planes (mdx_split_x6 layout) for mdx_gemm_x6
 };
 
 // the ROI a workgroup pools: XCD-contiguous ranges of the dispatch order (the
@@ -910,6 +911,25 @@ __device__ __forceinline__ void st16(T *p, const float *v) {
 #pragma unroll
     for (int i = 0; i < Vec16<T>::N; ++i) e[i] = (T)v[i];
     *reinterpret_cast<uint4 *>(p) = u;
+}
+// 4 fp32 values at element e (e % 4 == 0) of a row in the bf16 plane layout
+// (mdx_split_x6: per 16 values 96 B = hi | mid | lo, x = hi + mid + lo exactly)
+typedef __bf16 rbf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4_planes(char *row, long long e, const float *v) {
+    rbf16x4 h, m, l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 hb = (__bf16)v[i];
+        const float r1 = v[i] - (float)hb;
+        const __bf16 mb = (__bf16)r1;
+        h[i] = hb;
+        m[i] = mb;
+        l[i] = (__bf16)(r1 - (float)mb);
+    }
+    char *p = row + (e >> 4) * 96 + ((e >> 2) & 3) * 8;
+    *reinterpret_cast<rbf16x4 *>(p) = h;
+    *reinterpret_cast<rbf16x4 *>(p + 32) = m;
+    *reinterpret_cast<rbf16x4 *>(p + 64) = l;
 }
 
 // ROIAlign sample geometry of one ROI (ROIAlignV2 / ROIPooler semantics)
@@ -1315,12 +1335,21 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
     const int G = C / V;
     T *o = out + (long long)r * P * P * C;
     const int nitems = P * P * G;
+    // output of element e of this ROI's row: 16 B of T, or (planes, fp32) the
+    // three bf16 planes of the 4 values
+    char *const prow = sizeof(T) == 4 && rl.planes ? reinterpret_cast<char *>(out) + (long long)r * P * P * C * 6 : nullptr;
+    auto put = [&](long long e, const float *v) {
+        if (sizeof(T) == 4 && prow)
+            st4_planes(prow, e, v);
+        else
+            st16(o + e, v);
+    };
     // gridDim.y workgroups share one ROI's items (small ROI counts: mask /
     // keypoint poolers), each building the ROI's tables itself
     const int tstart = threadIdx.x + 256 * blockIdx.y, tstep = 256 * gridDim.y;
     if (ri >= counts[b]) {
         const float z[V] = {};
-        for (int i = tstart; i < nitems; i += tstep) st16(o + (long long)i * V, z);
+        for (int i = tstart; i < nitems; i += tstep) put((long long)i * V, z);
         return;
     }
     const RoiGeom g = roi_geom(rl, rois, r, b, sizeof(T));
@@ -1400,7 +1429,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
             }
 #pragma unroll
             for (int i = 0; i < V; ++i) acc[i] = acc[i] / g.count;
-            st16(o + (long long)t * V, acc);
+            put((long long)t * V, acc);
         }
         return;
     }
@@ -1466,7 +1495,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
                     }
 #pragma unroll
                     for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
-                    st16(o + ((long long)(ph * P + pw) * G + cg) * V, acc);
+                    put(((long long)(ph * P + pw) * G + cg) * V, acc);
                 }
                 __syncthreads();
             }
@@ -1530,7 +1559,7 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
         }
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
-        st16(o + (long long)t * V, acc);
+        put((long long)t * V, acc);
     }
 }
 
@@ -1580,6 +1609,7 @@ __global__ __launch_bounds__(256) void k_roi_order(RoiLevels rl, const float *__
 }
 
 static int g_roi_mode = 4, g_roi_xcd = 1, g_roi_sorted = 1;
+extern "C" int mdx_roi_align_get_mode(void) { return g_roi_mode; }
 extern "C" int mdx_roi_align_set_sorted(int on) {
     const int old = g_roi_sorted;
     g_roi_sorted = on;
@@ -2093,6 +2123,11 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
     rl.xcd_remap = g_roi_xcd;
     rl.order = nullptr;
+    // dtype 2: fp32 features, output rows as bf16 planes (mdx_split_x6 layout,
+    // the A operand of mdx_gemm_x6); separable kernels only
+    rl.planes = dtype == 2;
+    MDX_REQUIRE(dtype != 2 || ((g_roi_mode == 4 || g_roi_mode == 5) && P <= ROI_PMAX && (P * P * C) % 16 == 0),
+                "mdx_roi_align: plane output (dtype 2) needs the separable kernel and P*P*C %% 16 == 0");
     if (order_ws && g_roi_sorted) {
         hipLaunchKernelGGL(k_roi_order, dim3(R / per_image), dim3(256), 0, as_stream(stream), rl, rois, counts,
                            order_ws);

@@ -28,7 +28,7 @@ from .config import ModelConfig
 from .weights import pack_blob, resnet_stage_specs
 
 _DT = {"fp32": 0, "fp16": 1}
-_TDT = {0: torch.float32, 1: torch.float16, 2: torch.int32}
+_TDT = {0: torch.float32, 1: torch.float16, 2: torch.int32, 3: torch.bfloat16}
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -230,7 +230,11 @@ class MaskRCNN:
             inter["proposals"] = self.tensor("proposals")[..., 0]
             inter["proposal_scores"] = self.tensor("proposal_scores")[..., 0, 0]
             inter["proposal_count"] = self.tensor("proposal_count").view(B)
-            inter["box_pooled"] = self.tensor("box_pooled")
+            bp = self.tensor("box_pooled")
+            if bp.dtype == torch.bfloat16:  # split-plane mode: hi + mid + lo planes of each 16 values
+                P, C = cfg.box_pooler_resolution, cfg.fpn_out_channels
+                bp = bp.float().sum(2).reshape(bp.shape[0], P, P, C)
+            inter["box_pooled"] = bp
             inter["box_pred"] = self.tensor("box_pred")[..., 0, 0]
             if cfg.mask_on:
                 inter["mask_logits"] = self.tensor("mask_logits")

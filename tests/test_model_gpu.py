@@ -374,6 +374,15 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
             call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
                  2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(ref), None)
             assert torch.equal(out, ref)
+        if not half and mode in (4, 5) and (49 * C) % 16 == 0:
+            # dtype 2: the same rows written as bf16 planes (fc1's split-plane
+            # A operand); hi + mid + lo reconstructs every value exactly
+            pl = torch.empty((B * per, 49 * C // 16, 3, 16), dtype=torch.bfloat16, device="cuda")
+            call("mdx_roi_align_ex", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc,
+                 4, 2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, 2, P(order) if ordered else None, P(pl),
+                 None)
+            rec = pl.double().sum(2).float().reshape(out.shape)
+            assert torch.equal(rec, out)
     finally:
         call("mdx_roi_align_set_mode", old)
     got = out.cpu().float().permute(0, 3, 1, 2)
