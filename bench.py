@@ -48,8 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp16 secondary measurement")
-    ap.add_argument("--x6", action="store_true",
-                    help="also measure the fp32 loop with the split-plane kernels (mdx_conv_set_fp32_split(6))")
+    ap.add_argument("--no-x6", action="store_true",
+                    help="skip the secondary fp32 loop on the split-plane kernels (mdx_conv_set_fp32_split(6))")
     ap.add_argument("--no-h2d", action="store_true", help="raw batches already resident in HBM (no H2D in the loop)")
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
@@ -365,7 +365,7 @@ def main():
                               "note": "fp16 MFMA forward (fp32 accumulation), same loop; tolerance vs the fp32 "
                                       "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0-0]"}}
         del ex16
-    if not args.no_secondary and args.dtype == "fp32" and args.x6:
+    if not args.no_secondary and args.dtype == "fp32" and not args.no_x6:
         torch.cuda.synchronize()
         from moseq2_detectron_extract_amd._lib import call
         old = call("mdx_conv_set_fp32_split", 6)
@@ -377,7 +377,9 @@ def main():
             "value": round(frames_done / dtx, 2), "unit": "frames/s", "ms_per_step": round(dtx / args.steps * 1e3, 3),
             "dtype": "fp32 operands split exactly into 3 bf16 planes, 6 plane products on the bf16 matrix cores, "
                      "fp32 accumulation",
-            "note": "mdx_conv_set_fp32_split(6); per product the dropped terms are below one fp32 rounding; "
+            "note": "mdx_conv_set_fp32_split(6): conv layers on k_conv_x3 (split in registers), box head FCs on "
+                    "k_gemm_x6 (256x256 LDS-DMA over planes written by the box pooler / mdx_split_x6); per product the "
+                    "dropped terms are below one fp32 rounding; "
                     "full-frame parity vs the fp32 oracle at least as close as the f32-MFMA kernels' "
                     "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6], DESIGN.md section 3)"}
         del exx
