@@ -54,7 +54,10 @@ def parse():
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="run batches back to back on one stream instead of the multi-stream pipeline")
+                    help="run batches back to back on one stream (one forward at a time)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="software pipeline over streams (pipeline.OverlappedExtractor: front / forwards / tail of "
+                         "consecutive batches concurrently) instead of the default chunked loop")
     ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
@@ -62,7 +65,7 @@ def parse():
     ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT[,INT]",
                     help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
     ap.add_argument("--model-streams", type=int, default=2,
-                    help="forwards of consecutive batches in flight at once (one HIP stream each)")
+                    help="forwards in flight at once (one HIP stream each): batches per chunk in the default loop")
     return ap.parse_args()
 
 
@@ -226,8 +229,14 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
     cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
     pred = Predictor.from_config(cfg, dtype=dtype, seed=0)
-    ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B))
-    pipe = None if args.no_overlap else OverlappedExtractor(ex, args.model_streams)
+    ns = 1 if args.no_overlap else max(1, args.model_streams)
+    ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B, model_streams=ns))
+    pipe = OverlappedExtractor(ex, ns) if args.pipeline and not args.no_overlap else None
+    # default (chunked) loop: the reference's InferenceStep shape -- a chunk of
+    # ns batches is prepped / inpainted / cleaned, its ns batch_size-frame
+    # forwards run concurrently on ns streams (GPUExtractor.infer), then the
+    # chunk's moments / crops; `step` stays one 32-frame batch
+    chunk = 1 if pipe is not None else ns
     gstream = torch.cuda.Stream() if world > 1 else None
     h2d = torch.cuda.Stream()
     # the loop issues from a pool stream, not HIP's legacy NULL stream: an
@@ -245,16 +254,22 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
                 if "ready" in r:
                     gstream.wait_event(r["ready"])
                 payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
+                if gather_bufs is not None and payload.shape[0] != gather_bufs[0].shape[0]:
+                    gather_bufs[:] = [torch.empty_like(payload, device=gather_bufs[0].device) for _ in gather_bufs]
                 if gather_bufs is not None and gather_bufs[0].device.type == "cpu":
                     payload = payload.cpu()
                 dist.gather(payload, gather_bufs if rank == 0 else None, dst=0)
 
-    def upload(i):
-        if resident is not None:
+    def upload(i, n=1):
+        # batches i .. i+n-1 (the two pinned host batches alternate)
+        if resident is not None and n == 1:
             return resident[i % 2]
+        shape = (n * raw_host[0].shape[0],) + tuple(raw_host[0].shape[1:])
         with torch.cuda.stream(h2d):
-            raw = torch.empty(raw_host[0].shape, dtype=raw_host[0].dtype, device="cuda")
-            raw.copy_(raw_host[i % 2], non_blocking=True)
+            raw = torch.empty(shape, dtype=raw_host[0].dtype, device="cuda")
+            for q in range(n):
+                src = raw_host[(i + q) % 2] if resident is None else resident[(i + q) % 2]
+                raw[q * B:(q + 1) * B].copy_(src, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(h2d)
         issue_stream.wait_event(ev)
@@ -265,9 +280,12 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
         # nsteps batches through the path; with the pipeline the last batch is
         # flushed inside, so exactly nsteps batches complete
         with torch.cuda.stream(issue_stream):
-            for i in range(nsteps):
-                raw = upload(offset + i)
+            i = 0
+            while i < nsteps:
+                n = min(chunk, nsteps - i)
+                raw = upload(offset + i, n)
                 deliver(ex.step_device(raw) if pipe is None else pipe.submit(raw))
+                i += n
             if pipe is not None:
                 for r in pipe.flush():
                     deliver(r)
@@ -405,9 +423,13 @@ def main():
                        "parallelism": f"frame-sharded x{world}",
                        "h2d_in_timed_region": not args.no_h2d,
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                       "streams": "1" if args.no_overlap else f"{3 + args.model_streams} (H2D, prep/inpaint/clean of "
-                                  f"the newest batch, {args.model_streams} model forwards + mask selection of the "
-                                  f"next batches, moments/crop of the oldest)"},
+                       "streams": "1" if args.no_overlap else (
+                           f"{3 + args.model_streams} (H2D, prep/inpaint/clean of the newest batch, "
+                           f"{args.model_streams} model forwards + mask selection of the next batches, moments/crop "
+                           f"of the oldest)" if args.pipeline else
+                           f"chunks of {args.model_streams} batches: H2D on its own stream, prep/inpaint/clean of "
+                           f"the chunk, its {args.model_streams} forwards + mask selection concurrently on "
+                           f"{args.model_streams} streams, moments/crop of the chunk")},
             "roofline": roof, "cpu_baseline": cpu, "secondary": secondary,
         }
         print(json.dumps(line), flush=True)

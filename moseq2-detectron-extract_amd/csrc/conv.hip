@@ -351,18 +351,27 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
                     for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
             } else {
+                // B fragments first and the row tile outermost: the MFMAs of
+                // tile i start once bf and af[i] have arrived (per accumulator
+                // the e order is unchanged: bit-identical sums)
                 float4v af[TI], bf[TJ];
-#pragma unroll
-                for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
 #pragma unroll
                 for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
+                // (row tiles in groups of IG so >= 4 independent MFMAs separate
+                // two into one accumulator)
+                constexpr int IG = TJ >= 4 ? 1 : 4 / TJ;
 #pragma unroll
-                    for (int i = 0; i < TI; ++i)
+                for (int i0 = 0; i0 < TI; i0 += IG)
 #pragma unroll
-                        for (int j = 0; j < TJ; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int i = i0; i < i0 + IG; ++i)
+#pragma unroll
+                            for (int j = 0; j < TJ; ++j)
+                                acc[i][j] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
             }
         }
         if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
@@ -1064,10 +1073,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     auto mma = [&](int set) {
         if (PRIO) __builtin_amdgcn_s_setprio(1);  // the wave in its MFMA burst keeps the issue slots
         if constexpr (F32) {
+            // row tile outermost: the MFMAs of tile i need only fb and fa[i],
+            // so they start while the later A fragments are still arriving
+            // (same e order per accumulator: bit-identical sums)
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
+            for (int i = 0; i < TI; ++i)
 #pragma unroll
-                for (int i = 0; i < TI; ++i)
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[set][i][e], fb[set][j][e], acc[i][j], 0,
