@@ -996,6 +996,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         const int gn = n0 + r;
         b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * VEC : nullptr;
     }
+    // 1x1 / unpadded layers (FC layers, 1x1 convs): every valid row's source
+    // is in range, so the A piece address is a row pointer + the K offset
+    const bool pointwise = a.KH == 1 && a.KW == 1 && a.pad == 0;
+    const TIN *a_row[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        a_row[j] = a_ok[j] ? X + a_base[j] + ((long long)a_iy0[j] * a.W + a_ix0[j]) * a.Cin : nullptr;
     // issue state (uniform): the 64-chunk being issued and its tap
     // split-K: slice z = blockIdx.y multiplies substeps [s0, s0 + T) of the
     // K order (channel chunk outer, tap, half inner)
@@ -1015,10 +1022,15 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         const int kofs = i_kci + SUBK * i_half;
         if (p < 2) {
             const int j = p;
-            const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
-            const bool ok = a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            const void *src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kofs)
-                                 : (const void *)g_zero16;
+            const void *src;
+            if (pointwise) {
+                src = a_row[j] ? (const void *)(a_row[j] + kofs) : (const void *)g_zero16;
+            } else {
+                const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
+                const bool ok = a_ok[j] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kofs)
+                         : (const void *)g_zero16;
+            }
             glds16(src, smem + buf * SUB + 32 * wid * 64 + j * 1024);
         } else {
             const int j = p - 2;
@@ -1108,19 +1120,25 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     if (T > 2) issue(2);
     int issued = T < 3 ? T - 1 : 2;
     if constexpr (NSET == 1) {
-        // substep t: [wait t, barrier, read frags t, DMA t+3] then its MFMAs
+        // substep t: [wait t, barrier, DMA t+3, read frags t] then its MFMAs
         // (buffer (t+3)&3 == (t-1)&3: every wave drained its reads of t-1
-        // before the barrier)
+        // before the barrier).  DMA first, then all twelve fragment reads,
+        // then the burst: 6165 vs 6384 us on box fc1 for reads-then-DMA (a
+        // split burst overlapping the next substep's reads with the second
+        // half of the MFMAs measured 6374 us)
         for (int t = 0; t < T; ++t) {
             wait_landed(t, issued);
             MDX_WAIT_LGKM0();
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            read_frags(t, 0);
             if (t + 3 < T) {
                 issue((t + 3) & 3);
                 issued = t + 3;
             }
+            read_frags(t, 0);
+            // all fragment reads issue before the first MFMA (the scheduler
+            // would otherwise sink each A read to its use and wait on it alone)
+            __builtin_amdgcn_sched_barrier(0);
             mma(0);
         }
     } else {
