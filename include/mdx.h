@@ -259,6 +259,10 @@ int mdx_conv_winograd_min_cin(void);
  * batched launch has at least min_wgs workgroups, 2 whenever eligible; returns
  * the old mode. */
 int mdx_conv_set_winograd_dma(int mode, int min_wgs);
+/* fp32 1x1 layers with Cout <= 16 (the RPN / mask / box predictors) on the
+ * narrow-output kernel k_head_f32 (1, default) or the general kernels (0);
+ * returns the old value. */
+int mdx_conv_set_head_f32(int on);
 /* fp32 GEMM on the bf16 matrix cores over operands split once into bf16
  * planes (replaces the fp32 Linear layers of Detectron2's FastRCNNConvFCHead,
  * M/model/config.py:21-94 box head, when the model handle's x6 mode is on).

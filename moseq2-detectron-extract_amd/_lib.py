@@ -65,6 +65,7 @@ SIGNATURES = {
     "mdx_conv_set_winograd_min_cin": (I32, [I32]),
     "mdx_conv_winograd_min_cin": (I32, []),
     "mdx_conv_set_winograd_dma": (I32, [I32, I32]),
+    "mdx_conv_set_head_f32": (I32, [I32]),
     "mdx_x6_plane_bytes": (I64, [I64, I32]),
     "mdx_split_x6": (I32, [P, I64, I32, I64, P, P]),
     "mdx_gemm_x6": (I32, [P, P, P, I32, I32, I32, P, I32, P, P]),

@@ -893,6 +893,77 @@ __global__ __launch_bounds__(256) void k_conv1x1_head(ConvArgs a) {
     }
 }
 
+// Narrow-output fp32 1x1 kernel (RPN head 256 -> 15, mask predictor 256 ->
+// 1, box predictor 1024 -> 6): out[m][o] = sum_k W[o][k] X[m][k] + bias[o],
+// Cout <= 16, K % 16 == 0, K <= 1024.  D = W X^T on 16x16x4 f32 MFMAs: each
+// lane holds float4 pieces k = 16 c + 4 (lane >> 4) .. +3 of one weight row
+// (lane & 15) and of one pixel row, the four MFMAs of a piece take element e
+// of both (the same permutation of k on both operands); the wave keeps W in
+// registers and walks 16-pixel groups grid-stride, so the launch runs at the
+// activation read rate.
+template <int KC>
+__global__ __launch_bounds__(256) void k_head_f32(ConvArgs a) {
+    constexpr int K = 16 * KC;
+    // K in chunks of up to 256: the weights stay in registers when K <= 256,
+    // else each chunk's weight pieces are re-read (from L1 / L2) per group
+    constexpr int CH = KC < 16 ? KC : 16;
+    constexpr bool HOLD = KC <= 16;
+    const int lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
+    const float *X = reinterpret_cast<const float *>(a.x);
+    const float *Wt = reinterpret_cast<const float *>(a.w);
+    float *O = reinterpret_cast<float *>(a.out);
+    float4 wf[CH];
+    auto load_w = [&](int c0) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+            wf[c] = r16 < a.Cout ? *reinterpret_cast<const float4 *>(Wt + (long long)r16 * K + 16 * (c0 + c) + 4 * g)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    if (HOLD) load_w(0);
+    const long long groups = ((long long)a.M + 15) / 16;
+    const long long wave0 = (long long)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (long long)gridDim.x * 4;
+    for (long long grp = wave0; grp < groups; grp += nwaves) {
+        const long long m = grp * 16 + r16;
+        const bool ok = m < a.M;
+        const float *xr = X + (ok ? m : 0) * K + 4 * g;
+        float4v acc = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c0 = 0; c0 < KC; c0 += CH) {
+            if (!HOLD) load_w(c0);
+            float4 xf[CH];
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+                xf[c] = ok ? *reinterpret_cast<const float4 *>(xr + 16 * (c0 + c)) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c].x, xf[c].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c].y, xf[c].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c].z, xf[c].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[c].w, xf[c].w, acc, 0, 0, 0);
+            }
+        }
+        // D[o = 4 g + r][pixel = lane & 15]
+        if (ok) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = 4 * g + r;
+                if (o < a.Cout) {
+                    float v = acc[r] + (a.bias ? a.bias[o] : 0.f);
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                    O[m * a.Cout + o] = v;
+                }
+            }
+        }
+    }
+}
+
+// fp32 narrow-output 1x1 kernel (k_head_f32) for Cout <= 16: 1 on (default), 0 off
+static int g_head_f32 = 1;
+extern "C" int mdx_conv_set_head_f32(int on) {
+    const int old = g_head_f32;
+    g_head_f32 = on;
+    return old;
+}
 // streaming 1x1 kernel policy: 0 never, 1 for eligible layers with M >= g_stream_min_m (default),
 // 2 also for K = 256 layers with Cout > 64
 static int g_stream1x1 = 1, g_stream_min_m = 65536;
@@ -998,11 +1069,14 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     }
     // 1x1 / unpadded layers (FC layers, 1x1 convs): every valid row's source
     // is in range, so the A piece address is a row pointer + the K offset
-    const bool pointwise = a.KH == 1 && a.KW == 1 && a.pad == 0;
-    const TIN *a_row[2];
+    // (fp32 only: the fp16 tile has no registers to spare for the pointers)
+    const bool pointwise = F32 && a.KH == 1 && a.KW == 1 && a.pad == 0;
+    const TIN *a_row[2] = {nullptr, nullptr};
+    if constexpr (F32) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-        a_row[j] = a_ok[j] ? X + a_base[j] + ((long long)a_iy0[j] * a.W + a_ix0[j]) * a.Cin : nullptr;
+        for (int j = 0; j < 2; ++j)
+            a_row[j] = a_ok[j] ? X + a_base[j] + ((long long)a_iy0[j] * a.W + a_ix0[j]) * a.Cin : nullptr;
+    }
     // issue state (uniform): the 64-chunk being issued and its tap
     // split-K: slice z = blockIdx.y multiplies substeps [s0, s0 + T) of the
     // K order (channel chunk outer, tap, half inner)
@@ -1023,7 +1097,7 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         if (p < 2) {
             const int j = p;
             const void *src;
-            if (pointwise) {
+            if (F32 && pointwise) {
                 src = a_row[j] ? (const void *)(a_row[j] + kofs) : (const void *)g_zero16;
             } else {
                 const int iy = a_iy0[j] + i_kky, ix = a_ix0[j] + i_kkx;
@@ -1779,6 +1853,28 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.relu = relu;
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
+    // fp32 narrow-output 1x1 layers (RPN / mask / box predictors)
+    if (g_head_f32 && in_dtype == 0 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+        pad == 0 && !residual && Cout <= 16 && Cin % 16 == 0 && Cin <= 1024 && (ksplit == 1 || ksplit == 0)) {
+        a.tiles_n = 1;
+        a.tiles_total = 1;
+        a.ksplit = 1;
+        const long long groups = (M + 15) / 16;
+        const unsigned grid = (unsigned)std::min<long long>((groups + 3) / 4, 4096);
+        switch (Cin / 16) {
+#define MDX_HEAD_F32(KC_) \
+    case KC_: hipLaunchKernelGGL(k_head_f32<KC_>, dim3(grid), dim3(256), 0, s, a); break;
+            MDX_HEAD_F32(1) MDX_HEAD_F32(2) MDX_HEAD_F32(4) MDX_HEAD_F32(8) MDX_HEAD_F32(16) MDX_HEAD_F32(32)
+            MDX_HEAD_F32(64)
+#undef MDX_HEAD_F32
+            default: goto general;  // other K: the general kernels
+        }
+        t_plan_kernel = MDX_CONV_KERNEL_HEAD1X1;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
+general:
     // HBM-bound 1x1 layers: the streaming kernel
     if (g_stream1x1 && in_dtype == 1 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
         pad == 0 && !residual && (Cin == 64 || Cin == 128 || Cin == 256) && Cout <= 16 && (ksplit == 1 || ksplit == 0)) {

@@ -822,3 +822,34 @@ def test_gemm_x6_planes(mdx, M, N, K, relu, res):
     err = (out.cpu().double() - want).abs().max().item() / scale
     err_f32 = (ref.cpu().double() - want).abs().max().item() / scale
     assert err < 1e-5 and err <= 1.5 * err_f32 + 1e-7, (err, err_f32)
+
+
+@pytest.mark.parametrize("head", [1, 0], ids=["k_head_f32", "general"])
+@pytest.mark.parametrize("M,K,N,relu", [(458752 // 64, 256, 15, False), (1000, 1024, 6, False), (333, 256, 1, True),
+                                        (37, 32, 16, False)])
+def test_conv1x1_narrow_fp32(mdx, M, K, N, relu, head):
+    """fp32 1x1 layers with Cout <= 16 (RPN head, mask / box predictors) on
+    the narrow-output MFMA kernel vs fp64 (and the general kernel): 1e-5 of
+    the output scale; ragged M covers partial 16-pixel groups."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(M + K + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    want = x.double() @ w.double().T + b.double()
+    if relu:
+        want = want.clamp_min(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    xd, wd, bd = x.cuda(), w.cuda(), b.cuda()
+    out = torch.full((M, N), float("nan"), device="cuda")
+    old = call("mdx_conv_set_head_f32", head)
+    try:
+        call("mdx_conv2d", P(xd), M, 1, 1, K, P(wd), P(bd), N, 1, 1, 1, 0, None, int(relu), 0, 0, 0, P(out), None)
+        kid, ks_ = ctypes.c_int(), ctypes.c_int()
+        call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+    finally:
+        call("mdx_conv_set_head_f32", old)
+    assert (kid.value == 5) == bool(head)
+    err = (out.cpu().double() - want).abs().max().item() / want.abs().max().item()
+    assert err < 1e-5, err

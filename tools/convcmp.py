@@ -2,7 +2,7 @@
 import json
 import sys
 
-names = {0: 'c128', 1: 'c64', 2: 'g256', 3: 'g128', 6: 'wino', 7: 'x3_128', 8: 'x3_64', 9: 'x6dma'}
+names = {0: 'c128', 1: 'c64', 2: 'g256', 3: 'g128', 6: 'wino', 7: 'x3_128', 8: 'x3_64', 9: 'x6dma', 5: 'head', 4: 'strm'}
 a = json.load(open(sys.argv[1]))
 b = json.load(open(sys.argv[2]))
 ta = tb = 0
