@@ -250,9 +250,14 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
         if r is not None and world > 1:
             # on a side stream, so the hand-off never orders the caller's
             # stream (and the pipeline's next fronts) behind this batch
+            if "ready" not in r:  # chunked loop: the results were produced on the issuing stream
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+                r = dict(r, ready=ev)
+                for k in ("depth_frames", "mask_frames"):
+                    r[k].record_stream(gstream)
             with torch.cuda.stream(gstream):
-                if "ready" in r:
-                    gstream.wait_event(r["ready"])
+                gstream.wait_event(r["ready"])
                 payload = torch.stack([r["depth_frames"], r["mask_frames"]], 1).contiguous()
                 if gather_bufs is not None and payload.shape[0] != gather_bufs[0].shape[0]:
                     gather_bufs[:] = [torch.empty_like(payload, device=gather_bufs[0].device) for _ in gather_bufs]

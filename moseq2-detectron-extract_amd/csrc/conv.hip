@@ -1957,7 +1957,7 @@ general:
             return MDX_OK;
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && (in_dtype == 1 || g_dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 2048);
+        const bool big = Cout >= 192 && (in_dtype == 1 || g_dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 1024);
         // split-K on the 256x256 kernel for layers with few tiles but a deep
         // K (res4/res5 and head 3x3 convs): enough slices to fill the chip
         int ks256 = 1;
