@@ -295,6 +295,8 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
                 for r in pipe.flush():
                     deliver(r)
 
+    if pipe is not None:
+        pipe.prime(raw_host[0].cuda())
     run(args.warmup, 0)
     torch.cuda.synchronize()
     if world > 1:

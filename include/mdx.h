@@ -330,6 +330,11 @@ int mdx_preprocess(const uint8_t *frames, int B, int h, int w, const uint8_t lut
  * W'[o][ty][tx][(2dy+dx)*4+c] = W[o][c][2ty+dy][2tx+dx] (0 where 2ty+dy = 7). */
 int mdx_preprocess_s2d(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], const float *mean,
                        const float *stdv, int C, int Hp, int Wp, int dtype, void *out, mdx_stream_t stream);
+/* Same input in the 2-channel form of a stem with the normalisation folded
+ * into its weights: out (B, Hp/2+1, Wp/2+1, 8) = per 2x2 phase (scaled pixel,
+ * inside the image ? 1 : 0), zeros outside.  Used by fp32 model handles. */
+int mdx_preprocess_s2d_folded(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], int Hp, int Wp,
+                              int dtype, void *out, mdx_stream_t stream);
 
 /* max_pool2d(k, s, p), NHWC. */
 int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
@@ -516,6 +521,11 @@ typedef struct mdx_model_cfg {
 } mdx_model_cfg;
 
 typedef void *mdx_model_t;
+
+/* fp32 handles created afterwards fold the per-channel pixel normalisation
+ * into the stem weights (2-channel s2d input, K 256 -> 128): 1 on (default),
+ * 0 the 3-channel normalised input.  Returns the old value. */
+int mdx_model_set_stem_fold(int on);
 
 /* Weights blob: Detectron2 state-dict layout (parameter / buffer names of
  * GeneralizedRCNN, e.g. "backbone.bottom_up.res2.0.conv1.weight"), serialised

@@ -101,6 +101,7 @@ struct Model {
     mdx_model_cfg cfg{};
     int dev = 0;
     int dt = 0;        // 0 f32, 1 f16
+    bool stem_fold = false;  // stem over the 2-channel (value, inside) s2d input (fp32 handles)
     size_t es = 4;     // activation element size
     std::vector<void *> allocs;
     ConvW stem;
@@ -311,6 +312,36 @@ struct Packer {
         const int co = (int)w->shape[0], ci = (int)w->shape[1];
         std::vector<float> s, b;
         bn(p, co, s, b);
+        if (m.stem_fold) {
+            // every input channel is the same scaled pixel v, normalised per
+            // channel and zero outside the image: sum_c w_c (v - mean_c) /
+            // std_c = (sum_c w_c / std_c) v - (sum_c w_c mean_c / std_c) [inside]
+            // -> 2 channels (v, inside) per s2d phase, K = 4 x 4 x 8 (double sums, one rounding)
+            std::vector<float> pk((size_t)co * 128, 0.f);
+            for (int o = 0; o < co; ++o)
+                for (int ky = 0; ky < 7; ++ky)
+                    for (int kx = 0; kx < 7; ++kx) {
+                        double wv = 0, wi = 0;
+                        for (int ch = 0; ch < ci; ++ch) {
+                            const double wt = (double)w->v[(((size_t)o * ci + ch) * 7 + ky) * 7 + kx] * s[o];
+                            wv += wt / m.cfg.pixel_std[ch];
+                            wi -= wt * m.cfg.pixel_mean[ch] / m.cfg.pixel_std[ch];
+                        }
+                        const int ty = ky >> 1, dy = ky & 1, tx = kx >> 1, dx = kx & 1;
+                        const size_t q = (size_t)o * 128 + ((ty * 4 + tx) * 4 + dy * 2 + dx) * 2;
+                        pk[q] = (float)wv;
+                        pk[q + 1] = (float)wi;
+                    }
+            c.w = upload(pk, true);
+            c.b = upload_f32(b);
+            c.cin = 8;
+            c.cout = co;
+            c.k = 4;
+            c.stride = 1;
+            c.pad = 1;
+            c.kalg = 49 * ci;
+            return c;
+        }
         std::vector<float> pk((size_t)co * 256, 0.f);
         for (int o = 0; o < co; ++o)
             for (int ch = 0; ch < ci; ++ch)
@@ -591,13 +622,18 @@ struct Fwd {
         splitk = alloc(SPLITK_WS);
         // preprocess (+ scale LUT), space-to-depth for the stem
         const int Hs = Hp / 2 + 1, Ws = Wp / 2 + 1;
-        void *x = alloc((size_t)B * Hs * Ws * 16 * m.es);
+        const int s2c = m.stem_fold ? 8 : 16;
+        void *x = alloc((size_t)B * Hs * Ws * s2c * m.es);
         uint8_t ident[256];
         for (int i = 0; i < 256; ++i) ident[i] = (uint8_t)i;
-        if (!c.dry && ok())
-            chk(mdx_preprocess_s2d(frames, B, h, w, lut ? lut : ident, cfg.pixel_mean, cfg.pixel_std, cfg.in_channels,
-                                   Hp, Wp, m.dt, x, s));
-        name("input_s2d", x, B, Hs, Ws, 16, m.dt);
+        if (!c.dry && ok()) {
+            if (m.stem_fold)
+                chk(mdx_preprocess_s2d_folded(frames, B, h, w, lut ? lut : ident, Hp, Wp, m.dt, x, s));
+            else
+                chk(mdx_preprocess_s2d(frames, B, h, w, lut ? lut : ident, cfg.pixel_mean, cfg.pixel_std,
+                                       cfg.in_channels, Hp, Wp, m.dt, x, s));
+        }
+        name("input_s2d", x, B, Hs, Ws, s2c, m.dt);
         // backbone
         int H, W;
         void *y = conv(x, B, Hs, Ws, m.stem, true, H, W);
@@ -794,6 +830,15 @@ int reserve(Model &m, Ctx &c, int B, int h, int w, hipStream_t s) {
 
 using namespace mdx;
 
+// fp32 handles: the stem folded to the 2-channel (value, inside) form (1,
+// default) or over the normalised 3-channel input (0); read at mdx_model_create
+static int g_stem_fold = 1;
+extern "C" int mdx_model_set_stem_fold(int on) {
+    const int old = g_stem_fold;
+    g_stem_fold = on;
+    return old;
+}
+
 extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_model_cfg *cfg, int device,
                                 mdx_model_t *out) {
     MDX_REQUIRE(blob && cfg && out && blob_bytes >= 12, "mdx_model_create: null argument or blob shorter than its header");
@@ -816,6 +861,7 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     m->dev = device;
     m->dt = cfg->dtype;
     m->es = cfg->dtype == 1 ? 2 : 4;
+    m->stem_fold = cfg->dtype == 0 && g_stem_fold;
     std::string err;
     if (!pack(*m, sd, err)) {
         set_error("mdx_model_create: %s", err.c_str());

@@ -98,7 +98,10 @@ __global__ __launch_bounds__(256) void k_preprocess(const uint8_t *__restrict__ 
 // (2Y - 1 + dy, 2X - 1 + dx) in channels (2 dy + dx) * 4 + c (c < C, rest 0);
 // the stem becomes a 4x4 / stride-1 / pad-1 conv over 16 channels
 // (K = 256 instead of 7*7*8 = 392 with 16-B contiguous channel runs).
-template <typename T>
+// FOLD: the 2-channel form for a stem whose per-channel normalisation is
+// folded into its weights -- per phase (value, inside): the scaled pixel
+// (0 outside the image) and 1 / 0, 8 channels per s2d pixel instead of 16
+template <typename T, bool FOLD = false>
 __global__ __launch_bounds__(256) void k_preprocess_s2d(const uint8_t *__restrict__ fr, int B, int h, int w, int C,
                                                         int Hs, int Ws, PrepArgs pa, T *__restrict__ out) {
     const int total = B * Hs * Ws;
@@ -112,12 +115,17 @@ __global__ __launch_bounds__(256) void k_preprocess_s2d(const uint8_t *__restric
             const int y = 2 * Y - 1 + (q >> 1), x = 2 * X - 1 + (q & 1);
             const bool in = y >= 0 && y < h && x >= 0 && x < w;
             const float pix = in ? (float)pa.lut[fr[((long long)b * h + y) * w + x]] : 0.f;
+            if constexpr (FOLD) {
+                v[q * 2] = pix;
+                v[q * 2 + 1] = in ? 1.f : 0.f;
+            } else {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) v[q * 4 + c] = (in && c < C) ? (pix - pa.mean[c]) / pa.stdv[c] : 0.f;
+                for (int c = 0; c < 4; ++c) v[q * 4 + c] = (in && c < C) ? (pix - pa.mean[c]) / pa.stdv[c] : 0.f;
+            }
         }
-        T *o = out + (long long)p * 16;
+        T *o = out + (long long)p * (FOLD ? 8 : 16);
         st8(o, v);
-        st8(o + 8, v + 8);
+        if constexpr (!FOLD) st8(o + 8, v + 8);
     }
 }
 
@@ -1967,6 +1975,29 @@ extern "C" int mdx_preprocess_s2d(const uint8_t *frames, int B, int h, int w, co
         hipLaunchKernelGGL(k_preprocess_s2d<float>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), frames, B,
                            h, w, C, Hs, Ws, pa, (float *)out);
     MDX_CHECK_LAUNCH("mdx_preprocess_s2d");
+    return MDX_OK;
+}
+
+extern "C" int mdx_preprocess_s2d_folded(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], int Hp,
+                                         int Wp, int dtype, void *out, mdx_stream_t stream) {
+    MDX_REQUIRE(frames && lut && out, "mdx_preprocess_s2d_folded: null pointer");
+    MDX_REQUIRE(Hp >= h && Wp >= w && Hp % 2 == 0 && Wp % 2 == 0, "mdx_preprocess_s2d_folded: bad shape (even Hp, Wp)");
+    const int Hs = Hp / 2 + 1, Ws = Wp / 2 + 1;
+    MDX_REQUIRE((long long)B * Hs * Ws * 8 < (1ll << 31), "mdx_preprocess_s2d_folded: too many pixels");
+    PrepArgs pa;
+    for (int i = 0; i < 256; ++i) pa.lut[i] = lut[i];
+    for (int c = 0; c < 4; ++c) {
+        pa.mean[c] = 0.f;
+        pa.stdv[c] = 1.f;
+    }
+    const long long total = (long long)B * Hs * Ws;
+    if (dtype == 1)
+        hipLaunchKernelGGL((k_preprocess_s2d<_Float16, true>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                           frames, B, h, w, 1, Hs, Ws, pa, (_Float16 *)out);
+    else
+        hipLaunchKernelGGL((k_preprocess_s2d<float, true>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                           frames, B, h, w, 1, Hs, Ws, pa, (float *)out);
+    MDX_CHECK_LAUNCH("mdx_preprocess_s2d_folded");
     return MDX_OK;
 }
 

@@ -224,7 +224,7 @@ class MaskRCNN:
         call("mdx_model_forward", self._h, _p(frames), B, h, w, lut_p, ctypes.byref(o), _stream())
         if intermediates:
             Hp, Wp = self.padded_size(h, w)
-            inter = {"input": s2d_to_nhwc(self.tensor("input_s2d"), Hp, Wp)}
+            inter = {"input": s2d_to_nhwc(self.tensor("input_s2d"), Hp, Wp, cfg)}
             for k in ("res2", "res3", "res4", "res5", "p2", "p3", "p4", "p5", "p6"):
                 inter[k] = self.tensor(k)
             inter["proposals"] = self.tensor("proposals")[..., 0]
@@ -242,12 +242,27 @@ class MaskRCNN:
         return out
 
 
-def s2d_to_nhwc(x: torch.Tensor, Hp: int, Wp: int) -> torch.Tensor:
-    """(B, Hp/2+1, Wp/2+1, 16) space-to-depth input -> (B, Hp, Wp, 4) NHWC."""
-    B = x.shape[0]
-    t = x.view(B, Hp // 2 + 1, Wp // 2 + 1, 2, 2, 4).permute(0, 1, 3, 2, 4, 5)
-    t = t.reshape(B, Hp + 2, Wp + 2, 4)
-    return t[:, 1:Hp + 1, 1:Wp + 1].contiguous()
+def s2d_to_nhwc(x: torch.Tensor, Hp: int, Wp: int, cfg: Optional[ModelConfig] = None) -> torch.Tensor:
+    """(B, Hp/2+1, Wp/2+1, 16) space-to-depth input -> (B, Hp, Wp, 4) NHWC.
+    The folded stem's 8-channel form (per phase: scaled pixel, inside flag)
+    is expanded to the normalised input (x - mean_c) / std_c inside the image,
+    0 outside (cfg's pixel mean / std), channels beyond in_channels zero."""
+    B, C = x.shape[0], x.shape[-1]
+    t = x.view(B, Hp // 2 + 1, Wp // 2 + 1, 2, 2, C // 4).permute(0, 1, 3, 2, 4, 5)
+    t = t.reshape(B, Hp + 2, Wp + 2, C // 4)[:, 1:Hp + 1, 1:Wp + 1]
+    if C == 16:
+        return t.contiguous()
+    if cfg is None:
+        raise ValueError("s2d_to_nhwc: the folded 8-channel input needs the model config")
+    v, inside = t[..., 0], t[..., 1] > 0
+    out = torch.zeros(t.shape[:3] + (4,), dtype=t.dtype, device=t.device)
+    for c in range(cfg.in_channels):
+        # tensor operands: an IEEE division as in the preprocess kernel (a
+        # python-scalar divisor becomes a multiply by its reciprocal)
+        mean = torch.full_like(v, cfg.pixel_mean[c])
+        std = torch.full_like(v, cfg.pixel_std[c])
+        out[..., c] = torch.where(inside, (v - mean) / std, torch.zeros_like(v))
+    return out
 
 
 def flops_per_image(cfg: ModelConfig, h: int = 423, w: int = 511, proposals: int = 1000, dets: int = 4) -> float:

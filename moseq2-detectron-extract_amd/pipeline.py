@@ -425,6 +425,20 @@ class OverlappedExtractor:
         (stream or torch.cuda.current_stream()).wait_event(out["ready"])
         return out
 
+    def prime(self, raw: torch.Tensor):
+        """One batch through the whole path on every stream of the pipeline,
+        one stream at a time, synchronised: kernel code objects are loaded,
+        each model stream's workspace is reserved (mdx_model_reserve on first
+        use) and the allocator's per-stream pools are populated before any
+        two stages run concurrently."""
+        cur = torch.cuda.current_stream()
+        for st in (self.s_front, *self.s_models, self.s_tail):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                raw.record_stream(st)
+                self.ex.step_device(raw)
+            torch.cuda.synchronize()
+
     def submit(self, raw: torch.Tensor):
         # issue order: tail of the oldest modeled batch (once `depth` forwards
         # are in flight), forward of the fronted batch, front of `raw`; every
