@@ -10,12 +10,20 @@ step   : one pass of the hot path over one batch of 32 synthetic raw int16
          detections) -> mask-IoU NMS + instance-0 selection -> clean_frames
          (median3 + 3x open ellipse9) -> moments -> angle -> crop_and_rotate
          (depth + mask).
+loop   : chunks of --model-streams (2) batches, the extract loop's shape: the
+         chunk's H2D on its own stream, prep/inpaint/clean of the chunk, its
+         32-frame forwards concurrently on two HIP streams, moments/crop of the
+         chunk (GPUExtractor.step_device); --pipeline runs the staggered
+         five-stream pipeline instead (faults with the f32-MFMA kernels,
+         DESIGN.md section 3), --no-overlap one batch at a time.
 value  : frames processed by all ranks / max-over-ranks wall time.
 scaling: weak (every rank processes its own 32-frame batches; frames shard
          with no data-path collective; N>1 gathers each step's 80x80 crops to
          rank 0 over RCCL, the reference's result hand-off to the writer).
 secondary.fp16: the same loop with the fp16 MFMA forward (BASELINE config 5's
          precision), reported beside the fp32 headline, never as `value`.
+secondary.fp32_bf16x6: the same loop with the fp32 layers as exact bf16
+         plane products (mdx_conv_set_fp32_split(6)).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
         (N>1 via torch.distributed.run, one process per GPU)
