@@ -10,10 +10,10 @@ step   : one pass of the hot path over one batch of 32 synthetic raw int16
          detections) -> mask-IoU NMS + instance-0 selection -> clean_frames
          (median3 + 3x open ellipse9) -> moments -> angle -> crop_and_rotate
          (depth + mask).
-loop   : chunks of --model-streams (2) batches, the extract loop's shape: the
+loop   : chunks of --chunk-batches (8) batches, the extract loop's shape: the
          chunk's H2D on its own stream, prep/inpaint/clean of the chunk, its
-         32-frame forwards concurrently on two HIP streams, moments/crop of the
-         chunk (GPUExtractor.step_device); --pipeline runs the staggered
+         32-frame forwards alternating over two HIP streams, moments/crop of
+         the chunk (GPUExtractor.step_device); --pipeline runs the staggered
          five-stream pipeline instead (faults with the f32-MFMA kernels,
          DESIGN.md section 3), --no-overlap one batch at a time.
 value  : frames processed by all ranks / max-over-ranks wall time.
@@ -73,7 +73,9 @@ def parse():
     ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT[,INT]",
                     help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
     ap.add_argument("--model-streams", type=int, default=2,
-                    help="forwards in flight at once (one HIP stream each): batches per chunk in the default loop")
+                    help="forwards in flight at once (one HIP stream each)")
+    ap.add_argument("--chunk-batches", type=int, default=8,
+                    help="batches per chunk in the default loop (the chunk's forwards alternate over the streams)")
     return ap.parse_args()
 
 
@@ -241,10 +243,11 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
     ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B, model_streams=ns))
     pipe = OverlappedExtractor(ex, ns) if args.pipeline and not args.no_overlap else None
     # default (chunked) loop: the reference's InferenceStep shape -- a chunk of
-    # ns batches is prepped / inpainted / cleaned, its ns batch_size-frame
-    # forwards run concurrently on ns streams (GPUExtractor.infer), then the
+    # --chunk-batches batches is prepped / inpainted / cleaned, its
+    # batch_size-frame forwards alternate over ns streams (GPUExtractor.infer;
+    # the streams drift apart, so the forwards overlap out of phase), then the
     # chunk's moments / crops; `step` stays one 32-frame batch
-    chunk = 1 if pipe is not None else ns
+    chunk = 1 if pipe is not None else (max(1, args.chunk_batches) if ns > 1 else 1)
     gstream = torch.cuda.Stream() if world > 1 else None
     h2d = torch.cuda.Stream()
     # the loop issues from a pool stream, not HIP's legacy NULL stream: an
@@ -442,9 +445,9 @@ def main():
                            f"{3 + args.model_streams} (H2D, prep/inpaint/clean of the newest batch, "
                            f"{args.model_streams} model forwards + mask selection of the next batches, moments/crop "
                            f"of the oldest)" if args.pipeline else
-                           f"chunks of {args.model_streams} batches: H2D on its own stream, prep/inpaint/clean of "
-                           f"the chunk, its {args.model_streams} forwards + mask selection concurrently on "
-                           f"{args.model_streams} streams, moments/crop of the chunk")},
+                           f"chunks of {args.chunk_batches} batches: H2D on its own stream, prep/inpaint/clean of "
+                           f"the chunk, its forwards + mask selection alternating over {args.model_streams} "
+                           f"streams, moments/crop of the chunk")},
             "roofline": roof, "cpu_baseline": cpu, "secondary": secondary,
         }
         print(json.dumps(line), flush=True)
