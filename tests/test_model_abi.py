@@ -91,3 +91,36 @@ def test_create_rejects_bad_cfg(mdx):
     h = ctypes.c_void_p()
     with pytest.raises(MdxError, match="depth"):
         call("mdx_model_create", blob, len(blob), ctypes.byref(c), 0, ctypes.byref(h))
+
+
+def test_s2d_decode_folded_matches_normalised_input(mdx):
+    """The folded stem's 8-channel space-to-depth input (per 2x2 phase: scaled
+    pixel, inside flag) decodes to the normalised NHWC input of the reference
+    preprocess ((v - mean_c) / std_c inside the image, 0 in the padding),
+    bit for bit; the 16-channel form decodes by layout only."""
+    from moseq2_detectron_extract_amd.model.config import ModelConfig
+    from moseq2_detectron_extract_amd.model.runtime import s2d_to_nhwc
+    cfg = ModelConfig()
+    g = torch.Generator().manual_seed(0)
+    B, h, w, Hp, Wp = 2, 5, 7, 8, 10
+    v = torch.randint(0, 256, (B, h, w), generator=g).float()
+    inside = torch.zeros(B, Hp, Wp)
+    inside[:, :h, :w] = 1
+    vp = torch.zeros(B, Hp, Wp)
+    vp[:, :h, :w] = v
+    # pad by one on each side, then space-to-depth into (B, Hp/2+1, Wp/2+1, 2, 2, C) phases
+    def s2d(x):  # x (B, Hp, Wp, C)
+        C = x.shape[-1]
+        xp = torch.zeros(B, Hp + 2, Wp + 2, C)
+        xp[:, 1:Hp + 1, 1:Wp + 1] = x
+        return xp.view(B, Hp // 2 + 1, 2, Wp // 2 + 1, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(
+            B, Hp // 2 + 1, Wp // 2 + 1, 4 * C)
+    folded = s2d(torch.stack([vp, inside], -1))
+    got = s2d_to_nhwc(folded, Hp, Wp, cfg)
+    want = torch.zeros(B, Hp, Wp, 4)
+    for c in range(cfg.in_channels):
+        want[..., c] = torch.where(inside > 0, (vp - torch.full_like(vp, cfg.pixel_mean[c])) /
+                                   torch.full_like(vp, cfg.pixel_std[c]), torch.zeros_like(vp))
+    assert torch.equal(got, want)
+    plain = s2d(want)
+    assert torch.equal(s2d_to_nhwc(plain, Hp, Wp), want)
