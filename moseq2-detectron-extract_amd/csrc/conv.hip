@@ -1917,7 +1917,9 @@ general:
     // fp32 operands (Cin % 32 == 0, fp32 out): the 256x256 kernel on 16x16x4 f32
     // MFMAs, same LDS image (64-B rows of 16 floats)
     const bool x3 = in_dtype == 0 && out_dtype == 0 && g_fp32_split;
-    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32 && !x3;
+    // (mode 4: as 2, also while the split-plane mode routes the other fp32
+    // layers to k_conv_x3 -- a diagnostic for kernel-level A/B runs)
+    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32 && (!x3 || g_dma_f32 == 4);
     if (((in_dtype == 1 && Cin % 64 == 0) || dma_f32) && (ksplit == 1 || ksplit == 0) &&
         KH * KW * Cin > g_narrow_kmax) {
         const int subk = in_dtype == 1 ? 32 : 16;  // K elements per 64-B substep
