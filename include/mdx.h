@@ -298,6 +298,10 @@ enum {
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256
  * only when Cout == 64), 2 for every eligible layer with M >= min_m. */
 int mdx_conv_set_stream1x1(int mode, int min_m);
+/* Its fp32 form (f32 MFMAs; fp32 in and out, not in split-plane mode), same
+ * M threshold: 0 never, 1 (default) Cin == 64, 2 Cin in {64,128,256}.
+ * Returns the previous mode. */
+int mdx_conv_set_stream1x1_f32(int mode);
 
 /* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
  * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1

@@ -841,6 +841,104 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
     }
 }
 
+// fp32 streaming 1x1 kernel (K = Cin = 16 KQ in {64, 128, 256}, Cout % 64 ==
+// 0): the fp16 kernel's tiling on 16x16x4 f32 MFMAs.  A lane's 16-B load of
+// an activation row holds 4 consecutive K values; MFMA e of a 16-K block takes
+// component e from every lane group, i.e. K values 16 kq + 4 (l >> 4) + e --
+// a fixed permutation of K, the same for both operands:
+//   W operand = W[n0 + 16 ns + (l & 15)][16 kq + 4 (l >> 4) + e]
+//   X operand = X[m0 + 16 ms + (l & 15)][16 kq + 4 (l >> 4) + e]
+//   D[ms][ns][r] = out[m0 + 16 ms + (l & 15)][n0 + 16 ns + 4 (l >> 4) + r]
+// Each lane ends with 4 consecutive fp32 channels of one pixel = one 16-B
+// residual load and one 16-B store (no exchange, no LDS epilogue).
+template <int KQ>
+__global__ __launch_bounds__(256) void k_conv1x1_stream_f32(ConvArgs a) {
+    constexpr int K = 16 * KQ, WPITCH = 4 * K + 16;  // +16 B: rows (l & 15) land 4 banks apart
+    __shared__ __attribute__((aligned(16))) char sw[64 * WPITCH];
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int n0 = tn * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
+    const float *Wt = reinterpret_cast<const float *>(a.w);
+    const int m0 = tm * 128 + wid * 32;
+    // residual first (the longest stream, independent of everything else)
+    float4v rr[2][4];
+    if (a.res) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
+                                                                            0x00020000);
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms) {
+            const int m = m0 + 16 * ms + (lane & 15);
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns) {
+                const unsigned off =
+                    m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 16 * ns + 4 * g) * 4) : 0xFFFFFFF0u;
+                rr[ms][ns] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
+            }
+        }
+    }
+    // stage the 64 x K weight slice
+    for (int i = tid; i < 64 * K / 4; i += 256) {
+        const int r = i / (K / 4), c = i - r * (K / 4);
+        *reinterpret_cast<uint4 *>(sw + r * WPITCH + c * 16) =
+            *reinterpret_cast<const uint4 *>(Wt + (long long)(n0 + r) * K + c * 4);
+    }
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    float4v xf[2][KQ];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+        const int m = m0 + 16 * ms + (lane & 15);
+        const unsigned base = (unsigned)((long long)m * K * 4) + 16u * g;
+#pragma unroll
+        for (int kq = 0; kq < KQ; ++kq)
+            xf[ms][kq] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rx, m < a.M ? base + 64u * kq : 0xFFFFFFF0u, 0, 0));
+    }
+    __syncthreads();
+    float4v acc[2][4];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = float4v{0.f, 0.f, 0.f, 0.f};
+    const char *wl = sw + (lane & 15) * WPITCH + 16 * g;
+#pragma unroll
+    for (int kq = 0; kq < KQ; ++kq) {
+        float4v wf[4];
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) wf[ns] = *reinterpret_cast<const float4v *>(wl + 16 * ns * WPITCH + 64 * kq);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+                for (int ns = 0; ns < 4; ++ns)
+                    acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[ns][e], xf[ms][kq][e], acc[ms][ns], 0, 0, 0);
+    }
+    float *O = reinterpret_cast<float *>(a.out);
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) {
+        const int c = n0 + 16 * ns + 4 * g;
+        const float4v bv = a.bias ? *reinterpret_cast<const float4v *>(a.bias + c) : float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms) {
+            const int m = m0 + 16 * ms + (lane & 15);
+            if (m >= a.M) continue;
+            float4v v = acc[ms][ns] + bv;
+            if (a.res) v += rr[ms][ns];
+            if (a.relu) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+            }
+            *reinterpret_cast<float4v *>(O + (long long)m * a.Cout + c) = v;
+        }
+    }
+}
+
 // Narrow-output streaming 1x1 kernel (RPN head: 256 -> 15 logits/deltas,
 // fp32 out): one 16-row MFMA block of output channels (rows >= Cout read as
 // zero weights), no LDS and no barrier -- each wave loads its 16 x K weight
@@ -971,6 +1069,16 @@ extern "C" int mdx_conv_set_stream1x1(int mode, int min_m) {
     const int old = g_stream1x1;
     g_stream1x1 = mode;
     g_stream_min_m = min_m;
+    return old;
+}
+// fp32 streaming 1x1 kernel (k_conv1x1_stream_f32), layers with M >= g_stream_min_m: 0 never,
+// 1 Cin = 64 (default: measured 3-9 % faster than k_conv<float, float, 64> on the res2 1x1
+// layers; 8-27 % slower at Cin = 128 and 256, where the one-shot tile's 2 waves per SIMD
+// leave the f32 MFMAs idle), 2 Cin in {64, 128, 256}
+static int g_stream1x1_f32 = 1;
+extern "C" int mdx_conv_set_stream1x1_f32(int mode) {
+    const int old = g_stream1x1_f32;
+    g_stream1x1_f32 = mode;
     return old;
 }
 
@@ -1905,6 +2013,24 @@ general:
             hipLaunchKernelGGL(k_conv1x1_stream<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
         else
             hipLaunchKernelGGL(k_conv1x1_stream<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        t_plan_kernel = MDX_CONV_KERNEL_STREAM1X1;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
+    if (g_stream1x1_f32 && in_dtype == 0 && out_dtype == 0 && !g_fp32_split && out_mode == 0 && KH == 1 &&
+        KW == 1 && stride == 1 && pad == 0 &&
+        (Cin == 64 || (g_stream1x1_f32 == 2 && (Cin == 128 || Cin == 256))) && Cout % 64 == 0 &&
+        (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m) {
+        a.tiles_n = Cout / 64;
+        a.tiles_total = (int)(ceil_div(M, 128) * a.tiles_n);
+        a.ksplit = 1;
+        if (Cin == 64)
+            hipLaunchKernelGGL(k_conv1x1_stream_f32<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else if (Cin == 128)
+            hipLaunchKernelGGL(k_conv1x1_stream_f32<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_conv1x1_stream_f32<16>, dim3(a.tiles_total), dim3(256), 0, s, a);
         t_plan_kernel = MDX_CONV_KERNEL_STREAM1X1;
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");

@@ -93,9 +93,10 @@ def test_conv2d(mdx, dtype, case, ksplit):
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     dc = 1 if dtype == "fp16" else 0
     if ksplit == "stream":
-        if dtype != "fp16" or k != 1 or s != 1 or Cin not in (64, 128, 256) or Cout % 64:
-            pytest.skip("streaming 1x1 kernel: fp16, 1x1/s1, Cin in {64,128,256}, Cout % 64 == 0")
+        if k != 1 or s != 1 or Cin not in (64, 128, 256) or Cout % 64:
+            pytest.skip("streaming 1x1 kernels: 1x1/s1, Cin in {64,128,256}, Cout % 64 == 0")
         old = call("mdx_conv_set_stream1x1", 2, 0)
+        old_f = call("mdx_conv_set_stream1x1_f32", 2)
         try:
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
@@ -103,6 +104,7 @@ def test_conv2d(mdx, dtype, case, ksplit):
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
             assert kid.value == 4
         finally:
+            call("mdx_conv_set_stream1x1_f32", old_f)
             call("mdx_conv_set_stream1x1", old, 65536)
     elif ksplit == "split256":
         if Cin % (64 if dtype == "fp16" else 32) or Cout % 256:
