@@ -232,7 +232,7 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_compact(const uint8_t
 __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *__restrict__ invalid, int H, int W,
                                                                  int range, int *__restrict__ ws, InpLayout L) {
     __shared__ int sh[INP_SETUP_THREADS];
-    __shared__ int s_flag;
+    __shared__ int s_flag[2];
     const int tid = threadIdx.x;
     const long long f = blockIdx.x;
     int *base = ws + f * L.total;
@@ -265,9 +265,18 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
     __syncthreads();
     // clusters: min-label propagation over Chebyshev distance <= range + 1
     const int R = range + 1;
+    // two convergence flags, alternating per iteration: thread 0 clears the
+    // NEXT iteration's flag after this iteration's first barrier, when every
+    // thread has read it (as the previous iteration's flag) and before any
+    // thread can set it.  (One flag cleared at the top of the loop raced with
+    // the slower waves' read of the previous iteration's value: a wave that
+    // read the cleared flag left the loop alone, its barriers then paired
+    // with the other waves' loop barriers, and the label arrays were indexed
+    // before they had converged.)
+    if (tid == 0) s_flag[0] = s_flag[1] = 0;
     for (int iter = 0; iter < 1 << 20; ++iter) {
-        if (tid == 0) s_flag = 0;
         __syncthreads();
+        if (tid == 0) s_flag[(iter + 1) & 1] = 0;
         int changed = 0;
         for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
             const int i = ins[k];
@@ -292,9 +301,9 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
                 changed = 1;
             }
         }
-        if (changed) atomicOr(&s_flag, 1);
+        if (changed) atomicOr(&s_flag[iter & 1], 1);
         __syncthreads();
-        if (!s_flag) break;
+        if (!s_flag[iter & 1]) break;
     }
     // cluster ids for roots (lab[k] == k) in raster order, member counts, starts
     int ncl = 0;
