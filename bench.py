@@ -10,12 +10,12 @@ step   : one pass of the hot path over one batch of 32 synthetic raw int16
          detections) -> mask-IoU NMS + instance-0 selection -> clean_frames
          (median3 + 3x open ellipse9) -> moments -> angle -> crop_and_rotate
          (depth + mask).
-loop   : chunks of --chunk-batches (8) batches, the extract loop's shape: the
-         chunk's H2D on its own stream, prep/inpaint/clean of the chunk, its
-         32-frame forwards alternating over two HIP streams, moments/crop of
-         the chunk (GPUExtractor.step_device); --pipeline runs the staggered
-         five-stream pipeline instead (faults with the f32-MFMA kernels,
-         DESIGN.md section 3), --no-overlap one batch at a time.
+loop   : the staggered five-stream pipeline (pipeline.OverlappedExtractor):
+         H2D, prep/inpaint/clean of batch i+3, the forwards of batches i+1 and
+         i+2 on two HIP streams, moments/crop of batch i, all concurrent;
+         --chunked runs chunks of --chunk-batches (8) batches instead (the
+         chunk's stages one after another, its forwards alternating over two
+         streams: GPUExtractor.step_device), --no-overlap one batch at a time.
 value  : frames processed by all ranks / max-over-ranks wall time.
 scaling: weak (every rank processes its own 32-frame batches; frames shard
          with no data-path collective; N>1 gathers each step's 80x80 crops to
@@ -65,7 +65,10 @@ def parse():
                     help="run batches back to back on one stream (one forward at a time)")
     ap.add_argument("--pipeline", action="store_true",
                     help="software pipeline over streams (pipeline.OverlappedExtractor: front / forwards / tail of "
-                         "consecutive batches concurrently) instead of the default chunked loop")
+                         "consecutive batches concurrently) -- the default; kept for older command lines")
+    ap.add_argument("--chunked", action="store_true",
+                    help="the chunked loop (GPUExtractor.step_device over --chunk-batches batches) instead of the "
+                         "pipeline")
     ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
     ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
     ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
@@ -76,7 +79,9 @@ def parse():
                     help="forwards in flight at once (one HIP stream each)")
     ap.add_argument("--chunk-batches", type=int, default=8,
                     help="batches per chunk in the default loop (the chunk's forwards alternate over the streams)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.pipeline = not args.chunked and not args.no_overlap
+    return args
 
 
 # MDX_CONV_KERNEL_* (+10: fp32-output instance of an fp16 model) -> rocprofv3 symbol, per dtype

@@ -367,18 +367,6 @@ class OverlappedExtractor:
     flush() -> list of the results still in flight."""
 
     def __init__(self, extractor: GPUExtractor, model_streams: int = 2):
-        # DESIGN.md section 3: with fp32 models on the f32-MFMA kernels this
-        # pipeline faulted (illegal address) in every 300-step run; fp16 and
-        # the split-plane fp32 kernels ran clean, as does the chunked loop
-        # (GPUExtractor.infer over a chunk, extract.extract_session)
-        pred = getattr(extractor, "predictor", None)
-        if getattr(getattr(pred, "model", None), "dtype", None) == "fp32":
-            from ._lib import call
-            if call("mdx_conv_fp32_split") == 0:
-                import warnings
-                warnings.warn("OverlappedExtractor with an fp32 model on the f32-MFMA kernels: illegal-address "
-                              "faults measured under this pipeline (DESIGN.md section 3); prefer the chunked loop "
-                              "or mdx_conv_set_fp32_split(6)", RuntimeWarning, stacklevel=2)
         self.ex = extractor
         self.s_front = torch.cuda.Stream()
         self.s_models = [torch.cuda.Stream() for _ in range(max(1, model_streams))]
