@@ -229,12 +229,20 @@ def filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60) ->
 def iterative_filter_angles(angles: np.ndarray, window: int = 3, tolerance: float = 60,
                             max_iters: int = 1000) -> Tuple[np.ndarray, np.ndarray]:
     """filter_angles repeated until it stops changing (M/proc/proc.py:627-654);
-    returns (angles, flips).  Runs in libmdx (mdx_iterative_filter_angles, host
-    code) without holding the GIL: the reference loops up to 1000 times
-    whenever an angle is NaN."""
+    returns (angles, flips).  1-D angles with window <= 8 (the extract path:
+    window 3) run in libmdx (mdx_iterative_filter_angles, host code) without
+    holding the GIL: the reference loops up to 1000 times whenever an angle is
+    NaN.  Other shapes / windows take the numpy statement of the same loop."""
     a = np.ascontiguousarray(angles, dtype=np.float64)
     if a.ndim != 1 or not 1 <= window <= 8:
-        raise NotImplementedError("iterative_filter_angles: 1-D angles and window <= 8")
+        last, it = a, 0
+        while it <= max_iters:
+            it += 1
+            curr = filter_angles(last, window=window, tolerance=tolerance)
+            if np.allclose(curr, last):
+                break
+            last = curr
+        return curr, np.isclose(np.abs(curr - a), 180)
     out = np.empty_like(a)
     flips = np.empty(a.shape, dtype=np.uint8)
     call("mdx_iterative_filter_angles", _np(a), a.shape[0], int(window), float(tolerance), int(max_iters), _np(out),

@@ -32,7 +32,7 @@ class Predictor:
 
     @classmethod
     def from_config(cls, cfg: Union[ModelConfig, str], weights: Union[None, str, dict] = None,
-                    dtype: str = "fp16", device="cuda", seed: int = 0) -> "Predictor":
+                    dtype: str = "fp32", device="cuda", seed: int = 0) -> "Predictor":
         """cfg: ModelConfig or path to a Detectron2 config.yaml.  weights: path to
         a Detectron2 checkpoint (.pth, loaded weights_only), a state dict, or
         None for seeded synthetic weights (no trained checkpoint is available
@@ -48,7 +48,7 @@ class Predictor:
         return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype))
 
     @classmethod
-    def from_torchscript(cls, path: str, cfg: Optional[ModelConfig] = None, dtype: str = "fp16", device="cuda",
+    def from_torchscript(cls, path: str, cfg: Optional[ModelConfig] = None, dtype: str = "fp32", device="cuda",
                          **overrides) -> "Predictor":
         """An exported ``model.ts`` (M/model/predict.py:46-51, export
         M/model/deploy.py:77-121): its parameters, buffers and thresholds are

@@ -123,7 +123,7 @@ class MaskRCNN:
     """The reference model on one GPU behind the libmdx model handle
     (mdx_model_create / mdx_model_forward / mdx_model_destroy)."""
 
-    def __init__(self, cfg: ModelConfig, state_dict: Dict[str, torch.Tensor], device="cuda", dtype: str = "fp16"):
+    def __init__(self, cfg: ModelConfig, state_dict: Dict[str, torch.Tensor], device="cuda", dtype: str = "fp32"):
         if not torch.cuda.is_available():
             raise MdxError("MaskRCNN needs an AMD GPU; there is no CPU fallback")
         if dtype not in _DT:

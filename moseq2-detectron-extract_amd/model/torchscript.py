@@ -88,7 +88,7 @@ class _Unpickler(pickle.Unpickler):
         if module == "collections" and name == "OrderedDict":
             return OrderedDict
         if module == "torch.jit._pickle" and name in ("build_intlist", "build_tensorlist", "build_doublelist",
-                                                       "build_boollist", "build_intlist", "restore_type_tag"):
+                                                       "build_boollist", "restore_type_tag"):
             return _identity
         raise pickle.UnpicklingError(f"TorchScript import: refusing global {module}.{name}")
 
@@ -96,7 +96,9 @@ class _Unpickler(pickle.Unpickler):
         if not (isinstance(pid, tuple) and len(pid) >= 5 and pid[0] == "storage"):
             raise pickle.UnpicklingError(f"TorchScript import: unexpected persistent id {pid!r}")
         stype, key, _loc, numel = pid[1], str(pid[2]), pid[3], int(pid[4])
-        dtype = stype.dtype if isinstance(stype, _StorageType) else torch.float32
+        if not isinstance(stype, _StorageType):
+            raise pickle.UnpicklingError(f"TorchScript import: storage of unknown type {stype!r}")
+        dtype = stype.dtype
         if key not in self.storages:
             raw = self.zf.read(f"{self.prefix}data/{key}")
             itemsize = torch.empty((), dtype=dtype).element_size()

@@ -426,18 +426,30 @@ class OverlappedExtractor:
         return out
 
     def prime(self, raw: torch.Tensor):
-        """One batch through the whole path on every stream of the pipeline,
-        one stream at a time, synchronised: kernel code objects are loaded,
-        each model stream's workspace is reserved (mdx_model_reserve on first
-        use) and the allocator's per-stream pools are populated before any
-        two stages run concurrently."""
+        """One batch through each stage on that stage's stream, one stream at
+        a time, synchronised: kernel code objects are loaded, each model
+        stream's workspace is reserved (mdx_model_reserve on first use) and
+        the allocator's per-stream pools are populated before any two stages
+        run concurrently.  Only the model streams run a forward, so only they
+        get a model workspace."""
         cur = torch.cuda.current_stream()
         for st in (self.s_front, *self.s_models, self.s_tail):
             st.wait_stream(cur)
+        with torch.cuda.stream(self.s_front):
+            raw.record_stream(self.s_front)
+            prepped, cleaned = self.ex.front(raw)
+        torch.cuda.synchronize()
+        inf = None
+        for st in self.s_models:
             with torch.cuda.stream(st):
-                raw.record_stream(st)
-                self.ex.step_device(raw)
+                prepped.record_stream(st)
+                inf = self.ex.infer(prepped)
             torch.cuda.synchronize()
+        with torch.cuda.stream(self.s_tail):
+            for t in (prepped, cleaned, *[v for v in inf.values() if torch.is_tensor(v)]):
+                t.record_stream(self.s_tail)
+            self.ex.tail(prepped, cleaned, inf)
+        torch.cuda.synchronize()
 
     def submit(self, raw: torch.Tensor):
         # issue order: tail of the oldest modeled batch (once `depth` forwards

@@ -149,3 +149,21 @@ def test_flips_native_matches_numpy(F):
     f2, c2 = FR.flips_ref(kp, cen, ang, ln)
     np.testing.assert_array_equal(f1, f2)
     np.testing.assert_array_equal(c1, c2)
+
+
+def test_iterative_filter_angles_wide_window(F):
+    """Windows above the native loop's 8 (and 2-D input) take the numpy
+    statement of the same loop: equal to the checker."""
+    from oracle import features_ref as FR
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        n = int(rng.integers(1, 150))
+        a = rng.uniform(0, 360, n)
+        a[rng.random(n) < 0.3] += 180
+        if trial % 3 == 0:
+            a[rng.integers(0, n)] = np.nan
+        for w in (9, 15):
+            o1, f1 = F.iterative_filter_angles(a, w, 60, 50)
+            o2, f2 = FR.iterative_filter_angles_ref(a, w, 60, 50)
+            np.testing.assert_array_equal(o1, o2)
+            np.testing.assert_array_equal(f1, f2)

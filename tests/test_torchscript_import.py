@@ -11,37 +11,7 @@ import zipfile
 import pytest
 import torch
 
-
-class Node(torch.nn.Module):
-    def __init__(self):
-        super().__init__()
-
-
-class Adapter(torch.nn.Module):
-    def __init__(self, sd, scalars):
-        super().__init__()
-        root = Node()
-        self.add_module("model", root)
-        for k, v in sd.items():
-            parts = k.split(".")
-            m = root
-            for p in parts[:-1]:
-                if p not in m._modules:
-                    m.add_module(p, Node())
-                m = m._modules[p]
-            if k.endswith(("running_mean", "running_var")) or k.startswith("pixel"):
-                m.register_buffer(parts[-1], v.clone())
-            else:
-                m.register_parameter(parts[-1], torch.nn.Parameter(v.clone(), requires_grad=False))
-        for k, v in scalars.items():
-            parts = k.split(".")
-            m = root
-            for p in parts[:-1]:
-                m = m._modules[p]
-            setattr(m, parts[-1], v)
-
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return x
+from _ts_archive import write_archive
 
 
 @pytest.fixture(scope="module")
@@ -51,8 +21,7 @@ def archive(tmp_path_factory, mdx):
     sd = synthetic_state_dict(cfg, 5)
     scalars = {"roi_heads.box_predictor.test_score_thresh": 0.25, "roi_heads.box_predictor.test_topk_per_image": 3,
                "roi_heads.box_predictor.test_nms_thresh": 0.45}
-    path = str(tmp_path_factory.mktemp("ts") / "model.ts")
-    torch.jit.save(torch.jit.script(Adapter(sd, scalars)), path)
+    path = write_archive(tmp_path_factory.mktemp("ts") / "model.ts", sd, scalars)
     return path, sd
 
 
