@@ -24,6 +24,16 @@ secondary.fp16: the same loop with the fp16 MFMA forward (BASELINE config 5's
          precision), reported beside the fp32 headline, never as `value`.
 secondary.fp32_bf16x6: the same loop with the fp32 layers as exact bf16
          plane products (mdx_conv_set_fp32_split(6)).
+secondary.extract_loop: BASELINE config 3 -- extract.extract_session over a
+         10k-frame synthetic session written as depth.dat (chunks of 1000,
+         tracking on, fp32): frame source, device path, instance selection,
+         the native Kalman / flip angle step, scalars, keypoint tables, crops
+         and the result writers (results + keypoints TSV), frames / wall time.
+roofline: the MFMA kernel with the most GPU time per serial step (HIP events
+         around every conv launch; a Winograd layer's batched GEMM counts
+         under the kernel it runs on, at its executed FLOPs), the other top
+         kernels beside it, and frame_ops: the frame kernels' algorithmic HBM
+         bytes / their HIP-event time vs 8 TB/s (+ PMC bytes from profiles/).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
         (N>1 via torch.distributed.run, one process per GPU)
@@ -60,6 +70,9 @@ def parse():
                     help="skip the secondary fp32 loop on the split-plane kernels (mdx_conv_set_fp32_split(6))")
     ap.add_argument("--no-h2d", action="store_true", help="raw batches already resident in HBM (no H2D in the loop)")
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
+    ap.add_argument("--no-extract-loop", action="store_true", help="skip the config-3 extract-loop secondary")
+    ap.add_argument("--extract-frames", type=int, default=10000)
+    ap.add_argument("--extract-chunk", type=int, default=1000)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run batches back to back on one stream (one forward at a time)")
@@ -108,20 +121,34 @@ KERNEL_DEMANGLED = {
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
-                6: "Winograd F(2x2,3x3) (input transform + 16 batched k_conv GEMMs + output transform)",
                 7: "k_conv_x3<128> fp32 as bf16 plane products", 8: "k_conv_x3<64> fp32 as bf16 plane products",
                 9: "k_gemm_x6 256x256 LDS-DMA GEMM over bf16 planes (fp32 split, two plane products per MFMA)",
-                10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance"}
+                10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance",
+                12: "k_wino_in Winograd input transform", 13: "k_wino_out Winograd output transform"}
+KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
+                               12: "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf",
+                               13: "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf"})
+KERNEL_DEMANGLED.update({
+    "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE": "void mdx::k_conv1x1_stream_f32<4>(mdx::ConvArgs)",
+    "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf": "void mdx::k_wino_in<4>(float const*, int, int, int, int, int, int, float*)",
+    "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf":
+        "void mdx::k_wino_out<4>(float const*, int, int, int, int, int, int, float const*, int, float*)"})
+TRANSFORMS = (12, 13)  # records whose "flop" field holds algorithmic HBM bytes
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
-PMC_FILE = {"fp16": "r01_pmc_kernels.json", "fp32": "r02_pmc_kernels_fp32.json"}
+HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
+PMC_FILE = {"fp16": "r01_pmc_kernels.json", "fp32": "r03_pmc_kernels_fp32.json"}
+# frame kernels per stage (rocprofv3 symbol substrings) for the PMC bytes
+FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k_morph"),
+                 "moments": ("k_moments",), "crop": ("k_crop",)}
 
 
 def conv_roofline(extractor, raw, steps=3, dump=None):
     """Time every conv launch of `steps` serial steps with HIP events on the
     launch stream (mdx_model_profile: events recorded by the model handle
-    around each mdx_conv2d launch) and tag it with the kernel the library
-    chose.  Returns {kernel id: [algorithmic FLOP, seconds, launches, ksplit]}
-    per step."""
+    around each mdx_conv2d launch; a Winograd layer as its input transform,
+    batched GEMM and output transform) and tag it with the kernel the library
+    chose.  Returns {kernel id: [FLOP (executed; HBM bytes for the
+    transforms), seconds, launches, ksplit]} per step."""
     import torch
     model = extractor.predictor.model
     rec = []
@@ -149,41 +176,160 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
     return per
 
 
-def roofline_line(per, dtype):
-    """Roofline object for the dominant conv kernel (most time per step)."""
+def _pmc(dtype):
+    path = os.path.join(ROOT, "profiles", PMC_FILE[dtype])
+    try:
+        with open(path) as fh:
+            return json.load(fh)["kernels"]
+    except Exception:
+        return {}
+
+
+def _pmc_bytes(kern, sym):
+    rec = kern.get(sym) or kern.get(KERNEL_DEMANGLED.get(sym, ""), {})
+    return rec.get("hbm_bytes_per_launch")
+
+
+def roofline_line(per, dtype, model_flop_per_step):
+    """Roofline object for the dominant MFMA kernel: the one with the most GPU
+    time per serial step (a Winograd layer's batched GEMM counts under the
+    kernel it ran on, at its executed FLOPs).  `kernels` lists the top
+    kernels by time; the transforms are HBM-bound and listed in GB/s."""
+    from moseq2_detectron_extract_amd._lib import call
     peak = PEAK[dtype]
-    # a single kernel: the Winograd records (6) bracket three kernels and count
-    # direct-convolution FLOPs, so they are reported separately below
-    key = max((k for k in per if k != 6), key=lambda k: per[k][1])
+    kern = _pmc(dtype)
+    mfma = [k for k in per if k not in TRANSFORMS]
+    ranked = sorted(per, key=lambda k: -per[k][1])
+    key = max(mfma, key=lambda k: per[k][1])
     fl, sec, n, ks = per[key]
     ach = fl / sec / 1e12
-    traffic = None
     sym = KERNEL_SYMBOLS[dtype].get(key)
-    pmc = os.path.join(ROOT, "profiles", PMC_FILE[dtype])
-    if sym and os.path.exists(pmc):
-        try:
-            with open(pmc) as fh:
-                kern = json.load(fh)["kernels"]
-                rec = kern.get(sym) or kern.get(KERNEL_DEMANGLED.get(sym, ""), {})
-                traffic = rec.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    from moseq2_detectron_extract_amd._lib import call
-    wino_m = call("mdx_conv_winograd_enabled")
-    tot_f = sum(v[0] for v in per.values())
+    traffic = _pmc_bytes(kern, sym) if sym else None
+
+    def row(k):
+        f, t, c, _ = per[k]
+        r = {"kernel": KERNEL_NAMES.get(k, str(k)), "symbol": KERNEL_SYMBOLS[dtype].get(k),
+             "launches_per_step": round(c), "ms_per_step": round(t * 1e3, 3)}
+        if k in TRANSFORMS:
+            r.update(gbytes_per_step=round(f / 1e9, 3), achieved_gbs=round(f / t / 1e9, 1),
+                     frac_hbm=round(f / t / 1e9 / HBM_PEAK, 4))
+        else:
+            r.update(tflop_per_step=round(f / 1e12, 4), achieved_tflops=round(f / t / 1e12, 2),
+                     frac=round(f / t / 1e12 / peak, 4))
+        pb = _pmc_bytes(kern, r["symbol"]) if r["symbol"] else None
+        if pb is not None:
+            r["pmc_hbm_bytes_per_launch"] = round(pb)
+        return r
+
+    mf = sum(v[0] for k, v in per.items() if k not in TRANSFORMS)
     tot_s = sum(v[1] for v in per.values())
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
-            "kernel": f"{KERNEL_NAMES.get(key, key)} ({sym}): {n:.0f} launches/step, "
-                      f"{fl / n / 1e9:.1f} GFLOP and {sec / n * 1e6:.1f} us per launch (HIP events on the launch "
-                      f"stream, serial steps; traffic = PMC HBM bytes per launch, profiles/{PMC_FILE[dtype]})",
-            "all_conv": {"launches": round(sum(v[2] for v in per.values())), "tflop_per_step": round(tot_f / 1e12, 3),
-                         "ms_per_step": round(tot_s * 1e3, 3), "achieved": round(tot_f / tot_s / 1e12, 1),
-                         "note": "direct-convolution FLOPs; the Winograd layers' GEMMs execute 1/2.25 (F(2x2,3x3)) or 1/4 (F(4x4,3x3)) of them"},
-            **({"winograd": {"tile": wino_m, "layers_per_step": round(per[6][2]), "ms_per_step": round(per[6][1] * 1e3, 3),
-                             "direct_tflop_per_step": round(per[6][0] / 1e12, 3),
-                             "gemm_tflop_per_step_approx": round(per[6][0] / (2.25 if wino_m == 2 else 4.0) / 1e12, 3)}}
-               if 6 in per else {})}
+            "kernel": f"{KERNEL_NAMES.get(key, key)} ({sym}): {n:.0f} launches/step, {fl / 1e12:.3f} executed "
+                      f"TFLOP and {sec * 1e3:.3f} ms per step (HIP events on the launch stream, serial steps; "
+                      f"achieved = executed FLOP / time; traffic = PMC HBM bytes per launch, profiles/{PMC_FILE[dtype]})",
+            "kernels": [row(k) for k in ranked[:6]],
+            "all_conv": {"launches": round(sum(v[2] for k, v in per.items() if k not in TRANSFORMS)),
+                         "ms_per_step": round(tot_s * 1e3, 3),
+                         "executed_tflop_per_step": round(mf / 1e12, 3),
+                         "executed_tflops": round(mf / tot_s / 1e12, 1),
+                         "model_tflop_per_step": round(model_flop_per_step / 1e12, 3),
+                         "direct_equivalent_tflops": round(model_flop_per_step / tot_s / 1e12, 1),
+                         "note": "time = every conv launch incl. the Winograd transforms; executed = the FLOPs the "
+                                 "MFMA kernels perform (the Winograd GEMMs do 1/4 of the direct 3x3 FLOPs); "
+                                 "direct_equivalent = the model's algorithmic FLOPs (direct convolution, heads "
+                                 "included) over the same time, which can exceed the peak"},
+            "winograd_tile": call("mdx_conv_winograd_enabled")}
+
+
+def frame_ops_line(ex, raw, steps=5):
+    """HBM roofline of the frame kernels: each stage of the frame path timed
+    with HIP events on the issuing stream over `steps` repetitions on one
+    batch; algorithmic bytes per frame as SURVEY.md §8(d) counts them."""
+    import torch
+    from moseq2_detectron_extract_amd import proc
+    B, H, W = raw.shape
+    prepped, cleaned = ex.front(raw)
+    inf = ex.infer(prepped)
+    feats = proc.frame_moments(cleaned, inf["d2_mask"], float(ex.cfg.frame_threshold))
+    ang = torch.remainder(-torch.rad2deg(feats["orientation"]), 360)
+    ch, cw = ex.cfg.crop_size
+    px = prepped.shape[1] * prepped.shape[2]
+    stages = {
+        "prep_inpaint": (lambda: ex.prep(raw), 2 * H * W + px),
+        "clean": (lambda: proc.clean_frames(prepped, iters_tail=ex.cfg.iters_tail, strel_tail=ex.strel), 2 * px),
+        "moments": (lambda: proc.frame_moments(cleaned, inf["d2_mask"], float(ex.cfg.frame_threshold)), 2 * px),
+        "crop": (lambda: ex.crop(prepped, inf["d2_mask"], feats["centroid"], ang), 2 * 2 * ch * cw),
+    }
+    kern = _pmc("fp32")
+    out, tb, tt = {}, 0.0, 0.0
+    for name, (fn, bpf) in stages.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e-3 / steps
+        by = bpf * B
+        tb += by
+        tt += t
+        r = {"us_per_batch": round(t * 1e6, 1), "algorithmic_bytes_per_frame": bpf,
+             "achieved_gbs": round(by / t / 1e9, 1), "frac_hbm": round(by / t / 1e9 / HBM_PEAK, 4)}
+        pm = [v["hbm_bytes_per_launch"] * v["launches_per_step"] for k, v in kern.items()
+              if any(sub in k for sub in FRAME_KERNELS[name])]
+        if pm:
+            r["pmc_hbm_bytes_per_batch"] = round(sum(pm))
+        out[name] = r
+    out["total"] = {"us_per_batch": round(tt * 1e6, 1), "algorithmic_bytes_per_frame": round(tb / B),
+                    "achieved_gbs": round(tb / tt / 1e9, 1), "frac_hbm": round(tb / tt / 1e9 / HBM_PEAK, 4),
+                    "note": f"B={B}; HIP events on the issuing stream, serial; algorithmic bytes per SURVEY.md "
+                            f"section 8(d); pmc = FETCH_SIZE x2 + WRITE_SIZE per batch (profiles/{PMC_FILE['fp32']})"}
+    return out
+
+
+def extract_loop(args):
+    """BASELINE config 3: extract.extract_session over a synthetic session
+    written as depth.dat (frame source -> device path -> instance selection ->
+    native Kalman / flip step -> scalars, keypoint tables, crops -> result
+    writers), fp32, tracking on.  Disk write of the session is outside the
+    timed region; reading it is inside."""
+    import tempfile
+    import torch
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.extract import extract_session
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig
+    n, chunk = args.extract_frames, args.extract_chunk
+    workers = max(1, min(16, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", 16))))
+    s = synth.SyntheticSession(n, seed=9)
+    pred = Predictor.from_config(ModelConfig(depth=args.depth, score_thresh_test=0.0))
+    cfg = ExtractConfig(chunk_size=chunk, use_tracking=True)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        t0 = time.perf_counter()
+        s.write(td, workers=workers)
+        write_s = time.perf_counter() - t0
+        path = os.path.join(td, "depth.dat")
+        # warm-up over the first chunk (plans, workspaces, allocator pools)
+        extract_session(path, s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth, frame_trim=(0, n - chunk))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = extract_session(path, s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
+                              output_dir=os.path.join(td, "out"))
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        written = sorted(os.listdir(os.path.join(td, "out")))
+    assert out["frames"].shape[0] == n
+    return {"value": round(n / dt, 2), "unit": "frames/s", "seconds": round(dt, 3), "dtype": pred.model.dtype,
+            "config": f"{n} frames, chunks of {chunk}, use_tracking=True, R{args.depth}-FPN, batch "
+                      f"{cfg.batch_size}, {cfg.model_streams} model streams",
+            "written": written, "session_write_s": round(write_s, 1),
+            "note": "extract.extract_session (M/extract.py:22-139 without its control plane): .dat reads (page "
+                    "cache), prep+inpaint, R-CNN forward, mask NMS, instance selection (norfair semantics), "
+                    "clean, moments, native Kalman/flip angle step (host thread beside the next chunk's device "
+                    "pass), scalars, keypoint tables, crops, results + keypoints TSV writers"}
 
 
 def cpu_baseline(nframes: int, dtype_cfg, chunk: int = 16):
@@ -394,7 +540,8 @@ def main():
     if not args.no_roofline:
         raw_dev = raw_host[0].cuda()
         per = conv_roofline(ex, raw_dev, dump=args.dump_convs)
-        roof = roofline_line(per, args.dtype)
+        roof = roofline_line(per, args.dtype, flops_per_image(cfg) * B)
+        roof["frame_ops"] = frame_ops_line(ex, raw_dev)
     del ex
     torch.cuda.synchronize()
 
@@ -424,6 +571,14 @@ def main():
                     "full-frame parity vs the fp32 oracle at least as close as the f32-MFMA kernels' "
                     "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6], DESIGN.md section 3)"}
         del exx
+
+    if world == 1 and not args.no_secondary and not args.no_extract_loop and args.dtype == "fp32":
+        torch.cuda.synchronize()
+        secondary = secondary or {}
+        try:
+            secondary["extract_loop"] = extract_loop(args)
+        except Exception as e:  # a secondary must never sink the bench line
+            secondary["extract_loop"] = {"value": None, "error": repr(e)[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

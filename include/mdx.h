@@ -292,7 +292,11 @@ enum {
     MDX_CONV_KERNEL_WINOGRAD = 6,
     MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
     MDX_CONV_KERNEL_X3_64 = 8,
-    MDX_CONV_KERNEL_X6DMA = 9   /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
+    MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
+    /* profile records only (mdx_model_profile_read): the Winograd layers'
+     * transforms; their GEMM is recorded under the kernel it ran on */
+    MDX_CONV_KERNEL_WINO_IN = 12,
+    MDX_CONV_KERNEL_WINO_OUT = 13
 };
 /* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
  * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256
@@ -604,7 +608,12 @@ int mdx_model_debug_arena(mdx_model_t model, mdx_stream_t stream, const char *na
  * launch; host-only bookkeeping, off by default).  read: after the stream
  * is synchronised, up to max records {kernel (MDX_CONV_KERNEL_*), ksplit, M,
  * N, K, algorithmic FLOP, milliseconds} of the last profiled forward; returns
- * the number written. */
+ * the number written.  A Winograd layer gives three records: its input
+ * transform (MDX_CONV_KERNEL_WINO_IN; M = tiles, N = Cin, K = (m+2)^2, flop =
+ * the transform's algorithmic HBM bytes), the batched GEMM under the kernel
+ * that ran it (M = (m+2)^2 * tiles, N = Cout, K = Cin, flop = its executed
+ * FLOP) and the output transform (MDX_CONV_KERNEL_WINO_OUT, bytes as for the
+ * input). */
 typedef struct mdx_conv_record {
     int kernel, ksplit;
     int64_t M, N, K;

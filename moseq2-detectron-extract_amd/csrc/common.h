@@ -43,4 +43,14 @@ inline hipStream_t as_stream(mdx_stream_t s) { return reinterpret_cast<hipStream
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Profiling hook of the model handle (mdx_model_profile): while set on the
+// calling thread, mdx_conv3x3_winograd records ev[0] / ev[1] around its input
+// transform, ev[2] / ev[3] around the batched GEMM and ev[4] / ev[5] around
+// the output transform, and stores the GEMM's MDX_CONV_KERNEL_* id.
+struct WinoProbe {
+    hipEvent_t ev[6];
+    int gemm_kernel;
+};
+void wino_probe(WinoProbe *p);
+
 }  // namespace mdx

@@ -2300,6 +2300,9 @@ extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, in
     return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
 }
 
+static thread_local WinoProbe *t_wino_probe = nullptr;
+void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
+
 extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias,
                                     int Cout, int relu, int m, float *out, void *workspace, int64_t workspace_bytes,
                                     mdx_stream_t stream) {
@@ -2319,6 +2322,11 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     hipStream_t s = as_stream(stream);
     float *V = reinterpret_cast<float *>(workspace);
     float *Mx = V + NB * T * Cin;
+    WinoProbe *probe = t_wino_probe;
+    auto mark = [&](int i) {
+        if (probe) (void)hipEventRecord(probe->ev[i], s);
+    };
+    mark(0);
     {
         const long long items = T * Cin;
         const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
@@ -2327,6 +2335,9 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         else
             hipLaunchKernelGGL(k_wino_in<4>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
     }
+    mark(1);
+    mark(2);
+    int gemm_kernel;
     // NB GEMMs M[xi] (T x Cout) = V[xi] (T x Cin) U[xi]^T in one launch (grid.z)
     ConvArgs a{};
     a.x = V; a.w = U; a.bias = nullptr; a.res = nullptr; a.out = Mx;
@@ -2359,12 +2370,19 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         a.ksteps = Cin / 16;  // 16-float substeps
         hipLaunchKernelGGL((k_convg<float, float, 8, false>), dim3((unsigned)t256, 1, (unsigned)NB), dim3(G_THREADS),
                            G_LDS, s, a);
-    } else if (g_fp32_split)
+        gemm_kernel = MDX_CONV_KERNEL_DMA256;
+    } else if (g_fp32_split) {
         launch_x3(a, bn, grid, s);
-    else if (bn == 64)
+        gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
+    } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
-    else
+        gemm_kernel = MDX_CONV_KERNEL_REG64;
+    } else {
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
+        gemm_kernel = MDX_CONV_KERNEL_REG128;
+    }
+    mark(3);
+    mark(4);
     {
         const long long items = T * Cout;
         const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
@@ -2373,6 +2391,8 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         else
             hipLaunchKernelGGL(k_wino_out<4>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
     }
+    mark(5);
+    if (probe) probe->gemm_kernel = gemm_kernel;
     t_plan_kernel = MDX_CONV_KERNEL_WINOGRAD;
     t_plan_ksplit = 1;
     MDX_CHECK_LAUNCH("mdx_conv3x3_winograd");

@@ -559,7 +559,11 @@ struct Fwd {
         void *planes = x6 && !in_planes ? alloc((size_t)mdx_x6_plane_bytes((int64_t)N * H * W, cw.cin)) : nullptr;
         if (c.dry || !ok()) return out;
         ProfEv *pe = nullptr;
-        if (m.profile) {
+        WinoProbe probe{};
+        if (m.profile && wino) {
+            for (auto &e : probe.ev) (void)hipEventCreate(&e);
+            wino_probe(&probe);
+        } else if (m.profile) {
             c.prof.emplace_back();
             pe = &c.prof.back();
             (void)hipEventCreate(&pe->e0);
@@ -571,10 +575,27 @@ struct Fwd {
             if (!in_planes) chk(mdx_split_x6((const float *)x, rows, cw.cin, cw.cin, planes, s));
             chk(mdx_gemm_x6(in_planes ? x : planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
                             (float *)out, s));
-        } else if (wino)
+        } else if (wino) {
             chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
                                      (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
-        else
+            if (m.profile) {
+                wino_probe(nullptr);
+                // three records: input transform, batched GEMM, output transform
+                const int64_t A = wm + 2, T = (int64_t)N * ((H + wm - 1) / wm) * ((W + wm - 1) / wm);
+                const double px = (double)N * H * W;
+                const mdx_conv_record rs[3] = {
+                    {MDX_CONV_KERNEL_WINO_IN, 1, T, cw.cin, A * A, 4.0 * (px + (double)A * A * T) * cw.cin, 0.0},
+                    {probe.gemm_kernel, 1, A * A * T, cw.cout, cw.cin, 2.0 * (double)A * A * T * cw.cout * cw.cin, 0.0},
+                    {MDX_CONV_KERNEL_WINO_OUT, 1, T, cw.cout, A * A, 4.0 * ((double)A * A * T + px) * cw.cout, 0.0}};
+                for (int q = 0; q < 3; ++q) {
+                    c.prof.emplace_back();
+                    ProfEv &p = c.prof.back();
+                    p.e0 = probe.ev[2 * q];
+                    p.e1 = probe.ev[2 * q + 1];
+                    p.r = rs[q];
+                }
+            }
+        } else
             chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,
                                   relu ? 1 : 0, out_mode, m.dt, out_f32 ? 0 : m.dt, out, 0, splitk, SPLITK_WS, s));
         if (pe) {

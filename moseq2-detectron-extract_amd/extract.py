@@ -65,35 +65,48 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     if world > 1:  # contiguous block of whole chunks per rank, as shard.shard_chunks deals them
         c0, c1 = shard_chunk_range(len(batches), world, rank)
         batches = batches[c0:c1]
+    # the results file and keypoints TSV are written chunk by chunk as chunks
+    # finish (ResultWriterStep, its own process in the reference)
+    writer = _ChunkWriter(output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}"), src, bground_im,
+                          roi, true_depth, config, first_frame, status) if output_dir else None
+
+    def finished(d):
+        if writer is not None:
+            writer.write(d)
+        return _lighten(d)
+
     parts = []
     if exchange is None:  # two passes around the exchange step (needs torch.distributed initialised)
         exchange = world > 1 and (config.use_tracking or config.select_instances)
-    if exchange:
-        states = []
-        for idx, raw in src.iterate(device=True, batches=batches):
-            st, host = ex.features_pass(raw)
-            states.append((np.asarray(idx), st, host))
-        if config.select_instances:  # the instance tracker is sequential over the session too
-            _select_exchange(ex, states)
-        if config.use_tracking:
-            tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
-        else:  # per-chunk angle filtering: no sequential state across chunks
-            tracked = [ex.host_angles(h) for _, _, h in states]
-        for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
-            parts.append(_lighten(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)))
-        states.clear()
-    elif config.overlap_host:
-        parts = _run_overlapped(src, batches, ex, true_depth)
-    else:
-        for idx, raw in src.iterate(device=True, batches=batches):
-            parts.append(_lighten(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
-    src.close()
-    out: Dict[str, np.ndarray] = {}
+    try:
+        if exchange:
+            states = []
+            for idx, raw in src.iterate(device=True, batches=batches):
+                st, host = ex.features_pass(raw)
+                states.append((np.asarray(idx), st, host))
+            if config.select_instances:  # the instance tracker is sequential over the session too
+                _select_exchange(ex, states)
+            if config.use_tracking:
+                tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
+            else:  # per-chunk angle filtering: no sequential state across chunks
+                tracked = [ex.host_angles(h) for _, _, h in states]
+            for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
+                parts.append(finished(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0,
+                                                      true_depth)))
+            states.clear()
+        elif config.overlap_host:
+            parts = _run_overlapped(src, batches, ex, true_depth, finished)
+        else:
+            for idx, raw in src.iterate(device=True, batches=batches):
+                parts.append(finished(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
+    finally:
+        src.close()
+        if writer is not None:
+            writer.close()
     if output_dir:
-        _write_outputs(output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}"), parts, src, bground_im,
-                       roi, true_depth, config, first_frame, status)
         status["complete"] = True  # M/extract.py:129-131
         write_status(status_path, status)
+    out: Dict[str, np.ndarray] = {}
     if not parts:
         return out
     out["frame_idxs"] = np.concatenate([p["frame_idxs"] for p in parts])
@@ -130,27 +143,31 @@ def _load_metadata(path: str) -> dict:
     return {}
 
 
-def _write_outputs(output_dir, parts, src, bground_im, roi, true_depth, config, first_frame, status):
-    """results_00.h5 (or .npz without h5py) + keypoints_00.tsv, as
-    ResultWriterStep writes them (M/pipeline/write_results_step.py)."""
-    os.makedirs(output_dir, exist_ok=True)
-    ts_file = os.path.join(os.path.dirname(os.path.abspath(src.path)), "depth_ts.txt")
-    nframes = src.last_frame_idx
-    ts = np.loadtxt(ts_file)[:nframes] if os.path.exists(ts_file) else np.arange(nframes) * (1000 / 30)
-    cfg = {"nframes": nframes, "crop_size": config.crop_size, "frame_dtype": "uint8", "timestamps": ts,
-           "flip_classifier": "keypoints", "true_depth": true_depth, "roi": roi,
-           "first_frame": first_frame if first_frame is not None else src.read([0])[0], "bground_im": bground_im}
-    status = status or {"uuid": str(uuid.uuid4()), "parameters": {k: v for k, v in vars(config).items()},
-                        "metadata": {}}
-    h5 = open_results(output_dir)
-    tsv = KeypointsTSVWriter(output_dir)
-    try:
-        create_extract_h5(h5, cfg, status)
-        for d in parts:
-            write_extracted_chunk_to_h5(h5, d)
-            tsv.write(d)
-    finally:
-        h5.close()
+class _ChunkWriter:
+    """ResultWriterStep (M/pipeline/write_results_step.py:24-73): results_00.h5
+    (or .npz without h5py) + keypoints_00.tsv, the datasets created up front
+    (create_extract_h5) and filled chunk by chunk."""
+
+    def __init__(self, output_dir, src, bground_im, roi, true_depth, config, first_frame, status):
+        os.makedirs(output_dir, exist_ok=True)
+        ts_file = os.path.join(os.path.dirname(os.path.abspath(src.path)), "depth_ts.txt")
+        nframes = src.last_frame_idx
+        ts = np.loadtxt(ts_file)[:nframes] if os.path.exists(ts_file) else np.arange(nframes) * (1000 / 30)
+        cfg = {"nframes": nframes, "crop_size": config.crop_size, "frame_dtype": "uint8", "timestamps": ts,
+               "flip_classifier": "keypoints", "true_depth": true_depth, "roi": roi,
+               "first_frame": first_frame if first_frame is not None else src.read([0])[0], "bground_im": bground_im}
+        status = status or {"uuid": str(uuid.uuid4()), "parameters": {k: v for k, v in vars(config).items()},
+                            "metadata": {}}
+        self.h5 = open_results(output_dir)
+        self.tsv = KeypointsTSVWriter(output_dir)
+        create_extract_h5(self.h5, cfg, status)
+
+    def write(self, d: dict) -> None:
+        write_extracted_chunk_to_h5(self.h5, d)
+        self.tsv.write(d)
+
+    def close(self) -> None:
+        self.h5.close()
 
 
 def _select_exchange(ex, states):
@@ -190,12 +207,13 @@ def _lighten(d: dict) -> dict:
     return d
 
 
-def _run_overlapped(src, batches, ex, true_depth):
+def _run_overlapped(src, batches, ex, true_depth, finished=None):
     """Chunk loop with the host step off the critical path: the calling thread
     runs each chunk's device pass (prep, model, clean, moments) and hands it
     to a worker thread, which runs the sequential host step (angles / Kalman
     tracking, in chunk order) and the small device tail (scalars, keypoint z,
-    crops) on its own stream while the next chunk's device pass runs."""
+    crops) on its own stream while the next chunk's device pass runs, then
+    `finished` (the chunk writer) on the same thread."""
     import torch
     dev = torch.cuda.current_device()
     ctx = {}
@@ -221,7 +239,7 @@ def _run_overlapped(src, batches, ex, true_depth):
             ex.select_instances(st, host)
             cen, kp, ang, fl = ex.host_angles(host)
             d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
-        return _lighten(d)
+        return finished(d) if finished is not None else _lighten(d)
 
     return host_pipeline(produce(), consume, setup)
 

@@ -21,7 +21,10 @@ every chunk: O(n^2) in the session length); the file bytes are the same.
 """
 from __future__ import annotations
 
+import io
 import os
+import struct
+import zlib
 from typing import Dict, Optional
 
 import numpy as np
@@ -89,13 +92,94 @@ class MemoryH5:
 
     def close(self):
         if self.path:
-            np.savez_compressed(self.path, **{k: v.data for k, v in self.datasets.items()})
+            save_npz(self.path, {k: v.data for k, v in self.datasets.items()})
+            self.path = None
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
+
+
+_PIECE = 8 << 20  # bytes per independently deflated piece
+_ZIP64_AT = 0xFFFFFFFF  # sizes / offsets from which a member needs zip64 records (tests lower it)
+
+
+def _deflate_pieces(data: memoryview, level: int, pool) -> list:
+    """Raw deflate of `data` as one stream made of independently compressed
+    pieces (every piece but the last ends on a sync flush, the last one
+    finishes the stream -- pigz's layout), compressed in parallel: zlib
+    releases the GIL while it works."""
+    cuts = list(range(0, len(data), _PIECE)) or [0]
+
+    def one(i):
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        a = cuts[i]
+        out = c.compress(data[a:a + _PIECE])
+        return out + c.flush(zlib.Z_FINISH if i == len(cuts) - 1 else zlib.Z_SYNC_FLUSH)
+
+    return list(pool.map(one, range(len(cuts))))
+
+
+def save_npz(path: str, arrays: Dict[str, np.ndarray], level: int = 4, workers: int = 0) -> None:
+    """np.savez_compressed's file (a zip of ``<key>.npy`` members, deflated;
+    np.load reads it) written with the members' deflate streams compressed
+    in parallel pieces.  Level 4 is h5py's gzip default, the reference's
+    dataset compression (M/io/result.py:36-61).  Zip64 records are written
+    when a size or offset needs them."""
+    import concurrent.futures as cf
+    if any(np.asarray(a).dtype.hasobject for a in arrays.values()):
+        np.savez_compressed(path, **arrays)  # object arrays need np.save's pickling
+        return
+    workers = workers or max(1, min(16, len(os.sched_getaffinity(0))))
+    M32 = 0xFFFFFFFF
+    central = []
+    with open(path, "wb") as fh, cf.ThreadPoolExecutor(workers) as pool:
+        for key, arr in arrays.items():
+            a = np.asarray(arr)
+            a = a if a.flags.c_contiguous else a.copy(order="C")  # (ascontiguousarray would make 0-d arrays 1-d)
+            hdr = io.BytesIO()
+            np.lib.format.write_array_header_1_0(hdr, np.lib.format.header_data_from_array_1_0(a))
+            head = hdr.getvalue()
+            body = memoryview(a.reshape(-1).view(np.uint8)) if a.size else memoryview(b"")
+            crc = zlib.crc32(body, zlib.crc32(head))
+            size = len(head) + len(body)
+            if size <= _PIECE:
+                pieces = _deflate_pieces(memoryview(head + bytes(body)), level, pool)
+            else:  # header, then the body's pieces: one deflate stream
+                c = zlib.compressobj(level, zlib.DEFLATED, -15)
+                pieces = [c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)] + _deflate_pieces(body, level, pool)
+            csize = sum(len(x) for x in pieces)
+            name = (key + ".npy").encode()
+            off = fh.tell()
+            z64 = size >= _ZIP64_AT or csize >= _ZIP64_AT or off >= _ZIP64_AT
+            extra = struct.pack("<HHQQ", 1, 16, size, csize) if z64 else b""
+            fh.write(struct.pack("<IHHHHHIIIHH", 0x04034B50, 45 if z64 else 20, 0, 8, 0, 0x21, crc,
+                                 M32 if z64 else csize, M32 if z64 else size, len(name), len(extra)))
+            fh.write(name)
+            fh.write(extra)
+            for x in pieces:
+                fh.write(x)
+            central.append((name, crc, size, csize, off))
+        cd_off = fh.tell()
+        for name, crc, size, csize, off in central:
+            z64 = size >= _ZIP64_AT or csize >= _ZIP64_AT or off >= _ZIP64_AT
+            extra = struct.pack("<HHQQQ", 1, 24, size, csize, off) if z64 else b""
+            fh.write(struct.pack("<IHHHHHHIIIHHHHHII", 0x02014B50, 45, 45 if z64 else 20, 0, 8, 0, 0x21, crc,
+                                 M32 if z64 else csize, M32 if z64 else size, len(name), len(extra), 0, 0, 0,
+                                 0o600 << 16, M32 if z64 else off))
+            fh.write(name)
+            fh.write(extra)
+        cd_size = fh.tell() - cd_off
+        n = len(central)
+        if cd_off >= _ZIP64_AT or n >= 0xFFFF:
+            z_off = fh.tell()
+            fh.write(struct.pack("<IQHHIIQQQQ", 0x06064B50, 44, 45, 45, 0, 0, n, n, cd_size, cd_off))
+            fh.write(struct.pack("<IIQI", 0x07064B50, 0, z_off, 1))
+            fh.write(struct.pack("<IHHHHIIH", 0x06054B50, 0, 0, 0xFFFF, 0xFFFF, M32, M32, 0))
+        else:
+            fh.write(struct.pack("<IHHHHIIH", 0x06054B50, 0, 0, n, n, cd_size, cd_off, 0))
 
 
 def open_results(output_dir: str, bg_roi_index: int = 0):

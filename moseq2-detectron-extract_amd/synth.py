@@ -59,27 +59,48 @@ def trajectory(n: int, seed: int = 0, cfg: SynthConfig = SynthConfig()):
 
 def render(idx: np.ndarray, pos: np.ndarray, head: np.ndarray, seed: int = 0,
            cfg: SynthConfig = SynthConfig()) -> np.ndarray:
-    """Render frames `idx` (absolute frame numbers) -> int16 (len(idx), H, W)."""
+    """Render frames `idx` (absolute frame numbers) -> int16 (len(idx), H, W).
+    The animal's height is evaluated only inside the square around its centre
+    that holds the body and tail (outside it the height is exactly 0), so a
+    frame costs its two noise draws plus a small patch."""
     bg = background(cfg)
     yy, xx = np.mgrid[0:cfg.height, 0:cfg.width].astype(np.float64)
+    reach = int(np.ceil(np.hypot(cfg.semi_major + cfg.tail_len, max(cfg.semi_minor, 1.0)))) + 2
     out = np.empty((len(idx), cfg.height, cfg.width), np.int16)
     for o, i in enumerate(idx):
         rng = np.random.default_rng([seed, int(i)])
         cx, cy = pos[o]
         th = head[o]
         c, s = np.cos(th), np.sin(th)
-        u = (xx - cx) * c + (yy - cy) * s
-        v = -(xx - cx) * s + (yy - cy) * c
-        r2 = (u / cfg.semi_major) ** 2 + (v / cfg.semi_minor) ** 2
-        height = np.where(r2 <= 1, cfg.dome_min + (cfg.dome_max - cfg.dome_min) * np.sqrt(np.clip(1 - r2, 0, 1)), 0)
-        tail = (u < -cfg.semi_major) & (u > -cfg.semi_major - cfg.tail_len) & (np.abs(v) <= 1.0)
-        height = np.where(tail, 8.0, height)
+        y0, y1 = max(0, int(np.floor(cy)) - reach), min(cfg.height, int(np.floor(cy)) + reach + 1)
+        x0, x1 = max(0, int(np.floor(cx)) - reach), min(cfg.width, int(np.floor(cx)) + reach + 1)
+        height = np.zeros(bg.shape)
+        if y0 < y1 and x0 < x1:
+            px, py = xx[y0:y1, x0:x1], yy[y0:y1, x0:x1]
+            u = (px - cx) * c + (py - cy) * s
+            v = -(px - cx) * s + (py - cy) * c
+            r2 = (u / cfg.semi_major) ** 2 + (v / cfg.semi_minor) ** 2
+            h = np.where(r2 <= 1, cfg.dome_min + (cfg.dome_max - cfg.dome_min) * np.sqrt(np.clip(1 - r2, 0, 1)), 0)
+            tail = (u < -cfg.semi_major) & (u > -cfg.semi_major - cfg.tail_len) & (np.abs(v) <= 1.0)
+            height[y0:y1, x0:x1] = np.where(tail, 8.0, h)
         depth = bg - height + rng.normal(0, cfg.noise_mm, size=bg.shape)
         d = np.round(depth).astype(np.int16)
         if cfg.invalid_p > 0:
             d[rng.random(bg.shape) < cfg.invalid_p] = 0
         out[o] = d
     return out
+
+
+def _render_to_file(args):
+    """Process-pool worker of SyntheticSession.write: frames [a, b) into the
+    memory-mapped depth.dat."""
+    path, nframes, a, b, pos, head, seed, cfg = args
+    mm = np.memmap(path, dtype="<i2", mode="r+", shape=(nframes, cfg.height, cfg.width))
+    for s in range(a, b, 100):
+        e = min(s + 100, b)
+        mm[s:e] = render(np.arange(s, e), pos[s - a:e - a], head[s - a:e - a], seed, cfg)
+    mm.flush()
+    return b - a
 
 
 class SyntheticSession:
@@ -108,12 +129,27 @@ class SyntheticSession:
             e = min(s + chunk_size, self.nframes)
             yield np.arange(s, e), self.frames(s, e)
 
-    def write(self, dirname: str):
-        """Write depth.dat (<i2), metadata.json, depth_ts.txt like a real session."""
+    def write(self, dirname: str, workers: int = 0):
+        """Write depth.dat (<i2), metadata.json, depth_ts.txt like a real session.
+        workers > 1 renders blocks of frames in that many processes (frames are
+        a pure function of (seed, index), so the file is the same)."""
         os.makedirs(dirname, exist_ok=True)
-        with open(os.path.join(dirname, "depth.dat"), "wb") as fh:
-            for _, ch in self.iterate(500):
-                fh.write(ch.astype("<i2").tobytes())
+        path = os.path.join(dirname, "depth.dat")
+        n = self.nframes
+        if workers > 1 and n > 200:
+            with open(path, "wb") as fh:
+                fh.truncate(n * self.cfg.height * self.cfg.width * 2)
+            step = -(-n // workers)
+            jobs = [(path, n, a, min(a + step, n), self.pos[a:a + step], self.head[a:a + step], self.seed, self.cfg)
+                    for a in range(0, n, step)]
+            import concurrent.futures as cf
+            import multiprocessing as mp
+            with cf.ProcessPoolExecutor(max_workers=len(jobs), mp_context=mp.get_context("fork")) as ex:
+                assert sum(ex.map(_render_to_file, jobs)) == n
+        else:
+            with open(path, "wb") as fh:
+                for _, ch in self.iterate(500):
+                    fh.write(ch.astype("<i2").tobytes())
         with open(os.path.join(dirname, "metadata.json"), "w") as fh:
             json.dump({"DepthResolution": [self.cfg.width, self.cfg.height], "SubjectName": "synthetic",
                        "SessionName": f"seed{self.seed}"}, fh)

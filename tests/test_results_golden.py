@@ -103,3 +103,27 @@ def test_status_yaml_roundtrip(tmp_path, RS):
         d = yaml.safe_load(fh)
     assert d["parameters"]["crop_size"] == [80, 80] and d["parameters"]["chunk_size"] == 1000
     assert d["metadata"]["DepthResolution"] == [512, 424]
+
+
+def test_save_npz_parallel_pieces_round_trip(tmp_path, monkeypatch):
+    """MemoryH5's writer (results.save_npz): members deflated in parallel
+    pieces form one valid deflate stream per member; np.load and zipfile's
+    CRC check read it back exactly, with and without zip64 records."""
+    import zipfile
+    from moseq2_detectron_extract_amd import results as RS
+    rng = np.random.default_rng(0)
+    fr = np.zeros((700, 80, 80), np.uint8)  # 4.5 MB: several pieces with a small piece size
+    fr[:, 20:60, 10:70] = rng.integers(0, 60, (700, 40, 60))
+    arrs = {"frames": fr, "frames_mask": fr > 20, "scalars/x": rng.random(700).astype("float32"),
+            "metadata/uuid": np.array("abc-def"), "empty": np.zeros((0, 3)), "k": np.array(3.5),
+            "f": np.asfortranarray(rng.random((5, 7)))}
+    monkeypatch.setattr(RS, "_PIECE", 1 << 20)
+    for lim in (0xFFFFFFFF, 1):
+        monkeypatch.setattr(RS, "_ZIP64_AT", lim)
+        p = str(tmp_path / f"r{lim}.npz")
+        RS.save_npz(p, arrs)
+        assert zipfile.ZipFile(p).testzip() is None
+        z = np.load(p)
+        assert sorted(z.files) == sorted(arrs)
+        for k, v in arrs.items():
+            assert z[k].dtype == v.dtype and z[k].shape == v.shape and np.array_equal(z[k], v), k
