@@ -61,6 +61,11 @@ int mdx_prep_frames(const int16_t *raw, int64_t n, int H, int W, const double *b
 int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W);
 int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W,
                    int radius, void *workspace, mdx_stream_t stream);
+/* Frames whose inpaint cluster labelling failed its convergence check (every
+ * label must be its own root before the labels index the cluster tables) since
+ * the last reset; such a frame is left un-inpainted.  Synchronous (reads a
+ * device counter); reset != 0 clears it.  Expected 0: tests assert it. */
+int mdx_inpaint_errors(int reset);
 
 /* scale_raw_frames(frames, vmin, vmax, 'uint8') as a 256-entry LUT built on
  * the host in float64 (M/proc/proc.py:214-234).  int_vmin != 0 reproduces

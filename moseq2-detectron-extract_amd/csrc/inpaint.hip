@@ -229,10 +229,13 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_compact(const uint8_t
     }
 }
 
+// frames whose label propagation ended unconverged (see k_inp_setup)
+__device__ unsigned int g_inp_errors = 0;
+
 __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *__restrict__ invalid, int H, int W,
                                                                  int range, int *__restrict__ ws, InpLayout L) {
     __shared__ int sh[INP_SETUP_THREADS];
-    __shared__ int s_flag[2];
+    __shared__ int s_flag[2], s_bad;
     const int tid = threadIdx.x;
     const long long f = blockIdx.x;
     int *base = ws + f * L.total;
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
     // read the cleared flag left the loop alone, its barriers then paired
     // with the other waves' loop barriers, and the label arrays were indexed
     // before they had converged.)
-    if (tid == 0) s_flag[0] = s_flag[1] = 0;
+    if (tid == 0) s_flag[0] = s_flag[1] = s_bad = 0;
     for (int iter = 0; iter < 1 << 20; ++iter) {
         __syncthreads();
         if (tid == 0) s_flag[(iter + 1) & 1] = 0;
@@ -304,6 +307,27 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
         if (changed) atomicOr(&s_flag[iter & 1], 1);
         __syncthreads();
         if (!s_flag[iter & 1]) break;
+    }
+    // converged labels are roots (lab[lab[k]] == lab[k]); the cluster phase
+    // below indexes fill[] / cnt[] by them, so a frame that left the loop
+    // unconverged is counted in g_inp_errors (mdx_inpaint_errors) and left
+    // un-inpainted instead of indexing with a stray label.  (Its own flag:
+    // a slow wave may still be reading s_flag as it leaves the loop.)
+    {
+        int bad = 0;
+        for (int k = tid; k < nin; k += INP_SETUP_THREADS) {
+            const int l = lab[k];
+            bad |= l < 0 || l > k || lab[l] != l;
+        }
+        if (bad) atomicOr(&s_bad, 1);
+        __syncthreads();
+        if (s_bad) {
+            if (tid == 0) {
+                hdr[0] = hdr[1] = 0;
+                atomicAdd(&g_inp_errors, 1u);
+            }
+            return;
+        }
     }
     // cluster ids for roots (lab[k] == k) in raster order, member counts, starts
     int ncl = 0;
@@ -512,6 +536,16 @@ __global__ __launch_bounds__(64 * MARCH_WAVES) void k_inp_march(uint8_t *__restr
 }  // namespace mdx
 
 using namespace mdx;
+
+extern "C" int mdx_inpaint_errors(int reset) {
+    unsigned int v = 0;
+    MDX_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_inp_errors), sizeof(v)));
+    if (reset) {
+        const unsigned int z = 0;
+        MDX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_inp_errors), &z, sizeof(z)));
+    }
+    return (int)v;
+}
 
 extern "C" int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W) {
     if (n <= 0 || H <= 0 || W <= 0) return 0;

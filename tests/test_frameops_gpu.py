@@ -154,9 +154,40 @@ def test_inpaint_dense_holes(mdx, p, seed):
     f = rng.integers(0, 100, size=(2, 90, 120), dtype=np.uint8)
     m = (rng.random(f.shape) < p).astype(np.uint8)
     m[1, 30:60, 40:90] = 1  # a big blob
+    from moseq2_detectron_extract_amd._lib import call
+    call("mdx_inpaint_errors", 1)
     got = proc.fill_invalid_pixels(f.copy(), m)
     want = O.inpaint_ns(f, m)
     np.testing.assert_array_equal(got, want)
+    assert call("mdx_inpaint_errors", 1) == 0
+
+
+def test_inpaint_long_chain_converges(mdx):
+    """One hole cluster shaped as a long serpentine chain (runs of single
+    invalid pixels 3 px apart, rows 6 px apart joined at alternating ends):
+    the min-label propagation needs many iterations to carry the first
+    pixel's label to the far end.  Every label must converge to its root
+    (mdx_inpaint_errors stays 0) and the result equals the serial oracle."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    from moseq2_detectron_extract_amd._lib import call
+    H, W = 211, 255
+    rng = np.random.default_rng(5)
+    f = rng.integers(0, 100, size=(2, H, W), dtype=np.uint8)
+    m = np.zeros((2, H, W), np.uint8)
+    rows = list(range(4, H - 4, 6))
+    for r, y in enumerate(rows):
+        m[0, y, 4:W - 4:3] = 1
+        if r + 1 < len(rows):  # connector down to the next row at alternating ends
+            x = W - 5 if r % 2 == 0 else 4
+            m[0, y:y + 7:3, x] = 1
+    # a second frame: the same chain reversed in raster order (labels must
+    # travel the other way)
+    m[1] = m[0][::-1, ::-1]
+    call("mdx_inpaint_errors", 1)
+    got = proc.fill_invalid_pixels(f.copy(), m)
+    assert call("mdx_inpaint_errors", 1) == 0
+    np.testing.assert_array_equal(got, O.inpaint_ns(f, m))
 
 
 def test_frame_scalars_matches_oracle(mdx):
