@@ -231,6 +231,10 @@ int mdx_conv_set_mfma_prio256(int on);
  * routes the other fp32 layers to the split-plane kernel (diagnostic).
  * Returns the old value. */
 int mdx_conv_set_dma_f32(int on);
+/* fp32 layers on the register-staged 128-wide tile (no split-K, NHWC output;
+ * the Winograd GEMMs too) on v_mfma_f32_32x32x2_f32 with the epilogue stored
+ * straight from the accumulators: 1 on, 0 off.  Returns the old value. */
+int mdx_conv_set_f32_mfma32(int on);
 /* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
  * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
  * the products accumulate in fp32.  9: all nine plane products (the exact
@@ -298,6 +302,7 @@ enum {
     MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
     MDX_CONV_KERNEL_X3_64 = 8,
     MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
+    MDX_CONV_KERNEL_M32 = 14,   /* fp32 on 32x32x2 f32 MFMAs, epilogue from the accumulators (mdx_conv_set_f32_mfma32) */
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

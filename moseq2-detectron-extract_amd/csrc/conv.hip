@@ -456,6 +456,200 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// fp32 implicit GEMM on v_mfma_f32_32x32x2_f32 with the epilogue straight from
+// the accumulators (mdx_conv_set_f32_mfma32).  Same tile (128 x 128, 4 waves
+// of 64 x 64 = 2 x 2 MFMA blocks of 32 x 32), K-steps, register-staged loads
+// and swizzled LDS image as k_conv<float, float, 128>.  Per 8-deep K chunk,
+// lane half h = lane >> 5 reads the 16-B piece 2 kk + h of its row (one
+// ds_read_b128) and supplies k = 4 h + e to MFMA e = 0..3: the same
+// permutation on both operands, so each output sums every k exactly once
+// (order: per accumulator e = 0..3 over the pairs {e, 4 + e}).  A 32 x 32
+// accumulator register holds 32 consecutive columns of two rows, so every
+// epilogue store is two 128-B row segments (full rate, no LDS image, no
+// barrier): bias / residual / ReLU per register.  No split-K, NHWC output.
+// ---------------------------------------------------------------------------
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
+    constexpr int BK = 32, BN_ = 128;
+    constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
+    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
+    constexpr int STAGE = A_TILE + B_TILE;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *As = smem;
+    char *Bs = smem + A_TILE;
+    if (gridDim.z > 1) {  // batch entry z of a batched GEMM
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN_;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    const int kc = tid & 7;
+    const int lrow = tid >> 3;
+    int a_iy0[4], a_ix0[4];
+    long long a_base[4];
+    bool a_ok[4];
+    const int ohw = a.OH * a.OW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int gm = m0 + lrow + 32 * i;
+        a_ok[i] = gm < a.M;
+        const int gmc = a_ok[i] ? gm : 0;
+        const int b = gmc / ohw, rem = gmc - b * ohw;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_iy0[i] = oy * a.stride - a.pad;
+        a_ix0[i] = ox * a.stride - a.pad;
+        a_base[i] = (long long)b * a.H * a.W * a.Cin;
+    }
+    int kglob = kc * 4;
+    int kci = kglob % a.Cin;
+    int kr = kglob / a.Cin;
+    int kkx = kr % a.KW, kky = kr / a.KW;
+    uint4 ra[2][4], rb[2][BLOADS];
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
+        const bool kok = kglob < a.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
+            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
+            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i) {
+            const int gn = n0 + lrow + 32 * i;
+            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * 4ll);
+            Bv[i] = __builtin_bit_cast(uint4,
+                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
+        }
+    };
+    auto advance_k = [&]() {
+        kglob += BK;
+        kci += BK;
+        while (kci >= a.Cin) {
+            kci -= a.Cin;
+            if (++kkx == a.KW) {
+                kkx = 0;
+                ++kky;
+            }
+        }
+    };
+    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;
+    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = A[i];
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i)
+            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
+    };
+
+    float16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = (a.K + BK - 1) / BK;
+    load_global(ra[0], rb[0]);
+    advance_k();
+    store_lds(0, ra[0], rb[0]);
+    if (nk > 1) {
+        load_global(ra[1], rb[1]);
+        advance_k();
+    }
+    __syncthreads();
+    // fragment rows r = 32 blk + (lane & 31); piece 2 kk + (lane >> 5) at
+    // its swizzled position ((r >> 1) & 7 == (lane & 31) >> 1 & 7)
+    const int rsw = ((lane & 31) >> 1) & 7;
+    auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
+                     const uint4 (&Bs_)[BLOADS]) {
+        const int cur = kt & 1;
+        if (kt + 2 < nk) {
+            load_global(Ai, Bi);
+            advance_k();
+        }
+        const char *Ab = As + cur * STAGE + (wm * 64 + (lane & 31)) * PITCH;
+        const char *Bb = Bs + cur * STAGE + (wn * 64 + (lane & 31)) * PITCH;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int koff = ((2 * kk + (lane >> 5)) ^ rsw) * 16;
+            float4v af[2], bf[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 32 * PITCH + koff);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
+        __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+        kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+        kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
+    }
+    if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+
+    // epilogue straight from the accumulators: register r of block (i, j)
+    // holds row 32 i + 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column 32 j +
+    // (lane & 31) of the wave tile
+    float *O = reinterpret_cast<float *>(a.out);
+    const float *RS = reinterpret_cast<const float *>(a.res);
+    const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int gn = n0 + wn * 64 + 32 * j + (lane & 31);
+        const bool nok = gn < a.Cout;
+        const float bv = (a.bias && nok) ? a.bias[gn] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            float rv[16];
+            if (RS) {
+                const __amdgpu_buffer_rsrc_t rr_d =
+                    __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes, 0x00020000);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
+                    const unsigned off = (gm < a.M && nok) ? (unsigned)(((long long)gm * a.Cout + gn) * 4ll) : OOB;
+                    rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_d, off, 0, 0));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
+                float v = acc[i][j][r] + bv;
+                if (RS) v += rv[r];
+                if (a.relu) v = v > 0.f ? v : 0.f;
+                if (gm < a.M && nok) O[(long long)gm * a.Cout + gn] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // fp32 GEMM on the bf16 matrix cores (the fp32 model's layers when
 // mdx_conv_set_fp32_split(6 | 9)).  Every fp32 operand is split into three
 // bf16 values x = hi + mid + lo (hi = RN(x), mid = RN(x - hi), lo = x - hi -
@@ -1830,6 +2024,14 @@ extern "C" int mdx_conv_set_dma_f32(int on) {
     g_dma_f32 = on;
     return old;
 }
+// fp32 register-staged layers (128-wide tile, no split-K, NHWC out) on the
+// 32x32x2 f32 MFMA kernel with the direct epilogue (k_conv_m32): 0 off, 1 on
+static int g_f32_m32 = 0;
+extern "C" int mdx_conv_set_f32_mfma32(int on) {
+    const int old = g_f32_m32;
+    g_f32_m32 = on;
+    return old;
+}
 // fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
 static int g_fp32_split = 0;
 extern "C" int mdx_conv_set_fp32_split(int mode) {
@@ -2173,6 +2375,13 @@ general:
             hipLaunchKernelGGL((k_conv_reduce<TO_>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), \
                                0, s, a);                                                                    \
     } while (0)
+    if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && !narrow && a.ksplit == 1 && out_mode == 0) {
+        hipLaunchKernelGGL(k_conv_m32, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
+        t_plan_kernel = MDX_CONV_KERNEL_M32;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
     if (in_dtype == 1 && out_dtype == 1)
         MDX_LAUNCH_CONV(_Float16, _Float16);
     else if (in_dtype == 1 && out_dtype == 0)
@@ -2377,6 +2586,9 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG64;
+    } else if (g_f32_m32) {
+        hipLaunchKernelGGL(k_conv_m32, grid, dim3(CONV_THREADS), lds_main, s, a);
+        gemm_kernel = MDX_CONV_KERNEL_M32;
     } else {
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG128;
