@@ -233,8 +233,14 @@ int mdx_conv_set_mfma_prio256(int on);
 int mdx_conv_set_dma_f32(int on);
 /* fp32 layers on the register-staged 128-wide tile (no split-K, NHWC output;
  * the Winograd GEMMs too) on v_mfma_f32_32x32x2_f32 with the epilogue stored
- * straight from the accumulators: 1 on, 0 off.  Returns the old value. */
+ * straight from the accumulators: 1 on, 2 on with the persistent form for the
+ * plain GEMMs (1x1 / stride 1 / unpadded layers, Winograd GEMMs: each
+ * workgroup streams the K-steps of several tiles, the next tile's loads in
+ * flight during the previous one's epilogue), 0 off.  Returns the old value. */
 int mdx_conv_set_f32_mfma32(int on);
+/* Persistent GEMM grid: about `slots` workgroups over all batch entries (a
+ * multiple of 8 per entry, default 512 = two per CU).  Returns the old value. */
+int mdx_conv_set_m32p_slots(int slots);
 /* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
  * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
  * the products accumulate in fp32.  9: all nine plane products (the exact

@@ -650,6 +650,172 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent form of k_conv_m32 for plain GEMMs (1x1 / stride 1 / no padding:
+// the Winograd GEMMs and the pointwise convs, A row m = pixel m).  Each
+// workgroup walks the tiles L = blockIdx.x + i * gridDim.x of its batch entry
+// (gridDim.x a multiple of 8: every tile stays on the XCD of its workgroup,
+// XCD-contiguous ranges as in k_conv) as one stream of K-steps, so the loads
+// of a tile's first two K-steps are in flight while the previous tile
+// finishes and stores its outputs: a short-K GEMM (K = 128..512: 4..16
+// K-steps) no longer pays the prologue latency once per tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(CONV_THREADS, 2) void k_gemm_m32p(ConvArgs a) {
+    constexpr int BK = 32, BN_ = 128;
+    constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
+    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
+    constexpr int STAGE = A_TILE + B_TILE;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *As = smem;
+    char *Bs = smem + A_TILE;
+    if (gridDim.z > 1) {
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
+    const int G = gridDim.x, ntl = a.tiles_total;
+    if ((int)blockIdx.x >= ntl) return;
+    const int nmine = (ntl - (int)blockIdx.x + G - 1) / G;
+    const int nk = (a.K + BK - 1) / BK;
+    const int total = nmine * nk;
+    auto tile_origin = [&](int i, int &m0, int &n0) {
+        const int L = (int)blockIdx.x + i * G;
+        const int q = ntl / 8, r = ntl % 8, xcd = L % 8;
+        const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+        const int tm = tile / a.tiles_n;
+        m0 = tm * BM;
+        n0 = (tile - tm * a.tiles_n) * BN_;
+    };
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int kc = tid & 7, lrow = tid >> 3;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    // load side: the K-step (ld_i, ld_kt) of this workgroup's stream
+    int ld_i = 0, ld_kt = 0, ld_m0, ld_n0;
+    tile_origin(0, ld_m0, ld_n0);
+    uint4 ra[2][4], rb[2][BLOADS];
+    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
+        const int kg = ld_kt * BK + kc * 4;
+        const bool kok = kg < a.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int gm = ld_m0 + lrow + 32 * i;
+            const unsigned off = (unsigned)(((long long)gm * a.K + kg) * 4ll);
+            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && gm < a.M) ? off : OOB, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i) {
+            const int gn = ld_n0 + lrow + 32 * i;
+            const unsigned off = (unsigned)(((long long)gn * a.K + kg) * 4ll);
+            Bv[i] = __builtin_bit_cast(uint4,
+                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
+        }
+        if (++ld_kt == nk) {
+            ld_kt = 0;
+            if (++ld_i < nmine) tile_origin(ld_i, ld_m0, ld_n0);
+        }
+    };
+    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;
+    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = A[i];
+#pragma unroll
+        for (int i = 0; i < BLOADS; ++i)
+            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
+    };
+    float16v acc[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    };
+    zero_acc();
+    // compute side: the tile being multiplied and its K-step
+    int cm_i = 0, cm_kt = 0, cm_m0, cm_n0;
+    tile_origin(0, cm_m0, cm_n0);
+    float *O = reinterpret_cast<float *>(a.out);
+    const float *RS = reinterpret_cast<const float *>(a.res);
+    auto epilogue = [&]() {
+        const int rbase = cm_m0 + wm * 64 + 4 * (lane >> 5);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int gn = cm_n0 + wn * 64 + 32 * j + (lane & 31);
+            const bool nok = gn < a.Cout;
+            const float bv = (a.bias && nok) ? a.bias[gn] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                float rv[16];
+                if (RS) {
+                    const __amdgpu_buffer_rsrc_t rr_d =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes, 0x00020000);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
+                        const unsigned off = (gm < a.M && nok) ? (unsigned)(((long long)gm * a.Cout + gn) * 4ll) : OOB;
+                        rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_d, off, 0, 0));
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
+                    float v = acc[i][j][r] + bv;
+                    if (RS) v += rv[r];
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                    if (gm < a.M && nok) O[(long long)gm * a.Cout + gn] = v;
+                }
+            }
+        }
+    };
+    load_global(ra[0], rb[0]);
+    store_lds(0, ra[0], rb[0]);
+    if (total > 1) load_global(ra[1], rb[1]);
+    __syncthreads();
+    const int rsw = ((lane & 31) >> 1) & 7;
+    auto kstep = [&](int q, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4], const uint4 (&Bs_)[BLOADS]) {
+        const int cur = q & 1;
+        if (q + 2 < total) load_global(Ai, Bi);
+        const char *Ab = As + cur * STAGE + (wm * 64 + (lane & 31)) * PITCH;
+        const char *Bb = Bs + cur * STAGE + (wn * 64 + (lane & 31)) * PITCH;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int koff = ((2 * kk + (lane >> 5)) ^ rsw) * 16;
+            float4v af[2], bf[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 32 * PITCH + koff);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (q + 1 < total) store_lds(cur ^ 1, As_, Bs_);
+        __syncthreads();
+        if (++cm_kt == nk) {  // the tile is complete: store it, start the next
+            epilogue();
+            zero_acc();
+            cm_kt = 0;
+            if (++cm_i < nmine) tile_origin(cm_i, cm_m0, cm_n0);
+        }
+    };
+    int q = 0;
+    for (; q + 1 < total; q += 2) {
+        kstep(q, ra[0], rb[0], ra[1], rb[1]);
+        kstep(q + 1, ra[1], rb[1], ra[0], rb[0]);
+    }
+    if (q < total) kstep(q, ra[0], rb[0], ra[1], rb[1]);
+}
+
+// ---------------------------------------------------------------------------
 // fp32 GEMM on the bf16 matrix cores (the fp32 model's layers when
 // mdx_conv_set_fp32_split(6 | 9)).  Every fp32 operand is split into three
 // bf16 values x = hi + mid + lo (hi = RN(x), mid = RN(x - hi), lo = x - hi -
@@ -2025,8 +2191,24 @@ extern "C" int mdx_conv_set_dma_f32(int on) {
     return old;
 }
 // fp32 register-staged layers (128-wide tile, no split-K, NHWC out) on the
-// 32x32x2 f32 MFMA kernel with the direct epilogue (k_conv_m32): 0 off, 1 on
+// 32x32x2 f32 MFMA kernel with the direct epilogue (k_conv_m32): 0 off, 1 on,
+// 2 on with the persistent form (k_gemm_m32p) for the plain GEMMs (1x1 /
+// stride 1 / no padding layers and the Winograd GEMMs)
 static int g_f32_m32 = 0;
+// persistent grid: workgroups per batch entry (a multiple of 8, at least 8),
+// about g_m32p_slots over all batch entries
+static int g_m32p_slots = 512;
+extern "C" int mdx_conv_set_m32p_slots(int slots) {
+    const int old = g_m32p_slots;
+    g_m32p_slots = slots;
+    return old;
+}
+static unsigned m32p_grid(int tiles, int nb) {
+    int g = (g_m32p_slots + nb - 1) / nb;
+    g = (g + 7) / 8 * 8;
+    if (g < 8) g = 8;
+    return (unsigned)(g < tiles ? g : tiles);
+}
 extern "C" int mdx_conv_set_f32_mfma32(int on) {
     const int old = g_f32_m32;
     g_f32_m32 = on;
@@ -2376,7 +2558,11 @@ general:
                                0, s, a);                                                                    \
     } while (0)
     if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && !narrow && a.ksplit == 1 && out_mode == 0) {
-        hipLaunchKernelGGL(k_conv_m32, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
+        if (g_f32_m32 == 2 && KH == 1 && KW == 1 && stride == 1 && pad == 0)
+            hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, 1)), dim3(CONV_THREADS),
+                               2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
+        else
+            hipLaunchKernelGGL(k_conv_m32, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
         t_plan_kernel = MDX_CONV_KERNEL_M32;
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");
@@ -2586,6 +2772,10 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG64;
+    } else if (g_f32_m32 == 2) {
+        hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, NB), 1, (unsigned)NB), dim3(CONV_THREADS),
+                           2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
+        gemm_kernel = MDX_CONV_KERNEL_M32;
     } else if (g_f32_m32) {
         hipLaunchKernelGGL(k_conv_m32, grid, dim3(CONV_THREADS), lds_main, s, a);
         gemm_kernel = MDX_CONV_KERNEL_M32;

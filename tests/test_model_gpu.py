@@ -741,7 +741,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1, -2], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-m32"])
+@pytest.mark.parametrize("split", [0, 6, -1, -2, -3], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-m32", "f32-m32p"])
 @pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
@@ -772,9 +772,9 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
         pytest.skip("the 256x256 LDS-DMA GEMM needs Cout % 256 == 0 and Cin % 32 == 0")
     old = call("mdx_conv_set_fp32_split", max(split, 0))
     # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it;
-    # -2: the 32x32x2 f32 MFMA kernel (mdx_conv_set_f32_mfma32)
+    # -2 / -3: the 32x32x2 f32 MFMA kernel / its persistent form (mdx_conv_set_f32_mfma32)
     old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
-    old_m32 = call("mdx_conv_set_f32_mfma32", 1 if split == -2 else 0)
+    old_m32 = call("mdx_conv_set_f32_mfma32", {-2: 1, -3: 2}.get(split, 0))
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
     finally:
@@ -789,8 +789,9 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     assert err < 1e-4, err
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["m32", "m32-persistent"])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_fp32_m32(mdx, case):
+def test_conv2d_fp32_m32(mdx, case, mode):
     """fp32 layers on the 32x32x2 f32 MFMA kernel with the epilogue straight
     from the accumulators (k_conv_m32, mdx_conv_set_f32_mfma32) against the
     fp64 convolution: the fp32 tolerance (1e-4 of the output scale); ragged M
@@ -810,7 +811,7 @@ def test_conv2d_fp32_m32(mdx, case):
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
     out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
-    olds = [call("mdx_conv_set_f32_mfma32", 1), call("mdx_conv_set_dma_f32", 0), call("mdx_conv_set_head_f32", 0),
+    olds = [call("mdx_conv_set_f32_mfma32", mode), call("mdx_conv_set_dma_f32", 0), call("mdx_conv_set_head_f32", 0),
             call("mdx_conv_set_stream1x1_f32", 0), call("mdx_conv_set_narrow_kmax", 0)]
     try:
         call("mdx_conv2d", P(x.cuda()), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p,
