@@ -241,6 +241,9 @@ int mdx_conv_set_f32_mfma32(int on);
 /* Persistent GEMM grid: about `slots` workgroups over all batch entries (a
  * multiple of 8 per entry, default 512 = two per CU).  Returns the old value. */
 int mdx_conv_set_m32p_slots(int slots);
+/* Winograd transforms on 4 consecutive channels per thread (16-B accesses): 1
+ * on, 0 off.  Returns the old value. */
+int mdx_conv_set_wino_vec(int on);
 /* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
  * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
  * the products accumulate in fp32.  9: all nine plane products (the exact

@@ -2143,6 +2143,142 @@ __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, 
     }
 }
 
+// The same transforms on 4 consecutive channels per thread (C % 4 == 0): one
+// 16-B load / store per tap and plane instead of four 4-B ones, so a wave
+// instruction moves 1 KB (the 4-B form issues 4x the memory instructions for
+// the same bytes).  Row transform first (BT d, one input column at a time),
+// then the column transform; the arithmetic per channel is the 4-B form's.
+template <int M>
+__global__ __launch_bounds__(256) void k_wino_in_v4(const float *__restrict__ x, int N, int H, int W, int C, int TH,
+                                                    int TW, float *__restrict__ V) {
+    constexpr int A = WinoT<M>::A;
+    const int C4 = C >> 2;
+    const long long T = (long long)N * TH * TW;
+    const long long total = T * C4;
+    const long long xs = T * C;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const long long t = idx / C4;
+        const int c = (int)(idx - t * C4) * 4;
+        const int tx = (int)(t % TW);
+        const long long r = t / TW;
+        const int ty = (int)(r % TH), n = (int)(r / TH);
+        const int y0 = M * ty - 1, x0 = M * tx - 1;
+        float4 tt[A][A];  // B^T d: tt[i][j] = sum_k BT(i,k) d[k][j]
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            const int xx = x0 + j;
+            float4 d[A];
+#pragma unroll
+            for (int k = 0; k < A; ++k) {
+                const int yy = y0 + k;
+                d[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                           ? *reinterpret_cast<const float4 *>(x + (((long long)n * H + yy) * W + xx) * C + c)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < A; ++i) {
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(i, k) != 0.f) {
+                        const float b = WinoT<M>::BT(i, k);
+                        acc.x = acc.x + b * d[k].x;
+                        acc.y = acc.y + b * d[k].y;
+                        acc.z = acc.z + b * d[k].z;
+                        acc.w = acc.w + b * d[k].w;
+                    }
+                tt[i][j] = acc;
+            }
+        }
+        float *vo = V + t * C + c;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(j, k) != 0.f) {
+                        const float b = WinoT<M>::BT(j, k);
+                        acc.x = acc.x + tt[i][k].x * b;
+                        acc.y = acc.y + tt[i][k].y * b;
+                        acc.z = acc.z + tt[i][k].z * b;
+                        acc.w = acc.w + tt[i][k].w * b;
+                    }
+                *reinterpret_cast<float4 *>(vo + (A * i + j) * xs) = acc;
+            }
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void k_wino_out_v4(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
+                                                     int TW, const float *__restrict__ bias, int relu,
+                                                     float *__restrict__ out) {
+    constexpr int A = WinoT<M>::A;
+    const int K4 = K >> 2;
+    const long long T = (long long)N * TH * TW;
+    const long long total = T * K4;
+    const long long xs = T * K;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const long long t = idx / K4;
+        const int k = (int)(idx - t * K4) * 4;
+        const int tx = (int)(t % TW);
+        const long long r = t / TW;
+        const int ty = (int)(r % TH), n = (int)(r / TH);
+        const float *mi = Mx + t * K + k;
+        float4 sa[M][A];  // A^T m, one column of m at a time
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            float4 m[A];
+#pragma unroll
+            for (int q = 0; q < A; ++q) m[q] = *reinterpret_cast<const float4 *>(mi + (A * q + j) * xs);
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int q = 0; q < A; ++q)
+                    if (WinoT<M>::AT(i, q) != 0.f) {
+                        const float b = WinoT<M>::AT(i, q);
+                        acc.x = acc.x + b * m[q].x;
+                        acc.y = acc.y + b * m[q].y;
+                        acc.z = acc.z + b * m[q].z;
+                        acc.w = acc.w + b * m[q].w;
+                    }
+                sa[i][j] = acc;
+            }
+        }
+        const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int oy = M * ty + i;
+            if (oy >= OH) continue;
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                const int ox = M * tx + j;
+                if (ox >= OW) continue;
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int q = 0; q < A; ++q)
+                    if (WinoT<M>::AT(j, q) != 0.f) {
+                        const float b = WinoT<M>::AT(j, q);
+                        acc.x = acc.x + sa[i][q].x * b;
+                        acc.y = acc.y + sa[i][q].y * b;
+                        acc.z = acc.z + sa[i][q].z * b;
+                        acc.w = acc.w + sa[i][q].w * b;
+                    }
+                float4 v = make_float4(acc.x + bv.x, acc.y + bv.y, acc.z + bv.z, acc.w + bv.w);
+                if (relu) {
+                    v.x = v.x > 0.f ? v.x : 0.f;
+                    v.y = v.y > 0.f ? v.y : 0.f;
+                    v.z = v.z > 0.f ? v.z : 0.f;
+                    v.w = v.w > 0.f ? v.w : 0.f;
+                }
+                *reinterpret_cast<float4 *>(out + (((long long)n * OH + oy) * OW + ox) * K + k) = v;
+            }
+        }
+    }
+}
+
 }  // namespace mdx
 
 using namespace mdx;
@@ -2695,6 +2831,14 @@ extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, in
     return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
 }
 
+// Winograd transforms on 4 channels per thread (k_wino_in_v4 / k_wino_out_v4): 0 off, 1 on
+static int g_wino_vec = 0;
+extern "C" int mdx_conv_set_wino_vec(int on) {
+    const int old = g_wino_vec;
+    g_wino_vec = on;
+    return old;
+}
+
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
@@ -2722,7 +2866,14 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         if (probe) (void)hipEventRecord(probe->ev[i], s);
     };
     mark(0);
-    {
+    if (g_wino_vec) {
+        const long long items = T * (Cin / 4);
+        const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
+        if (m == 2)
+            hipLaunchKernelGGL(k_wino_in_v4<2>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+        else
+            hipLaunchKernelGGL(k_wino_in_v4<4>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+    } else {
         const long long items = T * Cin;
         const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
         if (m == 2)
@@ -2785,7 +2936,16 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     }
     mark(3);
     mark(4);
-    {
+    if (g_wino_vec) {
+        const long long items = T * (Cout / 4);
+        const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
+        if (m == 2)
+            hipLaunchKernelGGL(k_wino_out_v4<2>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu,
+                               out);
+        else
+            hipLaunchKernelGGL(k_wino_out_v4<4>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu,
+                               out);
+    } else {
         const long long items = T * Cout;
         const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
         if (m == 2)

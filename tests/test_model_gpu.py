@@ -741,7 +741,8 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1, -2, -3], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-m32", "f32-m32p"])
+@pytest.mark.parametrize("split", [0, 6, -1, -2, -3, -4],
+                         ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-m32", "f32-m32p", "f32-vec-transforms"])
 @pytest.mark.parametrize("m", [2, 4])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
@@ -775,12 +776,14 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     # -2 / -3: the 32x32x2 f32 MFMA kernel / its persistent form (mdx_conv_set_f32_mfma32)
     old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
     old_m32 = call("mdx_conv_set_f32_mfma32", {-2: 1, -3: 2}.get(split, 0))
+    old_vec = call("mdx_conv_set_wino_vec", 1 if split == -4 else 0)
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
     finally:
         call("mdx_conv_set_fp32_split", old)
         call("mdx_conv_set_winograd_dma", old_dma, 384)
         call("mdx_conv_set_f32_mfma32", old_m32)
+        call("mdx_conv_set_wino_vec", old_vec)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
