@@ -1318,6 +1318,13 @@ __global__ __launch_bounds__(256) void k_roi_align_full(RoiLevels rl, const floa
 // ((7 gw + 1) vs 7 (gw + 1) columns; rounding again ~1 ulp).  Spans wider
 // than ROI_SPAN_FLOATS / C columns take the mode-4 loop.
 constexpr int ROI_RMAX = 8, ROI_PMAX = 16, ROI_SPAN_FLOATS = 8192;
+// WIN (mode 6): the ROI's whole sample window of a slice of ROI_SWIN_SG 16-B
+// channel groups is staged in LDS once (each map pixel read once from L2
+// instead of once per bin that touches it: ~2x fewer tap loads for the box
+// pooler's 2-px bins), then every bin reads its taps from LDS in mode 4's
+// order (same sums, bit for bit).  Windows above ROI_SWIN_BYTES per slice take
+// mode 4's loop.
+constexpr int ROI_SWIN_SG = 8, ROI_SWIN_BYTES = 32768;
 
 // x / c for the bin average with the ROI's reciprocal r = RN(1/c): q = RN(x r)
 // refined by one FMA residual step (Markstein), 3 VALU instead of the ~10 of
@@ -1330,7 +1337,7 @@ __device__ __forceinline__ float div_count(float x, float c, float r) {
     return __builtin_fmaf(e, r, q);
 }
 
-template <typename T, bool ROWS = false>
+template <typename T, bool ROWS = false, bool WIN = false>
 __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float *__restrict__ rois,
                                                        const int *__restrict__ counts, T *__restrict__ out) {
     constexpr int V = Vec16<T>::N;
@@ -1504,6 +1511,79 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
 #pragma unroll
                     for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
                     put(((long long)(ph * P + pw) * G + cg) * V, acc);
+                }
+                __syncthreads();
+            }
+            return;
+        }
+    }
+    if constexpr (WIN) {
+        __shared__ int s_win[4];
+        __shared__ __attribute__((aligned(16))) uint4 sW[ROI_SWIN_BYTES / 16];
+        if (threadIdx.x == 0) {
+            int y0 = 1 << 30, y1 = 0, x0 = 1 << 30, x1 = 0;
+            for (int q = 0; q < P; ++q) {
+                if (s_nr[q] > 0) {
+                    y0 = s_r0[q] < y0 ? s_r0[q] : y0;
+                    y1 = s_r0[q] + s_nr[q] > y1 ? s_r0[q] + s_nr[q] : y1;
+                }
+                if (s_nc[q] > 0) {
+                    x0 = s_c0[q] < x0 ? s_c0[q] : x0;
+                    x1 = s_c0[q] + s_nc[q] > x1 ? s_c0[q] + s_nc[q] : x1;
+                }
+            }
+            if (y0 > y1) y0 = y1 = 0;
+            if (x0 > x1) x0 = x1 = 0;
+            s_win[0] = y0;
+            s_win[1] = y1 - y0;
+            s_win[2] = x0;
+            s_win[3] = x1 - x0;
+        }
+        __syncthreads();
+        const int wy0 = s_win[0], wr = s_win[1], wx0 = s_win[2], wc = s_win[3];
+        constexpr int SG = ROI_SWIN_SG;
+        if (G % SG == 0 && (long long)wr * wc * SG * 16 <= ROI_SWIN_BYTES && gridDim.y == 1) {
+            const int npx = wr * wc, nst = npx * SG, nit = P * P * SG;
+            for (int sl = 0; sl < G; sl += SG) {
+                // stage the window's pixels of channel groups sl .. sl + SG
+                for (int it = threadIdx.x; it < nst; it += 256) {
+                    const int px = it / SG, cg = it - px * SG;
+                    const int y = px / wc, x = px - y * wc;
+                    sW[it] = *reinterpret_cast<const uint4 *>(f + ((long long)(wy0 + y) * g.W + (wx0 + x)) * C +
+                                                              (sl + cg) * V);
+                }
+                __syncthreads();
+                for (int it = threadIdx.x; it < nit; it += 256) {
+                    const int bin = it / SG, cg = it - bin * SG;
+                    const int ph = bin / P, pw = bin - ph * P;
+                    const int nr = s_nr[ph], nc = s_nc[pw];
+                    const uint4 *wp = sW + ((s_r0[ph] - wy0) * wc + (s_c0[pw] - wx0)) * SG + cg;
+                    float acc[V];
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+                    for (int j = 0; j < nr; j += 2) {
+                        const bool two = j + 1 < nr;
+                        const float a0 = s_A[ph][j], a1 = two ? s_A[ph][j + 1] : 0.f;
+                        const uint4 *rp0 = wp + j * wc * SG;
+                        const uint4 *rp1 = two ? rp0 + wc * SG : rp0;
+                        for (int kc = 0; kc < nc; kc += 4) {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int k = kc + u < nc ? kc + u : nc - 1;
+                                const uint4 r0 = rp0[k * SG], r1 = rp1[k * SG];
+                                const float bk = kc + u < nc ? s_B[pw][kc + u] : 0.f;
+                                const float w0 = a0 * bk, w1 = a1 * bk;
+                                const T *e0 = reinterpret_cast<const T *>(&r0);
+                                const T *e1 = reinterpret_cast<const T *>(&r1);
+#pragma unroll
+                                for (int i = 0; i < V; ++i)
+                                    acc[i] = __builtin_fmaf(w1, (float)e1[i], __builtin_fmaf(w0, (float)e0[i], acc[i]));
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
+                    put(((long long)bin * G + sl + cg) * V, acc);
                 }
                 __syncthreads();
             }
@@ -2157,21 +2237,30 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
     // dtype 2: fp32 features, output rows as bf16 planes (mdx_split_x6 layout,
     // the A operand of mdx_gemm_x6); separable kernels only
     rl.planes = dtype == 2;
-    MDX_REQUIRE(dtype != 2 || ((g_roi_mode == 4 || g_roi_mode == 5) && P <= ROI_PMAX && (P * P * C) % 16 == 0),
+    MDX_REQUIRE(dtype != 2 || ((g_roi_mode >= 4 && g_roi_mode <= 7) && P <= ROI_PMAX && (P * P * C) % 16 == 0),
                 "mdx_roi_align: plane output (dtype 2) needs the separable kernel and P*P*C %% 16 == 0");
     if (order_ws && g_roi_sorted) {
         hipLaunchKernelGGL(k_roi_order, dim3(R / per_image), dim3(256), 0, as_stream(stream), rl, rois, counts,
                            order_ws);
         rl.order = order_ws;
     }
-    if (g_roi_mode == 5 && P <= ROI_PMAX) {
+    if (((g_roi_mode == 6 && R >= 1024) || g_roi_mode == 7) && P <= ROI_PMAX) {
+        // the box pooler (mode 6; 7: any ROI count, tests): each ROI's sample
+        // window staged in LDS per channel slice
+        if (dtype == 1)
+            hipLaunchKernelGGL((k_roi_align_sep<_Float16, false, true>), dim3(R), dim3(256), 0, as_stream(stream), rl,
+                               rois, counts, (_Float16 *)out);
+        else
+            hipLaunchKernelGGL((k_roi_align_sep<float, false, true>), dim3(R), dim3(256), 0, as_stream(stream), rl,
+                               rois, counts, (float *)out);
+    } else if (g_roi_mode == 5 && P <= ROI_PMAX) {
         if (dtype == 1)
             hipLaunchKernelGGL((k_roi_align_sep<_Float16, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (_Float16 *)out);
         else
             hipLaunchKernelGGL((k_roi_align_sep<float, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (float *)out);
-    } else if (g_roi_mode == 4 && P <= ROI_PMAX) {
+    } else if ((g_roi_mode == 4 || g_roi_mode == 6) && P <= ROI_PMAX) {
         // few ROIs (mask / keypoint heads: B x D): split each ROI's items over
         // up to 4 workgroups so the grid covers the CUs
         const int split = R >= 1024 ? 1 : (R >= 512 ? 2 : 4);

@@ -333,8 +333,8 @@ def test_rpn_proposals_from_identical_heads(mdx, sliced):
 
 
 @pytest.mark.parametrize("ordered", [False, True], ids=["roi-order", "level-band-order"])
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True)])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 7])
+@pytest.mark.parametrize("C,half", [(16, False), (64, False), (64, True), (256, True), (256, False)])
 def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
@@ -376,7 +376,15 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
             call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
                  2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(ref), None)
             assert torch.equal(out, ref)
-        if not half and mode in (4, 5) and (49 * C) % 16 == 0:
+        if mode == 7:
+            # the LDS-window form sums the same taps in mode 4's order
+            ref4 = torch.empty_like(out)
+            call("mdx_roi_align_set_mode", 4)
+            call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
+                 2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(ref4), None)
+            call("mdx_roi_align_set_mode", mode)
+            assert torch.equal(out, ref4)
+        if not half and mode in (4, 5, 7) and (49 * C) % 16 == 0:
             # dtype 2: the same rows written as bf16 planes (fc1's split-plane
             # A operand); hi + mid + lo reconstructs every value exactly
             pl = torch.empty((B * per, 49 * C // 16, 3, 16), dtype=torch.bfloat16, device="cuda")

@@ -3,11 +3,12 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "m32 or inpaint or winograd" > $O/tE1.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "m32 or inpaint or winograd or roi_align" > $O/tE1.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py > $O/g32_base.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py f32_mfma32=1 > $O/g32_m32.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py f32_mfma32=2 > $O/g32_m32p.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py f32_mfma32=2 wino_vec=1 > $O/g32_m32pv.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py winograd_dma=2,0 > $O/g32_wdma.log 2>&1 && \
+timeout -k 10 200 python3 -u tools/roibench.py fp32 > $O/roi32.log 2>&1 && \
 timeout -k 10 300 python3 -u tools/determinism.py fp32 150 > $O/det32.log 2>&1 ; \
 timeout -k 10 300 python3 -u tools/determinism.py fp16 150 > $O/det16.log 2>&1 ; echo EXIT $?

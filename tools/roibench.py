@@ -14,7 +14,8 @@ def main():
     from moseq2_detectron_extract_amd import proc, synth
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     cfg = ModelConfig(score_thresh_test=0.0)
-    pred = Predictor.from_config(cfg, dtype="fp16", seed=0)
+    dt = sys.argv[1] if len(sys.argv) > 1 else "fp32"
+    pred = Predictor.from_config(cfg, dtype=dt, seed=0)
     m = pred.model
     sess = synth.SyntheticSession(32, seed=1000)
     raw = torch.from_numpy(sess.frames(0, 32)).cuda()
@@ -46,7 +47,7 @@ def main():
     from moseq2_detectron_extract_amd._lib import call
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     outs = {}
-    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4"), (4, "separable"), (5, "separable, row-shared")):
+    for mode, name in ((0, "slice+LDS window"), (1, "rows x1"), (2, "rows x2"), (3, "rows x4"), (4, "separable"), (5, "separable, row-shared"), (6, "separable, LDS window")):
         old = call("mdx_roi_align_set_mode", mode)
         for _ in range(2):
             out = orig(feats, props, pcount, R, P, *a, **k)
