@@ -12,3 +12,7 @@ timeout -k 10 200 python3 -u tools/gemm32bench.py winograd_dma=2,0 > $O/g32_wdma
 timeout -k 10 200 python3 -u tools/roibench.py fp32 > $O/roi32.log 2>&1 && \
 timeout -k 10 300 python3 -u tools/determinism.py fp32 150 > $O/det32.log 2>&1 ; \
 timeout -k 10 300 python3 -u tools/determinism.py fp16 150 > $O/det16.log 2>&1 ; echo EXIT $?
+MDX_LIB_VARIANT=pk timeout -k 10 300 python3 -u tools/determinism.py fp32 150 > $O/det32pk.log 2>&1 ; \
+MDX_LIB_VARIANT=pk timeout -k 10 300 python3 -u tools/determinism.py fp16 150 > $O/det16pk.log 2>&1 ; \
+timeout -k 10 300 python3 -u bench.py --steps 40 --no-secondary --no-cpu-baseline --no-roofline > $O/bE1_base.json 2>/dev/null ; \
+MDX_LIB_VARIANT=pk timeout -k 10 300 python3 -u bench.py --steps 40 --no-secondary --no-cpu-baseline --no-roofline > $O/bE1_pk.json 2>/dev/null ; echo EXIT2 $?
