@@ -59,6 +59,7 @@ class ExtractConfig:
     overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
+    pipelined: bool = True           # features_pass: batches staggered over streams (OverlappedExtractor)
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -112,6 +113,7 @@ class GPUExtractor:
         self._frames_seen = 0
         self._tail_dets = {}  # session frame -> (mask planes (D,h,w), keypoints (D,K,3), keep_idx row)
         self._streams = []
+        self._pipe = None     # OverlappedExtractor of the pipelined features pass
 
     def infer(self, prepped: torch.Tensor):
         """Model forward over a prepped chunk in batch_size slices
@@ -272,7 +274,8 @@ class GPUExtractor:
         ang = torch.where(ang < 0, 360 + ang, ang) % 360
         depth, mask = self.crop(prepped, inf["d2_mask"], feats["centroid"], ang)
         return {"depth_frames": depth, "mask_frames": mask, "centroid": feats["centroid"], "angle": ang,
-                "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"]}
+                "axis_length": feats["axis_length"], "keypoints": inf["sel_keypoints"], "ndet": inf["ndet"],
+                "orientation": feats["orientation"]}
 
     def features_pass(self, raw):
         """Device part of one chunk up to the sequential host step: prep
@@ -280,6 +283,8 @@ class GPUExtractor:
         (device state kept for finish_chunk, host per-frame features
         {centroid, orientation (rad), axis_length, keypoints (n,K,3)})."""
         raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+        if self.cfg.pipelined and raw.shape[0] > self.cfg.batch_size:
+            return self._features_pass_pipelined(raw)
         prepped = self.prep(raw)
         inf = self.infer(prepped)
         d2 = inf["d2_mask"]
@@ -290,6 +295,36 @@ class GPUExtractor:
         if self.cfg.select_instances:  # inputs of the host instance-selection step (select_instances)
             state["inf"] = {k: inf[k] for k in ("masks", "keypoints", "keep_idx", "sel_keypoints")}
             host["centers"] = inf["centers"].cpu().numpy()
+        return state, host
+
+    def _features_pass_pipelined(self, raw: torch.Tensor):
+        """features_pass with the chunk's batch_size slices staggered over the
+        streams of an OverlappedExtractor (front: prep + inpaint + clean,
+        forwards + mask selection on model_streams streams, tail: moments):
+        the frame stages of one slice run beside the forwards of the next
+        ones, as in the bench loop.  Same results as the serial pass (the
+        kernels and their inputs are the same; the streams only reorder)."""
+        B = self.cfg.batch_size
+        if self._pipe is None:
+            self._pipe = OverlappedExtractor(self, max(1, int(self.cfg.model_streams)), keep=True)
+            self._pipe.prime(raw[:B])
+        pipe = self._pipe
+        outs = []
+        for i in range(0, raw.shape[0], B):
+            r = pipe.submit(raw[i:i + B])
+            if r is not None:
+                outs.append(r)
+        outs.extend(pipe.flush())  # the current stream now waits for every stage
+        cat = lambda key: torch.cat([o[key] for o in outs])  # noqa: E731
+        icat = lambda key: torch.cat([o["inf"][key] for o in outs])  # noqa: E731
+        prepped, cleaned, d2 = cat("prepped"), cat("cleaned"), icat("d2_mask")
+        host = {"centroid": cat("centroid").cpu().numpy(), "orientation": cat("orientation").cpu().numpy(),
+                "axis_length": cat("axis_length").cpu().numpy(), "keypoints": icat("sel_keypoints").cpu().numpy()}
+        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": icat("nkeep").cpu().numpy()}
+        if self.cfg.select_instances:
+            state["inf"] = {"masks": [m for o in outs for m in o["inf"]["masks"]], "keypoints": icat("keypoints"),
+                            "keep_idx": icat("keep_idx"), "sel_keypoints": icat("sel_keypoints")}
+            host["centers"] = icat("centers").cpu().numpy()
         return state, host
 
     def finish_chunk(self, state: dict, centroid, keypoints, angles, flips, axis_length, frame_idxs=None,
@@ -366,8 +401,9 @@ class OverlappedExtractor:
     earlier (or None);
     flush() -> list of the results still in flight."""
 
-    def __init__(self, extractor: GPUExtractor, model_streams: int = 2):
+    def __init__(self, extractor: GPUExtractor, model_streams: int = 2, keep: bool = False):
         self.ex = extractor
+        self.keep = keep  # results also carry the batch's prepped / cleaned frames and forward outputs
         self.s_front = torch.cuda.Stream()
         self.s_models = [torch.cuda.Stream() for _ in range(max(1, model_streams))]
         self.n_model = 0
@@ -411,6 +447,10 @@ class OverlappedExtractor:
             ready.record(self.s_tail)
         for v in out.values():
             v.record_stream(caller)
+        if self.keep:
+            for t in (prepped, cleaned, *[v for v in inf.values() if torch.is_tensor(v)], *inf["masks"]):
+                t.record_stream(caller)
+            out["prepped"], out["cleaned"], out["inf"] = prepped, cleaned, inf
         # the caller's stream does NOT wait here: a wait queued on it would
         # hold back every later front (and through it the next forwards)
         # until this batch's tail is done; consumers wait on out["ready"]

@@ -634,6 +634,36 @@ def test_overlapped_extractor_matches_serial(mdx):
             torch.testing.assert_close(g[k], w[k], rtol=0, atol=0, equal_nan=True)
 
 
+def test_features_pass_pipelined_matches_serial(mdx):
+    """The extract loop's pipelined device pass (the chunk's batch_size slices
+    staggered over the OverlappedExtractor streams, ragged last slice) returns
+    exactly the serial pass's state and host features, instance-selection
+    inputs included."""
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    s = synth.SyntheticSession(75, seed=8)
+    raw = torch.from_numpy(s.frames(0, 75)).cuda()
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0))
+    got = {}
+    for piped in (False, True):
+        ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=16, pipelined=piped))
+        st, host = ex.features_pass(raw)
+        torch.cuda.synchronize()
+        got[piped] = (st, host)
+    (s0, h0), (s1, h1) = got[False], got[True]
+    for k in ("centroid", "orientation", "axis_length", "keypoints", "centers"):
+        np.testing.assert_array_equal(h1[k], h0[k], err_msg=k)
+    for k in ("prepped", "d2", "cleaned"):
+        assert torch.equal(s1[k], s0[k]), k
+    np.testing.assert_array_equal(s1["nkeep"], s0["nkeep"])
+    for k in ("keypoints", "keep_idx", "sel_keypoints"):
+        assert torch.equal(s1["inf"][k], s0["inf"][k]), k
+    m0 = torch.cat(s0["inf"]["masks"])
+    m1 = torch.cat(s1["inf"]["masks"])
+    assert torch.equal(m1, m0)
+
+
 @pytest.mark.parametrize("use_tracking", [False, True])
 def test_process_chunk_data_dict(mdx, use_tracking):
     """Full chunk through the device path (tracking off and on): the writer's
