@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "m32 or inpaint or winograd or roi_align" > $O/tE1.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "m32 or inpaint or winograd or roi_align or pipelined or overlapped or config3 or extract_session" > $O/tE1.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py > $O/g32_base.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py f32_mfma32=1 > $O/g32_m32.log 2>&1 && \
 timeout -k 10 200 python3 -u tools/gemm32bench.py f32_mfma32=2 > $O/g32_m32p.log 2>&1 && \
