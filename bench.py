@@ -50,9 +50,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # HIP hardware queues: HIP's default (4) unless the launcher sets one (recorded
 # in the line).  8 measured +2.7 % at fp16 and +0.6 % at fp32 with two model
-# streams, but 8 queues with three model streams ended in an illegal-address
-# fault that is not root-caused, so the bench does not
-# raise the count itself.
+# streams -- within run-to-run noise at fp32 -- so the bench does not raise
+# the count itself.  (The illegal-address faults once seen with 8 queues and
+# three model streams were the inpaint set-up race, fixed: DESIGN.md section 3.)
 
 
 def parse():
