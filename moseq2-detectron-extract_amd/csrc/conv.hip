@@ -470,8 +470,10 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 // ---------------------------------------------------------------------------
 typedef float float16v __attribute__((ext_vector_type(16)));
 
+template <int BN_>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
-    constexpr int BK = 32, BN_ = 128;
+    constexpr int BK = 32;
+    constexpr int NJ = BN_ / 64;  // 32-column MFMA blocks per wave
     constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
     constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
     constexpr int STAGE = A_TILE + B_TILE;
@@ -558,11 +560,11 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
             *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
     };
 
-    float16v acc[2][2];
+    float16v acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -586,13 +588,13 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
             advance_k();
         }
         const char *Ab = As + cur * STAGE + (wm * 64 + (lane & 31)) * PITCH;
-        const char *Bb = Bs + cur * STAGE + (wn * 64 + (lane & 31)) * PITCH;
+        const char *Bb = Bs + cur * STAGE + (wn * (BN_ / 2) + (lane & 31)) * PITCH;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const int koff = ((2 * kk + (lane >> 5)) ^ rsw) * 16;
-            float4v af[2], bf[2];
+            float4v af[2], bf[NJ];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
+            for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
 #pragma unroll
             for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 32 * PITCH + koff);
 #pragma unroll
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
@@ -620,8 +622,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
     const float *RS = reinterpret_cast<const float *>(a.res);
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int gn = n0 + wn * 64 + 32 * j + (lane & 31);
+    for (int j = 0; j < NJ; ++j) {
+        const int gn = n0 + wn * (BN_ / 2) + 32 * j + (lane & 31);
         const bool nok = gn < a.Cout;
         const float bv = (a.bias && nok) ? a.bias[gn] : 0.f;
 #pragma unroll
@@ -2693,12 +2695,19 @@ general:
             hipLaunchKernelGGL((k_conv_reduce<TO_>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), \
                                0, s, a);                                                                    \
     } while (0)
+    if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && narrow && a.ksplit == 1 && out_mode == 0) {
+        hipLaunchKernelGGL(k_conv_m32<64>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
+        t_plan_kernel = MDX_CONV_KERNEL_M32;
+        t_plan_ksplit = 1;
+        MDX_CHECK_LAUNCH("mdx_conv2d");
+        return MDX_OK;
+    }
     if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && !narrow && a.ksplit == 1 && out_mode == 0) {
         if (g_f32_m32 == 2 && KH == 1 && KW == 1 && stride == 1 && pad == 0)
             hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, 1)), dim3(CONV_THREADS),
                                2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
         else
-            hipLaunchKernelGGL(k_conv_m32, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
+            hipLaunchKernelGGL(k_conv_m32<128>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
         t_plan_kernel = MDX_CONV_KERNEL_M32;
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");
@@ -2920,6 +2929,9 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     } else if (g_fp32_split) {
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
+    } else if (bn == 64 && g_f32_m32) {
+        hipLaunchKernelGGL(k_conv_m32<64>, grid, dim3(CONV_THREADS), lds_main, s, a);
+        gemm_kernel = MDX_CONV_KERNEL_M32;
     } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG64;
@@ -2928,7 +2940,7 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
                            2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
         gemm_kernel = MDX_CONV_KERNEL_M32;
     } else if (g_f32_m32) {
-        hipLaunchKernelGGL(k_conv_m32, grid, dim3(CONV_THREADS), lds_main, s, a);
+        hipLaunchKernelGGL(k_conv_m32<128>, grid, dim3(CONV_THREADS), lds_main, s, a);
         gemm_kernel = MDX_CONV_KERNEL_M32;
     } else {
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);

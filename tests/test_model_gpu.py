@@ -836,7 +836,8 @@ def test_conv2d_fp32_m32(mdx, case, mode):
     """fp32 layers on the 32x32x2 f32 MFMA kernel with the epilogue straight
     from the accumulators (k_conv_m32, mdx_conv_set_f32_mfma32) against the
     fp64 convolution: the fp32 tolerance (1e-4 of the output scale); ragged M
-    and Cout exercise the masked stores, residual / ReLU the epilogue."""
+    and Cout exercise the masked stores, residual / ReLU the epilogue; Cout
+    <= 64 takes the 64-wide tile."""
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
@@ -863,8 +864,7 @@ def test_conv2d_fp32_m32(mdx, case, mode):
         for f, o in zip(("mdx_conv_set_f32_mfma32", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
                          "mdx_conv_set_stream1x1_f32", "mdx_conv_set_narrow_kmax"), olds):
             call(f, o)
-    if Cout > 64:
-        assert kid.value == 14
+    assert kid.value == 14
     got = out.cpu().double()
     err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
     assert err < 1e-4, err
