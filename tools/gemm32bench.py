@@ -33,6 +33,7 @@ WINO = [  # N, H, W, Cin, Cout, count
     (32, 14, 16, 512, 512, 3),     # res5 conv2
     (128, 14, 14, 256, 256, 4),    # mask head
     (128, 7, 7, 512, 512, 7),      # keypoint head
+    (32, 112, 128, 64, 64, 0),     # res2 conv2 (direct in the model: Cin < winograd_min_cin), for comparison
 ]
 
 
