@@ -46,7 +46,8 @@ def main():
         name, val = kv.split("=")
         call(f"mdx_conv_set_{name}", *[int(v) for v in val.split(",")])
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-    ws = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
+    need = max([call("mdx_winograd_workspace_bytes", N, H, W, Ci, Co, 4) for N, H, W, Ci, Co, _ in WINO] + [1 << 28])
+    ws = torch.empty(need, dtype=torch.uint8, device="cuda")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kid, ks = ctypes.c_int(), ctypes.c_int()
 
