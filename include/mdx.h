@@ -312,6 +312,8 @@ enum {
     MDX_CONV_KERNEL_X3_64 = 8,
     MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
     MDX_CONV_KERNEL_M32 = 14,   /* fp32 on 32x32x2 f32 MFMAs, epilogue from the accumulators (mdx_conv_set_f32_mfma32) */
+    MDX_CONV_KERNEL_M32P = 15,  /* its persistent GEMM form for 1x1 / Winograd GEMMs (mdx_conv_set_f32_mfma32(2)) */
+    MDX_CONV_KERNEL_M32_64 = 16, /* its 64-wide N tile (narrow layers) */
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

@@ -2697,18 +2697,20 @@ general:
     } while (0)
     if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && narrow && a.ksplit == 1 && out_mode == 0) {
         hipLaunchKernelGGL(k_conv_m32<64>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
-        t_plan_kernel = MDX_CONV_KERNEL_M32;
+        t_plan_kernel = MDX_CONV_KERNEL_M32_64;
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
     if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && !narrow && a.ksplit == 1 && out_mode == 0) {
-        if (g_f32_m32 == 2 && KH == 1 && KW == 1 && stride == 1 && pad == 0)
+        if (g_f32_m32 == 2 && KH == 1 && KW == 1 && stride == 1 && pad == 0) {
             hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, 1)), dim3(CONV_THREADS),
                                2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
-        else
+            t_plan_kernel = MDX_CONV_KERNEL_M32P;
+        } else {
             hipLaunchKernelGGL(k_conv_m32<128>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
-        t_plan_kernel = MDX_CONV_KERNEL_M32;
+            t_plan_kernel = MDX_CONV_KERNEL_M32;
+        }
         t_plan_ksplit = 1;
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
@@ -2931,14 +2933,14 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64 && g_f32_m32) {
         hipLaunchKernelGGL(k_conv_m32<64>, grid, dim3(CONV_THREADS), lds_main, s, a);
-        gemm_kernel = MDX_CONV_KERNEL_M32;
+        gemm_kernel = MDX_CONV_KERNEL_M32_64;
     } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG64;
     } else if (g_f32_m32 == 2) {
         hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, NB), 1, (unsigned)NB), dim3(CONV_THREADS),
                            2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
-        gemm_kernel = MDX_CONV_KERNEL_M32;
+        gemm_kernel = MDX_CONV_KERNEL_M32P;
     } else if (g_f32_m32) {
         hipLaunchKernelGGL(k_conv_m32<128>, grid, dim3(CONV_THREADS), lds_main, s, a);
         gemm_kernel = MDX_CONV_KERNEL_M32;
