@@ -253,50 +253,61 @@ def roofline_line(per, dtype, model_flop_per_step):
 
 def frame_ops_line(ex, raw, steps=5):
     """HBM roofline of the frame kernels: each stage of the frame path timed
-    with HIP events on the issuing stream over `steps` repetitions on one
-    batch; algorithmic bytes per frame as SURVEY.md §8(d) counts them."""
+    with HIP events on the issuing stream over `steps` repetitions, on one
+    batch (the pipelined loop's launch: one workgroup per frame, so a 32-frame
+    launch covers an eighth of the CUs) and on a 1024-frame chunk (the extract
+    loop's launch: the batch tiled 32 times); algorithmic bytes per frame as
+    SURVEY.md §8(d) counts them."""
     import torch
     from moseq2_detectron_extract_amd import proc
-    B, H, W = raw.shape
-    prepped, cleaned = ex.front(raw)
-    inf = ex.infer(prepped)
-    feats = proc.frame_moments(cleaned, inf["d2_mask"], float(ex.cfg.frame_threshold))
-    ang = torch.remainder(-torch.rad2deg(feats["orientation"]), 360)
-    ch, cw = ex.cfg.crop_size
-    px = prepped.shape[1] * prepped.shape[2]
-    stages = {
-        "prep_inpaint": (lambda: ex.prep(raw), 2 * H * W + px),
-        "clean": (lambda: proc.clean_frames(prepped, iters_tail=ex.cfg.iters_tail, strel_tail=ex.strel), 2 * px),
-        "moments": (lambda: proc.frame_moments(cleaned, inf["d2_mask"], float(ex.cfg.frame_threshold)), 2 * px),
-        "crop": (lambda: ex.crop(prepped, inf["d2_mask"], feats["centroid"], ang), 2 * 2 * ch * cw),
-    }
     kern = _pmc("fp32")
-    out, tb, tt = {}, 0.0, 0.0
-    for name, (fn, bpf) in stages.items():
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(steps):
+
+    def measure(raw_, reps):
+        B, H, W = raw_.shape
+        prepped, cleaned = ex.front(raw_)
+        d2 = torch.cat([ex.infer(prepped[i:i + 32])["d2_mask"] for i in range(0, B, 32)])
+        feats = proc.frame_moments(cleaned, d2, float(ex.cfg.frame_threshold))
+        ang = torch.remainder(-torch.rad2deg(feats["orientation"]), 360)
+        ch, cw = ex.cfg.crop_size
+        px = prepped.shape[1] * prepped.shape[2]
+        stages = {
+            "prep_inpaint": (lambda: ex.prep(raw_), 2 * H * W + px),
+            "clean": (lambda: proc.clean_frames(prepped, iters_tail=ex.cfg.iters_tail, strel_tail=ex.strel), 2 * px),
+            "moments": (lambda: proc.frame_moments(cleaned, d2, float(ex.cfg.frame_threshold)), 2 * px),
+            "crop": (lambda: ex.crop(prepped, d2, feats["centroid"], ang), 2 * 2 * ch * cw),
+        }
+        out, tb, tt = {}, 0.0, 0.0
+        for name, (fn, bpf) in stages.items():
             fn()
-        e1.record()
-        torch.cuda.synchronize()
-        t = e0.elapsed_time(e1) * 1e-3 / steps
-        by = bpf * B
-        tb += by
-        tt += t
-        r = {"us_per_batch": round(t * 1e6, 1), "algorithmic_bytes_per_frame": bpf,
-             "achieved_gbs": round(by / t / 1e9, 1), "frac_hbm": round(by / t / 1e9 / HBM_PEAK, 4)}
-        pm = [v["hbm_bytes_per_launch"] * v["launches_per_step"] for k, v in kern.items()
-              if any(sub in k for sub in FRAME_KERNELS[name])]
-        if pm:
-            r["pmc_hbm_bytes_per_batch"] = round(sum(pm))
-        out[name] = r
-    out["total"] = {"us_per_batch": round(tt * 1e6, 1), "algorithmic_bytes_per_frame": round(tb / B),
-                    "achieved_gbs": round(tb / tt / 1e9, 1), "frac_hbm": round(tb / tt / 1e9 / HBM_PEAK, 4),
-                    "note": f"B={B}; HIP events on the issuing stream, serial; algorithmic bytes per SURVEY.md "
-                            f"section 8(d); pmc = FETCH_SIZE x2 + WRITE_SIZE per batch (profiles/{PMC_FILE['fp32']})"}
-    return out
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) * 1e-3 / reps
+            by = bpf * B
+            tb += by
+            tt += t
+            r = {"us": round(t * 1e6, 1), "algorithmic_bytes_per_frame": bpf,
+                 "achieved_gbs": round(by / t / 1e9, 1), "frac_hbm": round(by / t / 1e9 / HBM_PEAK, 4)}
+            if B == 32:
+                pm = [v["hbm_bytes_per_launch"] * v["launches_per_step"] for k, v in kern.items()
+                      if any(sub in k for sub in FRAME_KERNELS[name])]
+                if pm:
+                    r["pmc_hbm_bytes"] = round(sum(pm))
+            out[name] = r
+        out["total"] = {"us": round(tt * 1e6, 1), "algorithmic_bytes_per_frame": round(tb / B),
+                        "achieved_gbs": round(tb / tt / 1e9, 1), "frac_hbm": round(tb / tt / 1e9 / HBM_PEAK, 4)}
+        return out
+
+    res = {"batch_32": measure(raw, steps), "chunk_1024": measure(raw.repeat(32, 1, 1), 2)}
+    res["note"] = ("HIP events on the issuing stream, serial; algorithmic bytes per SURVEY.md section 8(d); "
+                   f"pmc = FETCH_SIZE x2 + WRITE_SIZE per 32-frame batch (profiles/{PMC_FILE['fp32']}); the "
+                   "frame kernels are latency-bound (one workgroup per frame, inpaint / contour following "
+                   "sequential inside a frame), not HBM-bound")
+    return res
 
 
 def extract_loop(args):
