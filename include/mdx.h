@@ -347,6 +347,15 @@ int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
                       int in_dtype, int out_dtype, void *out, int ksplit, void *workspace,
                       int64_t workspace_bytes, mdx_stream_t stream);
+/* A ResNet bottleneck's conv3 and its projection shortcut as one GEMM
+ * (Detectron2 BottleneckBlock.forward: out = relu(conv3(h) + shortcut(x)),
+ * M/model/config.py:21-94 builds it): out = act(x . W[:, :Cin] +
+ * x2[:, ::stride2, ::stride2] . W[:, Cin:] + bias), x (N,H,W,Cin),
+ * x2 (N,H2,W2,Cin2), w [Cout][Cin + Cin2], both 1x1.  Cin and Cin2 multiples
+ * of 32 (fp32) / 64 (fp16); dtype 0 f32, 1 f16 (in = out). */
+int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, const void *x2, int H2, int W2, int Cin2,
+                    int stride2, const void *w, const float *bias, int Cout, int relu, int dtype, void *out,
+                    void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
 
 /* scale_raw_frames LUT + replicate 1->C channels + (x - mean[c]) / std[c] + zero
  * pad to (Hp, Wp) with Cp (>= C) channels.  frames uint8 (B,h,w). */
@@ -557,6 +566,10 @@ typedef void *mdx_model_t;
  * into the stem weights (2-channel s2d input, K 256 -> 128): 1 on (default),
  * 0 the 3-channel normalised input.  Returns the old value. */
 int mdx_model_set_stem_fold(int on);
+/* Handles created afterwards run each bottleneck's projection shortcut and
+ * conv3 as one GEMM (mdx_conv2d_dual): 0 off, 1 fp32 handles, 2 fp32 and fp16
+ * handles.  Returns the old value. */
+int mdx_model_set_fuse_shortcut(int mode);
 
 /* Weights blob: Detectron2 state-dict layout (parameter / buffer names of
  * GeneralizedRCNN, e.g. "backbone.bottom_up.res2.0.conv1.weight"), serialised

@@ -89,6 +89,11 @@ struct ConvArgs {
     int xbytes, wbytes;  // operand sizes for the range-checked buffer descriptors (< 2^31)
     int rbytes;          // residual size (bytes), same purpose
     long long bsx, bsw, bso;  // batched GEMMs (grid.z): byte strides of x, w, out per batch entry
+    // second A source (k_conv<..., DUAL>): K values [K1, K) of row m = (b, oy, ox)
+    // come from x2[b][oy * stride2][ox * stride2][k - K1] (a bottleneck's
+    // projection shortcut concatenated onto its conv3 GEMM)
+    const void *x2;
+    int K1, H2, W2, Cin2, stride2, x2bytes;
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -203,7 +208,7 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
 
 // BN_: N tile (128 or 64).  4 waves as 2x2; wave tile (BM/2) x (BN_/2) =
 // TI x TJ MFMA tiles of 16x16.
-template <typename T, typename TO, int BN_>
+template <typename T, typename TO, int BN_, bool DUAL = false>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -237,6 +242,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     const int lrow = tid >> 3;
     int a_iy0[4], a_ix0[4];
     long long a_base[4];
+    unsigned a2_off[DUAL ? 4 : 1];  // DUAL: byte offset of row i's pixel in x2
     bool a_ok[4];
     const int ohw = a.OH * a.OW;
 #pragma unroll
@@ -249,6 +255,10 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         a_iy0[i] = oy * a.stride - a.pad;
         a_ix0[i] = ox * a.stride - a.pad;
         a_base[i] = (long long)b * a.H * a.W * a.Cin;
+        if constexpr (DUAL)
+            a2_off[i] = a_ok[i] ? (unsigned)((((long long)b * a.H2 + (long long)oy * a.stride2) * a.W2 +
+                                              (long long)ox * a.stride2) * a.Cin2 * (long long)sizeof(T))
+                                : 0xFFFFFFF0u;
     }
     const int kz = blockIdx.y;
     int kglob = kz * a.ksteps * BK + kc * VEC;
@@ -269,13 +279,25 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     constexpr unsigned OOB = 0xFFFFFFF0u;
     auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
         const bool kok = kglob < a.K;
+        // (K1 is a multiple of BK: the whole K-step reads one source)
+        if (DUAL && kglob >= a.K1) {
+            const __amdgpu_buffer_rsrc_t rx2 =
+                __builtin_amdgcn_make_buffer_rsrc((void *)a.x2, (short)0, a.x2bytes, 0x00020000);
+            const unsigned kb = (unsigned)((kglob - a.K1) * (int)sizeof(T));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
-            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            const unsigned off =
-                (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * (long long)sizeof(T));
-            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+            for (int i = 0; i < (DUAL ? 4 : 0); ++i)
+                A[i] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rx2, (kok && a2_off[i] != OOB) ? a2_off[i] + kb : OOB,
+                                                                 0, 0));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
+                const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                const unsigned off =
+                    (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * (long long)sizeof(T));
+                A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+            }
         }
 #pragma unroll
         for (int i = 0; i < BLOADS; ++i) {
@@ -2769,6 +2791,75 @@ extern "C" int mdx_gemm_x6(const void *a_planes, const void *b_planes, const flo
     t_plan_kernel = MDX_CONV_KERNEL_X6DMA;
     t_plan_ksplit = 1;
     MDX_CHECK_LAUNCH("mdx_gemm_x6");
+    return MDX_OK;
+}
+
+// A bottleneck's conv3 (1x1 over x, N x H x W x Cin) and its projection
+// shortcut (1x1 / stride2 over x2, N x H2 x W2 x Cin2) as ONE GEMM over the
+// concatenated K = Cin + Cin2: out = act(x . W[:, :Cin] + x2_strided .
+// W[:, Cin:] + bias), w packed [Cout][Cin + Cin2], bias = b3 + b_sc.  Saves
+// the shortcut's output write and its re-read as the residual.
+extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, const void *x2, int H2, int W2, int Cin2,
+                               int stride2, const void *w, const float *bias, int Cout, int relu, int dtype, void *out,
+                               void *workspace, int64_t workspace_bytes, mdx_stream_t stream) {
+    MDX_REQUIRE(x && x2 && w && out, "mdx_conv2d_dual: null pointer");
+    MDX_REQUIRE(dtype == 0 || dtype == 1, "mdx_conv2d_dual: dtype must be 0 (f32) or 1 (f16)");
+    const int BKd = dtype == 1 ? 64 : 32;
+    MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0 && stride2 > 0 && Cin > 0 && Cin2 > 0,
+                "mdx_conv2d_dual: bad shape");
+    MDX_REQUIRE(Cin % BKd == 0 && Cin2 % BKd == 0,
+                "mdx_conv2d_dual: Cin=%d and Cin2=%d must be multiples of %d", Cin, Cin2, BKd);
+    MDX_REQUIRE((H - 1) * stride2 < H2 && (W - 1) * stride2 < W2, "mdx_conv2d_dual: x2 too small for the stride");
+    const long long es = dtype == 1 ? 2 : 4;
+    const long long M = (long long)N * H * W;
+    const long long xb = M * Cin * es, x2b = (long long)N * H2 * W2 * Cin2 * es, wb = (long long)Cout * (Cin + Cin2) * es;
+    MDX_REQUIRE(M < (1ll << 31) && xb < (1ll << 31) && x2b < (1ll << 31) && wb < (1ll << 31),
+                "mdx_conv2d_dual: operands above 2 GiB are not supported");
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.res = nullptr; a.out = out;
+    a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+    a.OH = H; a.OW = W;
+    a.M = (int)M;
+    a.K = Cin + Cin2;
+    a.xbytes = (int)xb;
+    a.wbytes = (int)wb;
+    a.relu = relu;
+    a.out_mode = 0;
+    a.x2 = x2; a.K1 = Cin; a.H2 = H2; a.W2 = W2; a.Cin2 = Cin2; a.stride2 = stride2; a.x2bytes = (int)x2b;
+    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax;
+    const int bn = narrow ? 64 : BN;
+    a.tiles_n = (int)ceil_div(Cout, bn);
+    a.tiles_total = (int)(ceil_div(M, BM) * a.tiles_n);
+    const int nk = (a.K + BKd - 1) / BKd;
+    int ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes) : 1;
+    ksplit = ksplit > nk ? nk : ksplit;
+    a.ksteps = (nk + ksplit - 1) / ksplit;
+    a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
+    a.part = reinterpret_cast<float *>(workspace);
+    const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
+    const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
+    const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+    hipStream_t s = as_stream(stream);
+    const dim3 grid(a.tiles_total, a.ksplit);
+    if (dtype == 0) {
+        if (narrow)
+            hipLaunchKernelGGL((k_conv<float, float, 64, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_conv<float, float, 128, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        if (a.ksplit > 1)
+            hipLaunchKernelGGL((k_conv_reduce<float>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0, s, a);
+    } else {
+        if (narrow)
+            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 64, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 128, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        if (a.ksplit > 1)
+            hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0,
+                               s, a);
+    }
+    t_plan_kernel = narrow ? MDX_CONV_KERNEL_REG64 : MDX_CONV_KERNEL_REG128;
+    t_plan_ksplit = a.ksplit;
+    MDX_CHECK_LAUNCH("mdx_conv2d_dual");
     return MDX_OK;
 }
 

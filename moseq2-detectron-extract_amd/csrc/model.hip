@@ -65,6 +65,9 @@ struct Block {
     int stage;
     bool has_sc;
     ConvW sc, c1, c2, c3;
+    // conv3 and the projection shortcut as one GEMM over K = Cin3 + Cin_sc
+    // (mdx_conv2d_dual; packed when mdx_model_set_fuse_shortcut is on)
+    ConvW c3sc;
 };
 
 struct TensorRec {
@@ -102,6 +105,7 @@ struct Model {
     int dev = 0;
     int dt = 0;        // 0 f32, 1 f16
     bool stem_fold = false;  // stem over the 2-channel (value, inside) s2d input (fp32 handles)
+    bool fuse_sc = false;    // projection shortcuts fused into conv3 (Block::c3sc)
     size_t es = 4;     // activation element size
     std::vector<void *> allocs;
     ConvW stem;
@@ -294,6 +298,36 @@ struct Packer {
         bn(p, (int)w->shape[0], s, b);
         return conv(w, s.data(), &b, stride, pad);
     }
+    // conv3 (1x1, Cin3 -> Cout) and shortcut (1x1 / stride s, Cin_sc -> Cout),
+    // both FrozenBN-folded, as one [Cout][Cin3 + Cin_sc] matrix, bias b3 + b_sc
+    ConvW conv3_shortcut(const std::string &p3, const std::string &psc, int stride) {
+        const HostT *w3 = get(p3 + ".weight"), *ws = get(psc + ".weight");
+        ConvW c;
+        if (!w3 || !ws) return c;
+        if (w3->shape.size() != 4 || ws->shape.size() != 4 || w3->shape[2] != 1 || w3->shape[3] != 1 ||
+            ws->shape[2] != 1 || ws->shape[3] != 1 || w3->shape[0] != ws->shape[0]) {
+            if (err.empty()) err = "conv3 / shortcut must be 1x1 convs with the same Cout";
+            return c;
+        }
+        const int co = (int)w3->shape[0], c3 = (int)w3->shape[1], cs = (int)ws->shape[1];
+        std::vector<float> s3, b3, ss, bs;
+        bn(p3, co, s3, b3);
+        bn(psc, co, ss, bs);
+        std::vector<float> pk((size_t)co * (c3 + cs)), b(co);
+        for (int o = 0; o < co; ++o) {
+            for (int i = 0; i < c3; ++i) pk[(size_t)o * (c3 + cs) + i] = w3->v[(size_t)o * c3 + i] * s3[o];
+            for (int i = 0; i < cs; ++i) pk[(size_t)o * (c3 + cs) + c3 + i] = ws->v[(size_t)o * cs + i] * ss[o];
+            b[o] = b3[o] + bs[o];
+        }
+        c.w = upload(pk, true);
+        c.b = upload_f32(b);
+        c.cin = c3;  // the first source's channels; cout, stride of the second
+        c.cout = co;
+        c.k = 1;
+        c.stride = stride;
+        c.kalg = cs;  // (here: the shortcut's Cin)
+        return c;
+    }
     ConvW conv_plain(const std::string &p, int stride, int pad, bool need_bias) {
         const HostT *w = get(p + ".weight");
         const HostT *b = need_bias ? get(p + ".bias") : (has(p + ".bias") ? get(p + ".bias") : nullptr);
@@ -403,6 +437,7 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
             blk.c1 = P.conv_bn(p + ".conv1", s1, 0);
             blk.c2 = P.conv_bn(p + ".conv2", s3, 1);
             blk.c3 = P.conv_bn(p + ".conv3", 1, 0);
+            if (blk.has_sc && m.fuse_sc) blk.c3sc = P.conv3_shortcut(p + ".conv3", p + ".shortcut", s);
             m.blocks.push_back(blk);
         }
     }
@@ -608,6 +643,29 @@ struct Fwd {
         }
         return out;
     }
+    // conv3 over x (N,H,W,Cin3) + the projection shortcut over x2 (N,H2,W2,Cin_sc), one GEMM
+    void *conv3_shortcut(const void *x, int N, int H, int W, const void *x2, int H2, int W2, const ConvW &cw) {
+        void *out = alloc((size_t)N * H * W * cw.cout * m.es);
+        if (c.dry || !ok()) return out;
+        ProfEv *pe = nullptr;
+        if (m.profile) {
+            c.prof.emplace_back();
+            pe = &c.prof.back();
+            (void)hipEventCreate(&pe->e0);
+            (void)hipEventCreate(&pe->e1);
+            (void)hipEventRecord(pe->e0, s);
+        }
+        chk(mdx_conv2d_dual(x, N, H, W, cw.cin, x2, H2, W2, cw.kalg, cw.stride, cw.w, cw.b, cw.cout, 1, m.dt, out,
+                            splitk, SPLITK_WS, s));
+        if (pe) {
+            (void)hipEventRecord(pe->e1, s);
+            int kid = -1, ks = 0;
+            mdx_conv2d_last_plan(&kid, &ks);
+            const int64_t M = (int64_t)N * H * W, K = (int64_t)cw.cin + cw.kalg;
+            pe->r = mdx_conv_record{kid, ks, M, cw.cout, K, 2.0 * (double)M * cw.cout * K, 0.0};
+        }
+        return out;
+    }
     void *last_gn_ws = nullptr;
     size_t last_gn_ws_bytes = 0;
     void *groupnorm(const void *x, int N, int H, int W, const GnW &g, const void *up, int fuse) {
@@ -669,10 +727,17 @@ struct Fwd {
         for (const Block &blk : m.blocks) {
             int h1, w1, h2, w2, h3, w3;
             const void *sc = cur;
-            if (blk.has_sc) sc = conv(cur, B, H, W, blk.sc, false, h1, w1);
+            // (the split-plane mode runs every conv on its own kernels)
+            const bool fused = blk.c3sc.w && mdx_conv_fp32_split() == 0;
+            if (blk.has_sc && !fused) sc = conv(cur, B, H, W, blk.sc, false, h1, w1);
             void *t1 = conv(cur, B, H, W, blk.c1, true, h1, w1);
             void *t2 = conv(t1, B, h1, w1, blk.c2, true, h2, w2);
-            cur = conv(t2, B, h2, w2, blk.c3, true, h3, w3, sc);
+            if (fused) {
+                cur = conv3_shortcut(t2, B, h2, w2, cur, H, W, blk.c3sc);
+                h3 = h2;
+                w3 = w2;
+            } else
+                cur = conv(t2, B, h2, w2, blk.c3, true, h3, w3, sc);
             H = h3;
             W = w3;
             res[blk.stage] = cur;
@@ -853,6 +918,13 @@ using namespace mdx;
 
 // fp32 handles: the stem folded to the 2-channel (value, inside) form (1,
 // default) or over the normalised 3-channel input (0); read at mdx_model_create
+// 0 off, 1 fp32 handles (default), 2 fp32 and fp16 handles
+static int g_fuse_sc = 0;
+extern "C" int mdx_model_set_fuse_shortcut(int mode) {
+    const int old = g_fuse_sc;
+    g_fuse_sc = mode;
+    return old;
+}
 static int g_stem_fold = 1;
 extern "C" int mdx_model_set_stem_fold(int on) {
     const int old = g_stem_fold;
@@ -883,6 +955,7 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     m->dt = cfg->dtype;
     m->es = cfg->dtype == 1 ? 2 : 4;
     m->stem_fold = cfg->dtype == 0 && g_stem_fold;
+    m->fuse_sc = g_fuse_sc == 2 || (g_fuse_sc == 1 && cfg->dtype == 0);
     std::string err;
     if (!pack(*m, sd, err)) {
         set_error("mdx_model_create: %s", err.c_str());

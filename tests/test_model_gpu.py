@@ -940,3 +940,66 @@ def test_conv1x1_narrow_fp32(mdx, M, K, N, relu, head):
     assert (kid.value == 5) == bool(head)
     err = (out.cpu().double() - want).abs().max().item() / want.abs().max().item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16"])
+@pytest.mark.parametrize("N,H,W,Cin,Cout,H2,W2,Cin2,s2", [
+    (2, 28, 32, 64, 256, 28, 32, 64, 1),        # res2 block 0 shape (narrow: K = 128)
+    (2, 14, 16, 128, 512, 28, 32, 256, 2),      # res3 block 0
+    (1, 7, 8, 256, 1024, 14, 15, 512, 2),       # res4 block 0, odd x2 width
+    (3, 4, 4, 512, 2048, 7, 7, 1024, 2),        # res5 block 0 (few tiles: split-K)
+    (1, 9, 11, 64, 96, 17, 21, 128, 2),         # ragged Cout
+])
+def test_conv2d_dual_conv3_shortcut(mdx, dtype, N, H, W, Cin, Cout, H2, W2, Cin2, s2):
+    """mdx_conv2d_dual = conv3 (1x1 over x) + projection shortcut (1x1 / s2 over
+    x2), bias and ReLU, against the two convolutions in fp64 (tolerance as
+    test_conv2d: rel. 1e-4 of max fp32, 2e-3 fp16)."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(N * H + Cin + Cin2)
+    tdt = torch.float16 if dtype == "fp16" else torch.float32
+    x = torch.randn(N, H, W, Cin, generator=g).to(tdt)
+    x2 = torch.randn(N, H2, W2, Cin2, generator=g).to(tdt)
+    w3 = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).to(tdt)
+    ws = (torch.randn(Cout, Cin2, 1, 1, generator=g) / Cin2 ** 0.5).to(tdt)
+    b = torch.randn(Cout, generator=g)
+    sc = _conv_ref(x2.float(), ws.float(), None, s2, 0)
+    assert sc.shape[1:3] == (H, W)
+    want = _conv_ref(x.float(), w3.float(), b, 1, 0, sc, True)
+    wcat = torch.cat([w3.reshape(Cout, Cin), ws.reshape(Cout, Cin2)], 1).contiguous().cuda()
+    out = torch.full((N, H, W, Cout), float("nan"), dtype=tdt, device="cuda")
+    ws_bytes = 8 * N * H * W * Cout * 4
+    wsp = torch.empty(ws_bytes, dtype=torch.uint8, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    call("mdx_conv2d_dual", P(x.cuda()), N, H, W, Cin, P(x2.cuda()), H2, W2, Cin2, s2, P(wcat), P(b.cuda()), Cout, 1,
+         1 if dtype == "fp16" else 0, P(out), P(wsp), ws_bytes, None)
+    got = out.cpu().double()
+    err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-6)
+    assert err < (2e-3 if dtype == "fp16" else 1e-4), err
+
+
+def test_forward_fused_shortcut_matches_unfused(small_case):
+    """A handle with the projection shortcuts fused into conv3
+    (mdx_model_set_fuse_shortcut) gives the unfused handle's features to
+    fp32 rounding, and the oracle's within the backbone tolerance."""
+    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd.model import MaskRCNN
+    from oracle import model_ref as R
+    cfg, sd, _, imgs = small_case
+    old = call("mdx_model_set_fuse_shortcut", 0)
+    try:
+        m0 = MaskRCNN(cfg, sd, dtype="fp32")
+        call("mdx_model_set_fuse_shortcut", 1)
+        m1 = MaskRCNN(cfg, sd, dtype="fp32")
+    finally:
+        call("mdx_model_set_fuse_shortcut", old)
+    x = torch.from_numpy(imgs[..., 0]).cuda()
+    a = m0.forward(x, intermediates=True)["intermediates"]
+    b = m1.forward(x, intermediates=True)["intermediates"]
+    _, inter = R.forward(sd, cfg, imgs)
+    for k in ("res2", "res3", "res4", "res5", "p2", "p6"):
+        ga, gb = a[k].cpu().double(), b[k].cpu().double()
+        assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item(), k
+        want = inter[k].double()
+        err = (gb.permute(0, 3, 1, 2) - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+        assert err < 2e-4, f"{k}: rel err {err:.2e}"
