@@ -124,20 +124,11 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 7: "k_conv_x3<128> fp32 as bf16 plane products", 8: "k_conv_x3<64> fp32 as bf16 plane products",
                 9: "k_gemm_x6 256x256 LDS-DMA GEMM over bf16 planes (fp32 split, two plane products per MFMA)",
                 10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance",
-                12: "k_wino_in Winograd input transform", 13: "k_wino_out Winograd output transform",
-                14: "k_conv_m32<128> implicit GEMM on 32x32x2 f32 MFMAs, epilogue from the accumulators",
-                15: "k_gemm_m32p persistent GEMM on 32x32x2 f32 MFMAs (1x1 layers, Winograd GEMMs)",
-                16: "k_conv_m32<64> 64-wide N tile on 32x32x2 f32 MFMAs"}
-KERNEL_SYMBOLS["fp32"].update({14: "_ZN3mdx10k_conv_m32ILi128EEEvNS_8ConvArgsE",
-                               15: "_ZN3mdx11k_gemm_m32pENS_8ConvArgsE",
-                               16: "_ZN3mdx10k_conv_m32ILi64EEEvNS_8ConvArgsE",
-                               4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
+                12: "k_wino_in Winograd input transform", 13: "k_wino_out Winograd output transform"}
+KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
                                12: "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf",
                                13: "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf"})
 KERNEL_DEMANGLED.update({
-    "_ZN3mdx10k_conv_m32ILi128EEEvNS_8ConvArgsE": "void mdx::k_conv_m32<128>(mdx::ConvArgs)",
-    "_ZN3mdx11k_gemm_m32pENS_8ConvArgsE": "mdx::k_gemm_m32p(mdx::ConvArgs)",
-    "_ZN3mdx10k_conv_m32ILi64EEEvNS_8ConvArgsE": "void mdx::k_conv_m32<64>(mdx::ConvArgs)",
     "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE": "void mdx::k_conv1x1_stream_f32<4>(mdx::ConvArgs)",
     "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf": "void mdx::k_wino_in<4>(float const*, int, int, int, int, int, int, float*)",
     "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf":

@@ -231,19 +231,6 @@ int mdx_conv_set_mfma_prio256(int on);
  * routes the other fp32 layers to the split-plane kernel (diagnostic).
  * Returns the old value. */
 int mdx_conv_set_dma_f32(int on);
-/* fp32 layers on the register-staged 128-wide tile (no split-K, NHWC output;
- * the Winograd GEMMs too) on v_mfma_f32_32x32x2_f32 with the epilogue stored
- * straight from the accumulators: 1 on, 2 on with the persistent form for the
- * plain GEMMs (1x1 / stride 1 / unpadded layers, Winograd GEMMs: each
- * workgroup streams the K-steps of several tiles, the next tile's loads in
- * flight during the previous one's epilogue), 0 off.  Returns the old value. */
-int mdx_conv_set_f32_mfma32(int on);
-/* Persistent GEMM grid: about `slots` workgroups over all batch entries (a
- * multiple of 8 per entry, default 512 = two per CU).  Returns the old value. */
-int mdx_conv_set_m32p_slots(int slots);
-/* Winograd transforms on 4 consecutive channels per thread (16-B accesses): 1
- * on, 0 off.  Returns the old value. */
-int mdx_conv_set_wino_vec(int on);
 /* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
  * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
  * the products accumulate in fp32.  9: all nine plane products (the exact
@@ -311,9 +298,6 @@ enum {
     MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
     MDX_CONV_KERNEL_X3_64 = 8,
     MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
-    MDX_CONV_KERNEL_M32 = 14,   /* fp32 on 32x32x2 f32 MFMAs, epilogue from the accumulators (mdx_conv_set_f32_mfma32) */
-    MDX_CONV_KERNEL_M32P = 15,  /* its persistent GEMM form for 1x1 / Winograd GEMMs (mdx_conv_set_f32_mfma32(2)) */
-    MDX_CONV_KERNEL_M32_64 = 16, /* its 64-wide N tile (narrow layers) */
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

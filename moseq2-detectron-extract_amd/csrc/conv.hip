@@ -478,368 +478,6 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// fp32 implicit GEMM on v_mfma_f32_32x32x2_f32 with the epilogue straight from
-// the accumulators (mdx_conv_set_f32_mfma32).  Same tile (128 x 128, 4 waves
-// of 64 x 64 = 2 x 2 MFMA blocks of 32 x 32), K-steps, register-staged loads
-// and swizzled LDS image as k_conv<float, float, 128>.  Per 8-deep K chunk,
-// lane half h = lane >> 5 reads the 16-B piece 2 kk + h of its row (one
-// ds_read_b128) and supplies k = 4 h + e to MFMA e = 0..3: the same
-// permutation on both operands, so each output sums every k exactly once
-// (order: per accumulator e = 0..3 over the pairs {e, 4 + e}).  A 32 x 32
-// accumulator register holds 32 consecutive columns of two rows, so every
-// epilogue store is two 128-B row segments (full rate, no LDS image, no
-// barrier): bias / residual / ReLU per register.  No split-K, NHWC output.
-// ---------------------------------------------------------------------------
-typedef float float16v __attribute__((ext_vector_type(16)));
-
-template <int BN_>
-__global__ __launch_bounds__(CONV_THREADS, 2) void k_conv_m32(ConvArgs a) {
-    constexpr int BK = 32;
-    constexpr int NJ = BN_ / 64;  // 32-column MFMA blocks per wave
-    constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
-    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
-    constexpr int STAGE = A_TILE + B_TILE;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *As = smem;
-    char *Bs = smem + A_TILE;
-    if (gridDim.z > 1) {  // batch entry z of a batched GEMM
-        const long long z = blockIdx.z;
-        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
-        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
-        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
-    }
-    int tile;
-    {
-        const int L = blockIdx.x, nwg = a.tiles_total;
-        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
-        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-    }
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN_;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-
-    const int kc = tid & 7;
-    const int lrow = tid >> 3;
-    int a_iy0[4], a_ix0[4];
-    long long a_base[4];
-    bool a_ok[4];
-    const int ohw = a.OH * a.OW;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int gm = m0 + lrow + 32 * i;
-        a_ok[i] = gm < a.M;
-        const int gmc = a_ok[i] ? gm : 0;
-        const int b = gmc / ohw, rem = gmc - b * ohw;
-        const int oy = rem / a.OW, ox = rem - oy * a.OW;
-        a_iy0[i] = oy * a.stride - a.pad;
-        a_ix0[i] = ox * a.stride - a.pad;
-        a_base[i] = (long long)b * a.H * a.W * a.Cin;
-    }
-    int kglob = kc * 4;
-    int kci = kglob % a.Cin;
-    int kr = kglob / a.Cin;
-    int kkx = kr % a.KW, kky = kr / a.KW;
-    uint4 ra[2][4], rb[2][BLOADS];
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
-    constexpr unsigned OOB = 0xFFFFFFF0u;
-    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
-        const bool kok = kglob < a.K;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
-            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
-            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i) {
-            const int gn = n0 + lrow + 32 * i;
-            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * 4ll);
-            Bv[i] = __builtin_bit_cast(uint4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
-        }
-    };
-    auto advance_k = [&]() {
-        kglob += BK;
-        kci += BK;
-        while (kci >= a.Cin) {
-            kci -= a.Cin;
-            if (++kkx == a.KW) {
-                kkx = 0;
-                ++kky;
-            }
-        }
-    };
-    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;
-    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = A[i];
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i)
-            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
-    };
-
-    float16v acc[2][NJ];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int nk = (a.K + BK - 1) / BK;
-    load_global(ra[0], rb[0]);
-    advance_k();
-    store_lds(0, ra[0], rb[0]);
-    if (nk > 1) {
-        load_global(ra[1], rb[1]);
-        advance_k();
-    }
-    __syncthreads();
-    // fragment rows r = 32 blk + (lane & 31); piece 2 kk + (lane >> 5) at
-    // its swizzled position ((r >> 1) & 7 == (lane & 31) >> 1 & 7)
-    const int rsw = ((lane & 31) >> 1) & 7;
-    auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
-                     const uint4 (&Bs_)[BLOADS]) {
-        const int cur = kt & 1;
-        if (kt + 2 < nk) {
-            load_global(Ai, Bi);
-            advance_k();
-        }
-        const char *Ab = As + cur * STAGE + (wm * 64 + (lane & 31)) * PITCH;
-        const char *Bb = Bs + cur * STAGE + (wn * (BN_ / 2) + (lane & 31)) * PITCH;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int koff = ((2 * kk + (lane >> 5)) ^ rsw) * 16;
-            float4v af[2], bf[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 32 * PITCH + koff);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-        }
-        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
-        __syncthreads();
-    };
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-        kstep(kt, ra[0], rb[0], ra[1], rb[1]);
-        kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
-    }
-    if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
-
-    // epilogue straight from the accumulators: register r of block (i, j)
-    // holds row 32 i + 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column 32 j +
-    // (lane & 31) of the wave tile
-    float *O = reinterpret_cast<float *>(a.out);
-    const float *RS = reinterpret_cast<const float *>(a.res);
-    const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int gn = n0 + wn * (BN_ / 2) + 32 * j + (lane & 31);
-        const bool nok = gn < a.Cout;
-        const float bv = (a.bias && nok) ? a.bias[gn] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            float rv[16];
-            if (RS) {
-                const __amdgpu_buffer_rsrc_t rr_d =
-                    __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes, 0x00020000);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
-                    const unsigned off = (gm < a.M && nok) ? (unsigned)(((long long)gm * a.Cout + gn) * 4ll) : OOB;
-                    rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_d, off, 0, 0));
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
-                float v = acc[i][j][r] + bv;
-                if (RS) v += rv[r];
-                if (a.relu) v = v > 0.f ? v : 0.f;
-                if (gm < a.M && nok) O[(long long)gm * a.Cout + gn] = v;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent form of k_conv_m32 for plain GEMMs (1x1 / stride 1 / no padding:
-// the Winograd GEMMs and the pointwise convs, A row m = pixel m).  Each
-// workgroup walks the tiles L = blockIdx.x + i * gridDim.x of its batch entry
-// (gridDim.x a multiple of 8: every tile stays on the XCD of its workgroup,
-// XCD-contiguous ranges as in k_conv) as one stream of K-steps, so the loads
-// of a tile's first two K-steps are in flight while the previous tile
-// finishes and stores its outputs: a short-K GEMM (K = 128..512: 4..16
-// K-steps) no longer pays the prologue latency once per tile.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(CONV_THREADS, 2) void k_gemm_m32p(ConvArgs a) {
-    constexpr int BK = 32, BN_ = 128;
-    constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
-    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
-    constexpr int STAGE = A_TILE + B_TILE;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *As = smem;
-    char *Bs = smem + A_TILE;
-    if (gridDim.z > 1) {
-        const long long z = blockIdx.z;
-        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
-        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
-        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
-    }
-    const int G = gridDim.x, ntl = a.tiles_total;
-    if ((int)blockIdx.x >= ntl) return;
-    const int nmine = (ntl - (int)blockIdx.x + G - 1) / G;
-    const int nk = (a.K + BK - 1) / BK;
-    const int total = nmine * nk;
-    auto tile_origin = [&](int i, int &m0, int &n0) {
-        const int L = (int)blockIdx.x + i * G;
-        const int q = ntl / 8, r = ntl % 8, xcd = L % 8;
-        const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-        const int tm = tile / a.tiles_n;
-        m0 = tm * BM;
-        n0 = (tile - tm * a.tiles_n) * BN_;
-    };
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    const int kc = tid & 7, lrow = tid >> 3;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
-    constexpr unsigned OOB = 0xFFFFFFF0u;
-    // load side: the K-step (ld_i, ld_kt) of this workgroup's stream
-    int ld_i = 0, ld_kt = 0, ld_m0, ld_n0;
-    tile_origin(0, ld_m0, ld_n0);
-    uint4 ra[2][4], rb[2][BLOADS];
-    auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
-        const int kg = ld_kt * BK + kc * 4;
-        const bool kok = kg < a.K;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int gm = ld_m0 + lrow + 32 * i;
-            const unsigned off = (unsigned)(((long long)gm * a.K + kg) * 4ll);
-            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && gm < a.M) ? off : OOB, 0, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i) {
-            const int gn = ld_n0 + lrow + 32 * i;
-            const unsigned off = (unsigned)(((long long)gn * a.K + kg) * 4ll);
-            Bv[i] = __builtin_bit_cast(uint4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
-        }
-        if (++ld_kt == nk) {
-            ld_kt = 0;
-            if (++ld_i < nmine) tile_origin(ld_i, ld_m0, ld_n0);
-        }
-    };
-    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;
-    auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(As + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = A[i];
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i)
-            *reinterpret_cast<uint4 *>(Bs + buf * STAGE + (lrow + 32 * i) * PITCH + wpiece) = Bv[i];
-    };
-    float16v acc[2][2];
-    auto zero_acc = [&]() {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    };
-    zero_acc();
-    // compute side: the tile being multiplied and its K-step
-    int cm_i = 0, cm_kt = 0, cm_m0, cm_n0;
-    tile_origin(0, cm_m0, cm_n0);
-    float *O = reinterpret_cast<float *>(a.out);
-    const float *RS = reinterpret_cast<const float *>(a.res);
-    auto epilogue = [&]() {
-        const int rbase = cm_m0 + wm * 64 + 4 * (lane >> 5);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int gn = cm_n0 + wn * 64 + 32 * j + (lane & 31);
-            const bool nok = gn < a.Cout;
-            const float bv = (a.bias && nok) ? a.bias[gn] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                float rv[16];
-                if (RS) {
-                    const __amdgpu_buffer_rsrc_t rr_d =
-                        __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes, 0x00020000);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
-                        const unsigned off = (gm < a.M && nok) ? (unsigned)(((long long)gm * a.Cout + gn) * 4ll) : OOB;
-                        rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_d, off, 0, 0));
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int gm = rbase + 32 * i + 8 * (r >> 2) + (r & 3);
-                    float v = acc[i][j][r] + bv;
-                    if (RS) v += rv[r];
-                    if (a.relu) v = v > 0.f ? v : 0.f;
-                    if (gm < a.M && nok) O[(long long)gm * a.Cout + gn] = v;
-                }
-            }
-        }
-    };
-    load_global(ra[0], rb[0]);
-    store_lds(0, ra[0], rb[0]);
-    if (total > 1) load_global(ra[1], rb[1]);
-    __syncthreads();
-    const int rsw = ((lane & 31) >> 1) & 7;
-    auto kstep = [&](int q, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4], const uint4 (&Bs_)[BLOADS]) {
-        const int cur = q & 1;
-        if (q + 2 < total) load_global(Ai, Bi);
-        const char *Ab = As + cur * STAGE + (wm * 64 + (lane & 31)) * PITCH;
-        const char *Bb = Bs + cur * STAGE + (wn * 64 + (lane & 31)) * PITCH;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int koff = ((2 * kk + (lane >> 5)) ^ rsw) * 16;
-            float4v af[2], bf[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 32 * PITCH + koff);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 32 * PITCH + koff);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-        }
-        if (q + 1 < total) store_lds(cur ^ 1, As_, Bs_);
-        __syncthreads();
-        if (++cm_kt == nk) {  // the tile is complete: store it, start the next
-            epilogue();
-            zero_acc();
-            cm_kt = 0;
-            if (++cm_i < nmine) tile_origin(cm_i, cm_m0, cm_n0);
-        }
-    };
-    int q = 0;
-    for (; q + 1 < total; q += 2) {
-        kstep(q, ra[0], rb[0], ra[1], rb[1]);
-        kstep(q + 1, ra[1], rb[1], ra[0], rb[0]);
-    }
-    if (q < total) kstep(q, ra[0], rb[0], ra[1], rb[1]);
-}
-
-// ---------------------------------------------------------------------------
 // fp32 GEMM on the bf16 matrix cores (the fp32 model's layers when
 // mdx_conv_set_fp32_split(6 | 9)).  Every fp32 operand is split into three
 // bf16 values x = hi + mid + lo (hi = RN(x), mid = RN(x - hi), lo = x - hi -
@@ -2167,142 +1805,6 @@ __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, 
     }
 }
 
-// The same transforms on 4 consecutive channels per thread (C % 4 == 0): one
-// 16-B load / store per tap and plane instead of four 4-B ones, so a wave
-// instruction moves 1 KB (the 4-B form issues 4x the memory instructions for
-// the same bytes).  Row transform first (BT d, one input column at a time),
-// then the column transform; the arithmetic per channel is the 4-B form's.
-template <int M>
-__global__ __launch_bounds__(256) void k_wino_in_v4(const float *__restrict__ x, int N, int H, int W, int C, int TH,
-                                                    int TW, float *__restrict__ V) {
-    constexpr int A = WinoT<M>::A;
-    const int C4 = C >> 2;
-    const long long T = (long long)N * TH * TW;
-    const long long total = T * C4;
-    const long long xs = T * C;
-    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / C4;
-        const int c = (int)(idx - t * C4) * 4;
-        const int tx = (int)(t % TW);
-        const long long r = t / TW;
-        const int ty = (int)(r % TH), n = (int)(r / TH);
-        const int y0 = M * ty - 1, x0 = M * tx - 1;
-        float4 tt[A][A];  // B^T d: tt[i][j] = sum_k BT(i,k) d[k][j]
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-            const int xx = x0 + j;
-            float4 d[A];
-#pragma unroll
-            for (int k = 0; k < A; ++k) {
-                const int yy = y0 + k;
-                d[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W)
-                           ? *reinterpret_cast<const float4 *>(x + (((long long)n * H + yy) * W + xx) * C + c)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int i = 0; i < A; ++i) {
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int k = 0; k < A; ++k)
-                    if (WinoT<M>::BT(i, k) != 0.f) {
-                        const float b = WinoT<M>::BT(i, k);
-                        acc.x = acc.x + b * d[k].x;
-                        acc.y = acc.y + b * d[k].y;
-                        acc.z = acc.z + b * d[k].z;
-                        acc.w = acc.w + b * d[k].w;
-                    }
-                tt[i][j] = acc;
-            }
-        }
-        float *vo = V + t * C + c;
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-#pragma unroll
-            for (int j = 0; j < A; ++j) {
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int k = 0; k < A; ++k)
-                    if (WinoT<M>::BT(j, k) != 0.f) {
-                        const float b = WinoT<M>::BT(j, k);
-                        acc.x = acc.x + tt[i][k].x * b;
-                        acc.y = acc.y + tt[i][k].y * b;
-                        acc.z = acc.z + tt[i][k].z * b;
-                        acc.w = acc.w + tt[i][k].w * b;
-                    }
-                *reinterpret_cast<float4 *>(vo + (A * i + j) * xs) = acc;
-            }
-    }
-}
-
-template <int M>
-__global__ __launch_bounds__(256) void k_wino_out_v4(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
-                                                     int TW, const float *__restrict__ bias, int relu,
-                                                     float *__restrict__ out) {
-    constexpr int A = WinoT<M>::A;
-    const int K4 = K >> 2;
-    const long long T = (long long)N * TH * TW;
-    const long long total = T * K4;
-    const long long xs = T * K;
-    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / K4;
-        const int k = (int)(idx - t * K4) * 4;
-        const int tx = (int)(t % TW);
-        const long long r = t / TW;
-        const int ty = (int)(r % TH), n = (int)(r / TH);
-        const float *mi = Mx + t * K + k;
-        float4 sa[M][A];  // A^T m, one column of m at a time
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-            float4 m[A];
-#pragma unroll
-            for (int q = 0; q < A; ++q) m[q] = *reinterpret_cast<const float4 *>(mi + (A * q + j) * xs);
-#pragma unroll
-            for (int i = 0; i < M; ++i) {
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int q = 0; q < A; ++q)
-                    if (WinoT<M>::AT(i, q) != 0.f) {
-                        const float b = WinoT<M>::AT(i, q);
-                        acc.x = acc.x + b * m[q].x;
-                        acc.y = acc.y + b * m[q].y;
-                        acc.z = acc.z + b * m[q].z;
-                        acc.w = acc.w + b * m[q].w;
-                    }
-                sa[i][j] = acc;
-            }
-        }
-        const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-            const int oy = M * ty + i;
-            if (oy >= OH) continue;
-#pragma unroll
-            for (int j = 0; j < M; ++j) {
-                const int ox = M * tx + j;
-                if (ox >= OW) continue;
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int q = 0; q < A; ++q)
-                    if (WinoT<M>::AT(j, q) != 0.f) {
-                        const float b = WinoT<M>::AT(j, q);
-                        acc.x = acc.x + sa[i][q].x * b;
-                        acc.y = acc.y + sa[i][q].y * b;
-                        acc.z = acc.z + sa[i][q].z * b;
-                        acc.w = acc.w + sa[i][q].w * b;
-                    }
-                float4 v = make_float4(acc.x + bv.x, acc.y + bv.y, acc.z + bv.z, acc.w + bv.w);
-                if (relu) {
-                    v.x = v.x > 0.f ? v.x : 0.f;
-                    v.y = v.y > 0.f ? v.y : 0.f;
-                    v.z = v.z > 0.f ? v.z : 0.f;
-                    v.w = v.w > 0.f ? v.w : 0.f;
-                }
-                *reinterpret_cast<float4 *>(out + (((long long)n * OH + oy) * OW + ox) * K + k) = v;
-            }
-        }
-    }
-}
-
 }  // namespace mdx
 
 using namespace mdx;
@@ -2348,30 +1850,6 @@ static int g_dma_f32 = 2;
 extern "C" int mdx_conv_set_dma_f32(int on) {
     const int old = g_dma_f32;
     g_dma_f32 = on;
-    return old;
-}
-// fp32 register-staged layers (128-wide tile, no split-K, NHWC out) on the
-// 32x32x2 f32 MFMA kernel with the direct epilogue (k_conv_m32): 0 off, 1 on,
-// 2 on with the persistent form (k_gemm_m32p) for the plain GEMMs (1x1 /
-// stride 1 / no padding layers and the Winograd GEMMs)
-static int g_f32_m32 = 0;
-// persistent grid: workgroups per batch entry (a multiple of 8, at least 8),
-// about g_m32p_slots over all batch entries
-static int g_m32p_slots = 512;
-extern "C" int mdx_conv_set_m32p_slots(int slots) {
-    const int old = g_m32p_slots;
-    g_m32p_slots = slots;
-    return old;
-}
-static unsigned m32p_grid(int tiles, int nb) {
-    int g = (g_m32p_slots + nb - 1) / nb;
-    g = (g + 7) / 8 * 8;
-    if (g < 8) g = 8;
-    return (unsigned)(g < tiles ? g : tiles);
-}
-extern "C" int mdx_conv_set_f32_mfma32(int on) {
-    const int old = g_f32_m32;
-    g_f32_m32 = on;
     return old;
 }
 // fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
@@ -2717,26 +2195,6 @@ general:
             hipLaunchKernelGGL((k_conv_reduce<TO_>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), \
                                0, s, a);                                                                    \
     } while (0)
-    if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && narrow && a.ksplit == 1 && out_mode == 0) {
-        hipLaunchKernelGGL(k_conv_m32<64>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
-        t_plan_kernel = MDX_CONV_KERNEL_M32_64;
-        t_plan_ksplit = 1;
-        MDX_CHECK_LAUNCH("mdx_conv2d");
-        return MDX_OK;
-    }
-    if (g_f32_m32 && in_dtype == 0 && out_dtype == 0 && !narrow && a.ksplit == 1 && out_mode == 0) {
-        if (g_f32_m32 == 2 && KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-            hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, 1)), dim3(CONV_THREADS),
-                               2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
-            t_plan_kernel = MDX_CONV_KERNEL_M32P;
-        } else {
-            hipLaunchKernelGGL(k_conv_m32<128>, dim3(a.tiles_total), dim3(CONV_THREADS), lds_main, s, a);
-            t_plan_kernel = MDX_CONV_KERNEL_M32;
-        }
-        t_plan_ksplit = 1;
-        MDX_CHECK_LAUNCH("mdx_conv2d");
-        return MDX_OK;
-    }
     if (in_dtype == 1 && out_dtype == 1)
         MDX_LAUNCH_CONV(_Float16, _Float16);
     else if (in_dtype == 1 && out_dtype == 0)
@@ -2933,14 +2391,6 @@ extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, in
     return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
 }
 
-// Winograd transforms on 4 channels per thread (k_wino_in_v4 / k_wino_out_v4): 0 off, 1 on
-static int g_wino_vec = 0;
-extern "C" int mdx_conv_set_wino_vec(int on) {
-    const int old = g_wino_vec;
-    g_wino_vec = on;
-    return old;
-}
-
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
@@ -2968,14 +2418,7 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         if (probe) (void)hipEventRecord(probe->ev[i], s);
     };
     mark(0);
-    if (g_wino_vec) {
-        const long long items = T * (Cin / 4);
-        const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
-        if (m == 2)
-            hipLaunchKernelGGL(k_wino_in_v4<2>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
-        else
-            hipLaunchKernelGGL(k_wino_in_v4<4>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
-    } else {
+    {
         const long long items = T * Cin;
         const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
         if (m == 2)
@@ -3022,35 +2465,16 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     } else if (g_fp32_split) {
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
-    } else if (bn == 64 && g_f32_m32) {
-        hipLaunchKernelGGL(k_conv_m32<64>, grid, dim3(CONV_THREADS), lds_main, s, a);
-        gemm_kernel = MDX_CONV_KERNEL_M32_64;
     } else if (bn == 64) {
         hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG64;
-    } else if (g_f32_m32 == 2) {
-        hipLaunchKernelGGL(k_gemm_m32p, dim3(m32p_grid(a.tiles_total, NB), 1, (unsigned)NB), dim3(CONV_THREADS),
-                           2 * ((size_t)BM * PITCH + (size_t)BN * PITCH), s, a);
-        gemm_kernel = MDX_CONV_KERNEL_M32P;
-    } else if (g_f32_m32) {
-        hipLaunchKernelGGL(k_conv_m32<128>, grid, dim3(CONV_THREADS), lds_main, s, a);
-        gemm_kernel = MDX_CONV_KERNEL_M32;
     } else {
         hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
         gemm_kernel = MDX_CONV_KERNEL_REG128;
     }
     mark(3);
     mark(4);
-    if (g_wino_vec) {
-        const long long items = T * (Cout / 4);
-        const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
-        if (m == 2)
-            hipLaunchKernelGGL(k_wino_out_v4<2>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu,
-                               out);
-        else
-            hipLaunchKernelGGL(k_wino_out_v4<4>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu,
-                               out);
-    } else {
+    {
         const long long items = T * Cout;
         const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
         if (m == 2)
