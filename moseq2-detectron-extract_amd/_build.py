@@ -36,19 +36,21 @@ def _flags():
 # vectorises with AVX2 / FMA (every x86-64 host of an MI355X has them)
 HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mfma"]}
 
-# Device code is compiled without the packed FP32 VALU instructions
-# (v_pk_add/mul/fma_f32): the compiler forms them with op_sel / neg source
-# modifiers (broadcast operands), and with those (1) the GroupNorm statistics
-# came out nondeterministic on MI355X whenever two model forwards ran
-# concurrently on different hardware queues (~1e-3 relative errors in whole
-# channel halves; 0 of 24 runs without them against ~60 % with,
-# tools/dbg_race.py), and (2) once the Winograd output transform (the only
-# other kernel with such forms) was added, runs with more concurrency (three
-# forwards on eight hardware queues, or two processes on one GPU) ended in
-# illegal-address faults.  The target-feature switch reaches the host compile
-# too, where clang ignores it with a warning.
+# model_ops.hip (GroupNorm, RPN, ROIAlign, box / mask / keypoint post-processing)
+# is compiled without the packed FP32 VALU instructions (v_pk_add/mul/fma_f32,
+# which the compiler forms with op_sel / neg source modifiers): with them the
+# fp16 pipelined loop -- two model forwards on different hardware queues --
+# gave outputs different from the serial step in 133 of 150 steps, without
+# them in 0 of 150 (tools/determinism.py over the same tree, the build the
+# only variable: profiles/r03_determinism_packed_fp32.json).  The kernels
+# involved have no cross-workgroup sharing and each stream owns its
+# workspace, so the variable is the instruction form, not a data race.
+# conv.hip and inpaint.hip, once built the same way, are built with them again
+# (0 of 150 mismatches in fp16 and fp32 with packed forms there).  The
+# target-feature switch reaches the host compile too, where clang ignores it
+# with a warning.
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32, "conv.hip": NO_PACKED_FP32, "inpaint.hip": NO_PACKED_FP32}
+DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32}
 
 
 def sources():
@@ -63,6 +65,19 @@ def _deps_newer(target: str, srcs) -> bool:
     return any(os.path.getmtime(s) > t for s in list(srcs) + hdrs)
 
 
+def _cmd_flags(base: str) -> list:
+    return [*_flags(), *HOST_FLAGS.get(base, []), *DEVICE_FLAGS.get(base, [])]
+
+
+def _flags_changed(obj: str, flags: list) -> bool:
+    """The object was built with other flags (or its record is missing)."""
+    try:
+        with open(obj + ".flags") as fh:
+            return fh.read() != " ".join(flags)
+    except OSError:
+        return True
+
+
 def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(OBJ, exist_ok=True)
     cc = hipcc()
@@ -72,18 +87,20 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
-        if force or _deps_newer(o, [s]):
+        if force or _deps_newer(o, [s]) or _flags_changed(o, _cmd_flags(os.path.basename(s))):
             todo.append((s, o))
 
     def comp(so):
         s, o = so
-        base = os.path.basename(s)
-        cmd = [cc, *_flags(), *HOST_FLAGS.get(base, []), *DEVICE_FLAGS.get(base, []), "-c", s, "-o", o]
+        flags = _cmd_flags(os.path.basename(s))
+        cmd = [cc, *flags, "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+        with open(o + ".flags", "w") as fh:  # the flags this object was built with
+            fh.write(" ".join(flags))
         return o
 
     if todo:

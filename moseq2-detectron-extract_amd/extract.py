@@ -146,7 +146,11 @@ def _load_metadata(path: str) -> dict:
 class _ChunkWriter:
     """ResultWriterStep (M/pipeline/write_results_step.py:24-73): results_00.h5
     (or .npz without h5py) + keypoints_00.tsv, the datasets created up front
-    (create_extract_h5) and filled chunk by chunk."""
+    (create_extract_h5) and filled chunk by chunk.  As in the reference (its
+    own process there), the writes run beside the extraction: write() hands a
+    chunk's host results to a writer thread (in order, at most two queued),
+    which fills the datasets, deflates the completed crop rows and appends
+    the TSV; close() drains it and finishes the file."""
 
     def __init__(self, output_dir, src, bground_im, roi, true_depth, config, first_frame, status):
         os.makedirs(output_dir, exist_ok=True)
@@ -161,12 +165,39 @@ class _ChunkWriter:
         self.h5 = open_results(output_dir)
         self.tsv = KeypointsTSVWriter(output_dir)
         create_extract_h5(self.h5, cfg, status)
+        import queue
+        import threading
+        self._q: "queue.Queue" = queue.Queue(maxsize=2)
+        self._err: list = []
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self) -> None:
+        while True:
+            d = self._q.get()
+            if d is None:
+                return
+            if self._err:  # keep draining after an error so write() / close() never block
+                continue
+            try:
+                write_extracted_chunk_to_h5(self.h5, d)
+                self.tsv.write(d)
+            except BaseException as e:  # surfaced by write() / close()
+                self._err.append(e)
 
     def write(self, d: dict) -> None:
-        write_extracted_chunk_to_h5(self.h5, d)
-        self.tsv.write(d)
+        if self._err:
+            raise self._err[0]
+        f = d["features"]
+        self._q.put({"frame_idxs": d["frame_idxs"], "offset": d["offset"], "scalars": d["scalars"],
+                     "keypoints": d["keypoints"], "depth_frames": d["depth_frames"], "mask_frames": d["mask_frames"],
+                     "features": {"flips": f["flips"], "features": f["features"]}})
 
     def close(self) -> None:
+        self._q.put(None)
+        self._t.join()
+        if self._err:
+            raise self._err[0]
         self.h5.close()
 
 

@@ -127,3 +127,39 @@ def test_save_npz_parallel_pieces_round_trip(tmp_path, monkeypatch):
         assert sorted(z.files) == sorted(arrs)
         for k, v in arrs.items():
             assert z[k].dtype == v.dtype and z[k].shape == v.shape and np.array_equal(z[k], v), k
+
+
+@pytest.mark.parametrize("order", ["in-order", "reversed", "partial"])
+def test_streamed_npz_members(RS, tmp_path, monkeypatch, order):
+    """The crop stacks deflated chunk by chunk while the session runs
+    (MemoryH5.rows_written) load back equal to the arrays, with chunks
+    arriving in frame order, in reverse (nothing completes until the first
+    chunk: all compressed at close) and with rows never written (zeros);
+    small pieces so every member spans several."""
+    monkeypatch.setattr(RS, "_PIECE", 4096)
+    n, c = 50, 7
+    rng = np.random.default_rng(3)
+    path = str(tmp_path / "s.npz")
+    h = RS.MemoryH5(path)
+    h.create_dataset("frames", (n, 80, 80), "uint8")
+    h.create_dataset("frames_mask", (n, 80, 80), "bool")
+    h.create_dataset("scalars/x", (n,), "float32")
+    starts = list(range(0, n, c))
+    if order == "reversed":
+        starts = starts[::-1]
+    if order == "partial":
+        starts = starts[:-2]
+    for a in starts:
+        rows = np.arange(a, min(a + c, n))
+        h["frames"][rows] = rng.integers(0, 255, (len(rows), 80, 80))
+        h["frames_mask"][rows] = rng.random((len(rows), 80, 80)) > 0.5
+        h["scalars/x"][rows] = rng.random(len(rows))
+        h.rows_written(rows)
+    if order == "in-order":
+        assert h._streams["frames"].rows == n  # compressed before close
+    want = {k: v.data.copy() for k, v in h.datasets.items()}
+    h.close()
+    got = np.load(path)
+    for k, v in want.items():
+        assert got[k].dtype == v.dtype
+        np.testing.assert_array_equal(got[k], v, err_msg=k)
