@@ -98,33 +98,52 @@ def parse():
 
 
 # MDX_CONV_KERNEL_* (+10: fp32-output instance of an fp16 model) -> rocprofv3 symbol, per dtype
-KERNEL_SYMBOLS = {
-    "fp16": {0: "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE",
-             2: "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
-             3: "_ZN3mdx7k_convgIDF16_DF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
-             4: "k_conv1x1_stream<KC> (three instances by K)", 5: "k_conv1x1_head<KC> (three instances by K)",
-             10: "_ZN3mdx6k_convIDF16_fLi128EEEvNS_8ConvArgsE", 11: "_ZN3mdx6k_convIDF16_fLi64EEEvNS_8ConvArgsE"},
-    "fp32": {0: "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE", 1: "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE",
-             2: "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE"},
-}
+
+
+def _kconv(ti: str, to: str, bn: int, dual: bool, pw: bool):
+    """Mangled and demangled name of k_conv<TI, TO, BN, DUAL, PW>."""
+    m = {"f32": ("f", "float"), "f16": ("DF16_", "_Float16")}
+    b = lambda v: ("1", "true") if v else ("0", "false")  # noqa: E731
+    mangled = f"_ZN3mdx6k_convI{m[ti][0]}{m[to][0]}Li{bn}ELb{b(dual)[0]}ELb{b(pw)[0]}EEEvNS_8ConvArgsE"
+    return mangled, f"void mdx::k_conv<{m[ti][1]}, {m[to][1]}, {bn}, {b(dual)[1]}, {b(pw)[1]}>(mdx::ConvArgs)"
+
+
+# kernel id -> (BN, DUAL, PW) of the k_conv instance (ids +10: fp16 in, fp32 out)
+_KCONV_IDS = {0: (128, False, False), 1: (64, False, False), 14: (128, False, True), 15: (64, False, True),
+              16: (128, True, True), 17: (64, True, True)}
+KERNEL_SYMBOLS = {"fp16": {2: "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
+                           3: "_ZN3mdx7k_convgIDF16_DF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
+                           4: "k_conv1x1_stream<KC> (three instances by K)",
+                           5: "k_conv1x1_head<KC> (three instances by K)"},
+                  "fp32": {2: "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE"}}
 # rocprofv3 reports some kernels demangled
 KERNEL_DEMANGLED = {
-    "_ZN3mdx6k_convIffLi128EEEvNS_8ConvArgsE": "void mdx::k_conv<float, float, 128>(mdx::ConvArgs)",
-    "_ZN3mdx6k_convIffLi64EEEvNS_8ConvArgsE": "void mdx::k_conv<float, float, 64>(mdx::ConvArgs)",
-    "_ZN3mdx6k_convIDF16_DF16_Li128EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 128>(mdx::ConvArgs)",
-    "_ZN3mdx6k_convIDF16_DF16_Li64EEEvNS_8ConvArgsE": "void mdx::k_conv<_Float16, _Float16, 64>(mdx::ConvArgs)",
     "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
         "void mdx::k_convg<_Float16, _Float16, 8, false, false, false>(mdx::ConvArgs)",
     "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
         "void mdx::k_convg<float, float, 8, false, false, false>(mdx::ConvArgs)",
 }
+for _k, (_bn, _dual, _pw) in _KCONV_IDS.items():
+    for _dt, _t in (("fp32", "f32"), ("fp16", "f16")):
+        _m, _d = _kconv(_t, _t, _bn, _dual, _pw)
+        KERNEL_SYMBOLS[_dt][_k] = _m
+        KERNEL_DEMANGLED[_m] = _d
+    if not _dual:
+        _m, _d = _kconv("f16", "f32", _bn, False, _pw)
+        KERNEL_SYMBOLS["fp16"][_k + 10] = _m
+        KERNEL_DEMANGLED[_m] = _d
 KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> register-staged implicit GEMM",
                 2: "k_convg<8> 256x256 LDS-DMA implicit GEMM", 3: "k_convg<4> 128x128 LDS-DMA implicit GEMM",
                 4: "k_conv1x1_stream streaming 1x1 GEMM", 5: "k_conv1x1_head narrow-output streaming 1x1",
                 7: "k_conv_x3<128> fp32 as bf16 plane products", 8: "k_conv_x3<64> fp32 as bf16 plane products",
                 9: "k_gemm_x6 256x256 LDS-DMA GEMM over bf16 planes (fp32 split, two plane products per MFMA)",
                 10: "k_conv<128> fp32-output instance", 11: "k_conv<64> fp32-output instance",
-                12: "k_wino_in Winograd input transform", 13: "k_wino_out Winograd output transform"}
+                12: "k_wino_in Winograd input transform", 13: "k_wino_out Winograd output transform",
+                14: "k_conv<128, PW> register-staged implicit GEMM, pointwise addressing",
+                15: "k_conv<64, PW> register-staged implicit GEMM, pointwise addressing",
+                16: "k_conv<128, DUAL> conv3 + projection shortcut GEMM",
+                17: "k_conv<64, DUAL> conv3 + projection shortcut GEMM",
+                24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance"}
 KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
                                12: "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf",
                                13: "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf"})

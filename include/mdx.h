@@ -298,6 +298,10 @@ enum {
     MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
     MDX_CONV_KERNEL_X3_64 = 8,
     MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
+    MDX_CONV_KERNEL_PW128 = 14, /* REG128 / REG64 on a pointwise layer (1x1 unpadded, Winograd GEMMs): */
+    MDX_CONV_KERNEL_PW64 = 15,  /* per-row precomputed addresses (mdx_conv_set_pointwise) */
+    MDX_CONV_KERNEL_DUAL128 = 16, /* mdx_conv2d_dual (conv3 + projection shortcut in one GEMM) */
+    MDX_CONV_KERNEL_DUAL64 = 17,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,
@@ -326,6 +330,10 @@ int mdx_conv_set_split256(int mode, int min_sub);
  * Returns the old setting. */
 int mdx_conv_set_dma_after(int on);
 int mdx_conv2d_last_plan(int *kernel, int *ksplit);
+/* Pointwise layers (1x1, unpadded, any stride) and the Winograd GEMMs on the
+ * register-staged kernel's instance with per-row precomputed load addresses:
+ * 1 on (default), 0 the general instance.  Returns the old value. */
+int mdx_conv_set_pointwise(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

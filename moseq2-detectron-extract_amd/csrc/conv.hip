@@ -208,7 +208,11 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
 
 // BN_: N tile (128 or 64).  4 waves as 2x2; wave tile (BM/2) x (BN_/2) =
 // TI x TJ MFMA tiles of 16x16.
-template <typename T, typename TO, int BN_, bool DUAL = false>
+// PW: pointwise layer (1x1, no padding, any stride -- the 1x1 convs and the
+// Winograd GEMMs): a row's A bytes start at its pixel's offset, so every load
+// address is that offset + k, precomputed per row (no per-K-step bounds
+// arithmetic, which compiles to exec-masked branches around every load).
+template <typename T, typename TO, int BN_, bool DUAL = false, bool PW = false>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -259,6 +263,10 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
             a2_off[i] = a_ok[i] ? (unsigned)((((long long)b * a.H2 + (long long)oy * a.stride2) * a.W2 +
                                               (long long)ox * a.stride2) * a.Cin2 * (long long)sizeof(T))
                                 : 0xFFFFFFF0u;
+        if constexpr (PW)  // (a_base[i] reused: byte offset of the row's pixel, or OOB)
+            a_base[i] = a_ok[i] ? (long long)(((long long)b * a.H + (long long)oy * a.stride) * a.W +
+                                              (long long)ox * a.stride) * a.Cin * (long long)sizeof(T)
+                                : 0xFFFFFFF0ll;
     }
     const int kz = blockIdx.y;
     int kglob = kz * a.ksteps * BK + kc * VEC;
@@ -289,6 +297,14 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
                 A[i] = __builtin_bit_cast(
                     uint4, __builtin_amdgcn_raw_buffer_load_b128(rx2, (kok && a2_off[i] != OOB) ? a2_off[i] + kb : OOB,
                                                                  0, 0));
+        } else if constexpr (PW) {
+            const unsigned kb = (unsigned)(kglob * (int)sizeof(T));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const unsigned ro = (unsigned)a_base[i];
+                A[i] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && ro != OOB) ? ro + kb : OOB, 0, 0));
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -309,6 +325,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     };
     auto advance_k = [&]() {
         kglob += BK;
+        if constexpr (PW) return;
         kci += BK;
         while (kci >= a.Cin) {
             kci -= a.Cin;
@@ -1852,6 +1869,14 @@ extern "C" int mdx_conv_set_dma_f32(int on) {
     g_dma_f32 = on;
     return old;
 }
+// pointwise layers (1x1, unpadded) and the Winograd GEMMs on k_conv's PW
+// instances (addresses precomputed per row): 1 (default), 0 the general instances
+static int g_pw = 1;
+extern "C" int mdx_conv_set_pointwise(int on) {
+    const int old = g_pw;
+    g_pw = on;
+    return old;
+}
 // fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
 static int g_fp32_split = 0;
 extern "C" int mdx_conv_set_fp32_split(int mode) {
@@ -2184,11 +2209,16 @@ general:
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
+    const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
-        if (narrow)                                                                                         \
+        if (narrow && pw)                                                                                   \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);    \
+        else if (narrow)                                                                                    \
             hipLaunchKernelGGL((k_conv<TI_, TO_, 64>), grid, dim3(CONV_THREADS), lds, s, a);                 \
+        else if (pw)                                                                                        \
+            hipLaunchKernelGGL((k_conv<TI_, TO_, 128, false, true>), grid, dim3(CONV_THREADS), lds, s, a);   \
         else                                                                                                \
             hipLaunchKernelGGL((k_conv<TI_, TO_, 128>), grid, dim3(CONV_THREADS), lds, s, a);                \
         if (a.ksplit > 1)                                                                                   \
@@ -2204,7 +2234,8 @@ general:
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
-    t_plan_kernel = narrow ? MDX_CONV_KERNEL_REG64 : MDX_CONV_KERNEL_REG128;
+    t_plan_kernel = narrow ? (pw ? MDX_CONV_KERNEL_PW64 : MDX_CONV_KERNEL_REG64)
+                           : (pw ? MDX_CONV_KERNEL_PW128 : MDX_CONV_KERNEL_REG128);
     t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d");
     return MDX_OK;
@@ -2301,21 +2332,21 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
     const dim3 grid(a.tiles_total, a.ksplit);
     if (dtype == 0) {
         if (narrow)
-            hipLaunchKernelGGL((k_conv<float, float, 64, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            hipLaunchKernelGGL((k_conv<float, float, 64, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         else
-            hipLaunchKernelGGL((k_conv<float, float, 128, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            hipLaunchKernelGGL((k_conv<float, float, 128, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         if (a.ksplit > 1)
             hipLaunchKernelGGL((k_conv_reduce<float>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0, s, a);
     } else {
         if (narrow)
-            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 64, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 64, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         else
-            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 128, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            hipLaunchKernelGGL((k_conv<_Float16, _Float16, 128, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         if (a.ksplit > 1)
             hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0,
                                s, a);
     }
-    t_plan_kernel = narrow ? MDX_CONV_KERNEL_REG64 : MDX_CONV_KERNEL_REG128;
+    t_plan_kernel = narrow ? MDX_CONV_KERNEL_DUAL64 : MDX_CONV_KERNEL_DUAL128;
     t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d_dual");
     return MDX_OK;
@@ -2466,11 +2497,21 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64) {
-        hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
-        gemm_kernel = MDX_CONV_KERNEL_REG64;
+        if (g_pw) {
+            hipLaunchKernelGGL((k_conv<float, float, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            gemm_kernel = MDX_CONV_KERNEL_PW64;
+        } else {
+            hipLaunchKernelGGL((k_conv<float, float, 64>), grid, dim3(CONV_THREADS), lds, s, a);
+            gemm_kernel = MDX_CONV_KERNEL_REG64;
+        }
     } else {
-        hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
-        gemm_kernel = MDX_CONV_KERNEL_REG128;
+        if (g_pw) {
+            hipLaunchKernelGGL((k_conv<float, float, 128, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
+            gemm_kernel = MDX_CONV_KERNEL_PW128;
+        } else {
+            hipLaunchKernelGGL((k_conv<float, float, 128>), grid, dim3(CONV_THREADS), lds, s, a);
+            gemm_kernel = MDX_CONV_KERNEL_REG128;
+        }
     }
     mark(3);
     mark(4);

@@ -12,7 +12,8 @@ the reference's fp32) and ``from_torchscript`` on an archive written here.
 Tolerances (fp32, as tests/test_parity_full.py): same detection count and
 classes; every oracle box matched by a box of IoU >= 0.98 and |score diff|
 <= 1e-3; matched masks differ in <= max(4, 3 % of the union) pixels;
->= 90 % of keypoints within 1 px, keypoint scores within 1e-3 absolute;
+>= 90 % of keypoints within 1 px, keypoint scores (heatmap-maximum logits,
+up to ~50) within 1e-3 absolute + 1e-4 relative;
 heatmap logits within 1e-3 of the largest |logit|."""
 import numpy as np
 import pytest
@@ -75,7 +76,7 @@ def _check(preds, want, hw):
         gk, wk = ins.pred_keypoints.numpy()[m], w["pred_keypoints"].numpy()
         assert gk.shape == wk.shape == (n, 8, 3)
         assert (np.abs(gk[..., :2] - wk[..., :2]).max(-1) < 1.0).mean() >= 0.9
-        np.testing.assert_allclose(gk[..., 2], wk[..., 2], atol=1e-3, rtol=0)
+        np.testing.assert_allclose(gk[..., 2], wk[..., 2], atol=1e-3, rtol=1e-4)
         gh, wh = ins.pred_keypoint_heatmaps.numpy()[m], w["pred_keypoint_heatmaps"].numpy()
         assert gh.shape == wh.shape == (n, 8, 28, 28)
         assert np.abs(gh - wh).max() <= 1e-3 * np.abs(wh).max()
