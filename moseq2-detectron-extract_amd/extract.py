@@ -254,11 +254,15 @@ def _run_overlapped(src, batches, ex, true_depth, finished=None):
         ctx["ws"] = torch.cuda.Stream()
 
     def produce():
-        for idx, raw in src.iterate(device=True, batches=batches):
-            st, host = ex.features_pass(raw)
+        chunks = ((np.asarray(idx), raw) for idx, raw in src.iterate(device=True, batches=batches))
+        if ex.cfg.pipelined:  # one device pipeline across the chunk boundaries
+            passes = ex.features_passes(chunks)
+        else:
+            passes = ((idx, *ex.features_pass(raw)) for idx, raw in chunks)
+        for idx, st, host in passes:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
-            yield np.asarray(idx), st, host, ev
+            yield idx, st, host, ev
 
     def consume(item):
         idx, st, host, ev = item
