@@ -148,6 +148,15 @@ int mdx_iterative_filter_angles(const double *angles, int64_t n, int window, dou
 int mdx_flips_from_keypoints(const double *kp, int64_t n, int K, const double *centroid,
                              const double *angle_deg, const double *length, uint8_t *flips, double *conf);
 
+/* Keypoints TSV rows as ResultWriterStep writes them with pandas'
+ * DataFrame.to_csv(sep="\t", index=False) (M/pipeline/write_results_step.py:
+ * 54-73): columns cols[c] of nrows values, kinds[c] 0 float64 (Python repr,
+ * NaN as an empty field), 1 bool (uint8: True / False), 2 int64; rows end in
+ * '\n', no header.  Host code (no GPU): returns the bytes written into out
+ * (cap >= nrows * (ncols * 40 + 1)), or a negative error. */
+int64_t mdx_format_tsv_rows(const void *const *cols, const int *kinds, int ncols, int64_t nrows, char *out,
+                            int64_t cap);
+
 /* Host (CPU) function: the no-tracking angle branch of instances_to_features
  * (M/proc/proc.py:720-724, 827-839): angle = clamp_angles_deg(-rad2deg(
  * orientation)); +180 where mdx_flips_from_keypoints (length = max axis)

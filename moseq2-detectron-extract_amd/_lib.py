@@ -79,6 +79,7 @@ SIGNATURES = {
     "mdx_conv2d_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "mdx_conv2d_splitk": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, I32,
                                 P, I64, P]),
+    "mdx_format_tsv_rows": (I64, [P, P, I32, I64, P, I64]),
     "mdx_conv2d_dual": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_model_set_fuse_shortcut": (I32, [I32]),
     "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),

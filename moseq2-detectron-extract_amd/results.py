@@ -385,14 +385,48 @@ class KeypointsTSVWriter:
         for k, v in data["keypoints"].items():
             cols[k] = np.asarray(v)
         # the bytes of pandas.DataFrame(cols).to_csv(sep="\t", index=False)
-        # (shortest round-trip floats, NaN as an empty field), ~3x faster
-        cells = [_tsv_cells(v) for v in cols.values()]
-        text = "".join("\t".join(r) + "\n" for r in zip(*cells))
-        if self._header:
-            text = "\t".join(cols) + "\n" + text
-        with open(self.path, "w" if self._header else "a", encoding="utf-8") as fh:
-            fh.write(text)
+        # (shortest round-trip floats, NaN as an empty field): formatted in
+        # libmdx's host code (no GIL held) when every column is float64 /
+        # bool / integer, else here
+        body = _tsv_rows_native(list(cols.values()))
+        if body is None:
+            cells = [_tsv_cells(v) for v in cols.values()]
+            body = "".join("\t".join(r) + "\n" for r in zip(*cells)).encode()
+        with open(self.path, "wb" if self._header else "ab") as fh:
+            if self._header:
+                fh.write(("\t".join(cols) + "\n").encode())
+            fh.write(body)
         self._header = False
+
+
+def _tsv_rows_native(columns) -> Optional[bytes]:
+    """mdx_format_tsv_rows over the columns, or None when a column's dtype
+    has no native form (float32 / float16: numpy's own shortest repr)."""
+    import ctypes
+    kinds, keep = [], []
+    for a in columns:
+        a = np.asarray(a)
+        if a.dtype == np.float64:
+            kinds.append(0)
+            keep.append(np.ascontiguousarray(a))
+        elif a.dtype == np.bool_:
+            kinds.append(1)
+            keep.append(np.ascontiguousarray(a).view(np.uint8))
+        elif a.dtype.kind in "iu" and a.dtype.itemsize <= 8 and (a.dtype.kind == "i" or a.dtype.itemsize < 8):
+            kinds.append(2)
+            keep.append(np.ascontiguousarray(a, dtype=np.int64))
+        else:
+            return None
+    n = len(keep[0]) if keep else 0
+    if any(len(k) != n for k in keep):
+        raise ValueError("keypoints TSV: columns of different lengths")
+    from ._lib import call
+    ptrs = (ctypes.c_void_p * len(keep))(*[k.ctypes.data for k in keep])
+    kd = (ctypes.c_int * len(kinds))(*kinds)
+    cap = n * (len(keep) * 40 + 1) + 1
+    buf = ctypes.create_string_buffer(cap)
+    nb = call("mdx_format_tsv_rows", ptrs, kd, len(keep), n, buf, cap)
+    return buf.raw[:nb]
 
 
 def _tsv_cells(a: np.ndarray) -> list:

@@ -163,3 +163,22 @@ def test_streamed_npz_members(RS, tmp_path, monkeypatch, order):
     for k, v in want.items():
         assert got[k].dtype == v.dtype
         np.testing.assert_array_equal(got[k], v, err_msg=k)
+
+
+def test_native_tsv_rows_match_python_repr(RS):
+    """libmdx's TSV formatter (mdx_format_tsv_rows, host code) against the
+    Python formatter (repr of each float, '' for NaN, True / False, ints) on
+    values across the whole double range, the positional / exponent
+    thresholds (1e-4, 1e16), signed zeros, infinities and subnormals."""
+    rng = np.random.default_rng(7)
+    n = 20000
+    a = rng.standard_normal(n) * 10.0 ** rng.integers(-30, 30, n)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e16, 9999999999999998.0, 1e15, 1e-4, 9.999999999999999e-05,
+                        1e-5, 0.1, 5.0, -123456789.125, 5e-324, 2.2250738585072014e-308, 1.7976931348623157e308,
+                        123456789012345678.0, 0.30000000000000004])
+    cols = [np.arange(n + special.size, dtype=np.int64) - 5, rng.random(n + special.size) > 0.5,
+            np.concatenate([a, special]), np.concatenate([special, a])]
+    native = RS._tsv_rows_native(cols)
+    cells = [RS._tsv_cells(c) for c in cols]
+    want = "".join("\t".join(r) + "\n" for r in zip(*cells)).encode()
+    assert native == want
