@@ -255,7 +255,7 @@ def _run_overlapped(src, batches, ex, true_depth, finished=None):
 
     def produce():
         chunks = ((np.asarray(idx), raw) for idx, raw in src.iterate(device=True, batches=batches))
-        if ex.cfg.pipelined:  # one device pipeline across the chunk boundaries
+        if ex.cfg.pipelined and ex.cfg.cross_chunk:  # one device pipeline across the chunk boundaries
             passes = ex.features_passes(chunks)
         else:
             passes = ((idx, *ex.features_pass(raw)) for idx, raw in chunks)

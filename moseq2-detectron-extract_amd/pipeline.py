@@ -60,6 +60,8 @@ class ExtractConfig:
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
     pipelined: bool = True           # features_pass: batches staggered over streams (OverlappedExtractor)
+    cross_chunk: bool = False        # extract loop: one such pipeline across the chunks (features_passes;
+                                     # measured equal in steady state, slower on a session's first run)
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
