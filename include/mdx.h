@@ -569,7 +569,7 @@ typedef void *mdx_model_t;
 int mdx_model_set_stem_fold(int on);
 /* Handles created afterwards run each bottleneck's projection shortcut and
  * conv3 as one GEMM (mdx_conv2d_dual): 0 off, 1 fp32 handles, 2 fp32 and fp16
- * handles (default).  Returns the old value. */
+ * handles.  Default 1.  Returns the old value. */
 int mdx_model_set_fuse_shortcut(int mode);
 
 /* Weights blob: Detectron2 state-dict layout (parameter / buffer names of
