@@ -311,6 +311,10 @@ enum {
     MDX_CONV_KERNEL_PW64 = 15,  /* per-row precomputed addresses (mdx_conv_set_pointwise) */
     MDX_CONV_KERNEL_DUAL128 = 16, /* mdx_conv2d_dual (conv3 + projection shortcut in one GEMM) */
     MDX_CONV_KERNEL_DUAL64 = 17,
+    MDX_CONV_KERNEL_SB128 = 18, /* PW128 / PW64 on the single-LDS-stage k_conv_sb (mdx_conv_set_single_stage) */
+    MDX_CONV_KERNEL_SB64 = 19,
+    MDX_CONV_KERNEL_SBDUAL128 = 20, /* DUAL128 / DUAL64 on k_conv_sb */
+    MDX_CONV_KERNEL_SBDUAL64 = 21,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,
@@ -343,6 +347,11 @@ int mdx_conv2d_last_plan(int *kernel, int *ksplit);
  * register-staged kernel's instance with per-row precomputed load addresses:
  * 1 on (default), 0 the general instance.  Returns the old value. */
 int mdx_conv_set_pointwise(int on);
+/* fp32 pointwise layers / Winograd GEMMs on the single-LDS-stage instance
+ * k_conv_sb (three workgroups per CU, two barriers per K-step, the same
+ * sums bit for bit): 1 on (default), 0 the two-stage instance.  Returns the
+ * old value. */
+int mdx_conv_set_single_stage(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
     "mdx_conv_set_dma_f32": (I32, [I32]),
     "mdx_conv_set_pointwise": (I32, [I32]),
+    "mdx_conv_set_single_stage": (I32, [I32]),
     "mdx_conv_set_fp32_split": (I32, [I32]),
     "mdx_conv_fp32_split": (I32, []),
     "mdx_roi_align_get_mode": (I32, []),

@@ -212,8 +212,11 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
 // Winograd GEMMs): a row's A bytes start at its pixel's offset, so every load
 // address is that offset + k, precomputed per row (no per-K-step bounds
 // arithmetic, which compiles to exec-masked branches around every load).
-template <typename T, typename TO, int BN_, bool DUAL = false, bool PW = false>
-__global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
+// SB: one LDS stage instead of two (a second barrier per K-step before the
+// next stage overwrites it), so three workgroups fit a CU instead of two
+// (launched as k_conv_sb).
+template <typename T, typename TO, int BN_, bool DUAL, bool PW, bool SB>
+__device__ __forceinline__ void conv_body(ConvArgs &a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
     constexpr int A_TILE = BM * PITCH, B_TILE = BN_ * PITCH;
@@ -360,7 +363,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     advance_k();
     store_lds(0, ra[0], rb[0]);
     if (nk > 1) {
-        load_global(ra[1], rb[1]);
+        // (SB: one register stage; step 1 reuses set 0 once its store issued)
+        load_global(ra[SB ? 0 : 1], rb[SB ? 0 : 1]);
         advance_k();
     }
     __syncthreads();
@@ -368,8 +372,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     // 1) & 1] hold step kt + 1
     auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
                      const uint4 (&Bs_)[BLOADS]) {
-        const int cur = kt & 1;
-        if (kt + 2 < nk) {
+        const int cur = SB ? 0 : (kt & 1);
+        if (!SB && kt + 2 < nk) {
             load_global(Ai, Bi);
             advance_k();
         }
@@ -413,15 +417,30 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
                                     __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
             }
         }
-        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
+        if constexpr (SB) {
+            // one LDS stage, one register stage: [MFMAs of kt] barrier [store
+            // kt + 1, then load kt + 2 into the same registers] barrier
+            __syncthreads();  // every wave is done reading the stage
+            if (kt + 1 < nk) store_lds(0, Ai, Bi);
+            if (kt + 2 < nk) {
+                load_global(Ai, Bi);
+                advance_k();
+            }
+        } else if (kt + 1 < nk) {
+            store_lds(cur ^ 1, As_, Bs_);
+        }
         __syncthreads();
     };
     int kt = 0;
+    if constexpr (SB) {
+        for (; kt < nk; ++kt) kstep(kt, ra[0], rb[0], ra[0], rb[0]);
+    } else {
     for (; kt + 1 < nk; kt += 2) {
         kstep(kt, ra[0], rb[0], ra[1], rb[1]);
         kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
     }
     if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
+    }
 
     // ---- epilogue, in two halves of BM/2 rows (the LDS image is half the
     // tile, so a one-step-K launch fits 4 workgroups per CU): the waves owning
@@ -474,6 +493,15 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
         }
         if (h == 0) __syncthreads();
     }
+}
+
+template <typename T, typename TO, int BN_, bool DUAL = false, bool PW = false>
+__global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
+    conv_body<T, TO, BN_, DUAL, PW, false>(a);
+}
+template <typename T, typename TO, int BN_, bool DUAL = false>
+__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sb(ConvArgs a) {
+    conv_body<T, TO, BN_, DUAL, true, true>(a);
 }
 
 // split-K reduction: sum the slices (fixed order) and apply the epilogue
@@ -1877,6 +1905,23 @@ extern "C" int mdx_conv_set_pointwise(int on) {
     g_pw = on;
     return old;
 }
+// fp32 PW instances with a single LDS stage and a single register stage,
+// three (128-wide) / four (64-wide) workgroups per CU (k_conv_sb): 1 on
+// (default: GEMM microbench 14.35 -> 13.92 ms per forward, bench loop
+// 1281 -> 1306 fps), 0 the two-stage k_conv instances
+static int g_conv_sb = 1;
+extern "C" int mdx_conv_set_single_stage(int on) {
+    const int old = g_conv_sb;
+    g_conv_sb = on;
+    return old;
+}
+// LDS of a k_conv launch: stage buffers (one when the whole K is one step or
+// the single-stage instance, else two) or the half-tile fp32 epilogue image
+static size_t conv_lds(int bn, int ksteps, bool sb) {
+    const size_t main_ = (ksteps == 1 || sb ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
+    const size_t epi = (size_t)(BM / 2) * (bn + 4) * 4;
+    return main_ > epi ? main_ : epi;
+}
 // fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
 static int g_fp32_split = 0;
 extern "C" int mdx_conv_set_fp32_split(int mode) {
@@ -2210,10 +2255,17 @@ general:
         return MDX_OK;
     }
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
+    const bool sb = g_conv_sb && in_dtype == 0 && out_dtype == 0;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
-        if (narrow && pw)                                                                                   \
+        if (narrow && pw && sb)                                                                             \
+            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64>), grid, dim3(CONV_THREADS),          \
+                               conv_lds(64, a.ksteps, true), s, a);                                         \
+        else if (!narrow && pw && sb)                                                                       \
+            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 128>), grid, dim3(CONV_THREADS),         \
+                               conv_lds(128, a.ksteps, true), s, a);                                        \
+        else if (narrow && pw)                                                                              \
             hipLaunchKernelGGL((k_conv<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);    \
         else if (narrow)                                                                                    \
             hipLaunchKernelGGL((k_conv<TI_, TO_, 64>), grid, dim3(CONV_THREADS), lds, s, a);                 \
@@ -2234,8 +2286,8 @@ general:
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
-    t_plan_kernel = narrow ? (pw ? MDX_CONV_KERNEL_PW64 : MDX_CONV_KERNEL_REG64)
-                           : (pw ? MDX_CONV_KERNEL_PW128 : MDX_CONV_KERNEL_REG128);
+    t_plan_kernel = narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64) : MDX_CONV_KERNEL_REG64)
+                           : (pw ? (sb ? MDX_CONV_KERNEL_SB128 : MDX_CONV_KERNEL_PW128) : MDX_CONV_KERNEL_REG128);
     t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d");
     return MDX_OK;
@@ -2330,8 +2382,15 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     hipStream_t s = as_stream(stream);
     const dim3 grid(a.tiles_total, a.ksplit);
+    const bool sb = dtype == 0 && g_conv_sb;
     if (dtype == 0) {
-        if (narrow)
+        if (narrow && sb)
+            hipLaunchKernelGGL((k_conv_sb<float, float, 64, true>), grid, dim3(CONV_THREADS),
+                               conv_lds(64, a.ksteps, true), s, a);
+        else if (sb)
+            hipLaunchKernelGGL((k_conv_sb<float, float, 128, true>), grid, dim3(CONV_THREADS),
+                               conv_lds(128, a.ksteps, true), s, a);
+        else if (narrow)
             hipLaunchKernelGGL((k_conv<float, float, 64, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         else
             hipLaunchKernelGGL((k_conv<float, float, 128, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
@@ -2346,7 +2405,8 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
             hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)), dim3(256), 0,
                                s, a);
     }
-    t_plan_kernel = narrow ? MDX_CONV_KERNEL_DUAL64 : MDX_CONV_KERNEL_DUAL128;
+    t_plan_kernel = narrow ? (sb ? MDX_CONV_KERNEL_SBDUAL64 : MDX_CONV_KERNEL_DUAL64)
+                           : (sb ? MDX_CONV_KERNEL_SBDUAL128 : MDX_CONV_KERNEL_DUAL128);
     t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d_dual");
     return MDX_OK;
@@ -2497,7 +2557,11 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64) {
-        if (g_pw) {
+        if (g_pw && g_conv_sb) {
+            hipLaunchKernelGGL((k_conv_sb<float, float, 64>), grid, dim3(CONV_THREADS),
+                               conv_lds(64, a.ksteps, true), s, a);
+            gemm_kernel = MDX_CONV_KERNEL_SB64;
+        } else if (g_pw) {
             hipLaunchKernelGGL((k_conv<float, float, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
             gemm_kernel = MDX_CONV_KERNEL_PW64;
         } else {
@@ -2505,7 +2569,11 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
             gemm_kernel = MDX_CONV_KERNEL_REG64;
         }
     } else {
-        if (g_pw) {
+        if (g_pw && g_conv_sb) {
+            hipLaunchKernelGGL((k_conv_sb<float, float, 128>), grid, dim3(CONV_THREADS),
+                               conv_lds(128, a.ksteps, true), s, a);
+            gemm_kernel = MDX_CONV_KERNEL_SB128;
+        } else if (g_pw) {
             hipLaunchKernelGGL((k_conv<float, float, 128, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
             gemm_kernel = MDX_CONV_KERNEL_PW128;
         } else {

@@ -987,3 +987,48 @@ def test_features_passes_across_chunks_matches_per_chunk(mdx):
         for k in ("keypoints", "keep_idx", "sel_keypoints"):
             assert torch.equal(s1["inf"][k], s0["inf"][k]), k
         assert torch.equal(torch.cat(s1["inf"]["masks"]), torch.cat(s0["inf"]["masks"]))
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 1 and c[7] == 0])
+def test_conv2d_fp32_pointwise_instances(mdx, case):
+    """fp32 pointwise layers (1x1, unpadded, stride 1 or 2) on k_conv's PW
+    instances, with two LDS stages and with one (k_conv_sb,
+    mdx_conv_set_single_stage), split-K 1 and 3 (Cout % 8 == 0), against the
+    fp64 convolution (rel. 1e-4 of the output scale) and against each other
+    bit for bit (same MFMA order per accumulator)."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    N, H, W, Cin, Cout, k, s, p, use_res, relu = case
+    g = torch.Generator().manual_seed(Cin * 7 + Cout)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5
+    b = torch.randn(Cout, generator=g)
+    OH, OW = (H - 1) // s + 1, (W - 1) // s + 1
+    res = torch.randn(N, OH, OW, Cout, generator=g) if use_res else None
+    want = _conv_ref(x, w, b, s, 0, res, relu)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    xd, wd, bd = x.cuda(), w.reshape(Cout, Cin).contiguous().cuda(), b.cuda()
+    rd = res.cuda() if res is not None else None
+    nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, 1, 1, s, 0)
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    olds = [call("mdx_conv_set_single_stage", 0), call("mdx_conv_set_dma_f32", 0),
+            call("mdx_conv_set_head_f32", 0), call("mdx_conv_set_stream1x1_f32", 0)]
+    try:
+        for ks in ((1, 3) if Cout % 8 == 0 else (1,)):
+            outs = []
+            for single in (0, 1):
+                call("mdx_conv_set_single_stage", single)
+                out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
+                call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0, 0,
+                     0, P(out), ks, P(ws), nb, None)
+                kid, ks_ = ctypes.c_int(), ctypes.c_int()
+                call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+                assert kid.value in ((18, 19) if single else (14, 15)), kid.value
+                err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+                assert err < 1e-4, (ks, single, err)
+                outs.append(out)
+            assert torch.equal(outs[0], outs[1]), ks
+    finally:
+        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
+                         "mdx_conv_set_stream1x1_f32"), olds):
+            call(f, o)
