@@ -127,6 +127,10 @@ for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  #
     _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
     KERNEL_SYMBOLS["fp32"][_k] = _m
     KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
+for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<float, float, BN>: single stage, general layers
+    _m = f"_ZN3mdx10k_conv_sbgIffLi{_bn}EEEvNS_8ConvArgsE"
+    KERNEL_SYMBOLS["fp32"][_k] = _m
+    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sbg<float, float, {_bn}>(mdx::ConvArgs)"
 for _k, (_bn, _dual, _pw) in _KCONV_IDS.items():
     for _dt, _t in (("fp32", "f32"), ("fp16", "f16")):
         _m, _d = _kconv(_t, _t, _bn, _dual, _pw)
@@ -151,6 +155,8 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 19: "k_conv_sb<64> register-staged implicit GEMM, pointwise, single LDS stage (4 WG/CU)",
                 20: "k_conv_sb<128, DUAL> conv3 + projection shortcut GEMM, single LDS stage",
                 21: "k_conv_sb<64, DUAL> conv3 + projection shortcut GEMM, single LDS stage",
+                22: "k_conv_sbg<128> register-staged implicit GEMM, single LDS stage",
+                23: "k_conv_sbg<64> register-staged implicit GEMM, single LDS stage",
                 24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance"}
 KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
                                12: "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf",

@@ -315,6 +315,8 @@ enum {
     MDX_CONV_KERNEL_SB64 = 19,
     MDX_CONV_KERNEL_SBDUAL128 = 20, /* DUAL128 / DUAL64 on k_conv_sb */
     MDX_CONV_KERNEL_SBDUAL64 = 21,
+    MDX_CONV_KERNEL_SBG128 = 22, /* REG128 / REG64 on the single-stage k_conv_sbg (mdx_conv_set_single_stage(2)) */
+    MDX_CONV_KERNEL_SBG64 = 23,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

@@ -503,6 +503,12 @@ template <typename T, typename TO, int BN_, bool DUAL = false>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sb(ConvArgs a) {
     conv_body<T, TO, BN_, DUAL, true, true>(a);
 }
+// the single-stage schedule for general layers (padded / KxK: the stem, the
+// Cin < 128 3x3 layers)
+template <typename T, typename TO, int BN_>
+__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sbg(ConvArgs a) {
+    conv_body<T, TO, BN_, false, false, true>(a);
+}
 
 // split-K reduction: sum the slices (fixed order) and apply the epilogue
 template <typename TO>
@@ -1908,7 +1914,8 @@ extern "C" int mdx_conv_set_pointwise(int on) {
 // fp32 PW instances with a single LDS stage and a single register stage,
 // three (128-wide) / four (64-wide) workgroups per CU (k_conv_sb): 1 on
 // (default: GEMM microbench 14.35 -> 13.92 ms per forward, bench loop
-// 1281 -> 1306 fps), 0 the two-stage k_conv instances
+// 1281 -> 1306 fps), 2 the general (padded / KxK) fp32 layers too
+// (k_conv_sbg), 0 the two-stage k_conv instances
 static int g_conv_sb = 1;
 extern "C" int mdx_conv_set_single_stage(int on) {
     const int old = g_conv_sb;
@@ -2256,6 +2263,7 @@ general:
     }
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
     const bool sb = g_conv_sb && in_dtype == 0 && out_dtype == 0;
+    const bool sbg = g_conv_sb == 2 && !pw && in_dtype == 0 && out_dtype == 0;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
@@ -2264,6 +2272,12 @@ general:
                                conv_lds(64, a.ksteps, true), s, a);                                         \
         else if (!narrow && pw && sb)                                                                       \
             hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 128>), grid, dim3(CONV_THREADS),         \
+                               conv_lds(128, a.ksteps, true), s, a);                                        \
+        else if (narrow && sbg)                                                                             \
+            hipLaunchKernelGGL((k_conv_sbg<TI_, TO_, 64>), grid, dim3(CONV_THREADS),                         \
+                               conv_lds(64, a.ksteps, true), s, a);                                         \
+        else if (!narrow && sbg)                                                                            \
+            hipLaunchKernelGGL((k_conv_sbg<TI_, TO_, 128>), grid, dim3(CONV_THREADS),                        \
                                conv_lds(128, a.ksteps, true), s, a);                                        \
         else if (narrow && pw)                                                                              \
             hipLaunchKernelGGL((k_conv<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);    \
@@ -2286,8 +2300,10 @@ general:
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
-    t_plan_kernel = narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64) : MDX_CONV_KERNEL_REG64)
-                           : (pw ? (sb ? MDX_CONV_KERNEL_SB128 : MDX_CONV_KERNEL_PW128) : MDX_CONV_KERNEL_REG128);
+    t_plan_kernel = narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64)
+                                 : (sbg ? MDX_CONV_KERNEL_SBG64 : MDX_CONV_KERNEL_REG64))
+                           : (pw ? (sb ? MDX_CONV_KERNEL_SB128 : MDX_CONV_KERNEL_PW128)
+                                 : (sbg ? MDX_CONV_KERNEL_SBG128 : MDX_CONV_KERNEL_REG128));
     t_plan_ksplit = a.ksplit;
     MDX_CHECK_LAUNCH("mdx_conv2d");
     return MDX_OK;

@@ -1032,3 +1032,43 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
         for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
                          "mdx_conv_set_stream1x1_f32"), olds):
             call(f, o)
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if not (c[5] == 1 and c[7] == 0) and c[3] % 4 == 0])
+def test_conv2d_fp32_single_stage_general(mdx, case):
+    """General fp32 layers (KxK / padded: the stem's shape, 3x3 / 7x7 with
+    stride) on the single-stage schedule (k_conv_sbg,
+    mdx_conv_set_single_stage(2)) against the fp64 convolution (rel. 1e-4 of
+    the output scale) and against the two-stage kernel bit for bit."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    N, H, W, Cin, Cout, k, s, p, use_res, relu = case
+    g = torch.Generator().manual_seed(Cin * 11 + Cout + k)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = torch.randn(N, OH, OW, Cout, generator=g) if use_res else None
+    want = _conv_ref(x, w, b, s, p, res, relu)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    xd, bd = x.cuda(), b.cuda()
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
+    rd = res.cuda() if res is not None else None
+    olds = [call("mdx_conv_set_single_stage", 1), call("mdx_conv_set_dma_f32", 0), call("mdx_conv_set_winograd", 0)]
+    try:
+        outs = []
+        for mode in (1, 2):
+            call("mdx_conv_set_single_stage", mode)
+            out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
+            call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 0, 0, P(out),
+                 None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            assert kid.value in ((22, 23) if mode == 2 else (0, 1)), kid.value
+            err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+            assert err < 1e-4, (mode, err)
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_winograd"), olds):
+            call(f, o)
