@@ -234,8 +234,9 @@ int mdx_conv_set_mfma_prio(int on);
 /* s_setprio(1) around the MFMA bursts of the 256x256 LDS-DMA kernel (0/1). */
 int mdx_conv_set_mfma_prio256(int on);
 /* fp32 layers (Cin % 32 == 0, fp32 output) on the LDS-DMA kernels (16x16x4
- * f32 MFMAs): 0 never, 1 the 128x128 tile (>= 512 tiles), 2 the 256x256 tile
- * for layers with >= 500 such tiles and K >= 1024 (default), 3 the 256x256
+ * f32 MFMAs): 0 never (default: the register-staged single-stage kernel is
+ * faster on every fp32 layer, box fc1 included), 1 the 128x128 tile (>= 512
+ * tiles), 2 the 256x256 tile for layers with >= 500 such tiles and K >= 1024, 3 the 256x256
  * tile under the fp16 policy, 4 as 2 also while mdx_conv_set_fp32_split
  * routes the other fp32 layers to the split-plane kernel (diagnostic).
  * Returns the old value. */

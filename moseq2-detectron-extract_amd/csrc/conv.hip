@@ -1892,12 +1892,12 @@ extern "C" int mdx_conv_set_dma_after(int on) {
     g_dma_after = on;
     return old;
 }
-// fp32 layers on the LDS-DMA kernels: 0 never, 1 the 128x128 tile for layers
-// with >= 512 tiles, 2 the 256x256 tile for the big deep-K layers (default:
-// measured +1-2 % on the FPN/RPN p2 3x3 and box fc1 layers; the 128x128 tile
-// and the 256x256 tile on smaller layers lose to k_conv<128>), 3 the 256x256
-// tile under the fp16 policy
-static int g_dma_f32 = 2;
+// fp32 layers on the LDS-DMA kernels: 0 never (default since round 3: box
+// fc1 on the single-stage k_conv_sb runs at 0.86 of the f32 peak, 6.10 ms,
+// against 0.83 on the 256x256 tile; bench loop 1324 -> 1338 fps), 1 the
+// 128x128 tile for layers with >= 512 tiles, 2 the 256x256 tile for the big
+// deep-K layers (the round-2 default), 3 the 256x256 tile under the fp16 policy
+static int g_dma_f32 = 0;
 extern "C" int mdx_conv_set_dma_f32(int on) {
     const int old = g_dma_f32;
     g_dma_f32 = on;
