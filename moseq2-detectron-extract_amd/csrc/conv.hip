@@ -2262,8 +2262,10 @@ general:
         return MDX_OK;
     }
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
-    const bool sb = g_conv_sb && in_dtype == 0 && out_dtype == 0;
-    const bool sbg = g_conv_sb == 2 && !pw && in_dtype == 0 && out_dtype == 0;
+    // (mode 3: the fp16 register-staged layers too -- an A/B knob; the fp16
+    // model's big layers are on the LDS-DMA kernels unless mdx_conv_set_large_tiles(0))
+    const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb == 3 && in_dtype == 1 && out_dtype == 1));
+    const bool sbg = g_conv_sb >= 2 && !pw && in_dtype == 0 && out_dtype == 0;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
