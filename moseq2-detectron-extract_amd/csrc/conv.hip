@@ -1911,12 +1911,14 @@ extern "C" int mdx_conv_set_pointwise(int on) {
     g_pw = on;
     return old;
 }
-// fp32 PW instances with a single LDS stage and a single register stage,
-// three (128-wide) / four (64-wide) workgroups per CU (k_conv_sb): 1 on
-// (default: GEMM microbench 14.35 -> 13.92 ms per forward, bench loop
-// 1281 -> 1306 fps), 2 the general (padded / KxK) fp32 layers too
-// (k_conv_sbg), 0 the two-stage k_conv instances
-static int g_conv_sb = 1;
+// PW layers on the instances with a single LDS stage and a single register
+// stage, three (128-wide) / four (64-wide) workgroups per CU (k_conv_sb, the
+// same sums bit for bit): 1 fp32 (GEMM microbench 14.35 -> 13.92 ms per
+// forward, bench loop 1281 -> 1306 fps), 2 also the general (padded / KxK)
+// fp32 layers (k_conv_sbg: res2 conv2 306 -> 284 us, loop unchanged), 3 also
+// the fp16 register-staged PW layers (default: fp16 loop 3924 -> 4009 fps,
+// config 5 3310 -> 3320), 0 the two-stage k_conv instances
+static int g_conv_sb = 3;
 extern "C" int mdx_conv_set_single_stage(int on) {
     const int old = g_conv_sb;
     g_conv_sb = on;
@@ -2262,8 +2264,8 @@ general:
         return MDX_OK;
     }
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
-    // (mode 3: the fp16 register-staged layers too -- an A/B knob; the fp16
-    // model's big layers are on the LDS-DMA kernels unless mdx_conv_set_large_tiles(0))
+    // (mode 3: the fp16 register-staged PW layers too; the fp16 model's big
+    // layers stay on the LDS-DMA kernels)
     const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb == 3 && in_dtype == 1 && out_dtype == 1));
     const bool sbg = g_conv_sb >= 2 && !pw && in_dtype == 0 && out_dtype == 0;
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
