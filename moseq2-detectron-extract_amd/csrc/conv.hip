@@ -1756,102 +1756,102 @@ struct WinoT<4> {
     }
 };
 
-// one thread per (tile, channel); sums over nonzero coefficients only
+// one thread per (tile, channel): workgroup (blockIdx.x = tile, blockIdx.y =
+// channel block of blockDim.x), so the tile coordinates are workgroup-uniform
+// scalars (the per-thread 64-bit div / mod of a flat index cost more than the
+// loads); sums over nonzero coefficients only
 template <int M>
 __global__ __launch_bounds__(256) void k_wino_in(const float *__restrict__ x, int N, int H, int W, int C, int TH,
                                                  int TW, float *__restrict__ V) {
     constexpr int A = WinoT<M>::A;
+    const int t = blockIdx.x;
+    const int c = blockIdx.y * blockDim.x + threadIdx.x;
+    if (c >= C) return;
     const long long T = (long long)N * TH * TW;
-    const long long total = T * C;
     const long long xs = T * C;  // stride between xi planes
-    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / C;
-        const int c = (int)(idx - t * C);
-        const int tx = (int)(t % TW);
-        const long long r = t / TW;
-        const int ty = (int)(r % TH), n = (int)(r / TH);
-        const int y0 = M * ty - 1, x0 = M * tx - 1;
-        float d[A][A];
+    const int tx = t % TW, r = t / TW;
+    const int ty = r % TH, n = r / TH;
+    const int y0 = M * ty - 1, x0 = M * tx - 1;
+    const float *xb = x + (long long)n * H * W * C + c;
+    float d[A][A];
 #pragma unroll
-        for (int i = 0; i < A; ++i)
+    for (int i = 0; i < A; ++i)
 #pragma unroll
-            for (int j = 0; j < A; ++j) {
-                const int yy = y0 + i, xx = x0 + j;
-                d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? x[(((long long)n * H + yy) * W + xx) * C + c] : 0.f;
-            }
-        float tt[A][A];  // B^T d
+        for (int j = 0; j < A; ++j) {
+            const int yy = y0 + i, xx = x0 + j;
+            d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? xb[((long long)yy * W + xx) * C] : 0.f;
+        }
+    float tt[A][A];  // B^T d
 #pragma unroll
-        for (int i = 0; i < A; ++i)
+    for (int i = 0; i < A; ++i)
 #pragma unroll
-            for (int j = 0; j < A; ++j) {
-                float acc = 0.f;
+        for (int j = 0; j < A; ++j) {
+            float acc = 0.f;
 #pragma unroll
-                for (int k = 0; k < A; ++k)
-                    if (WinoT<M>::BT(i, k) != 0.f) acc = acc + WinoT<M>::BT(i, k) * d[k][j];
-                tt[i][j] = acc;
-            }
-        float *vo = V + t * C + c;
+            for (int k = 0; k < A; ++k)
+                if (WinoT<M>::BT(i, k) != 0.f) acc = acc + WinoT<M>::BT(i, k) * d[k][j];
+            tt[i][j] = acc;
+        }
+    float *vo = V + (long long)t * C + c;
 #pragma unroll
-        for (int i = 0; i < A; ++i)
+    for (int i = 0; i < A; ++i)
 #pragma unroll
-            for (int j = 0; j < A; ++j) {  // (B^T d) B
-                float acc = 0.f;
+        for (int j = 0; j < A; ++j) {  // (B^T d) B
+            float acc = 0.f;
 #pragma unroll
-                for (int k = 0; k < A; ++k)
-                    if (WinoT<M>::BT(j, k) != 0.f) acc = acc + tt[i][k] * WinoT<M>::BT(j, k);
-                vo[(A * i + j) * xs] = acc;
-            }
-    }
+            for (int k = 0; k < A; ++k)
+                if (WinoT<M>::BT(j, k) != 0.f) acc = acc + tt[i][k] * WinoT<M>::BT(j, k);
+            vo[(A * i + j) * xs] = acc;
+        }
 }
 
+// one thread per (tile, output channel), laid out as k_wino_in
 template <int M>
 __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
                                                   int TW, const float *__restrict__ bias, int relu,
                                                   float *__restrict__ out) {
     constexpr int A = WinoT<M>::A;
+    const int t = blockIdx.x;
+    const int k = blockIdx.y * blockDim.x + threadIdx.x;
+    if (k >= K) return;
     const long long T = (long long)N * TH * TW;
-    const long long total = T * K;
     const long long xs = T * K;
-    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long t = idx / K;
-        const int k = (int)(idx - t * K);
-        const int tx = (int)(t % TW);
-        const long long r = t / TW;
-        const int ty = (int)(r % TH), n = (int)(r / TH);
-        const float *mi = Mx + t * K + k;
-        float m[A][A];
+    const int tx = t % TW, r = t / TW;
+    const int ty = r % TH, n = r / TH;
+    const float *mi = Mx + (long long)t * K + k;
+    float m[A][A];
 #pragma unroll
-        for (int i = 0; i < A; ++i)
+    for (int i = 0; i < A; ++i)
 #pragma unroll
-            for (int j = 0; j < A; ++j) m[i][j] = mi[(A * i + j) * xs];
-        float sa[M][A];  // A^T m
+        for (int j = 0; j < A; ++j) m[i][j] = mi[(A * i + j) * xs];
+    float sa[M][A];  // A^T m
 #pragma unroll
-        for (int i = 0; i < M; ++i)
+    for (int i = 0; i < M; ++i)
 #pragma unroll
-            for (int j = 0; j < A; ++j) {
-                float acc = 0.f;
+        for (int j = 0; j < A; ++j) {
+            float acc = 0.f;
 #pragma unroll
-                for (int q = 0; q < A; ++q)
-                    if (WinoT<M>::AT(i, q) != 0.f) acc = acc + WinoT<M>::AT(i, q) * m[q][j];
-                sa[i][j] = acc;
-            }
-        const float bv = bias ? bias[k] : 0.f;
+            for (int q = 0; q < A; ++q)
+                if (WinoT<M>::AT(i, q) != 0.f) acc = acc + WinoT<M>::AT(i, q) * m[q][j];
+            sa[i][j] = acc;
+        }
+    const float bv = bias ? bias[k] : 0.f;
+    float *ob = out + (long long)n * OH * OW * K + k;
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
-            const int oy = M * ty + i;
-            if (oy >= OH) continue;
+    for (int i = 0; i < M; ++i) {
+        const int oy = M * ty + i;
+        if (oy >= OH) continue;
 #pragma unroll
-            for (int j = 0; j < M; ++j) {
-                const int ox = M * tx + j;
-                if (ox >= OW) continue;
-                float acc = 0.f;
+        for (int j = 0; j < M; ++j) {
+            const int ox = M * tx + j;
+            if (ox >= OW) continue;
+            float acc = 0.f;
 #pragma unroll
-                for (int q = 0; q < A; ++q)
-                    if (WinoT<M>::AT(j, q) != 0.f) acc = acc + sa[i][q] * WinoT<M>::AT(j, q);
-                float v = acc + bv;
-                if (relu) v = v > 0.f ? v : 0.f;
-                out[(((long long)n * OH + oy) * OW + ox) * K + k] = v;
-            }
+            for (int q = 0; q < A; ++q)
+                if (WinoT<M>::AT(j, q) != 0.f) acc = acc + sa[i][q] * WinoT<M>::AT(j, q);
+            float v = acc + bv;
+            if (relu) v = v > 0.f ? v : 0.f;
+            ob[((long long)oy * OW + ox) * K] = v;
         }
     }
 }
@@ -2529,13 +2529,18 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         if (probe) (void)hipEventRecord(probe->ev[i], s);
     };
     mark(0);
+    // transforms: workgroup = (tile, block of up to 256 channels)
+    auto tgrid = [&](int ch, unsigned &bd) {
+        bd = (unsigned)std::min(256, (ch + 63) / 64 * 64);
+        return dim3((unsigned)T, (unsigned)((ch + (int)bd - 1) / (int)bd));
+    };
     {
-        const long long items = T * Cin;
-        const unsigned grid = (unsigned)std::min<long long>((items + 255) / 256, 65536);
+        unsigned bd;
+        const dim3 grid = tgrid(Cin, bd);
         if (m == 2)
-            hipLaunchKernelGGL(k_wino_in<2>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+            hipLaunchKernelGGL(k_wino_in<2>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
         else
-            hipLaunchKernelGGL(k_wino_in<4>, dim3(grid), dim3(256), 0, s, x, N, H, W, Cin, TH, TW, V);
+            hipLaunchKernelGGL(k_wino_in<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
     }
     mark(1);
     mark(2);
@@ -2604,12 +2609,12 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     mark(3);
     mark(4);
     {
-        const long long items = T * Cout;
-        const unsigned grid2 = (unsigned)std::min<long long>((items + 255) / 256, 65536);
+        unsigned bd;
+        const dim3 grid2 = tgrid(Cout, bd);
         if (m == 2)
-            hipLaunchKernelGGL(k_wino_out<2>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
+            hipLaunchKernelGGL(k_wino_out<2>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
         else
-            hipLaunchKernelGGL(k_wino_out<4>, dim3(grid2), dim3(256), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
+            hipLaunchKernelGGL(k_wino_out<4>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
     }
     mark(5);
     if (probe) probe->gemm_kernel = gemm_kernel;
