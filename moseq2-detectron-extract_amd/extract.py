@@ -254,15 +254,11 @@ def _run_overlapped(src, batches, ex, true_depth, finished=None):
         ctx["ws"] = torch.cuda.Stream()
 
     def produce():
-        chunks = ((np.asarray(idx), raw) for idx, raw in src.iterate(device=True, batches=batches))
-        if ex.cfg.pipelined and ex.cfg.cross_chunk:  # one device pipeline across the chunk boundaries
-            passes = ex.features_passes(chunks)
-        else:
-            passes = ((idx, *ex.features_pass(raw)) for idx, raw in chunks)
-        for idx, st, host in passes:
+        for idx, raw in src.iterate(device=True, batches=batches):
+            st, host = ex.features_pass(raw)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
-            yield idx, st, host, ev
+            yield np.asarray(idx), st, host, ev
 
     def consume(item):
         idx, st, host, ev = item

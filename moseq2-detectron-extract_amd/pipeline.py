@@ -60,8 +60,6 @@ class ExtractConfig:
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
     pipelined: bool = True           # features_pass: batches staggered over streams (OverlappedExtractor)
-    cross_chunk: bool = False        # extract loop: one such pipeline across the chunks (features_passes;
-                                     # measured equal in steady state, slower on a session's first run)
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -321,56 +319,6 @@ class GPUExtractor:
             self._pipe = OverlappedExtractor(self, max(1, int(self.cfg.model_streams)), keep=True)
             self._pipe.prime(first)
         return self._pipe
-
-    def features_passes(self, chunks):
-        """features_pass over a stream of (frame_idxs, raw device chunk),
-        yielding (frame_idxs, state, host) per chunk in order, with ONE
-        pipeline running across the chunk boundaries: a chunk is collected
-        once its last slice has left the pipeline, which happens while the
-        next chunk's first slices are already submitted, so the device never
-        drains between chunks (features_pass flushes the pipeline per chunk).
-        The collection (concatenation, host copies) runs on a stream of its
-        own: a wait queued on the issuing stream would hold back every later
-        front.  Same results as features_pass chunk by chunk."""
-        B = self.cfg.batch_size
-        pending = collections.deque()  # (frame_idxs, slices submitted, outs so far)
-        pipe = None
-        cs = torch.cuda.Stream()
-
-        def attach(r):
-            for ent in pending:
-                if len(ent[2]) < ent[1]:
-                    ent[2].append(r)
-                    return
-            raise RuntimeError("pipeline returned more slices than were submitted")
-
-        def collect(ent):
-            with torch.cuda.stream(cs):
-                for o in ent[2]:
-                    cs.wait_event(o["ready"])
-                    for v in (o["prepped"], o["cleaned"], *o.values(), *o["inf"].values(), *o["inf"]["masks"]):
-                        if torch.is_tensor(v):
-                            v.record_stream(cs)
-                state, host = self._collect(ent[2])  # (its host copies synchronise cs)
-            return ent[0], state, host
-
-        for idx, raw in chunks:
-            raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else \
-                torch.from_numpy(np.ascontiguousarray(raw)).cuda()
-            if pipe is None:
-                pipe = self._pipeline(raw[:B])
-            pending.append((idx, (raw.shape[0] + B - 1) // B, []))
-            for i in range(0, raw.shape[0], B):
-                r = pipe.submit(raw[i:i + B])
-                if r is not None:
-                    attach(r)
-                while pending and len(pending[0][2]) == pending[0][1]:
-                    yield collect(pending.popleft())
-        if pipe is not None:
-            for r in pipe.flush():
-                attach(r)
-        while pending:
-            yield collect(pending.popleft())
 
     def _collect(self, outs):
         """One chunk's pipeline results -> (device state, host features)."""

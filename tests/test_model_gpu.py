@@ -959,36 +959,6 @@ def test_forward_fused_shortcut_matches_unfused(small_case):
         assert err < 2e-4, f"{k}: rel err {err:.2e}"
 
 
-def test_features_passes_across_chunks_matches_per_chunk(mdx):
-    """The extract loop's device pass with one pipeline across the chunk
-    boundaries (GPUExtractor.features_passes: a chunk collected on its own
-    stream while the next chunk's slices run) returns, chunk by chunk,
-    exactly what features_pass returns per chunk -- ragged chunks and slices."""
-    from moseq2_detectron_extract_amd import synth
-    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
-    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
-    s = synth.SyntheticSession(150, seed=12)
-    raw = torch.from_numpy(s.frames(0, 150)).cuda()
-    cuts = [(0, 48), (48, 95), (95, 150)]  # 3, 3 (ragged) and 4 (ragged) slices of 16
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0))
-    cfg = ExtractConfig(batch_size=16)
-    want = [GPUExtractor(s.bground_im, s.roi, pred, cfg).features_pass(raw[a:b]) for a, b in cuts]
-    torch.cuda.synchronize()
-    ex = GPUExtractor(s.bground_im, s.roi, pred, cfg)
-    got = list(ex.features_passes((np.arange(a, b), raw[a:b]) for a, b in cuts))
-    torch.cuda.synchronize()
-    assert [int(g[0][0]) for g in got] == [a for a, _ in cuts]
-    for (_, s1, h1), (s0, h0) in zip(got, want):
-        for k in ("centroid", "orientation", "axis_length", "keypoints", "centers"):
-            np.testing.assert_array_equal(h1[k], h0[k], err_msg=k)
-        for k in ("prepped", "d2", "cleaned"):
-            assert torch.equal(s1[k], s0[k]), k
-        np.testing.assert_array_equal(s1["nkeep"], s0["nkeep"])
-        for k in ("keypoints", "keep_idx", "sel_keypoints"):
-            assert torch.equal(s1["inf"][k], s0["inf"][k]), k
-        assert torch.equal(torch.cat(s1["inf"]["masks"]), torch.cat(s0["inf"]["masks"]))
-
-
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 1 and c[7] == 0])
 def test_conv2d_fp32_pointwise_instances(mdx, case):
     """fp32 pointwise layers (1x1, unpadded, stride 1 or 2) on k_conv's PW

@@ -36,18 +36,6 @@ def main():
         # warm-up on a short prefix (model plans, allocator)
         extract_session(path, s.bground_im, s.roi, pred, ExtractConfig(chunk_size=64, use_tracking=False),
                         true_depth=s.true_depth, frame_trim=(0, n - 64))
-        if os.environ.get("EXTRACT_AB"):  # cross-chunk pipeline A/B with the writers on (the bench secondary's shape)
-            for rep in range(2):
-                for cross in (False, True):
-                    torch.cuda.synchronize()
-                    t0 = time.perf_counter()
-                    out = extract_session(path, s.bground_im, s.roi, pred,
-                                          ExtractConfig(chunk_size=chunk, use_tracking=True, cross_chunk=cross),
-                                          true_depth=s.true_depth, output_dir=os.path.join(td, f"out{rep}{int(cross)}"))
-                    torch.cuda.synchronize()
-                    res[f"writers_cross{int(cross)}_fps_{rep}"] = round(n / (time.perf_counter() - t0), 1)
-                    print(json.dumps(res), flush=True)
-            return
         for rep in range(int(os.environ.get("EXTRACT_REPS", "2"))):
             for overlap in (True,) if os.environ.get("EXTRACT_OVERLAP_ONLY") else (False, True):
                 for tracking in (False, True):
