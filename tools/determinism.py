@@ -1,7 +1,7 @@
 """Soak test of the stream-pipelined loop: every output of OverlappedExtractor
 (5 streams, two forwards in flight, frame stages beside them) compared bit
 for bit with the serial step on the same batch, over many steps.
-Usage: python tools/determinism.py [fp32|fp16] [steps] [batch]"""
+Usage: python tools/determinism.py [fp32|fp16] [steps] [batch] [model_streams]"""
 import json
 import os
 import sys
@@ -15,6 +15,7 @@ def main():
     dtype = sys.argv[1] if len(sys.argv) > 1 else "fp32"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+    ms = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     import torch
     import mdx_pkg
     mdx_pkg.load()
@@ -33,7 +34,7 @@ def main():
         r = ex.step_device(b)
         torch.cuda.synchronize()
         want.append({k: r[k].clone() for k in keys})
-    pipe = OverlappedExtractor(ex, 2)
+    pipe = OverlappedExtractor(ex, ms)
     pipe.prime(batches[0])
     bad, done, t0 = [], 0, time.time()
 
