@@ -162,14 +162,17 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 22: "k_conv_sbg<128> register-staged implicit GEMM, single LDS stage",
                 23: "k_conv_sbg<64> register-staged implicit GEMM, single LDS stage",
                 24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance"}
+# the transforms: one instance per Winograd tile size the default policy runs
+# (F(6,3) on the large maps, F(4,3) on the rest)
 KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
-                               12: "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf",
-                               13: "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf"})
-KERNEL_DEMANGLED.update({
-    "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE": "void mdx::k_conv1x1_stream_f32<4>(mdx::ConvArgs)",
-    "_ZN3mdx9k_wino_inILi4EEEvPKfiiiiiiPf": "void mdx::k_wino_in<4>(float const*, int, int, int, int, int, int, float*)",
-    "_ZN3mdx10k_wino_outILi4EEEvPKfiiiiiiS2_iPf":
-        "void mdx::k_wino_out<4>(float const*, int, int, int, int, int, int, float const*, int, float*)"})
+                               12: tuple(f"_ZN3mdx9k_wino_inILi{m}EEEvPKfiiiiiiPf" for m in (4, 6)),
+                               13: tuple(f"_ZN3mdx10k_wino_outILi{m}EEEvPKfiiiiiiS2_iPf" for m in (4, 6))})
+KERNEL_DEMANGLED["_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE"] = "void mdx::k_conv1x1_stream_f32<4>(mdx::ConvArgs)"
+for _m in (4, 6):
+    KERNEL_DEMANGLED[f"_ZN3mdx9k_wino_inILi{_m}EEEvPKfiiiiiiPf"] = \
+        f"void mdx::k_wino_in<{_m}>(float const*, int, int, int, int, int, int, float*)"
+    KERNEL_DEMANGLED[f"_ZN3mdx10k_wino_outILi{_m}EEEvPKfiiiiiiS2_iPf"] = \
+        f"void mdx::k_wino_out<{_m}>(float const*, int, int, int, int, int, int, float const*, int, float*)"
 TRANSFORMS = (12, 13)  # records whose "flop" field holds algorithmic HBM bytes
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
@@ -223,6 +226,13 @@ def _pmc(dtype):
 
 
 def _pmc_bytes(kern, sym):
+    """PMC HBM bytes per launch of a kernel symbol; for a tuple of instances
+    (the Winograd transforms of both tile sizes) the launch-weighted mean."""
+    if isinstance(sym, tuple):
+        recs = [kern.get(s) or kern.get(KERNEL_DEMANGLED.get(s, ""), {}) for s in sym]
+        recs = [r for r in recs if r.get("hbm_bytes_per_launch") is not None]
+        n = sum(r.get("launches_per_step", 0) for r in recs)
+        return sum(r["hbm_bytes_per_launch"] * r.get("launches_per_step", 0) for r in recs) / n if n else None
     rec = kern.get(sym) or kern.get(KERNEL_DEMANGLED.get(sym, ""), {})
     return rec.get("hbm_bytes_per_launch")
 

@@ -252,7 +252,7 @@ int mdx_conv_fp32_split(void);
 /* Tuning knob: 1 (default) runs every split-plane launch on the 64-wide N
  * tile (two workgroups per CU), 0 the 128-wide tile where Cout > 64. */
 int mdx_conv_set_x3_narrow(int on);
-/* Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride-1 / pad-1
+/* Winograd F(m x m, 3x3), m = 2, 4 or 6, for fp32 3x3 / stride-1 / pad-1
  * convolutions (NHWC): the algorithm the model handle uses for such layers
  * with Cin >= 256 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
  * 3x3 convs).  weights: w float32 OIHW [Cout][Cin][3][3] -> U float32
@@ -260,13 +260,17 @@ int mdx_conv_set_x3_narrow(int on);
  * above, bias [Cout] or NULL, optional ReLU -> out (N,H,W,Cout); workspace
  * (16-B aligned) >= mdx_winograd_workspace_bytes.  Cin % 4 == 0, Cout % 8 == 0.
  * set_winograd: the model handle's policy (0 off (direct), 2 F(2x2,3x3),
- * 4 F(4x4,3x3) default); returns the old one. */
+ * 4 F(4x4,3x3), 6 F(6x6,3x3) on the layers where winograd_tile picks it and
+ * F(4x4,3x3) on the rest (default)); returns the old one.  winograd_tile: the m
+ * a policy runs an H x W layer with (policy 6: 6 where the 8x8 tiles execute
+ * under 0.9x the tile products of F(4,3)'s 6x6, else 4). */
 int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U);
 int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m);
 int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias, int Cout,
                          int relu, int m, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
+int mdx_winograd_tile(int H, int W, int mode);
 /* Minimum Cin of the layers the model handle runs on Winograd (default 128;
  * handles pack the transformed weights of the fp32 3x3 layers with Cin >= 128). */
 int mdx_conv_set_winograd_min_cin(int cin);

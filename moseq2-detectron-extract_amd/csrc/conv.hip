@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(X6_THREADS, 1) void k_gemm_x6(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Winograd F(m x m, 3x3), m = 2 or 4, for fp32 3x3 / stride 1 / pad 1
+// Winograd F(m x m, 3x3), m = 2, 4 or 6, for fp32 3x3 / stride 1 / pad 1
 // convolutions (NHWC), a = m + 2:
 //   V[xi][t][c] = (B^T d B)[xi] of the a x a input patch of output tile t
 //   M[xi][t][k] = sum_c V[xi][t][c] U[xi][k][c]   (a*a batched GEMMs)
@@ -1726,7 +1726,9 @@ __global__ __launch_bounds__(X6_THREADS, 1) void k_gemm_x6(ConvArgs a) {
 // with U = G g G^T packed once per layer.  F(2,3): 2.25x fewer multiplies,
 // transforms of 0/+-1 coefficients (error ~7e-7 relative in fp32 on
 // 256-channel layers vs ~4e-7 direct); F(4,3): 4x fewer, coefficients up to
-// 8 (Lavin's points 0, +-1, +-2; error ~1e-5).
+// 8 (Lavin's points 0, +-1, +-2; error ~1e-5); F(6,3): 5.06x fewer on whole
+// tiles, points 0, +-1, +-2, +-1/2 (coefficients up to 32; error ~2x F(4,3)'s),
+// used on the large maps where its 8x8 tiles waste little at the edges.
 // ---------------------------------------------------------------------------
 template <int M>
 struct WinoT;
@@ -1752,6 +1754,26 @@ struct WinoT<4> {
     }
     __device__ static constexpr float AT(int i, int j) {
         constexpr float t[4][6] = {{1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+        return t[i][j];
+    }
+};
+template <>
+struct WinoT<6> {
+    static constexpr int A = 8;
+    __device__ static constexpr float BT(int i, int j) {
+        constexpr float t[8][8] = {{1, 0, -5.25f, 0, 5.25f, 0, -1, 0},       {0, 1, 1, -4.25f, -4.25f, 1, 1, 0},
+                                   {0, -1, 1, 4.25f, -4.25f, -1, 1, 0},      {0, 0.5f, 0.25f, -2.5f, -1.25f, 2, 1, 0},
+                                   {0, -0.5f, 0.25f, 2.5f, -1.25f, -2, 1, 0}, {0, 2, 4, -2.5f, -5, 0.5f, 1, 0},
+                                   {0, -2, 4, 2.5f, -5, -0.5f, 1, 0},        {0, -1, 0, 5.25f, 0, -5.25f, 0, 1}};
+        return t[i][j];
+    }
+    __device__ static constexpr float AT(int i, int j) {
+        constexpr float t[6][8] = {{1, 1, 1, 1, 1, 1, 1, 0},
+                                   {0, 1, -1, 2, -2, 0.5f, -0.5f, 0},
+                                   {0, 1, 1, 4, 4, 0.25f, 0.25f, 0},
+                                   {0, 1, -1, 8, -8, 0.125f, -0.125f, 0},
+                                   {0, 1, 1, 16, 16, 0.0625f, 0.0625f, 0},
+                                   {0, 1, -1, 32, -32, 0.03125f, -0.03125f, 1}};
         return t[i][j];
     }
 };
@@ -2442,7 +2464,7 @@ extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
 // ---------------------------------------------------------------------------
 // Winograd F(m x m, 3x3) host side
 // ---------------------------------------------------------------------------
-static int g_winograd = 4;
+static int g_winograd = 6;
 extern "C" int mdx_conv_set_winograd(int mode) {
     const int old = g_winograd;
     g_winograd = mode;
@@ -2470,7 +2492,7 @@ extern "C" int mdx_conv_set_winograd_dma(int mode, int min_wgs) {
 }
 
 extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U) {
-    MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4), "mdx_winograd_weights: bad args");
+    MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4 || m == 6), "mdx_winograd_weights: bad args");
     // U = G g G^T (in double, rounded once)
     static const double G2[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
     static const double G4[6][3] = {{1.0 / 4, 0, 0},
@@ -2479,13 +2501,21 @@ extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, fl
                                     {1.0 / 24, 1.0 / 12, 1.0 / 6},
                                     {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                     {0, 0, 1}};
+    static const double G6[8][3] = {{1, 0, 0},
+                                    {-2.0 / 9, -2.0 / 9, -2.0 / 9},
+                                    {-2.0 / 9, 2.0 / 9, -2.0 / 9},
+                                    {1.0 / 90, 1.0 / 45, 2.0 / 45},
+                                    {1.0 / 90, -1.0 / 45, 2.0 / 45},
+                                    {32.0 / 45, 16.0 / 45, 8.0 / 45},
+                                    {32.0 / 45, -16.0 / 45, 8.0 / 45},
+                                    {0, 0, 1}};
     const int A = m + 2;
-    auto G = [&](int i, int j) { return m == 2 ? G2[i][j] : G4[i][j]; };
+    auto G = [&](int i, int j) { return m == 2 ? G2[i][j] : m == 4 ? G4[i][j] : G6[i][j]; };
     const long long plane = (long long)Cout * Cin;
     for (int o = 0; o < Cout; ++o)
         for (int i = 0; i < Cin; ++i) {
             const float *g = w + ((long long)o * Cin + i) * 9;
-            double tg[6][3];
+            double tg[8][3];
             for (int a = 0; a < A; ++a)
                 for (int c = 0; c < 3; ++c) tg[a][c] = G(a, 0) * g[0 * 3 + c] + G(a, 1) * g[1 * 3 + c] + G(a, 2) * g[2 * 3 + c];
             for (int a = 0; a < A; ++a)
@@ -2497,9 +2527,18 @@ extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, fl
 }
 
 extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m) {
-    if (m != 2 && m != 4) return -1;
+    if (m != 2 && m != 4 && m != 6) return -1;
     const long long T = (long long)N * ((H + m - 1) / m) * ((W + m - 1) / m);
     return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
+}
+
+// policy 6: F(6,3) where its 8x8 tiles execute under 0.9x the tile products
+// of F(4,3)'s 6x6 (the large maps; edge tiles of the small ones waste the
+// gain), else F(4,3)
+extern "C" int mdx_winograd_tile(int H, int W, int mode) {
+    if (mode != 6) return mode;
+    const long long p6 = 64ll * ((H + 5) / 6) * ((W + 5) / 6), p4 = 36ll * ((H + 3) / 4) * ((W + 3) / 4);
+    return 10 * p6 < 9 * p4 ? 6 : 4;
 }
 
 static thread_local WinoProbe *t_wino_probe = nullptr;
@@ -2509,7 +2548,7 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
                                     int Cout, int relu, int m, float *out, void *workspace, int64_t workspace_bytes,
                                     mdx_stream_t stream) {
     MDX_REQUIRE(x && U && out && workspace, "mdx_conv3x3_winograd: null pointer");
-    MDX_REQUIRE(m == 2 || m == 4, "mdx_conv3x3_winograd: tile m must be 2 or 4");
+    MDX_REQUIRE(m == 2 || m == 4 || m == 6, "mdx_conv3x3_winograd: tile m must be 2, 4 or 6");
     MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cin % 4 == 0 && Cout % 8 == 0,
                 "mdx_conv3x3_winograd: Cin %% 4 == 0 and Cout %% 8 == 0 required");
     MDX_REQUIRE(workspace_bytes >= mdx_winograd_workspace_bytes(N, H, W, Cin, Cout, m),
@@ -2539,8 +2578,10 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         const dim3 grid = tgrid(Cin, bd);
         if (m == 2)
             hipLaunchKernelGGL(k_wino_in<2>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
-        else
+        else if (m == 4)
             hipLaunchKernelGGL(k_wino_in<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
+        else
+            hipLaunchKernelGGL(k_wino_in<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
     }
     mark(1);
     mark(2);
@@ -2613,8 +2654,10 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         const dim3 grid2 = tgrid(Cout, bd);
         if (m == 2)
             hipLaunchKernelGGL(k_wino_out<2>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
-        else
+        else if (m == 4)
             hipLaunchKernelGGL(k_wino_out<4>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
+        else
+            hipLaunchKernelGGL(k_wino_out<6>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
     }
     mark(5);
     if (probe) probe->gemm_kernel = gemm_kernel;

@@ -51,7 +51,7 @@ struct ConvW {
     int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, kalg = 0;
     // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
     // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 128)
-    float *wino2 = nullptr, *wino4 = nullptr;
+    float *wino2 = nullptr, *wino4 = nullptr, *wino6 = nullptr;
     // fp32 Linear layers: the weights split once into bf16 planes for
     // mdx_gemm_x6 (used while mdx_conv_fp32_split() != 0)
     void *x6 = nullptr;
@@ -276,6 +276,9 @@ struct Packer {
             u.resize((size_t)36 * co * ci);
             mdx_winograd_weights(oihw.data(), co, ci, 4, u.data());
             c.wino4 = upload_f32(u);
+            u.resize((size_t)64 * co * ci);
+            mdx_winograd_weights(oihw.data(), co, ci, 6, u.data());
+            c.wino6 = upload_f32(u);
         }
         return c;
     }
@@ -576,8 +579,8 @@ struct Fwd {
         OW = (W + 2 * cw.pad - cw.k) / cw.stride + 1;
         const size_t oes = out_f32 ? 4 : m.es;
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
-        const int wm = mdx_conv_winograd_enabled();
-        const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : nullptr;
+        const int wm = mdx_winograd_tile(H, W, mdx_conv_winograd_enabled());
+        const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : wm == 6 ? cw.wino6 : nullptr;
         const bool wino = wu && !residual && out_mode == 0 && cw.cin >= mdx_conv_winograd_min_cin();
         if (wino) {
             const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout, wm);

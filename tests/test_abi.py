@@ -52,3 +52,42 @@ def test_no_gpu_means_loud_failure(mdx):
     from moseq2_detectron_extract_amd import MdxError, proc
     with pytest.raises(MdxError):
         proc.clean_frames(np.zeros((1, 8, 8), np.uint8), iters_tail=1)
+
+
+@pytest.mark.parametrize("m", [2, 4, 6])
+def test_winograd_weight_transform_host(mdx, m):
+    """mdx_winograd_weights (a host function): U = G g G^T for F(m x m, 3x3),
+    checked by running one m x m output tile through the transform algebra in
+    fp64 (Y = A^T [U . (B^T d B)] A, B^T / A^T the kernels' matrices, Lavin's
+    points; F(6,3): 0, +-1, +-2, +-1/2) against the direct 3x3 correlation;
+    and the policy-6 tile choice per map size."""
+    import ctypes
+    import numpy as np
+    from moseq2_detectron_extract_amd._lib import call
+    BT = {2: [[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]],
+          4: [[4, 0, -5, 0, 1, 0], [0, -4, -4, 1, 1, 0], [0, 4, -4, -1, 1, 0], [0, -2, -1, 2, 1, 0],
+              [0, 2, -1, -2, 1, 0], [0, 4, 0, -5, 0, 1]],
+          6: [[1, 0, -5.25, 0, 5.25, 0, -1, 0], [0, 1, 1, -4.25, -4.25, 1, 1, 0], [0, -1, 1, 4.25, -4.25, -1, 1, 0],
+              [0, .5, .25, -2.5, -1.25, 2, 1, 0], [0, -.5, .25, 2.5, -1.25, -2, 1, 0], [0, 2, 4, -2.5, -5, .5, 1, 0],
+              [0, -2, 4, 2.5, -5, -.5, 1, 0], [0, -1, 0, 5.25, 0, -5.25, 0, 1]]}[m]
+    AT = {2: [[1, 1, 1, 0], [0, 1, -1, -1]],
+          4: [[1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, 0], [0, 1, 1, 4, 4, 0], [0, 1, -1, 8, -8, 1]],
+          6: [[1, 1, 1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, .5, -.5, 0], [0, 1, 1, 4, 4, .25, .25, 0],
+              [0, 1, -1, 8, -8, .125, -.125, 0], [0, 1, 1, 16, 16, .0625, .0625, 0],
+              [0, 1, -1, 32, -32, .03125, -.03125, 1]]}[m]
+    BT, AT = np.array(BT, float), np.array(AT, float)
+    a, Cout, Cin = m + 2, 3, 5
+    rng = np.random.default_rng(m)
+    w = rng.standard_normal((Cout, Cin, 3, 3)).astype(np.float32)
+    U = np.empty((a * a, Cout, Cin), np.float32)
+    call("mdx_winograd_weights", w.ctypes.data_as(ctypes.c_void_p), Cout, Cin, m, U.ctypes.data_as(ctypes.c_void_p))
+    U = U.reshape(a, a, Cout, Cin).astype(np.float64)
+    d = rng.standard_normal((Cin, a, a))
+    V = np.einsum("ij,cjk,lk->ilc", BT, d, BT)
+    Y = np.einsum("ij,jko,lk->oil", AT, np.einsum("jkoc,jkc->jko", U, V), AT)
+    want = np.array([[[np.sum(w[o].astype(np.float64) * d[:, y:y + 3, x:x + 3]) for x in range(m)]
+                      for y in range(m)] for o in range(Cout)])
+    np.testing.assert_allclose(Y, want, rtol=0, atol=1e-5 * np.abs(want).max())
+    assert call("mdx_winograd_tile", 112, 128, 6) == 6 and call("mdx_winograd_tile", 56, 64, 6) == 6
+    assert call("mdx_winograd_tile", 28, 32, 6) == 4 and call("mdx_winograd_tile", 7, 7, 6) == 4
+    assert call("mdx_winograd_tile", 112, 128, 4) == 4 and call("mdx_winograd_tile", 5, 5, 2) == 2

@@ -780,14 +780,16 @@ def test_extract_session_from_dat(mdx, tmp_path):
 
 
 @pytest.mark.parametrize("split", [0, 6, -1], ids=["f32-mfma", "bf16x6", "f32-dma256"])
-@pytest.mark.parametrize("m", [2, 4])
+@pytest.mark.parametrize("m", [2, 4, 6])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
-                                                 (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True)])
+                                                 (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True),
+                                                 (2, 56, 64, 256, 256, True)])
 def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     """Winograd F(m x m, 3x3) (fp32: input transform, (m+2)^2 batched GEMMs,
     output transform + bias + ReLU) against the fp64 direct convolution:
     within the fp32 direct kernels' tolerance (1e-4 relative to the output
-    scale; F(2,3) ~1e-6, F(4,3) ~1e-5), ragged sizes exercise partial tiles."""
+    scale; F(2,3) ~1e-6, F(4,3) ~1e-5, F(6,3) ~2e-5), ragged sizes exercise
+    partial tiles."""
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
     g = torch.Generator().manual_seed(N * 1000 + H)

@@ -166,12 +166,14 @@ def _oracle(depth, B):
     return res
 
 
-@pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 2, 0),
+@pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 6, 0),
+                                                      (50, 32, "fp32", 2, 0),
                                                       (50, 32, "fp32", 0, 0), (50, 32, "fp32", 4, 6),
                                                       (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0)])
 def test_forward_full_frame(mdx, depth, B, dtype, wino, split):
     """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
-    2 = F(2x2,3x3), 0 = direct); split: the fp32 layers as exact bf16 plane
+    6 = F(6x6,3x3) on the large maps and F(4x4,3x3) elsewhere, 2 = F(2x2,3x3),
+    0 = direct); split: the fp32 layers as exact bf16 plane
     products (mdx_conv_set_fp32_split, 0 = the f32 MFMA kernels); the same
     fp32 tolerances hold for all."""
     from moseq2_detectron_extract_amd._lib import call

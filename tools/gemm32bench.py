@@ -1,6 +1,7 @@
 """fp32 convolution GEMMs of the R50-FPN B=32 forward, one launch shape at a
 time, HIP events over 10 launches: the direct layers through
-mdx_conv2d_splitk and the 3x3 layers through mdx_conv3x3_winograd (F(4,3);
+mdx_conv2d_splitk and the 3x3 layers through mdx_conv3x3_winograd (the tile
+the library's Winograd policy picks per layer, mdx_winograd_tile; the
 GEMM timed apart from the transforms by the model's profiling hook is not
 available here, so the whole layer is timed).  Knobs: name=value calls
 mdx_conv_set_<name>(value) first.
@@ -46,7 +47,9 @@ def main():
         name, val = kv.split("=")
         call(f"mdx_conv_set_{name}", *[int(v) for v in val.split(",")])
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-    need = max([call("mdx_winograd_workspace_bytes", N, H, W, Ci, Co, 4) for N, H, W, Ci, Co, _ in WINO] + [1 << 28])
+    policy = call("mdx_conv_winograd_enabled") or 4
+    need = max([call("mdx_winograd_workspace_bytes", N, H, W, Ci, Co, call("mdx_winograd_tile", H, W, policy))
+                for N, H, W, Ci, Co, _ in WINO] + [1 << 28])
     ws = torch.empty(need, dtype=torch.uint8, device="cuda")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kid, ks = ctypes.c_int(), ctypes.c_int()
@@ -62,7 +65,7 @@ def main():
         return e0.elapsed_time(e1) / reps * 1e-3
 
     res = {"direct": [], "winograd": []}
-    tot = 0.0
+    tot = wtot = 0.0
     for N, H, W, Cin, Cout, k, s, p, r, cnt in DIRECT:
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N, H, W, Cin, device="cuda")
@@ -85,23 +88,28 @@ def main():
     for N, H, W, Cin, Cout, cnt in WINO:
         x = torch.randn(N, H, W, Cin, device="cuda")
         w = torch.randn(Cout, Cin, 3, 3) / (9 * Cin) ** 0.5
-        U = torch.empty(36 * Cout * Cin)
-        call("mdx_winograd_weights", P(w), Cout, Cin, 4, P(U))
+        m = call("mdx_winograd_tile", H, W, policy)
+        U = torch.empty((m + 2) ** 2 * Cout * Cin)
+        call("mdx_winograd_weights", P(w), Cout, Cin, m, P(U))
         U = U.cuda()
         b = torch.randn(Cout, device="cuda")
         out = torch.empty(N, H, W, Cout, device="cuda")
-        T = N * ((H + 3) // 4) * ((W + 3) // 4)
-        gfl = 2.0 * 36 * T * Cin * Cout
+        T = N * ((H + m - 1) // m) * ((W + m - 1) // m)
+        gfl = 2.0 * (m + 2) ** 2 * T * Cin * Cout
 
         def go():
-            call("mdx_conv3x3_winograd", P(x), N, H, W, Cin, P(U), P(b), Cout, 1, 4, P(out), P(ws), ws.numel(), None)
+            call("mdx_conv3x3_winograd", P(x), N, H, W, Cin, P(U), P(b), Cout, 1, m, P(out), P(ws), ws.numel(), None)
         t = timeit(go)
         tot += t * cnt
-        res["winograd"].append({"N": N, "H": H, "W": W, "Cin": Cin, "Cout": Cout, "us": round(t * 1e6, 1),
+        wtot += t * cnt
+        res["winograd"].append({"N": N, "H": H, "W": W, "Cin": Cin, "Cout": Cout, "m": m, "us": round(t * 1e6, 1),
                                 "gemm_tflops_if_all_gemm": round(gfl / t / 1e12, 1), "count": cnt})
         print(json.dumps(res["winograd"][-1]), flush=True)
     res["weighted_ms_per_forward"] = round(tot * 1e3, 3)
-    print(json.dumps({"weighted_ms_per_forward": res["weighted_ms_per_forward"], "knobs": sys.argv[1:]}), flush=True)
+    res["winograd_layers_ms_per_forward"] = round(wtot * 1e3, 3)
+    print(json.dumps({"weighted_ms_per_forward": res["weighted_ms_per_forward"],
+                      "winograd_layers_ms_per_forward": res["winograd_layers_ms_per_forward"],
+                      "policy": policy, "knobs": sys.argv[1:]}), flush=True)
 
 
 if __name__ == "__main__":
