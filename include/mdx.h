@@ -254,7 +254,7 @@ int mdx_conv_fp32_split(void);
 int mdx_conv_set_x3_narrow(int on);
 /* Winograd F(m x m, 3x3), m = 2, 4 or 6, for fp32 3x3 / stride-1 / pad-1
  * convolutions (NHWC): the algorithm the model handle uses for such layers
- * with Cin >= 256 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
+ * with Cin >= 64 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
  * 3x3 convs).  weights: w float32 OIHW [Cout][Cin][3][3] -> U float32
  * [(m+2)^2][Cout][Cin] (host function).  conv: x float32 (N,H,W,Cin), U as
  * above, bias [Cout] or NULL, optional ReLU -> out (N,H,W,Cout); workspace
@@ -271,8 +271,9 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
 int mdx_winograd_tile(int H, int W, int mode);
-/* Minimum Cin of the layers the model handle runs on Winograd (default 128;
- * handles pack the transformed weights of the fp32 3x3 layers with Cin >= 128). */
+/* Minimum Cin of the layers the model handle runs on Winograd (default 64,
+ * so res2's 64-channel 3x3 layers run F(6,3) too; handles pack the
+ * transformed weights of the fp32 3x3 layers with Cin >= 64). */
 int mdx_conv_set_winograd_min_cin(int cin);
 int mdx_conv_winograd_min_cin(void);
 /* Winograd GEMMs with Cout % 256 == 0 and Cin % 32 == 0 on the 256x256

@@ -265,7 +265,7 @@ struct Packer {
         c.k = kh;
         c.stride = stride;
         c.pad = pad;
-        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 128 && ci % 4 == 0 && co % 8 == 0 &&
+        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 64 && ci % 4 == 0 && co % 8 == 0 &&
             err.empty()) {
             std::vector<float> oihw((size_t)co * ci * 9), u((size_t)16 * co * ci);
             for (int o = 0; o < co; ++o)
