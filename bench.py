@@ -131,10 +131,11 @@ for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  #
     _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
     KERNEL_SYMBOLS["fp32"][_k] = _m
     KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
-for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<float, float, BN>: single stage, general layers
-    _m = f"_ZN3mdx10k_conv_sbgIffLi{_bn}EEEvNS_8ConvArgsE"
-    KERNEL_SYMBOLS["fp32"][_k] = _m
-    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sbg<float, float, {_bn}>(mdx::ConvArgs)"
+for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<T, T, BN>: single stage, general layers
+    for _dt, _mt, _dm in (("fp32", "ff", "float, float"), ("fp16", "DF16_DF16_", "_Float16, _Float16")):
+        _m = f"_ZN3mdx10k_conv_sbgI{_mt}Li{_bn}EEEvNS_8ConvArgsE"
+        KERNEL_SYMBOLS[_dt][_k] = _m
+        KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sbg<{_dm}, {_bn}>(mdx::ConvArgs)"
 for _k, (_bn, _dual, _pw) in _KCONV_IDS.items():
     for _dt, _t in (("fp32", "f32"), ("fp16", "f16")):
         _m, _d = _kconv(_t, _t, _bn, _dual, _pw)

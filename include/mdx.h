@@ -359,7 +359,8 @@ int mdx_conv_set_pointwise(int on);
  * instance k_conv_sb (three workgroups per CU, two barriers per K-step, the
  * same sums bit for bit as the two-stage instance): 1 fp32, 2 also the
  * fp32 KxK layers (k_conv_sbg), 3 also the fp16 register-staged pointwise
- * layers (default), 0 the two-stage instances.  Returns the old value. */
+ * layers, 4 also the fp16 register-staged KxK layers (default), 0 the
+ * two-stage instances.  Returns the old value. */
 int mdx_conv_set_single_stage(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,

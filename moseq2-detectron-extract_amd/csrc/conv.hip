@@ -1940,7 +1940,7 @@ extern "C" int mdx_conv_set_pointwise(int on) {
 // fp32 layers (k_conv_sbg: res2 conv2 306 -> 284 us, loop unchanged), 3 also
 // the fp16 register-staged PW layers (default: fp16 loop 3924 -> 4009 fps,
 // config 5 3310 -> 3320), 0 the two-stage k_conv instances
-static int g_conv_sb = 3;
+static int g_conv_sb = 4;
 extern "C" int mdx_conv_set_single_stage(int on) {
     const int old = g_conv_sb;
     g_conv_sb = on;
@@ -2288,8 +2288,10 @@ general:
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
     // (mode 3: the fp16 register-staged PW layers too; the fp16 model's big
     // layers stay on the LDS-DMA kernels)
-    const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb == 3 && in_dtype == 1 && out_dtype == 1));
-    const bool sbg = g_conv_sb >= 2 && !pw && in_dtype == 0 && out_dtype == 0;
+    // (mode 4: as 3, plus the fp16 KxK layers the LDS-DMA kernels do not take)
+    const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 3 && in_dtype == 1 && out_dtype == 1));
+    const bool sbg = g_conv_sb >= 2 && !pw &&
+                     ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb == 4 && in_dtype == 1 && out_dtype == 1));
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \

@@ -1006,6 +1006,46 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
             call(f, o)
 
 
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if not (c[5] == 1 and c[7] == 0) and c[3] % 8 == 0])
+def test_conv2d_fp16_single_stage_general(mdx, case):
+    """fp16 KxK / padded layers on the register-staged kernels (the LDS-DMA
+    tiles off): the single-stage schedule (k_conv_sbg, single_stage mode 4,
+    the default) against the two-stage kernel (mode 3) bit for bit, and
+    against the fp64 convolution within fp16 output rounding."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    N, H, W, Cin, Cout, k, s, p, use_res, relu = case
+    g = torch.Generator().manual_seed(Cin * 13 + Cout + k)
+    x = torch.randn(N, H, W, Cin, generator=g).half()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).half()
+    b = torch.randn(Cout, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = torch.randn(N, OH, OW, Cout, generator=g).half() if use_res else None
+    want = _conv_ref(x.float(), w.float(), b, s, p, res.float() if res is not None else None, relu)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    xd, bd = x.cuda(), b.cuda()
+    wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
+    rd = res.cuda() if res is not None else None
+    olds = [call("mdx_conv_set_single_stage", 3), call("mdx_conv_set_large_tiles", 0)]
+    try:
+        outs = []
+        for mode in (3, 4):
+            call("mdx_conv_set_single_stage", mode)
+            out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda", dtype=torch.float16)
+            call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 1, 1, P(out),
+                 None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            assert kid.value in ((22, 23) if mode == 4 else (0, 1)), kid.value
+            err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+            assert err < 5e-3, (mode, err)
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_large_tiles"), olds):
+            call(f, o)
+
+
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if not (c[5] == 1 and c[7] == 0) and c[3] % 4 == 0])
 def test_conv2d_fp32_single_stage_general(mdx, case):
     """General fp32 layers (KxK / padded: the stem's shape, 3x3 / 7x7 with
