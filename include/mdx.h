@@ -362,6 +362,9 @@ int mdx_conv_set_pointwise(int on);
  * layers, 4 also the fp16 register-staged KxK layers (default), 0 the
  * two-stage instances.  Returns the old value. */
 int mdx_conv_set_single_stage(int on);
+/* Resident workgroups the split-K slice model assumes for the register-staged
+ * kernels (default 512 = two per CU); returns the old value. */
+int mdx_conv_set_ksplit_slots(int slots);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,

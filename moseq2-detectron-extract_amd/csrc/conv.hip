@@ -2017,6 +2017,15 @@ extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
     return old;
 }
 
+// resident workgroups the split-K model assumes for the register-staged
+// kernels (512: two per CU)
+static long long g_ks_slots = 512;
+extern "C" int mdx_conv_set_ksplit_slots(int slots) {
+    const int old = (int)g_ks_slots;
+    g_ks_slots = slots > 0 ? slots : 512;
+    return old;
+}
+
 // split-K slice count for a launch of `tiles` output tiles and nk K-steps:
 // minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
 // with `slots` resident workgroups (2 on each of the 256 CUs; 1 for k_conv_x3)
@@ -2263,7 +2272,7 @@ general:
     a.tiles_total = tiles_m * tiles_n;
     const int nk = (a.K + (in_dtype == 1 ? 64 : 32) - 1) / (in_dtype == 1 ? 64 : 32);
     if (ksplit <= 0)
-        ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes, x3 ? 256 : 512)
+        ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes, x3 ? 256 : g_ks_slots)
                                               : 1;
     MDX_REQUIRE(ksplit == 1 || (workspace && Cout % 8 == 0 && (long long)ksplit * M * Cout * 4 <= workspace_bytes),
                 "mdx_conv2d: split-K needs Cout %% 8 == 0 and a workspace of ksplit*M*Cout*4 bytes");
@@ -2416,7 +2425,7 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
     a.tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_total = (int)(ceil_div(M, BM) * a.tiles_n);
     const int nk = (a.K + BKd - 1) / BKd;
-    int ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes) : 1;
+    int ksplit = (workspace && Cout % 8 == 0) ? choose_ksplit(a.tiles_total, nk, M, Cout, workspace_bytes, g_ks_slots) : 1;
     ksplit = ksplit > nk ? nk : ksplit;
     a.ksteps = (nk + ksplit - 1) / ksplit;
     a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
