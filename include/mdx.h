@@ -271,6 +271,9 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
 int mdx_winograd_tile(int H, int W, int mode);
+/* Policy 6's threshold in percent (default 90: F(6,3) where its tile products
+ * are under 0.9x F(4,3)'s); returns the old value. */
+int mdx_conv_set_winograd6_ratio(int pct);
 /* Minimum Cin of the layers the model handle runs on Winograd (default 64,
  * so res2's 64-channel 3x3 layers run F(6,3) too; handles pack the
  * transformed weights of the fp32 3x3 layers with Cin >= 64). */

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mdx_conv_set_winograd": (I32, [I32]),
     "mdx_conv_winograd_enabled": (I32, []),
     "mdx_winograd_tile": (I32, [I32, I32, I32]),
+    "mdx_conv_set_winograd6_ratio": (I32, [I32]),
     "mdx_conv_set_ksplit_slots": (I32, [I32]),
     "mdx_conv_set_winograd_min_cin": (I32, [I32]),
     "mdx_conv_winograd_min_cin": (I32, []),

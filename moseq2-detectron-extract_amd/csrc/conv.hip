@@ -2547,10 +2547,16 @@ extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, in
 // policy 6: F(6,3) where its 8x8 tiles execute under 0.9x the tile products
 // of F(4,3)'s 6x6 (the large maps; edge tiles of the small ones waste the
 // gain), else F(4,3)
+static int g_wino6_pct = 90;
+extern "C" int mdx_conv_set_winograd6_ratio(int pct) {
+    const int old = g_wino6_pct;
+    g_wino6_pct = pct;
+    return old;
+}
 extern "C" int mdx_winograd_tile(int H, int W, int mode) {
     if (mode != 6) return mode;
     const long long p6 = 64ll * ((H + 5) / 6) * ((W + 5) / 6), p4 = 36ll * ((H + 3) / 4) * ((W + 3) / 4);
-    return 10 * p6 < 9 * p4 ? 6 : 4;
+    return 100 * p6 < g_wino6_pct * p4 ? 6 : 4;
 }
 
 static thread_local WinoProbe *t_wino_probe = nullptr;
