@@ -364,7 +364,7 @@ def extract_loop(args):
     n, chunk = args.extract_frames, args.extract_chunk
     workers = max(1, min(16, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", 16))))
     s = synth.SyntheticSession(n, seed=9)
-    pred = Predictor.from_config(ModelConfig(depth=args.depth, score_thresh_test=0.0))
+    pred = Predictor.from_config(ModelConfig(depth=args.depth, score_thresh_test=0.0), weights="synthetic")
     cfg = ExtractConfig(chunk_size=chunk, use_tracking=True)
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         t0 = time.perf_counter()
@@ -448,7 +448,7 @@ def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
     cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
-    pred = Predictor.from_config(cfg, dtype=dtype, seed=0)
+    pred = Predictor.from_config(cfg, dtype=dtype, seed=0, weights="synthetic")
     ns = 1 if args.no_overlap else max(1, args.model_streams)
     ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B, model_streams=ns))
     pipe = OverlappedExtractor(ex, ns) if args.pipeline and not args.no_overlap else None

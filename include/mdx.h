@@ -271,9 +271,6 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
 int mdx_winograd_tile(int H, int W, int mode);
-/* Policy 6's threshold in percent (default 90: F(6,3) where its tile products
- * are under 0.9x F(4,3)'s); returns the old value. */
-int mdx_conv_set_winograd6_ratio(int pct);
 /* Minimum Cin of the layers the model handle runs on Winograd (default 64,
  * so res2's 64-channel 3x3 layers run F(6,3) too; handles pack the
  * transformed weights of the fp32 3x3 layers with Cin >= 64). */
@@ -365,9 +362,6 @@ int mdx_conv_set_pointwise(int on);
  * layers, 4 also the fp16 register-staged KxK layers (default), 0 the
  * two-stage instances.  Returns the old value. */
 int mdx_conv_set_single_stage(int on);
-/* Resident workgroups the split-K slice model assumes for the register-staged
- * kernels (default 512 = two per CU); returns the old value. */
-int mdx_conv_set_ksplit_slots(int slots);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
@@ -422,13 +416,15 @@ int mdx_rpn_set_sliced(int on);
 /* RPN find_top_rpn_proposals: per level head tensor float32 (B,H_l,W_l,A*5)
  * = [objectness(A), deltas(A*4)]; cell_anchors float32 [L][A][4].
  * out_boxes (B,post_topk,4), out_scores (B,post_topk) (logits, -inf pad),
- * out_count (B).  workspace >= mdx_rpn_workspace_bytes(B, L, pre_topk). */
+ * out_count (B).  A in 1..8.  reg_weights: RPN.BBOX_REG_WEIGHTS (wx, wy, ww, wh)
+ * of Box2BoxTransform, NULL = (1, 1, 1, 1).
+ * workspace >= mdx_rpn_workspace_bytes(B, L, pre_topk). */
 int64_t mdx_rpn_workspace_bytes(int B, int L, int pre_topk);
 int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
                       int L, int B, int A, const float *cell_anchors, float offset, int img_h, int img_w,
                       int pre_topk, int post_topk, float nms_thresh, float min_size, float clampv,
-                      float *out_boxes, float *out_scores, int *out_count, void *workspace,
-                      mdx_stream_t stream);
+                      const float *reg_weights, float *out_boxes, float *out_scores, int *out_count,
+                      void *workspace, mdx_stream_t stream);
 
 /* ROIPooler(ROIAlignV2): rois float32 (R,4) XYXY, R = B*per_image, rows with
  * index >= counts[b] produce zeros.  out (R,P,P,C).  dtype 0 fp32, 1 fp16
@@ -551,8 +547,8 @@ typedef struct mdx_model_cfg {
     float gn_eps;                  /* 1e-5 */
     int n_anchor_sizes;            /* 5, one per level p2..p6 */
     float anchor_sizes[5];         /* 32 64 128 256 512 */
-    int n_aspect_ratios;           /* 3 */
-    float aspect_ratios[4];        /* 0.5 1 2 */
+    int n_aspect_ratios;           /* 3 (1..8, the same at every level) */
+    float aspect_ratios[8];        /* 0.5 1 2 */
     float anchor_offset;           /* 0 */
     int rpn_pre_nms_topk;          /* PRE_NMS_TOPK_TEST 1000 */
     int rpn_post_nms_topk;         /* POST_NMS_TOPK_TEST 1000 */
@@ -584,6 +580,7 @@ typedef struct mdx_model_cfg {
     float pixel_mean[3];           /* 1.12 x3 (M/model/config.py:141-148) */
     float pixel_std[3];            /* 5.79 x3 */
     int size_divisibility;         /* 32 */
+    float rpn_bbox_reg_weights[4]; /* RPN.BBOX_REG_WEIGHTS 1 1 1 1 */
 } mdx_model_cfg;
 
 typedef void *mdx_model_t;

@@ -66,8 +66,6 @@ SIGNATURES = {
     "mdx_conv_set_winograd": (I32, [I32]),
     "mdx_conv_winograd_enabled": (I32, []),
     "mdx_winograd_tile": (I32, [I32, I32, I32]),
-    "mdx_conv_set_winograd6_ratio": (I32, [I32]),
-    "mdx_conv_set_ksplit_slots": (I32, [I32]),
     "mdx_conv_set_winograd_min_cin": (I32, [I32]),
     "mdx_conv_winograd_min_cin": (I32, []),
     "mdx_conv_set_winograd_dma": (I32, [I32, I32]),
@@ -95,7 +93,7 @@ SIGNATURES = {
     "mdx_groupnorm": (I32, [P, I32, I32, I32, I32, I32, F32, P, P, P, I32, I32, P, P, P]),
     "mdx_rpn_workspace_bytes": (I64, [I32, I32, I32]),
     "mdx_rpn_proposals": (I32, [P, P, P, P, I32, I32, I32, P, F32, I32, I32, I32, I32, F32, F32, F32,
-                                P, P, P, P, P]),
+                                P, P, P, P, P, P]),
     "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "mdx_roi_align_ex": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P, P]),
     "mdx_roi_align_set_sorted": (I32, [I32]),

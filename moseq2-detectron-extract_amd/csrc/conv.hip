@@ -2018,13 +2018,8 @@ extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
 }
 
 // resident workgroups the split-K model assumes for the register-staged
-// kernels (512: two per CU)
-static long long g_ks_slots = 512;
-extern "C" int mdx_conv_set_ksplit_slots(int slots) {
-    const int old = (int)g_ks_slots;
-    g_ks_slots = slots > 0 ? slots : 512;
-    return old;
-}
+// kernels (512: two per CU; 384-1024 measured neutral in round 3)
+static const long long g_ks_slots = 512;
 
 // split-K slice count for a launch of `tiles` output tiles and nk K-steps:
 // minimise (block waves) x (K-steps per block + fixed cost) + reduction cost,
@@ -2547,12 +2542,7 @@ extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, in
 // policy 6: F(6,3) where its 8x8 tiles execute under 0.9x the tile products
 // of F(4,3)'s 6x6 (the large maps; edge tiles of the small ones waste the
 // gain), else F(4,3)
-static int g_wino6_pct = 90;
-extern "C" int mdx_conv_set_winograd6_ratio(int pct) {
-    const int old = g_wino6_pct;
-    g_wino6_pct = pct;
-    return old;
-}
+static const int g_wino6_pct = 90;
 extern "C" int mdx_winograd_tile(int H, int W, int mode) {
     if (mode != 6) return mode;
     const long long p6 = 64ll * ((H + 5) / 6) * ((W + 5) / 6), p4 = 36ll * ((H + 3) / 4) * ((W + 3) / 4);

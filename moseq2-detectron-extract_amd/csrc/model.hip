@@ -814,7 +814,8 @@ struct Fwd {
         if (!c.dry && ok())
             chk(mdx_rpn_proposals(heads, fh, fw, strides, 5, B, cfg.n_aspect_ratios, m.cell_anchors.data(),
                                   cfg.anchor_offset, h, w, cfg.rpn_pre_nms_topk, post, cfg.rpn_nms_thresh,
-                                  cfg.rpn_min_box_size, (float)std::log(1000.0 / 16), props, pscores, pcount, rws, s));
+                                  cfg.rpn_min_box_size, (float)std::log(1000.0 / 16), cfg.rpn_bbox_reg_weights, props,
+                                  pscores, pcount, rws, s));
         name("proposals", props, B, post, 4, 1, 0);
         name("proposal_scores", pscores, B, post, 1, 1, 0);
         name("proposal_count", pcount, B, 1, 1, 1, 2);
@@ -944,8 +945,13 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     MDX_REQUIRE(cfg->depth == 50 || cfg->depth == 101, "mdx_model_create: depth must be 50 or 101");
     MDX_REQUIRE(cfg->dtype == 0 || cfg->dtype == 1, "mdx_model_create: dtype must be 0 (f32) or 1 (f16)");
     MDX_REQUIRE(cfg->num_classes == 1, "mdx_model_create: the extraction model has one class (NUM_CLASSES=1)");
-    MDX_REQUIRE(cfg->n_anchor_sizes == 5 && cfg->n_aspect_ratios >= 1 && cfg->n_aspect_ratios <= 4,
-                "mdx_model_create: 5 anchor sizes (p2..p6) and 1..4 aspect ratios");
+    MDX_REQUIRE(cfg->n_anchor_sizes == 5 && cfg->n_aspect_ratios >= 1 && cfg->n_aspect_ratios <= 8,
+                "mdx_model_create: 5 anchor sizes (one per level p2..p6) and 1..8 aspect ratios");
+    MDX_REQUIRE(cfg->rpn_bbox_reg_weights[0] > 0.f && cfg->rpn_bbox_reg_weights[1] > 0.f &&
+                    cfg->rpn_bbox_reg_weights[2] > 0.f && cfg->rpn_bbox_reg_weights[3] > 0.f &&
+                    cfg->box_reg_weights[0] > 0.f && cfg->box_reg_weights[1] > 0.f && cfg->box_reg_weights[2] > 0.f &&
+                    cfg->box_reg_weights[3] > 0.f,
+                "mdx_model_create: box regression weights must be positive");
     MDX_REQUIRE(cfg->fpn_out_channels % 8 == 0 && cfg->gn_groups > 0 && cfg->detections_per_image >= 1 &&
                     cfg->detections_per_image <= 16 && cfg->n_keypoint_convs >= 0 && cfg->n_keypoint_convs <= 16 &&
                     cfg->in_channels >= 1 && cfg->in_channels <= 3 && cfg->size_divisibility >= 2 &&

@@ -381,7 +381,8 @@ __device__ void bitonic_desc(unsigned *key, unsigned *val, int n) {
 struct RpnLevels {
     const float *head[MAX_LEVELS];  // (B, H, W, A*5) f32: [obj(A), deltas(A*4)]
     int H[MAX_LEVELS], W[MAX_LEVELS], stride[MAX_LEVELS];
-    float cell[MAX_LEVELS][4][4];  // up to 4 aspect ratios
+    float cell[MAX_LEVELS][8][4];  // up to 8 aspect ratios
+    float wts[4];                  // RPN.BBOX_REG_WEIGHTS
     int L, A, B, pre_topk;
     float offset, img_h, img_w, min_size, clampv;
 };
@@ -398,7 +399,7 @@ __device__ void rpn_decode(const RpnLevels &rl, int seg, int k, const unsigned *
     float *ob = ws_boxes + (long long)seg * rl.pre_topk * 4;
     float *os = ws_scores + (long long)seg * rl.pre_topk;
     int *ov = ws_valid + (long long)seg * rl.pre_topk;
-    const float wts[4] = {1.f, 1.f, 1.f, 1.f};
+    const float wts[4] = {rl.wts[0], rl.wts[1], rl.wts[2], rl.wts[3]};
     for (int r = threadIdx.x; r < k; r += blockDim.x) {
         const int i = (int)s_val[r];
         const int pix = i / A, a = i - pix * A;
@@ -2149,11 +2150,11 @@ extern "C" int mdx_rpn_set_sliced(int on) {
 extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
                                  int L, int B, int A, const float *cell_anchors, float offset, int img_h, int img_w,
                                  int pre_topk, int post_topk, float nms_thresh, float min_size, float clampv,
-                                 float *out_boxes, float *out_scores, int *out_count, void *workspace,
-                                 mdx_stream_t stream) {
+                                 const float *reg_weights, float *out_boxes, float *out_scores, int *out_count,
+                                 void *workspace, mdx_stream_t stream) {
     MDX_REQUIRE(head && lvl_h && lvl_w && strides && cell_anchors && out_boxes && out_scores && out_count && workspace,
                 "mdx_rpn_proposals: null pointer");
-    MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && A >= 1 && A <= 4, "mdx_rpn_proposals: L or A out of range");
+    MDX_REQUIRE(L >= 1 && L <= MAX_LEVELS && A >= 1 && A <= 8, "mdx_rpn_proposals: L or A out of range");
     MDX_REQUIRE(pre_topk >= 1 && pre_topk <= TOPK_MAX && (pre_topk + 63) / 64 <= NMS_MAXW,
                 "mdx_rpn_proposals: pre_topk must be in [1, %d]", TOPK_MAX);
     MDX_REQUIRE(post_topk >= 1 && L * pre_topk <= MERGE_MAX, "mdx_rpn_proposals: too many candidates to merge");
@@ -2166,6 +2167,7 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
         for (int a = 0; a < A; ++a)
             for (int c = 0; c < 4; ++c) rl.cell[l][a][c] = cell_anchors[(l * A + a) * 4 + c];
     }
+    for (int c = 0; c < 4; ++c) rl.wts[c] = reg_weights ? reg_weights[c] : 1.f;
     rl.L = L; rl.A = A; rl.B = B; rl.pre_topk = pre_topk;
     rl.offset = offset; rl.img_h = (float)img_h; rl.img_w = (float)img_w; rl.min_size = min_size; rl.clampv = clampv;
     const long long segs = (long long)B * L;

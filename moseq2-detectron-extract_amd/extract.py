@@ -22,8 +22,8 @@ from typing import Dict, Optional
 import numpy as np
 
 from .pipeline import ExtractConfig, GPUExtractor
-from .results import (KeypointsTSVWriter, check_completion_status, create_extract_h5, open_results, status_filename,
-                      write_extracted_chunk_to_h5, write_status)
+from .results import (KeypointsTSVWriter, MemoryH5, check_completion_status, create_extract_h5, open_results,
+                      status_filename, write_extracted_chunk_to_h5, write_status)
 from .session import RawDepthSource
 from .shard import instance_exchange, pass_tail_forward, tracking_exchange
 
@@ -78,6 +78,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     parts = []
     if exchange is None:  # two passes around the exchange step (needs torch.distributed initialised)
         exchange = world > 1 and (config.use_tracking or config.select_instances)
+    ok = False
     try:
         if exchange:
             states = []
@@ -99,10 +100,14 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         else:
             for idx, raw in src.iterate(device=True, batches=batches):
                 parts.append(finished(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
+        ok = True
     finally:
         src.close()
         if writer is not None:
-            writer.close()
+            if ok:
+                writer.close()
+            else:  # the extraction's own exception propagates; the results file is left unfinished
+                writer.abort()
     if output_dir:
         status["complete"] = True  # M/extract.py:129-131
         write_status(status_path, status)
@@ -199,6 +204,22 @@ class _ChunkWriter:
         if self._err:
             raise self._err[0]
         self.h5.close()
+
+    def abort(self) -> None:
+        """Stop the writer thread after a failed extraction without finishing
+        the results file and without raising: the extraction's exception is
+        the one that propagates.  Without h5py nothing is written (the .npz
+        is only saved by close()); an h5py file is closed as it stands, its
+        status file still saying complete: False (M/extract.py:129-131), so
+        the session is re-run."""
+        self._err.append(RuntimeError("extraction failed"))  # the thread skips the queued chunks
+        self._q.put(None)
+        self._t.join()
+        if not isinstance(self.h5, MemoryH5):
+            try:
+                self.h5.close()
+            except Exception:
+                pass
 
 
 def _select_exchange(ex, states):

@@ -1,8 +1,10 @@
 """Predictor -- drop-in for the reference's DefaultPredictor-shaped wrapper
 (M/model/predict.py:12-102), backed by the MI355X-native runtime.
 
-Same constructors (``from_config``; ``from_torchscript`` reads an exported
-archive weights-only, see model/torchscript.py),
+Same constructors (``from_config`` loads ``MODEL.WEIGHTS`` of the config;
+``from_model_dir`` is InferenceStep's model-directory set-up;
+``from_torchscript`` reads an exported archive weights-only, see
+model/torchscript.py),
 same ``device`` property and the same call contract: uint8 ``(H,W,C)`` or
 ``(N,H,W,C)`` (numpy or torch) -> ``{'instances': Instances}`` or a list of
 them, with Detectron2's field names.
@@ -18,7 +20,7 @@ import torch
 from .config import ModelConfig
 from .runtime import MaskRCNN
 from .structures import Boxes, Instances
-from .weights import load_state_dict, synthetic_state_dict
+from .weights import check_state_dict, load_state_dict, synthetic_state_dict
 
 
 class Predictor:
@@ -31,21 +33,33 @@ class Predictor:
         return self.model.device
 
     @classmethod
-    def from_config(cls, cfg: Union[ModelConfig, str], weights: Union[None, str, dict] = None,
+    def from_config(cls, cfg: Union[ModelConfig, str, dict], weights: Union[None, str, dict] = None,
                     dtype: str = "fp32", device="cuda", seed: int = 0) -> "Predictor":
-        """cfg: ModelConfig or path to a Detectron2 config.yaml.  weights: path to
-        a Detectron2 checkpoint (.pth, loaded weights_only), a state dict, or
-        None for seeded synthetic weights (no trained checkpoint is available
-        offline)."""
-        if isinstance(cfg, str):
-            cfg = ModelConfig.from_yaml(cfg)
-        if weights is None:
-            sd = synthetic_state_dict(cfg, seed)
-        elif isinstance(weights, str):
-            sd = load_state_dict(weights)
-        else:
-            sd = weights
+        """The reference constructor (M/model/predict.py:31-44): build the
+        model of `cfg`, load ``cfg.MODEL.WEIGHTS`` and check the input format.
+
+        cfg: a ModelConfig, a path to a Detectron2 ``config.yaml`` or its
+        loaded mapping (ModelConfig.from_yaml: every inference key read,
+        unsupported settings refused).  weights: None loads MODEL.WEIGHTS
+        (``cfg.weights``; a ``.pth`` read weights-only) and raises when it is
+        empty or missing; a path or a state dict overrides it; the string
+        ``"synthetic"`` selects seeded synthetic weights of this architecture
+        (benchmarks and tests: no trained checkpoint exists offline).  The
+        state dict must carry every parameter of the configuration with its
+        shape (weights.check_state_dict)."""
+        cfg, sd = resolve_model(cfg, weights, seed)
         return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype))
+
+    @classmethod
+    def from_model_dir(cls, model_dir: str, checkpoint: Union[str, int] = "last", instance_threshold: float = 0.5,
+                       allowed_detections: int = 4, dtype: str = "fp32", device="cuda") -> "Predictor":
+        """What InferenceStep.initialize does with a trained model directory
+        (M/pipeline/inference_step.py:35-52): ``<model_dir>/config.yaml``,
+        MODEL.WEIGHTS = the last checkpoint (``last_checkpoint`` file) or the
+        one of iteration `checkpoint`, SCORE_THRESH_TEST = --instance-threshold,
+        DETECTIONS_PER_IMAGE = --allowed-detections, then from_config."""
+        cfg = model_dir_config(model_dir, checkpoint, instance_threshold, allowed_detections)
+        return cls.from_config(cfg, dtype=dtype, device=device)
 
     @classmethod
     def from_torchscript(cls, path: str, cfg: Optional[ModelConfig] = None, dtype: str = "fp32", device="cuda",
@@ -93,6 +107,43 @@ class Predictor:
         if not return_as_list:
             return preds[0]
         return preds
+
+
+def model_dir_config(model_dir: str, checkpoint: Union[str, int] = "last", instance_threshold: float = 0.5,
+                     allowed_detections: int = 4) -> ModelConfig:
+    """The ModelConfig InferenceStep.initialize builds for a model directory
+    (M/pipeline/inference_step.py:35-51), MODEL.WEIGHTS resolved."""
+    from .util import get_last_checkpoint, get_specific_checkpoint
+    cfg = ModelConfig.from_yaml(os.path.join(model_dir, "config.yaml"))
+    cfg.weights = (get_last_checkpoint(model_dir) if checkpoint == "last"
+                   else get_specific_checkpoint(model_dir, checkpoint))
+    cfg.score_thresh_test = float(instance_threshold)
+    cfg.detections_per_image = int(allowed_detections)
+    return cfg
+
+
+def resolve_model(cfg: Union[ModelConfig, str, dict], weights: Union[None, str, dict] = None, seed: int = 0):
+    """The host half of from_config (no GPU needed): the ModelConfig and the
+    checked state dict it will run."""
+    if not isinstance(cfg, ModelConfig):
+        cfg = ModelConfig.from_yaml(cfg)
+    cfg.validate()
+    if isinstance(weights, str) and weights == "synthetic":
+        sd, source = synthetic_state_dict(cfg, seed), "synthetic"
+    elif weights is None:
+        if not cfg.weights:
+            raise ValueError("MODEL.WEIGHTS is empty: set it (or pass weights=<checkpoint path | state dict>); "
+                             "weights='synthetic' runs seeded synthetic weights")
+        sd, source = load_state_dict(cfg.weights), cfg.weights
+    elif isinstance(weights, (str, os.PathLike)):
+        sd, source = load_state_dict(str(weights)), str(weights)
+    else:
+        sd, source = weights, "state dict"
+    # DetectionCheckpointer.load + `assert model.input_format ==
+    # cfg.INPUT.FORMAT`: every parameter of the configuration, the stem
+    # taking the configured channels
+    check_state_dict(sd, cfg, source)
+    return cfg, sd
 
 
 def outputs_to_instances(out: dict, h: int, w: int):

@@ -46,7 +46,7 @@ class ModelCfgC(ctypes.Structure):
         ("res2_out_channels", ctypes.c_int), ("width_per_group", ctypes.c_int), ("stride_in_1x1", ctypes.c_int),
         ("fpn_out_channels", ctypes.c_int), ("fpn_fuse_avg", ctypes.c_int), ("gn_groups", ctypes.c_int),
         ("gn_eps", ctypes.c_float), ("n_anchor_sizes", ctypes.c_int), ("anchor_sizes", ctypes.c_float * 5),
-        ("n_aspect_ratios", ctypes.c_int), ("aspect_ratios", ctypes.c_float * 4), ("anchor_offset", ctypes.c_float),
+        ("n_aspect_ratios", ctypes.c_int), ("aspect_ratios", ctypes.c_float * 8), ("anchor_offset", ctypes.c_float),
         ("rpn_pre_nms_topk", ctypes.c_int), ("rpn_post_nms_topk", ctypes.c_int), ("rpn_nms_thresh", ctypes.c_float),
         ("rpn_min_box_size", ctypes.c_float), ("num_classes", ctypes.c_int), ("score_thresh", ctypes.c_float),
         ("nms_thresh", ctypes.c_float), ("detections_per_image", ctypes.c_int),
@@ -58,6 +58,7 @@ class ModelCfgC(ctypes.Structure):
         ("pooler_sampling_ratio", ctypes.c_int), ("pooler_aligned", ctypes.c_int),
         ("canonical_box_size", ctypes.c_float), ("canonical_level", ctypes.c_float), ("in_channels", ctypes.c_int),
         ("pixel_mean", ctypes.c_float * 3), ("pixel_std", ctypes.c_float * 3), ("size_divisibility", ctypes.c_int),
+        ("rpn_bbox_reg_weights", ctypes.c_float * 4),
     ]
 
 
@@ -76,12 +77,7 @@ class ConvRecordC(ctypes.Structure):
 
 def model_cfg_c(cfg: ModelConfig, dtype: str) -> ModelCfgC:
     """ModelConfig (Detectron2 CfgNode keys) -> struct mdx_model_cfg."""
-    if cfg.fpn_norm != "GN":
-        raise NotImplementedError("FPN.NORM must be 'GN' (M/model/config.py:82)")
-    if cfg.num_groups != 1:
-        raise NotImplementedError("RESNETS.NUM_GROUPS must be 1")
-    if len(cfg.keypoint_conv_dims) > 16 or len(cfg.anchor_sizes) != 5 or len(cfg.aspect_ratios) > 4:
-        raise NotImplementedError("unsupported head / anchor configuration")
+    cfg.validate()
     c = ModelCfgC()
     c.depth, c.dtype = cfg.depth, _DT[dtype]
     c.stem_out_channels, c.res2_out_channels, c.width_per_group = (cfg.stem_out_channels, cfg.res2_out_channels,
@@ -116,6 +112,7 @@ def model_cfg_c(cfg: ModelConfig, dtype: str) -> ModelCfgC:
     c.pixel_mean[:] = [float(v) for v in (list(cfg.pixel_mean) * 3)[:3]]
     c.pixel_std[:] = [float(v) for v in (list(cfg.pixel_std) * 3)[:3]]
     c.size_divisibility = cfg.size_divisibility
+    c.rpn_bbox_reg_weights[:] = [float(v) for v in cfg.rpn_bbox_reg_weights]
     return c
 
 

@@ -111,6 +111,7 @@ class GPUExtractor:
         # ProcessFeaturesStep's norfair instance tracker (process_features_step.py:35-38), per session
         self.instance_tracker = INS.InstanceTracker(config.expected_instances)
         self._frames_seen = 0
+        self._inpaint_errors_seen = call("mdx_inpaint_errors", 0)  # process-wide device counter
         self._tail_dets = {}  # session frame -> (mask planes (D,h,w), keypoints (D,K,3), keep_idx row)
         self._streams = []
         self._pipe = None     # OverlappedExtractor of the pipelined features pass
@@ -352,6 +353,7 @@ class GPUExtractor:
                                   z_data=z.cpu().numpy())
         depth, mask = self.crop(prepped, d2, torch.from_numpy(np.ascontiguousarray(centroid, dtype=np.float64)).cuda(),
                                 torch.from_numpy(track["orientation"]).cuda())
+        self._check_inpaint()
         return {
             "chunk": prepped, "frame_idxs": frame_idxs, "offset": offset,
             "features": {"cleaned_frames": cleaned, "masks": d2, "features": track, "flips": flips,
@@ -359,6 +361,17 @@ class GPUExtractor:
             "scalars": scalars, "keypoints": kpd,
             "depth_frames": depth.cpu().numpy(), "mask_frames": mask.cpu().numpy(),
         }
+
+    def _check_inpaint(self) -> None:
+        """Once per chunk: frames whose inpaint cluster labelling did not
+        converge are left un-inpainted by k_inp_setup and counted on the
+        device (mdx_inpaint_errors); such frames would differ from the
+        reference's, so a new count is raised here rather than written."""
+        n = call("mdx_inpaint_errors", 0)
+        if n > self._inpaint_errors_seen:
+            self._inpaint_errors_seen = n
+            raise proc.MdxError(f"inpaint: {n} frame(s) whose invalid-pixel labelling did not converge "
+                                "(mdx_inpaint_errors); their prepped frames would differ from the reference's")
 
     def host_angles(self, host: dict):
         """The sequential host step of instances_to_features

@@ -144,7 +144,17 @@ class SyntheticSession:
                     for a in range(0, n, step)]
             import concurrent.futures as cf
             import multiprocessing as mp
-            with cf.ProcessPoolExecutor(max_workers=len(jobs), mp_context=mp.get_context("fork")) as ex:
+            import sys
+            # spawned, not forked: callers may already hold a HIP context (its
+            # runtime threads and device mappings must not be duplicated); the
+            # workers only need numpy and this module, registered under its
+            # package name by mdx_pkg.load (the repository root is on sys.path)
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            if root not in sys.path:
+                sys.path.insert(0, root)
+            import mdx_pkg
+            with cf.ProcessPoolExecutor(max_workers=len(jobs), mp_context=mp.get_context("spawn"),
+                                        initializer=mdx_pkg.load) as ex:
                 assert sum(ex.map(_render_to_file, jobs)) == n
         else:
             with open(path, "wb") as fh:

@@ -281,16 +281,23 @@ def test_backbone_fpn_fp32(small_case):
         assert err < 2e-4, f"{k}: rel err {err:.2e}"
 
 
+@pytest.mark.parametrize("anchors", ["default", "5ratios"])
 @pytest.mark.parametrize("sliced", [1, 0])
-def test_rpn_proposals_from_identical_heads(mdx, sliced):
+def test_rpn_proposals_from_identical_heads(mdx, sliced, anchors):
     """Same head tensors into the GPU and the oracle proposal selection, with
-    the top-k split over several workgroups per (image, level) and not."""
+    the top-k split over several workgroups per (image, level) and not; also
+    for the reference notebook's five aspect ratios
+    (notebooks/Moseq-detectron.ipynb: ASPECT_RATIOS [[0.5, 1, 2, 3, 4]]) with
+    non-unit RPN.BBOX_REG_WEIGHTS and an anchor offset."""
     import ctypes
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import ModelConfig
     from oracle import model_ref as R
     cfg = ModelConfig()
-    B, A = 2, 3
+    if anchors == "5ratios":
+        cfg = ModelConfig(aspect_ratios=(0.5, 1.0, 2.0, 3.0, 4.0), rpn_bbox_reg_weights=(2.0, 2.0, 1.0, 1.0),
+                          anchor_offset=0.5, anchor_sizes=(24, 48, 96, 192, 384))
+    B, A = 2, len(cfg.aspect_ratios)
     sizes = [(112, 128), (56, 64), (28, 32), (14, 16), (7, 8)]
     g = torch.Generator().manual_seed(1)
     heads, logits, deltas, anchors = [], [], [], []
@@ -319,8 +326,9 @@ def test_rpn_proposals_from_identical_heads(mdx, sliced):
     old = call("mdx_rpn_set_sliced", sliced)
     try:
         call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]),
-             5, B, A, cells.ctypes.data_as(ctypes.c_void_p), 0.0, 423, 511, 1000, post, 0.7, 0.0,
-             cfg.bbox_reg_clamp, P(boxes), P(scores), P(cnt), P(ws), None)
+             5, B, A, cells.ctypes.data_as(ctypes.c_void_p), cfg.anchor_offset, 423, 511, 1000, post, 0.7, 0.0,
+             cfg.bbox_reg_clamp, (ctypes.c_float * 4)(*cfg.rpn_bbox_reg_weights), P(boxes), P(scores), P(cnt),
+             P(ws), None)
     finally:
         call("mdx_rpn_set_sliced", old)
     for b in range(B):
@@ -548,7 +556,7 @@ def test_forward_r101_fp16_batch64_runs(mdx):
 
 def test_predictor_instances(mdx):
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
-    p = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    p = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16", weights="synthetic")
     rng = np.random.default_rng(1)
     img = rng.integers(0, 256, size=(3, 96, 128, 1), dtype=np.uint8)
     res = p(img)
@@ -603,7 +611,7 @@ def test_gpu_extractor_step(mdx):
     from oracle import frameops as O
     s = synth.SyntheticSession(4, seed=2)
     raw = s.frames(0, 4)
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16", weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
     r = ex.step_device(torch.from_numpy(raw).cuda())
     assert r["depth_frames"].shape == (4, 80, 80) and r["mask_frames"].shape == (4, 80, 80)
@@ -621,7 +629,7 @@ def test_overlapped_extractor_matches_serial(mdx):
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
     s = synth.SyntheticSession(12, seed=5)
     raw = torch.from_numpy(s.frames(0, 12)).cuda()
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16", weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4))
     batches = [raw[i:i + 4] for i in range(0, 12, 4)]
     want = [ex.step_device(b) for b in batches]
@@ -644,7 +652,7 @@ def test_features_pass_pipelined_matches_serial(mdx):
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
     s = synth.SyntheticSession(75, seed=8)
     raw = torch.from_numpy(s.frames(0, 75)).cuda()
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0))
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), weights="synthetic")
     got = {}
     for piped in (False, True):
         ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=16, pipelined=piped))
@@ -678,7 +686,7 @@ def test_process_chunk_data_dict(mdx, use_tracking):
     from oracle import frameops as O
     s = synth.SyntheticSession(6, seed=4)
     raw = s.frames(0, 6)
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16", weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=4, use_tracking=use_tracking))
     d = ex.process_chunk(raw, np.arange(100, 106), 0, true_depth=s.true_depth)
     for k in ("chunk", "frame_idxs", "offset", "features", "scalars", "keypoints", "depth_frames", "mask_frames"):
@@ -714,7 +722,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
     s = synth.SyntheticSession(10, seed=6)
     s.write(str(tmp_path))
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16")
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype="fp16", weights="synthetic")
     cfg = ExtractConfig(chunk_size=4, batch_size=4, use_tracking=False)
     out = extract_session(str(tmp_path / "depth.dat"), s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth)
     assert out["frames"].shape == (10, 80, 80) and list(out["frame_idxs"]) == list(range(10))

@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 import torch
 
+from _d2_config import d2_config, write_model_dir
 from _ts_archive import write_archive
 
 pytestmark = pytest.mark.gpu
@@ -42,7 +43,11 @@ def case(mdx, tmp_path_factory):
     scalars = {"roi_heads.box_predictor.test_score_thresh": 0.0, "roi_heads.box_predictor.test_topk_per_image": 4,
                "roi_heads.box_predictor.test_nms_thresh": 0.5}
     path = write_archive(tmp_path_factory.mktemp("ts") / "model.ts", sd, scalars)
-    return cfg, sd, img, want, path
+    # the same weights as a trained model directory (config.yaml dumped by
+    # Detectron2, model_XXXXXXX.pth, last_checkpoint)
+    mdir = tmp_path_factory.mktemp("model_dir")
+    write_model_dir(mdir, d2_config(), sd)
+    return cfg, sd, img, want, path, str(mdir)
 
 
 def _iou(a, b):
@@ -84,7 +89,7 @@ def _check(preds, want, hw):
 
 def test_predictor_from_config_matches_oracle(case):
     from moseq2_detectron_extract_amd.model import Predictor
-    cfg, sd, img, want, _ = case
+    cfg, sd, img, want, _, _ = case
     pred = Predictor.from_config(cfg, weights=sd)  # reference constructor, default dtype
     assert pred.model.dtype == "fp32" and not pred.is_torchscript
     assert pred.device.type == "cuda"
@@ -108,9 +113,53 @@ def test_predictor_from_torchscript_matches_oracle(case):
     """M/model/predict.py:46-51 + M/model/util.py:45-62: the archive's
     weights and test thresholds drive the same native forward."""
     from moseq2_detectron_extract_amd.model import Predictor
-    cfg, _, img, want, path = case
+    cfg, _, img, want, path, _ = case
     pred = Predictor.from_torchscript(path)
     assert pred.is_torchscript and pred.model.dtype == "fp32"
     c = pred.model.cfg
     assert (c.depth, c.score_thresh_test, c.detections_per_image, c.nms_thresh_test) == (50, 0.0, 4, 0.5)
+    _check(pred(img), want, img.shape[1:3])
+
+
+def test_predictor_from_model_dir_matches_oracle(case):
+    """The reference's model-directory path (M/pipeline/inference_step.py:35-52):
+    <dir>/config.yaml read, MODEL.WEIGHTS = the last checkpoint, loaded
+    weights-only, --instance-threshold / --allowed-detections applied, then
+    Predictor.from_config(cfg) with no weights argument."""
+    from moseq2_detectron_extract_amd.model import Predictor
+    from moseq2_detectron_extract_amd.model.predict import model_dir_config
+    _, _, img, want, _, mdir = case
+    cfg = model_dir_config(mdir, "last", instance_threshold=0.0, allowed_detections=4)
+    assert cfg.weights.endswith(".pth")
+    pred = Predictor.from_config(cfg)
+    _check(pred(img), want, img.shape[1:3])
+    pred2 = Predictor.from_model_dir(mdir, instance_threshold=0.0, allowed_detections=4)
+    a, b = pred(img[:1]), pred2(img[:1])
+    assert torch.equal(a[0]["instances"].pred_boxes.tensor, b[0]["instances"].pred_boxes.tensor)
+
+
+def test_predictor_non_default_anchors_match_oracle(mdx, tmp_path):
+    """A model directory whose config differs from the zoo defaults in the
+    anchor generator (the reference notebook's five aspect ratios, other
+    sizes and offset) and the RPN / box regression weights: the native
+    forward follows the file, as the oracle does."""
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor, synthetic_state_dict
+    from oracle import frameops as O
+    from oracle import model_ref as R
+    y = d2_config(**{"MODEL.ANCHOR_GENERATOR.ASPECT_RATIOS": [[0.5, 1.0, 2.0, 3.0, 4.0]],
+                     "MODEL.ANCHOR_GENERATOR.SIZES": [[24], [48], [96], [192], [384]],
+                     "MODEL.ANCHOR_GENERATOR.OFFSET": 0.5,
+                     "MODEL.RPN.BBOX_REG_WEIGHTS": [2.0, 2.0, 1.0, 1.0],
+                     "MODEL.ROI_BOX_HEAD.BBOX_REG_WEIGHTS": [8.0, 8.0, 4.0, 4.0],
+                     "MODEL.ROI_HEADS.SCORE_THRESH_TEST": 0.0, "TEST.DETECTIONS_PER_IMAGE": 4})
+    cfg = ModelConfig.from_yaml(y)
+    sd = synthetic_state_dict(cfg, 2)
+    write_model_dir(tmp_path / "m", y, sd)
+    s = synth.SyntheticSession(2, seed=SEED + 1)
+    prepped, _ = O.prep_raw_frames(s.frames(0, 2), s.bground_im, s.roi, 0, 100)
+    img = np.ascontiguousarray(O.scale_raw_frames(prepped, 0, 100)[..., None])
+    want, _ = R.forward(sd, cfg, img, keep_intermediates=False)
+    pred = Predictor.from_model_dir(str(tmp_path / "m"), instance_threshold=0.0, allowed_detections=4)
+    assert len(pred.model.cfg.aspect_ratios) == 5
     _check(pred(img), want, img.shape[1:3])

@@ -21,13 +21,13 @@ if os.environ.get("MDX_DEBUG_SHADOW"):
     order = order[:4] + ["shadow_gnws5", "gnws5"] + [f"{k}{l}" for l in (5, 4, 3, 2) for k in ("fpn_lateral", "shadow_inner", "fpn_inner",
                                                                      "fpn_output", "shadow_p", "p")]
 s = synth.SyntheticSession(8, seed=5)
-pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt)
+pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt, weights="synthetic")
 prep = proc.FramePrep(s.bground_im, s.roi, 0, 100)
 x = prep(torch.from_numpy(s.frames(0, 8)).cuda())
 xa, xb = x[:4].contiguous(), x[4:].contiguous()
 lut = proc.scale_lut(0, 100)
 m = pred.model
-mb = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt).model if mode == "other" else m
+mb = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt, weights="synthetic").model if mode == "other" else m
 import ctypes
 from moseq2_detectron_extract_amd._lib import call
 P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731

@@ -26,7 +26,7 @@ def main():
     s = synth.SyntheticSession(nb * B, seed=21)
     raw = torch.from_numpy(s.frames(0, nb * B)).cuda()
     batches = [raw[i * B:(i + 1) * B] for i in range(nb)]
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype)
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype, weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=B))
     keys = ("depth_frames", "mask_frames", "centroid", "angle", "keypoints", "ndet")
     want = []

@@ -26,7 +26,7 @@ def main():
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig
     s = synth.SyntheticSession(n, seed=9)
-    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype)
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype, weights="synthetic")
     res = {"nframes": n, "chunk": chunk, "dtype": dtype}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         t0 = time.perf_counter()

@@ -21,7 +21,7 @@ def main():
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     cfg = ModelConfig(score_thresh_test=0.0)
     dt = sys.argv[1] if len(sys.argv) > 1 else "fp32"
-    m = Predictor.from_config(cfg, dtype=dt, seed=0).model
+    m = Predictor.from_config(cfg, dtype=dt, seed=0, weights="synthetic").model
     sess = synth.SyntheticSession(32, seed=1000)
     raw = torch.from_numpy(sess.frames(0, 32)).cuda()
     prepped = proc.FramePrep(sess.bground_im, sess.roi, 0, 100, True)(raw)

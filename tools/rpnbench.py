@@ -43,7 +43,7 @@ def main():
     def run():
         call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]),
              5, B, A, cells.ctypes.data_as(ctypes.c_void_p), 0.0, 423, 511, 1000, 1000, 0.7, 0.0, math.log(1000 / 16),
-             P(boxes), P(scores), P(cnt), P(ws), ctypes.c_void_p(stream.cuda_stream))
+             None, P(boxes), P(scores), P(cnt), P(ws), ctypes.c_void_p(stream.cuda_stream))
 
     for _ in range(3):
         run()
