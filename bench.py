@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--dtype", default="fp32", choices=["fp16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp16", "fp32", "mixed"],
+                    help="mixed: fp32 backbone / FPN / RPN / box head, fp16 mask + keypoint heads (config 5 as stated)")
     ap.add_argument("--depth", type=int, default=50, choices=[50, 101])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -599,7 +600,7 @@ def main():
     if not args.no_roofline:
         raw_dev = raw_host[0].cuda()
         per = conv_roofline(ex, raw_dev, dump=args.dump_convs)
-        roof = roofline_line(per, args.dtype, flops_per_image(cfg) * B)
+        roof = roofline_line(per, "fp32" if args.dtype == "mixed" else args.dtype, flops_per_image(cfg) * B)
         roof["frame_ops"] = frame_ops_line(ex, raw_dev)
     del ex
     torch.cuda.synchronize()

@@ -396,6 +396,10 @@ int mdx_preprocess_s2d(const uint8_t *frames, int B, int h, int w, const uint8_t
 int mdx_preprocess_s2d_folded(const uint8_t *frames, int B, int h, int w, const uint8_t lut[256], int Hp, int Wp,
                               int dtype, void *out, mdx_stream_t stream);
 
+/* y = x converted between float32 (0) and float16 (1), round to nearest
+ * even; n (elements) a multiple of 8. */
+int mdx_convert(const void *x, int64_t n, int in_dtype, void *out, int out_dtype, mdx_stream_t stream);
+
 /* max_pool2d(k, s, p), NHWC. */
 int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, int s, int p, int dtype, void *out,
                   mdx_stream_t stream);
@@ -581,6 +585,9 @@ typedef struct mdx_model_cfg {
     float pixel_std[3];            /* 5.79 x3 */
     int size_divisibility;         /* 32 */
     float rpn_bbox_reg_weights[4]; /* RPN.BBOX_REG_WEIGHTS 1 1 1 1 */
+    int head_dtype;                /* mask + keypoint heads: 0 = dtype, 1 = float16 (with dtype 0: the
+                                      fp32 trunk / RPN / box head and fp16 mask + keypoint heads of
+                                      BASELINE config 5; pooled in fp32, converted) */
 } mdx_model_cfg;
 
 typedef void *mdx_model_t;

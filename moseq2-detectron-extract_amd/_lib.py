@@ -89,6 +89,7 @@ SIGNATURES = {
     "mdx_preprocess_s2d_folded": (I32, [P, I32, I32, I32, P, I32, I32, I32, P, P]),
     "mdx_model_set_stem_fold": (I32, [I32]),
     "mdx_maxpool2d": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "mdx_convert": (I32, [P, I64, I32, P, I32, P]),
     "mdx_groupnorm_workspace_bytes": (I64, [I32, I32, I32, I32]),
     "mdx_groupnorm": (I32, [P, I32, I32, I32, I32, I32, F32, P, P, P, I32, I32, P, P, P]),
     "mdx_rpn_workspace_bytes": (I64, [I32, I32, I32]),

@@ -49,6 +49,7 @@ struct ConvW {
     void *w = nullptr;
     float *b = nullptr;
     int cin = 0, cout = 0, k = 1, stride = 1, pad = 0, kalg = 0;
+    int dt = 0;  // operand / activation dtype of the layer: 0 f32, 1 f16
     // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
     // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 128)
     float *wino2 = nullptr, *wino4 = nullptr, *wino6 = nullptr;
@@ -103,7 +104,8 @@ struct Ctx {
 struct Model {
     mdx_model_cfg cfg{};
     int dev = 0;
-    int dt = 0;        // 0 f32, 1 f16
+    int dt = 0;        // 0 f32, 1 f16 (backbone, FPN, RPN, box head)
+    int hdt = 0;       // mask + keypoint heads (cfg.head_dtype; = dt unless mixed)
     bool stem_fold = false;  // stem over the 2-channel (value, inside) s2d input (fp32 handles)
     bool fuse_sc = false;    // projection shortcuts fused into conv3 (Block::c3sc)
     size_t es = 4;     // activation element size
@@ -200,6 +202,7 @@ struct Packer {
     Model &m;
     std::unordered_map<std::string, HostT> &sd;
     std::string err;
+    int cur_dt = 0;  // dtype of the layers being packed (m.dt, or m.hdt for the mask / keypoint heads)
 
     const HostT *get(const std::string &k, std::initializer_list<int64_t> shape = {}) {
         auto it = sd.find(k);
@@ -223,7 +226,7 @@ struct Packer {
     void *upload(const std::vector<float> &v, bool as_act_dtype) {
         if (!err.empty()) return nullptr;
         void *d = nullptr;
-        const bool h = as_act_dtype && m.dt == 1;
+        const bool h = as_act_dtype && cur_dt == 1;
         const size_t bytes = v.size() * (h ? 2 : 4);
         if (hipMalloc(&d, bytes ? bytes : 4) != hipSuccess) {
             err = "device allocation of weights failed";
@@ -241,6 +244,18 @@ struct Packer {
     }
     float *upload_f32(const std::vector<float> &v) { return (float *)upload(v, false); }
 
+    // Winograd tile sizes to pack for the next 3x3 layers: the ones the
+    // policy current at create time can pick (mdx_winograd_tile); the heads
+    // set the map size they run on (map_hw > 0), the trunk leaves it 0 (any
+    // size: F(6,3) and F(4,3) under policy 6).  A mode switched later to a
+    // size that was not packed runs those layers direct.
+    int map_hw = 0;
+    bool want_tile(int m_) const {
+        const int pol = mdx_conv_winograd_enabled();
+        if (pol == 0) return false;
+        if (map_hw > 0) return mdx_winograd_tile(map_hw, map_hw, pol) == m_;
+        return pol == 6 ? (m_ == 4 || m_ == 6) : pol == m_;
+    }
     // OIHW (optionally scaled per output channel) -> [Cout][KH][KW][Cin]
     ConvW conv(const HostT *w, const float *scale, const std::vector<float> *bias, int stride, int pad) {
         ConvW c;
@@ -265,20 +280,19 @@ struct Packer {
         c.k = kh;
         c.stride = stride;
         c.pad = pad;
-        if (m.dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 64 && ci % 4 == 0 && co % 8 == 0 &&
+        c.dt = cur_dt;
+        if (cur_dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 64 && ci % 4 == 0 && co % 8 == 0 &&
             err.empty()) {
-            std::vector<float> oihw((size_t)co * ci * 9), u((size_t)16 * co * ci);
+            std::vector<float> oihw((size_t)co * ci * 9), u;
             for (int o = 0; o < co; ++o)
                 for (size_t q = 0; q < (size_t)ci * 9; ++q)
                     oihw[(size_t)o * ci * 9 + q] = w->v[(size_t)o * ci * 9 + q] * (scale ? scale[o] : 1.f);
-            mdx_winograd_weights(oihw.data(), co, ci, 2, u.data());
-            c.wino2 = upload_f32(u);
-            u.resize((size_t)36 * co * ci);
-            mdx_winograd_weights(oihw.data(), co, ci, 4, u.data());
-            c.wino4 = upload_f32(u);
-            u.resize((size_t)64 * co * ci);
-            mdx_winograd_weights(oihw.data(), co, ci, 6, u.data());
-            c.wino6 = upload_f32(u);
+            for (int m_ : {2, 4, 6}) {
+                if (!want_tile(m_)) continue;
+                u.resize((size_t)(m_ + 2) * (m_ + 2) * co * ci);
+                mdx_winograd_weights(oihw.data(), co, ci, m_, u.data());
+                (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = upload_f32(u);
+            }
         }
         return c;
     }
@@ -324,6 +338,7 @@ struct Packer {
         }
         c.w = upload(pk, true);
         c.b = upload_f32(b);
+        c.dt = cur_dt;
         c.cin = c3;  // the first source's channels; cout, stride of the second
         c.cout = co;
         c.k = 1;
@@ -371,6 +386,7 @@ struct Packer {
                     }
             c.w = upload(pk, true);
             c.b = upload_f32(b);
+            c.dt = cur_dt;
             c.cin = 8;
             c.cout = co;
             c.k = 4;
@@ -390,6 +406,7 @@ struct Packer {
                     }
         c.w = upload(pk, true);
         c.b = upload_f32(b);
+        c.dt = cur_dt;
         c.cin = 16;
         c.cout = co;
         c.k = 4;
@@ -405,7 +422,8 @@ struct Packer {
         c.b = upload_f32(b);
         c.cin = in;
         c.cout = out;
-        if (x6 && m.dt == 0 && in % 16 == 0 && err.empty()) {
+        c.dt = cur_dt;
+        if (x6 && cur_dt == 0 && in % 16 == 0 && err.empty()) {
             void *d = nullptr;
             if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes(out, in)) != hipSuccess) {
                 err = "device allocation of weight planes failed";
@@ -423,7 +441,7 @@ struct Packer {
 
 bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err) {
     const mdx_model_cfg &cfg = m.cfg;
-    Packer P{m, sd, ""};
+    Packer P{m, sd, "", m.dt};
     const std::string bu = "backbone.bottom_up";
     m.stem = P.stem(bu + ".stem.conv1");
     const int nb50[4] = {3, 4, 6, 3}, nb101[4] = {3, 4, 23, 3};
@@ -511,7 +529,9 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
             m.box_pred = P.linear(w, 5 * nc + 1, F, b);
         }
     }
+    P.cur_dt = m.hdt;  // the mask and keypoint heads (fp16 in the mixed configuration)
     if (cfg.mask_on) {
+        P.map_hw = cfg.mask_pooler_resolution;
         for (int i = 0; i < cfg.mask_num_conv; ++i)
             m.mask_convs.push_back(P.conv_plain("roi_heads.mask_head.mask_fcn" + std::to_string(i + 1), 1, 1, true));
         const int cin = cfg.mask_num_conv ? cfg.mask_conv_dim : C, co = cfg.mask_conv_dim;
@@ -530,6 +550,7 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
         m.mask_pred = P.conv_plain("roi_heads.mask_head.predictor", 1, 0, true);
     }
     if (cfg.keypoint_on) {
+        P.map_hw = cfg.keypoint_pooler_resolution;
         for (int i = 0; i < cfg.n_keypoint_convs; ++i)
             m.kp_convs.push_back(
                 P.conv_plain("roi_heads.keypoint_head.conv_fcn" + std::to_string(i + 1), 1, 1, true));
@@ -577,7 +598,23 @@ struct Fwd {
                bool in_planes = false) {
         OH = (H + 2 * cw.pad - cw.k) / cw.stride + 1;
         OW = (W + 2 * cw.pad - cw.k) / cw.stride + 1;
-        const size_t oes = out_f32 ? 4 : m.es;
+        const size_t oes = out_f32 ? 4 : (cw.dt == 1 ? 2 : 4);
+        // a Linear layer whose A operand passes the 2 GiB range of a buffer
+        // descriptor (fp32 box fc1 at B = 64: 64000 x 12544 x 4 B) runs as
+        // row slices of the same GEMM
+        const size_t ies = cw.dt == 1 ? 2 : 4;
+        if (cw.k == 1 && H == 1 && W == 1 && !in_planes && (size_t)N * cw.cin * ies >= (1ull << 31)) {
+            if (!out) out = alloc((size_t)N * cw.cout * oes);
+            const int rows = (int)(((1ull << 30) / ((size_t)cw.cin * ies)) / 256 * 256);
+            for (int r0 = 0; r0 < N; r0 += rows) {
+                const int n = std::min(rows, N - r0);
+                int oh_, ow_;
+                conv((const char *)x + (size_t)r0 * cw.cin * ies, n, 1, 1, cw, relu, oh_, ow_,
+                     residual ? (const char *)residual + (size_t)r0 * cw.cout * oes : nullptr, out_f32, out_mode,
+                     (char *)out + (size_t)r0 * cw.cout * oes);
+            }
+            return out;
+        }
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
         const int wm = mdx_winograd_tile(H, W, mdx_conv_winograd_enabled());
         const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : wm == 6 ? cw.wino6 : nullptr;
@@ -588,7 +625,7 @@ struct Fwd {
         }
         // fp32 Linear layers in split-plane mode: activations split into bf16
         // planes, GEMM on the bf16 matrix cores (mdx_gemm_x6)
-        const bool x6 = cw.x6 && m.dt == 0 && !out_f32 && out_mode == 0 && cw.k == 1 && cw.stride == 1 &&
+        const bool x6 = cw.x6 && cw.dt == 0 && !out_f32 && out_mode == 0 && cw.k == 1 && cw.stride == 1 &&
                         mdx_conv_fp32_split() == 6;
         if (in_planes && !x6 && rc == MDX_OK) {
             set_error("model forward: plane input for a layer not in split-plane mode");
@@ -635,13 +672,13 @@ struct Fwd {
             }
         } else
             chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,
-                                  relu ? 1 : 0, out_mode, m.dt, out_f32 ? 0 : m.dt, out, 0, splitk, SPLITK_WS, s));
+                                  relu ? 1 : 0, out_mode, cw.dt, out_f32 ? 0 : cw.dt, out, 0, splitk, SPLITK_WS, s));
         if (pe) {
             (void)hipEventRecord(pe->e1, s);
             int kid = -1, ks = 0;
             mdx_conv2d_last_plan(&kid, &ks);
             const int64_t M = (int64_t)N * OH * OW, K = (int64_t)cw.k * cw.k * cw.cin;
-            pe->r = mdx_conv_record{kid + (out_f32 && m.dt == 1 ? 10 : 0), ks, M, cw.cout, K,
+            pe->r = mdx_conv_record{kid + (out_f32 && cw.dt == 1 ? 10 : 0), ks, M, cw.cout, K,
                                     2.0 * (double)M * cw.cout * (cw.kalg ? cw.kalg : K), 0.0};
         }
         return out;
@@ -682,9 +719,17 @@ struct Fwd {
         return out;
     }
     // planes: fp32 pooled rows written as bf16 planes (mdx_roi_align dtype 2)
+    // out_dt: dtype of the pooled rows (the heads' dtype); pooled in the
+    // trunk's dtype and converted when they differ (mixed configuration)
     void *roi_align(void *const *feats, const int *fh, const int *fw, const float *rois, const int *counts, int R,
-                    int per_image, int P, bool planes = false) {
+                    int per_image, int P, bool planes = false, int out_dt = -1) {
         const int C = m.cfg.fpn_out_channels;
+        if (out_dt >= 0 && out_dt != m.dt && !planes) {
+            void *pooled = roi_align(feats, fh, fw, rois, counts, R, per_image, P);
+            void *cvt = alloc((size_t)R * P * P * C * (out_dt == 1 ? 2 : 4));
+            if (!c.dry && ok()) chk(mdx_convert(pooled, (int64_t)R * P * P * C, m.dt, cvt, out_dt, s));
+            return cvt;
+        }
         void *out = alloc(planes ? (size_t)mdx_x6_plane_bytes(R, P * P * C) : (size_t)R * P * P * C * m.es);
         // the box pooler (per_image = post-NMS proposals) runs in level/band order
         int *order = per_image >= 256 ? (int *)alloc((size_t)R * sizeof(int)) : nullptr;
@@ -842,7 +887,7 @@ struct Fwd {
         const int R2 = B * D;
         if (cfg.mask_on) {
             const int M = cfg.mask_pooler_resolution;
-            const void *t = roi_align(feat, fh, fw, o ? o->boxes : nullptr, o ? o->ndet : nullptr, R2, D, M);
+            const void *t = roi_align(feat, fh, fw, o ? o->boxes : nullptr, o ? o->ndet : nullptr, R2, D, M, false, m.hdt);
             for (const ConvW &cw : m.mask_convs) t = conv(t, R2, M, M, cw, true, oh, ow);
             t = conv(t, R2, M, M, m.mask_deconv, true, oh, ow, nullptr, false, 1);
             float *logits = (float *)conv(t, R2, 2 * M, 2 * M, m.mask_pred, false, oh, ow, nullptr, true);
@@ -853,7 +898,7 @@ struct Fwd {
         }
         if (cfg.keypoint_on) {
             const int Pk = cfg.keypoint_pooler_resolution, K = cfg.num_keypoints;
-            const void *t = roi_align(feat, fh, fw, o ? o->boxes : nullptr, o ? o->ndet : nullptr, R2, D, Pk);
+            const void *t = roi_align(feat, fh, fw, o ? o->boxes : nullptr, o ? o->ndet : nullptr, R2, D, Pk, false, m.hdt);
             for (const ConvW &cw : m.kp_convs) t = conv(t, R2, Pk, Pk, cw, true, oh, ow);
             float *yk = (float *)conv(t, R2, Pk, Pk, m.kp_deconv, false, oh, ow, nullptr, true);
             float *low = (float *)alloc((size_t)R2 * K * 4 * Pk * Pk * 4);
@@ -944,6 +989,8 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     *out = nullptr;
     MDX_REQUIRE(cfg->depth == 50 || cfg->depth == 101, "mdx_model_create: depth must be 50 or 101");
     MDX_REQUIRE(cfg->dtype == 0 || cfg->dtype == 1, "mdx_model_create: dtype must be 0 (f32) or 1 (f16)");
+    MDX_REQUIRE(cfg->head_dtype == 0 || cfg->head_dtype == 1,
+                "mdx_model_create: head_dtype must be 0 (as dtype) or 1 (f16 mask + keypoint heads)");
     MDX_REQUIRE(cfg->num_classes == 1, "mdx_model_create: the extraction model has one class (NUM_CLASSES=1)");
     MDX_REQUIRE(cfg->n_anchor_sizes == 5 && cfg->n_aspect_ratios >= 1 && cfg->n_aspect_ratios <= 8,
                 "mdx_model_create: 5 anchor sizes (one per level p2..p6) and 1..8 aspect ratios");
@@ -964,6 +1011,7 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     m->cfg = *cfg;
     m->dev = device;
     m->dt = cfg->dtype;
+    m->hdt = cfg->head_dtype == 1 ? 1 : cfg->dtype;
     m->es = cfg->dtype == 1 ? 2 : 4;
     m->stem_fold = cfg->dtype == 0 && g_stem_fold;
     m->fuse_sc = g_fuse_sc == 2 || (g_fuse_sc == 1 && cfg->dtype == 0);

@@ -164,6 +164,18 @@ __global__ __launch_bounds__(256) void k_maxpool(const T *__restrict__ x, int N,
 }
 
 // ---------------------------------------------------------------------------
+// dtype conversion (f32 <-> f16, round to nearest even), 8 values per lane
+// ---------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void k_convert(const TI *__restrict__ x, long long n8, TO *__restrict__ y) {
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+        float v[8];
+        ld8(x + i * 8, v);
+        st8(y + i * 8, v);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // GroupNorm
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float block_sum(float v, float *red) {
@@ -2101,6 +2113,24 @@ extern "C" int mdx_maxpool2d(const void *x, int N, int H, int W, int C, int k, i
 extern "C" int64_t mdx_groupnorm_workspace_bytes(int N, int H, int W, int G) {
     const long long nch = ((long long)H * W + GN_CHUNK_PIX - 1) / GN_CHUNK_PIX;
     return (long long)N * G * 2 * 4 + (long long)N * G * nch * 3 * 4 + 64;
+}
+
+extern "C" int mdx_convert(const void *x, int64_t n, int in_dtype, void *out, int out_dtype, mdx_stream_t stream) {
+    MDX_REQUIRE(x && out && n >= 0 && n % 8 == 0, "mdx_convert: null pointer or n not a multiple of 8");
+    MDX_REQUIRE((in_dtype == 0 || in_dtype == 1) && (out_dtype == 0 || out_dtype == 1), "mdx_convert: bad dtype");
+    if (n == 0) return MDX_OK;
+    const unsigned grid = (unsigned)std::min<long long>((n / 8 + 255) / 256, 8192);
+    hipStream_t s = as_stream(stream);
+    if (in_dtype == 0 && out_dtype == 1)
+        hipLaunchKernelGGL((k_convert<float, _Float16>), dim3(grid), dim3(256), 0, s, (const float *)x, n / 8,
+                           (_Float16 *)out);
+    else if (in_dtype == 1 && out_dtype == 0)
+        hipLaunchKernelGGL((k_convert<_Float16, float>), dim3(grid), dim3(256), 0, s, (const _Float16 *)x, n / 8,
+                           (float *)out);
+    else
+        MDX_HIP(hipMemcpyAsync(out, x, (size_t)n * (in_dtype == 1 ? 2 : 4), hipMemcpyDeviceToDevice, s));
+    MDX_CHECK_LAUNCH("mdx_convert");
+    return MDX_OK;
 }
 
 extern "C" int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, const float *gamma,

@@ -27,7 +27,10 @@ from .._lib import MdxError, call, lib
 from .config import ModelConfig
 from .weights import pack_blob, resnet_stage_specs
 
-_DT = {"fp32": 0, "fp16": 1}
+# "mixed": fp32 backbone / FPN / RPN / box head, fp16 mask + keypoint heads
+# (BASELINE config 5: "Keypoint+Mask heads fp16")
+_DT = {"fp32": 0, "fp16": 1, "mixed": 0}
+_HEAD_DT = {"fp32": 0, "fp16": 0, "mixed": 1}
 _TDT = {0: torch.float32, 1: torch.float16, 2: torch.int32, 3: torch.bfloat16}
 
 
@@ -58,7 +61,7 @@ class ModelCfgC(ctypes.Structure):
         ("pooler_sampling_ratio", ctypes.c_int), ("pooler_aligned", ctypes.c_int),
         ("canonical_box_size", ctypes.c_float), ("canonical_level", ctypes.c_float), ("in_channels", ctypes.c_int),
         ("pixel_mean", ctypes.c_float * 3), ("pixel_std", ctypes.c_float * 3), ("size_divisibility", ctypes.c_int),
-        ("rpn_bbox_reg_weights", ctypes.c_float * 4),
+        ("rpn_bbox_reg_weights", ctypes.c_float * 4), ("head_dtype", ctypes.c_int),
     ]
 
 
@@ -113,6 +116,7 @@ def model_cfg_c(cfg: ModelConfig, dtype: str) -> ModelCfgC:
     c.pixel_std[:] = [float(v) for v in (list(cfg.pixel_std) * 3)[:3]]
     c.size_divisibility = cfg.size_divisibility
     c.rpn_bbox_reg_weights[:] = [float(v) for v in cfg.rpn_bbox_reg_weights]
+    c.head_dtype = _HEAD_DT[dtype]
     return c
 
 
@@ -124,7 +128,7 @@ class MaskRCNN:
         if not torch.cuda.is_available():
             raise MdxError("MaskRCNN needs an AMD GPU; there is no CPU fallback")
         if dtype not in _DT:
-            raise ValueError("dtype must be 'fp16' or 'fp32'")
+            raise ValueError("dtype must be 'fp32', 'fp16' or 'mixed' (fp32 trunk, fp16 mask + keypoint heads)")
         if cfg.num_classes != 1:
             raise NotImplementedError("the extraction model has one class (ROI_HEADS.NUM_CLASSES=1)")
         self.cfg = cfg

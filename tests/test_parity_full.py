@@ -57,7 +57,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, cen=0.5, ang=1.0, margin=0.0),
-       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05)}
+       "fp16": dict(feat=3e-2, box_iou=0.9, score=2e-2, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05),
+       # BASELINE config 5 as stated: fp32 trunk / RPN / box head (the fp32
+       # feature and box bounds), fp16 mask + keypoint heads (the fp16 mask,
+       # keypoint and pose bounds)
+       "mixed": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05)}
 MASK_PX_FLOOR = 4       # pixels: the seeded-weight masks can be a handful of pixels
 MIN_POSES = 8           # non-NaN poses (both sides) per case
 MIN_SEL_EXACT = 0.9     # fp32: fraction of frames whose selected mask is the oracle's, pixel for pixel
@@ -169,7 +173,8 @@ def _oracle(depth, B):
 @pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 6, 0),
                                                       (50, 32, "fp32", 2, 0),
                                                       (50, 32, "fp32", 0, 0), (50, 32, "fp32", 4, 6),
-                                                      (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0)])
+                                                      (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0),
+                                                      (101, 64, "mixed", 6, 0), (101, 64, "fp32", 6, 0)])
 def test_forward_full_frame(mdx, depth, B, dtype, wino, split):
     """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
     6 = F(6x6,3x3) on the large maps and F(4x4,3x3) elsewhere, 2 = F(2x2,3x3),

@@ -1,0 +1,114 @@
+// Minimal reproduction of the fp16 GroupNorm statistics that changed from
+// run to run under concurrency when model_ops.hip was compiled with the
+// packed-FP32 VALU forms ("Concurrency").  The GroupNorm
+// kernels are the library's own (model_ops.hip is included, not copied);
+// the host loop launches k_gn_partial + k_gn_final on stream A over the same
+// fp16 input again and again while stream B runs a background load, and
+// compares every result with the first one bit for bit.  A pure function
+// of its input must never change; any change means a race, a read of
+// uninitialised memory or an execution hazard.
+//
+// Build (two binaries, the flag the only difference):
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I. -munsafe-fp-atomics \
+//     tools/native/gn_repro.hip -o gn_repro_pk
+//   ... -Xclang -target-feature -Xclang -packed-fp32-ops ... -o gn_repro_nopk
+// Run: gn_repro_<v> REPS BG (BG: 0 none, 1 VALU loop, 2 HBM copy, 3 both)
+#include "moseq2-detectron-extract_amd/csrc/model_ops.hip"
+namespace mdx {
+void set_error(const char *, ...) {}
+}
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));         \
+            exit(2);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+// background VALU load: long dependent FMA chains on registers
+__global__ __launch_bounds__(256) void k_bg_valu(float *out, int iters) {
+    float a = threadIdx.x * 1e-3f, b = blockIdx.x * 1e-4f, c = 1.0001f;
+    for (int i = 0; i < iters; ++i) {
+        a = fmaf(a, c, b);
+        b = fmaf(b, c, a);
+    }
+    if (a == 12345.f) out[threadIdx.x] = a + b;  // keep the loop
+}
+
+// background HBM load: streaming copy
+__global__ __launch_bounds__(256) void k_bg_copy(const float4 *src, float4 *dst, long long n) {
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    const int bg = argc > 2 ? atoi(argv[2]) : 3;
+    const int N = 4, H = 112, W = 128, C = 256, G = 32, HW = H * W;
+    const int nch = (HW + mdx::GN_CHUNK_PIX - 1) / mdx::GN_CHUNK_PIX;
+    const size_t nx = (size_t)N * HW * C;
+    std::vector<_Float16> hx(nx);
+    unsigned s = 12345u;
+    for (size_t i = 0; i < nx; ++i) {
+        s = s * 1664525u + 1013904223u;
+        hx[i] = (_Float16)(((s >> 8) & 0xffff) / 65536.0f * 8.0f - 3.0f);
+    }
+    _Float16 *x;
+    float *part, *stats, *bgout;
+    float4 *bsrc, *bdst;
+    const long long nbg = 64ll << 20;  // 1 GiB each way
+    CK(hipMalloc(&x, nx * 2));
+    CK(hipMalloc(&part, (size_t)N * G * nch * 3 * 4));
+    CK(hipMalloc(&stats, (size_t)N * G * 2 * 4));
+    CK(hipMalloc(&bgout, 4096));
+    CK(hipMalloc(&bsrc, nbg * 16));
+    CK(hipMalloc(&bdst, nbg * 16));
+    CK(hipMemset(bsrc, 0, nbg * 16));
+    CK(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+    hipStream_t sa, sb;
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    const size_t npart = (size_t)N * G * nch * 3, nstat = (size_t)N * G * 2;
+    std::vector<float> p0(npart), s0(nstat), p1(npart), s1(nstat);
+    int bad_part = 0, bad_stat = 0;
+    for (int r = 0; r <= reps; ++r) {
+        CK(hipMemsetAsync(part, 0xff, npart * 4, sa));  // stale partials would show as NaN
+        if (r > 0 && (bg & 1))
+            hipLaunchKernelGGL(k_bg_valu, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
+        if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
+        hipLaunchKernelGGL(mdx::k_gn_partial<_Float16>, dim3(nch, N), dim3(256), 0, sa, x, HW, C, G, part);
+        hipLaunchKernelGGL(mdx::k_gn_final, dim3((N * G + 3) / 4), dim3(256), 0, sa, part, N * G, nch, 1e-5f, stats);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        std::vector<float> &pp = r == 0 ? p0 : p1, &ss = r == 0 ? s0 : s1;
+        CK(hipMemcpy(pp.data(), part, npart * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(ss.data(), stats, nstat * 4, hipMemcpyDeviceToHost));
+        if (r == 0) continue;
+        if (memcmp(p0.data(), p1.data(), npart * 4)) {
+            ++bad_part;
+            if (bad_part <= 3) {
+                int nd = 0, first = -1;
+                for (size_t i = 0; i < npart; ++i)
+                    if (memcmp(&p0[i], &p1[i], 4)) {
+                        if (first < 0) first = (int)i;
+                        ++nd;
+                    }
+                // partial index -> (image, group, chunk, field)
+                const int f = first % 3, ch = (first / 3) % nch, g = (first / 3 / nch) % G, n = first / 3 / nch / G;
+                printf("rep %d: %d partial floats differ; first: image %d group %d chunk %d field %d: %.9g vs %.9g\n",
+                       r, nd, n, g, ch, f, p0[first], p1[first]);
+            }
+        }
+        if (memcmp(s0.data(), s1.data(), nstat * 4)) ++bad_stat;
+    }
+    printf("{\"reps\": %d, \"background\": %d, \"partials_differ\": %d, \"stats_differ\": %d}\n", reps, bg, bad_part,
+           bad_stat);
+    return 0;
+}
