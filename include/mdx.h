@@ -268,6 +268,14 @@ int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U);
 int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m);
 int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias, int Cout,
                          int relu, int m, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
+/* Split-plane mode (mdx_conv_set_fp32_split(6)): the same layer with U also
+ * split once into bf16 planes (mdx_split_x6 of U as NB*Cout rows of Cin):
+ * the input transform writes V as planes and the NB GEMMs run on the 256x256
+ * LDS-DMA plane kernel (k_gemm_x6) when they give it >= 384 workgroups;
+ * otherwise as mdx_conv3x3_winograd.  Cin % 16 == 0 for the plane path. */
+int mdx_conv3x3_winograd_x6(const float *x, int N, int H, int W, int Cin, const float *U, const void *U_planes,
+                            const float *bias, int Cout, int relu, int m, float *out, void *workspace,
+                            int64_t workspace_bytes, mdx_stream_t stream);
 int mdx_conv_set_winograd(int mode);
 int mdx_conv_winograd_enabled(void);
 int mdx_winograd_tile(int H, int W, int mode);

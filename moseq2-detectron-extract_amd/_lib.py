@@ -63,6 +63,7 @@ SIGNATURES = {
     "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),
     "mdx_winograd_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32]),
     "mdx_conv3x3_winograd": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
+    "mdx_conv3x3_winograd_x6": (I32, [P, I32, I32, I32, I32, P, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_conv_set_winograd": (I32, [I32]),
     "mdx_conv_winograd_enabled": (I32, []),
     "mdx_winograd_tile": (I32, [I32, I32, I32]),

@@ -1827,6 +1827,83 @@ __global__ __launch_bounds__(256) void k_wino_in(const float *__restrict__ x, in
         }
 }
 
+// k_wino_in writing V straight into the bf16 plane layout of k_gemm_x6
+// (split-plane mode): each thread transforms one channel of the tile into
+// LDS ([xi][channel] fp32), then the workgroup re-reads 8 consecutive
+// channels of one xi per item, splits them (x = hi + mid + lo exactly, as
+// k_split_x6) and stores the three 16-B plane pieces.  Channel block = 256
+// (or C); C % 16 == 0.
+template <int M>
+__global__ __launch_bounds__(256) void k_wino_in_x6(const float *__restrict__ x, int N, int H, int W, int C, int TH,
+                                                    int TW, char *__restrict__ Vp) {
+    constexpr int A = WinoT<M>::A, NB = A * A;
+    __shared__ float s_v[NB * 256];
+    const int t = blockIdx.x;
+    const int cb = blockIdx.y * blockDim.x;
+    const int c = cb + threadIdx.x;
+    const long long T = (long long)N * TH * TW;
+    const int tx = t % TW, r = t / TW;
+    const int ty = r % TH, n = r / TH;
+    const int y0 = M * ty - 1, x0 = M * tx - 1;
+    if (c < C) {
+        const float *xb = x + (long long)n * H * W * C + c;
+        float d[A][A];
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                const int yy = y0 + i, xx = x0 + j;
+                d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? xb[((long long)yy * W + xx) * C] : 0.f;
+            }
+        float tt[A][A];
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(i, k) != 0.f) acc = acc + WinoT<M>::BT(i, k) * d[k][j];
+                tt[i][j] = acc;
+            }
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < A; ++k)
+                    if (WinoT<M>::BT(j, k) != 0.f) acc = acc + tt[i][k] * WinoT<M>::BT(j, k);
+                s_v[(A * i + j) * 256 + threadIdx.x] = acc;
+            }
+    }
+    __syncthreads();
+    const int g8n = (int)blockDim.x / 8;  // 8-channel groups of this block
+    const long long rowb = (long long)C * 6;   // plane bytes of one V row (tile)
+    for (int it = threadIdx.x; it < NB * g8n; it += blockDim.x) {
+        const int xi = it / g8n, g8 = it - xi * g8n;
+        const int c0 = cb + 8 * g8;
+        if (c0 >= C) continue;
+        const float4 u = *reinterpret_cast<const float4 *>(s_v + xi * 256 + 8 * g8);
+        const float4 v = *reinterpret_cast<const float4 *>(s_v + xi * 256 + 8 * g8 + 4);
+        const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        bf16x8 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const __bf16 hb = (__bf16)f[e];
+            const float r1 = f[e] - (float)hb;
+            const __bf16 mb = (__bf16)r1;
+            h[e] = hb;
+            m[e] = mb;
+            l[e] = (__bf16)(r1 - (float)mb);
+        }
+        char *o = Vp + ((long long)xi * T + t) * rowb + (long long)(c0 >> 4) * X6_ROWB + ((c0 >> 3) & 1) * 16;
+        *reinterpret_cast<bf16x8 *>(o) = h;
+        *reinterpret_cast<bf16x8 *>(o + 32) = m;
+        *reinterpret_cast<bf16x8 *>(o + 64) = l;
+    }
+}
+
 // one thread per (tile, output channel), laid out as k_wino_in
 template <int M>
 __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
@@ -2536,7 +2613,8 @@ extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, fl
 extern "C" int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m) {
     if (m != 2 && m != 4 && m != 6) return -1;
     const long long T = (long long)N * ((H + m - 1) / m) * ((W + m - 1) / m);
-    return (long long)(m + 2) * (m + 2) * T * (Cin + Cout) * 4 + 256;
+    // fp32 V + M, or (split-plane mode) V as bf16 planes (6 B per value) + M
+    return (long long)(m + 2) * (m + 2) * T * (Cin * 6 + Cout * 4) + 256;
 }
 
 // policy 6: F(6,3) where its 8x8 tiles execute under 0.9x the tile products
@@ -2552,9 +2630,30 @@ extern "C" int mdx_winograd_tile(int H, int W, int mode) {
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
+// split-plane Winograd GEMMs on k_gemm_x6 when the batch gives it at least
+// this many 256 x 256 workgroups (below: k_conv_x3)
+static int g_wino_x6_min_wgs = 384;
+
+static int winograd_impl(const float *x, int N, int H, int W, int Cin, const float *U, const void *Up,
+                         const float *bias, int Cout, int relu, int m, float *out, void *workspace,
+                         int64_t workspace_bytes, mdx_stream_t stream);
+
 extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias,
                                     int Cout, int relu, int m, float *out, void *workspace, int64_t workspace_bytes,
                                     mdx_stream_t stream) {
+    return winograd_impl(x, N, H, W, Cin, U, nullptr, bias, Cout, relu, m, out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mdx_conv3x3_winograd_x6(const float *x, int N, int H, int W, int Cin, const float *U,
+                                       const void *U_planes, const float *bias, int Cout, int relu, int m, float *out,
+                                       void *workspace, int64_t workspace_bytes, mdx_stream_t stream) {
+    MDX_REQUIRE(U_planes, "mdx_conv3x3_winograd_x6: null U planes");
+    return winograd_impl(x, N, H, W, Cin, U, U_planes, bias, Cout, relu, m, out, workspace, workspace_bytes, stream);
+}
+
+static int winograd_impl(const float *x, int N, int H, int W, int Cin, const float *U, const void *Up,
+                         const float *bias, int Cout, int relu, int m, float *out, void *workspace,
+                         int64_t workspace_bytes, mdx_stream_t stream) {
     MDX_REQUIRE(x && U && out && workspace, "mdx_conv3x3_winograd: null pointer");
     MDX_REQUIRE(m == 2 || m == 4 || m == 6, "mdx_conv3x3_winograd: tile m must be 2, 4 or 6");
     MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cin % 4 == 0 && Cout % 8 == 0,
@@ -2569,8 +2668,14 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
                     (long long)Cout * Cin * 4 < (1ll << 31),
                 "mdx_conv3x3_winograd: layer too large");
     hipStream_t s = as_stream(stream);
+    // split-plane mode with the U planes: V written as planes, the NB GEMMs on
+    // the 256 x 256 LDS-DMA plane kernel (if the batch fills the chip)
+    const long long x6_wgs = ceil_div(T, X6_BM) * ceil_div(Cout, X6_BN) * NB;
+    const bool planes = Up && g_fp32_split == 6 && Cin % 16 == 0 && x6_wgs >= g_wino_x6_min_wgs &&
+                        T * Cin * 6 < (1ll << 31) && (long long)Cout * Cin * 6 < (1ll << 31);
     float *V = reinterpret_cast<float *>(workspace);
-    float *Mx = V + NB * T * Cin;
+    float *Mx = planes ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + NB * T * Cin * 6)
+                       : V + NB * T * Cin;
     WinoProbe *probe = t_wino_probe;
     auto mark = [&](int i) {
         if (probe) (void)hipEventRecord(probe->ev[i], s);
@@ -2581,7 +2686,17 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
         bd = (unsigned)std::min(256, (ch + 63) / 64 * 64);
         return dim3((unsigned)T, (unsigned)((ch + (int)bd - 1) / (int)bd));
     };
-    {
+    if (planes) {
+        unsigned bd;
+        const dim3 grid = tgrid(Cin, bd);
+        char *Vp = reinterpret_cast<char *>(workspace);
+        if (m == 2)
+            hipLaunchKernelGGL(k_wino_in_x6<2>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
+        else if (m == 4)
+            hipLaunchKernelGGL(k_wino_in_x6<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
+        else
+            hipLaunchKernelGGL(k_wino_in_x6<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
+    } else {
         unsigned bd;
         const dim3 grid = tgrid(Cin, bd);
         if (m == 2)
@@ -2620,7 +2735,18 @@ extern "C" int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin
     const long long t256 = ceil_div(T, G_BM) * (Cout / G_BN);
     const bool dma = !g_fp32_split && Cin % 32 == 0 && Cout % G_BN == 0 &&
                      (g_wino_dma == 2 || (g_wino_dma == 1 && t256 * NB >= g_wino_dma_min_wgs));
-    if (dma) {
+    if (planes) {
+        a.x = workspace;
+        a.w = Up;
+        a.xbytes = 0;
+        a.wbytes = 0;
+        a.bsx = T * Cin * 6;
+        a.bsw = (long long)Cout * Cin * 6;
+        a.tiles_n = (int)ceil_div(Cout, X6_BN);
+        a.tiles_total = (int)(ceil_div(T, X6_BM) * a.tiles_n);
+        hipLaunchKernelGGL(k_gemm_x6, dim3((unsigned)a.tiles_total, 1, (unsigned)NB), dim3(X6_THREADS), X6_LDS, s, a);
+        gemm_kernel = MDX_CONV_KERNEL_X6DMA;
+    } else if (dma) {
         a.tiles_n = Cout / G_BN;
         a.tiles_total = (int)t256;
         a.ksteps = Cin / 16;  // 16-float substeps

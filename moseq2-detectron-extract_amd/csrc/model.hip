@@ -53,6 +53,9 @@ struct ConvW {
     // Winograd weights U = G g G^T of F(2x2,3x3) [16][Cout][Cin] and F(4x4,3x3)
     // [36][Cout][Cin] (fp32 3x3/s1/p1 layers with Cin >= 128)
     float *wino2 = nullptr, *wino4 = nullptr, *wino6 = nullptr;
+    // the same U split into bf16 planes (split-plane mode handles):
+    // winox6[m / 2 - 1] for F(m x m, 3x3)
+    void *winox6[3] = {nullptr, nullptr, nullptr};
     // fp32 Linear layers: the weights split once into bf16 planes for
     // mdx_gemm_x6 (used while mdx_conv_fp32_split() != 0)
     void *x6 = nullptr;
@@ -289,9 +292,24 @@ struct Packer {
                     oihw[(size_t)o * ci * 9 + q] = w->v[(size_t)o * ci * 9 + q] * (scale ? scale[o] : 1.f);
             for (int m_ : {2, 4, 6}) {
                 if (!want_tile(m_)) continue;
-                u.resize((size_t)(m_ + 2) * (m_ + 2) * co * ci);
+                const int nb = (m_ + 2) * (m_ + 2);
+                u.resize((size_t)nb * co * ci);
                 mdx_winograd_weights(oihw.data(), co, ci, m_, u.data());
-                (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = upload_f32(u);
+                float *ud = upload_f32(u);
+                (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = ud;
+                // split-plane handles: U as bf16 planes too (k_gemm_x6's B operand)
+                if (mdx_conv_fp32_split() == 6 && ci % 16 == 0 && ud && err.empty()) {
+                    void *d = nullptr;
+                    if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes((int64_t)nb * co, ci)) != hipSuccess) {
+                        err = "device allocation of Winograd weight planes failed";
+                        break;
+                    }
+                    m.allocs.push_back(d);
+                    if (mdx_split_x6(ud, (int64_t)nb * co, ci, ci, d, nullptr) != MDX_OK ||
+                        hipDeviceSynchronize() != hipSuccess)
+                        err = "Winograd weight plane split failed";
+                    c.winox6[m_ / 2 - 1] = d;
+                }
             }
         }
         return c;
@@ -651,8 +669,13 @@ struct Fwd {
             chk(mdx_gemm_x6(in_planes ? x : planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
                             (float *)out, s));
         } else if (wino) {
-            chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
-                                     (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
+            const void *wx6 = mdx_conv_fp32_split() == 6 ? cw.winox6[wm / 2 - 1] : nullptr;
+            if (wx6)
+                chk(mdx_conv3x3_winograd_x6((const float *)x, N, H, W, cw.cin, wu, wx6, cw.b, cw.cout, relu ? 1 : 0,
+                                            wm, (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
+            else
+                chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
+                                         (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
             if (m.profile) {
                 wino_probe(nullptr);
                 // three records: input transform, batched GEMM, output transform
