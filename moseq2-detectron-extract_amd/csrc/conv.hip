@@ -19,6 +19,8 @@
 // Blocks are remapped XCD-contiguously so the tiles that share an input row
 // panel run on one XCD's L2.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "common.h"
@@ -94,6 +96,15 @@ struct ConvArgs {
     // projection shortcut concatenated onto its conv3 GEMM)
     const void *x2;
     int K1, H2, W2, Cin2, stride2, x2bytes;
+    // K lock-step pacing of a row panel's column tiles (k_conv_sb, deep-K
+    // layers: box fc1): pace[tm] counts the K chunks of pace_steps steps the
+    // panel's tiles have finished; a tile that is pace_lag chunks ahead of
+    // its slowest sibling waits (bounded: after pace_spin polls it stops
+    // pacing), so the panel's A rows are fetched into the XCD's L2 once and
+    // read there by all tiles_n tiles.  Performance only: the sums do not
+    // depend on it.  null = off.
+    int *pace;
+    int pace_steps, pace_lag, pace_spin;
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -433,7 +444,34 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
     };
     int kt = 0;
     if constexpr (SB) {
-        for (; kt < nk; ++kt) kstep(kt, ra[0], rb[0], ra[0], rb[0]);
+        if (a.pace) {
+            // thread 0 publishes each finished chunk and, ahead of the
+            // workgroup's next barrier, waits for the lagging siblings (the
+            // other waves wait at that barrier); relaxed agent-scope atomics
+            // in a divergent branch (vector memory instructions).  A wait
+            // that times out (a sibling not resident, e.g. beside another
+            // stream's kernels) ends pacing for this tile.
+            int *pace = a.pace + tm;
+            for (; kt < nk; ++kt) {
+                kstep(kt, ra[0], rb[0], ra[0], rb[0]);
+                if ((kt + 1) % a.pace_steps == 0 && kt + 1 < nk) {
+                    if (tid == 0 && pace) {
+                        __hip_atomic_fetch_add(pace, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const int need = ((kt + 1) / a.pace_steps - a.pace_lag) * a.tiles_n;
+                        int it = 0;
+                        while (__hip_atomic_load(pace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&
+                               it < a.pace_spin) {
+                            __builtin_amdgcn_s_sleep(1);
+                            ++it;
+                        }
+                        if (it >= a.pace_spin) pace = nullptr;
+                    }
+                    __syncthreads();
+                }
+            }
+        } else {
+            for (; kt < nk; ++kt) kstep(kt, ra[0], rb[0], ra[0], rb[0]);
+        }
     } else {
     for (; kt + 1 < nk; kt += 2) {
         kstep(kt, ra[0], rb[0], ra[1], rb[1]);
@@ -2367,6 +2405,27 @@ general:
         return MDX_OK;
     }
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
+    // K lock-step pacing of deep-K fp32 pointwise GEMMs (box fc1): counters
+    // at the start of the (unused, ksplit == 1) split-K workspace
+    {
+        static const int pace_env = [] {
+            const char *e = getenv("MDX_PACE");  // A/B: "steps,lag" ("0" off)
+            return e ? atoi(e) : 0;
+        }();
+        static const int pace_lag = [] {
+            const char *e = getenv("MDX_PACE");
+            const char *c = e ? strchr(e, ',') : nullptr;
+            return c ? atoi(c + 1) : 1;
+        }();
+        if (pace_env > 0 && pw && g_conv_sb && in_dtype == 0 && out_dtype == 0 && a.ksplit == 1 && a.K >= 4096 &&
+            a.tiles_n >= 4 && workspace && (long long)tiles_m * 4 <= workspace_bytes) {
+            a.pace = reinterpret_cast<int *>(workspace);
+            a.pace_steps = pace_env;
+            a.pace_lag = pace_lag;
+            a.pace_spin = 2000;
+            MDX_HIP(hipMemsetAsync(workspace, 0, (size_t)tiles_m * 4, s));
+        }
+    }
     // (mode 3: the fp16 register-staged PW layers too; the fp16 model's big
     // layers stay on the LDS-DMA kernels)
     // (mode 4: as 3, plus the fp16 KxK layers the LDS-DMA kernels do not take)

@@ -13,3 +13,7 @@ echo "det pk rc=$rc"; tail -1 $O/det_pk_$T.log
 [ $rc -le 1 ] || exit $rc   # 1 = mismatches found; anything else: stop here
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -k "rpn_proposals or winograd_planes or benched_config" > $O/t$T.log 2>&1; echo "tests rc=$?"
 tail -8 $O/t$T.log
+# box fc1 alone: HBM bytes and time, pacing off / on
+bash tools/gpu_fc1_pmc.sh B0 || exit 1
+MDX_PACE=4,1 bash tools/gpu_fc1_pmc.sh B4 || exit 1
+MDX_PACE=2,1 bash tools/gpu_fc1_pmc.sh B2 || exit 1
