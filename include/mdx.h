@@ -219,7 +219,9 @@ int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const
  * bias/residual/ReLU.  ksplit 0 = choose from the grid size and workspace_bytes
  * (falls back to 1 slice when it does not pay or does not fit). */
 /* Policy for the 256x256 fp16 kernel (Cin % 64 == 0): 0 never, 1 auto (default:
- * when the layer fills the chip), 2 whenever eligible.  Returns the old mode. */
+ * when the layer fills the chip), 2 whenever eligible; 3 / 4 as 2 / 1 with
+ * the fp16 layers on the 256x128 tile (two workgroups per CU) instead.
+ * Returns the old mode. */
 int mdx_conv_set_large_tiles(int mode);
 /* Layers with KH*KW*Cin <= kmax use the 64-wide output-channel tile (more
  * workgroups per CU for HBM-bound small-K layers).  Returns the old value. */

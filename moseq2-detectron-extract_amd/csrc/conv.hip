@@ -1193,19 +1193,23 @@ extern "C" int mdx_conv_set_stream1x1_f32(int mode) {
     return old;
 }
 
-// NW waves (8: 256x256 tile, 4: 128x128 tile); tile = 32 NW rows of A and of
-// B.  Waves form WM_(2) x (NW/2); wave tile (BM/2) x (BN/(NW/2)).
+// Tile codes: 8 = 256x256 (8 waves), 4 = 128x128 (4 waves), both 4 LDS
+// buffers; 6 = 256x128 (4 waves, 3 buffers: 72 KiB, so two workgroups share
+// a CU and fill each other's barrier gaps).  Waves form 2 x WN; wave tile
+// (BM/2) x (BN/WN).
 template <int NW>
 struct GTile {
-    static constexpr int THREADS = 64 * NW, BM = 32 * NW, BN = 32 * NW;
-    static constexpr int WM = 2, WN = NW / 2;
+    static constexpr int WAVES = NW == 6 ? 4 : NW;
+    static constexpr int THREADS = 64 * WAVES, BM = NW == 6 ? 256 : 32 * NW, BN = NW == 6 ? 128 : 32 * NW;
+    static constexpr int WM = 2, WN = WAVES / 2;
     static constexpr int WROWS = BM / WM, WCOLS = BN / WN;      // wave tile
     static constexpr int TI = WROWS / 16, TJ = WCOLS / 16;      // MFMA tiles per wave
+    static constexpr int AJ = BM / (16 * WAVES), BJ = BN / (16 * WAVES);  // DMA instructions per wave and substep
     static constexpr int SUB = (BM + BN) * 64;                  // bytes per 32-deep K-substep
-    static constexpr int NBUF = 4;
+    static constexpr int NBUF = NW == 6 ? 3 : 4;
     static constexpr int EPI_PITCH = 68;                        // fp32 pitch of a wave's 64-column block
     static constexpr int EPI_ROWS = 64;                         // rows per epilogue pass
-    static constexpr int EPI = NW * EPI_ROWS * EPI_PITCH * 4;
+    static constexpr int EPI = WAVES * EPI_ROWS * EPI_PITCH * 4;
     static constexpr int LDS = NBUF * SUB > EPI ? NBUF * SUB : EPI;
 };
 constexpr int G_BM = GTile<8>::BM, G_BN = GTile<8>::BN, G_THREADS = GTile<8>::THREADS;
@@ -1237,9 +1241,10 @@ __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 // A K "chunk" is one 128-B run of input channels (64 halves / 32 floats),
 // split into two 64-B substeps.
 template <typename TIN, typename TO, int NW, bool ILV, bool PRIO = false, bool DMA_AFTER = false>
-__global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(ConvArgs a) {
+__global__ __launch_bounds__(GTile<NW>::THREADS, NW == 8 ? 1 : 2) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
+    constexpr int AJ = GT::AJ, BJ = GT::BJ, NBUF = GT::NBUF, PIECES = AJ + BJ;
     constexpr bool F32 = sizeof(TIN) == 4;
     constexpr int VEC = 16 / (int)sizeof(TIN);  // elements per 16-B piece
     constexpr int SUBK = 4 * VEC;               // K elements per substep (one 64-B row)
@@ -1263,17 +1268,18 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / GT::WN, wn = wid - wm * GT::WN;
 
-    // DMA descriptors: instruction j of wave w fills LDS rows 32w + 16j .. +16
+    // DMA descriptors: A instruction j of wave w fills LDS rows 16 (AJ w + j)
+    // .. +16, B instruction j rows 16 (BJ w + j) .. +16
     const TIN *X = reinterpret_cast<const TIN *>(a.x);
     const TIN *Wt = reinterpret_cast<const TIN *>(a.w);
     const int ohw = a.OH * a.OW;
-    int a_iy0[2], a_ix0[2];
-    long long a_base[2];
-    bool a_ok[2];
-    const TIN *b_src[2];
+    int a_iy0[AJ], a_ix0[AJ];
+    long long a_base[AJ];
+    bool a_ok[AJ];
+    const TIN *b_src[BJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int r = 32 * wid + 16 * j + (lane >> 2);
+    for (int j = 0; j < AJ; ++j) {
+        const int r = 16 * (AJ * wid + j) + (lane >> 2);
         const int c = (lane & 3) ^ g_swz(r);
         const int gm = m0 + r;
         a_ok[j] = gm < a.M;
@@ -1283,6 +1289,11 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         a_iy0[j] = oy * a.stride - a.pad;
         a_ix0[j] = ox * a.stride - a.pad;
         a_base[j] = (long long)b * a.H * a.W * a.Cin + c * VEC;
+    }
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+        const int r = 16 * (BJ * wid + j) + (lane >> 2);
+        const int c = (lane & 3) ^ g_swz(r);
         const int gn = n0 + r;
         b_src[j] = gn < a.Cout ? Wt + (long long)gn * a.K + c * VEC : nullptr;
     }
@@ -1290,10 +1301,10 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     // is in range, so the A piece address is a row pointer + the K offset
     // (fp32 only: the fp16 tile has no registers to spare for the pointers)
     const bool pointwise = F32 && a.KH == 1 && a.KW == 1 && a.pad == 0;
-    const TIN *a_row[2] = {nullptr, nullptr};
+    const TIN *a_row[AJ] = {};
     if constexpr (F32) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < AJ; ++j)
             a_row[j] = a_ok[j] ? X + a_base[j] + ((long long)a_iy0[j] * a.W + a_ix0[j]) * a.Cin : nullptr;
     }
     // issue state (uniform): the 64-chunk being issued and its tap
@@ -1309,11 +1320,11 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         i_kky = tap / a.KW;
         i_kkx = tap - i_kky * a.KW;
     }
-    // DMA piece p of the substep being issued into buffer buf: p = 0, 1 the A
-    // rows of instruction j = p, p = 2, 3 the B rows of j = p - 2
+    // DMA piece p of the substep being issued into buffer buf: p < AJ the A
+    // rows of instruction j = p, then the B rows of j = p - AJ
     auto issue_piece = [&](int buf, int p) {
         const int kofs = i_kci + SUBK * i_half;
-        if (p < 2) {
+        if (p < AJ) {
             const int j = p;
             const void *src;
             if (F32 && pointwise) {
@@ -1324,17 +1335,17 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
                 src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + kofs)
                          : (const void *)g_zero16;
             }
-            glds16(src, smem + buf * SUB + 32 * wid * 64 + j * 1024);
+            glds16(src, smem + buf * SUB + 16 * AJ * wid * 64 + j * 1024);
         } else {
-            const int j = p - 2;
+            const int j = p - AJ;
             const int kglob = (i_kky * a.KW + i_kkx) * a.Cin + kofs;
             glds16(b_src[j] ? (const void *)(b_src[j] + kglob) : (const void *)g_zero16,
-                   smem + buf * SUB + BM * 64 + 32 * wid * 64 + j * 1024);
+                   smem + buf * SUB + BM * 64 + 16 * BJ * wid * 64 + j * 1024);
         }
     };
     auto issue = [&](int buf) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) issue_piece(buf, p);
+        for (int p = 0; p < PIECES; ++p) issue_piece(buf, p);
         // next substep: half, then tap, then channel chunk
         if (++i_half == 2) {
             i_half = 0;
@@ -1365,11 +1376,13 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
     // fp16: register double-buffered fragments; fp32: one set (its MFMA burst
     // per substep is 8x longer, the other wave of the SIMD covers the reads,
     // and two sets would spill at the 256-VGPR budget)
-    constexpr int NSET = (F32 && NW == 8) ? 1 : 2;
+    // (the 256x128 tile: one set, so two workgroups fit a CU's registers;
+    // the other workgroup's waves cover the fragment reads)
+    constexpr int NSET = ((F32 && NW == 8) || NW == 6) ? 1 : 2;
     frag_t fa[NSET][TI], fb[NSET][TJ];
     auto read_frags = [&](int t, int set) {
-        const char *Ab = Abase + (t & 3) * SUB;
-        const char *Bb = Bbase + (t & 3) * SUB;
+        const char *Ab = Abase + (t % NBUF) * SUB;
+        const char *Bb = Bbase + (t % NBUF) * SUB;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) fb[set][j] = *reinterpret_cast<const frag_t *>(Bb + j * 16 * 64);
 #pragma unroll
@@ -1398,20 +1411,21 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
         }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
     };
-    // wait until substep u has landed (4 DMAs per thread per substep)
+    // wait until substep u has landed (PIECES DMAs per thread per substep;
+    // at most NBUF - 2 substeps in flight beyond it)
     auto wait_landed = [&](int u, int issued_upto) {
         const int ahead = issued_upto - u;
-        if (ahead >= 2)
-            MDX_WAIT_VM(8);
-        else if (ahead == 1)
-            MDX_WAIT_VM(4);
+        if (NBUF >= 4 && ahead >= 2)
+            MDX_WAIT_VM(2 * PIECES);
+        else if (ahead >= 1)
+            MDX_WAIT_VM(PIECES);
         else
             MDX_WAIT_VM(0);
     };
     issue(0);
     if (T > 1) issue(1);
-    if (T > 2) issue(2);
-    int issued = T < 3 ? T - 1 : 2;
+    if (NBUF >= 4 && T > 2) issue(2);
+    int issued = T < NBUF ? T - 1 : NBUF - 2;
     if constexpr (NSET == 1) {
         // substep t: [wait t, barrier, DMA t+3, read frags t] then its MFMAs
         // (buffer (t+3)&3 == (t-1)&3: every wave drained its reads of t-1
@@ -1424,9 +1438,9 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 4 ? 2 : 1) void k_convg(C
             MDX_WAIT_LGKM0();
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (t + 3 < T) {
-                issue((t + 3) & 3);
-                issued = t + 3;
+            if (t + NBUF - 1 < T) {
+                issue((t + NBUF - 1) % NBUF);
+                issued = t + NBUF - 1;
             }
             read_frags(t, 0);
             // all fragment reads issue before the first MFMA (the scheduler
@@ -2340,7 +2354,27 @@ general:
             }
             if (g_split256 == 1 && t256 * ks256 < 192) ks256 = 1;  // still too few workgroups: the 128-row kernel
         }
-        if (g_large_tiles == 2 || (g_large_tiles == 1 && big) || ks256 > 1) {
+        // fp16: the 256x128 tile (two workgroups per CU) in place of 256x256
+        // (large-tile modes 3: whenever eligible, 4: the layers mode 1 takes)
+        if (in_dtype == 1 && ks256 == 1 && (g_large_tiles == 3 || (g_large_tiles == 4 && big))) {
+            using G6 = GTile<6>;
+            a.tiles_n = (int)ceil_div(Cout, G6::BN);
+            a.tiles_total = (int)(ceil_div(M, G6::BM) * a.tiles_n);
+            a.ksplit = 1;
+            a.ksteps = a.K / subk;
+            if (out_dtype == 1)
+                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 6, false>), dim3(a.tiles_total), dim3(G6::THREADS),
+                                   G6::LDS, s, a);
+            else
+                hipLaunchKernelGGL((k_convg<_Float16, float, 6, false>), dim3(a.tiles_total), dim3(G6::THREADS),
+                                   G6::LDS, s, a);
+            t_plan_kernel = MDX_CONV_KERNEL_DMA256;
+            t_plan_ksplit = 1;
+            MDX_CHECK_LAUNCH("mdx_conv2d");
+            return MDX_OK;
+        }
+        if (g_large_tiles == 2 || g_large_tiles == 3 || ((g_large_tiles == 1 || g_large_tiles == 4) && big) ||
+            ks256 > 1) {
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
             a.ksplit = ks256;

@@ -73,7 +73,7 @@ def test_conv_head_1x1_fp32_out(mdx, Cin, Cout, M, relu):
     assert err < 1e-3, err
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large", "dma128", "stream", "split256"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "large128", "dma128", "stream", "split256"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -128,11 +128,11 @@ def test_conv2d(mdx, dtype, case, ksplit):
             call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_split256", old, 18)
             call("mdx_conv_set_narrow_kmax", old_nk)
-    elif ksplit in ("large", "dma128"):
-        if (dtype != "fp16" and ksplit == "dma128") or Cin % (64 if dtype == "fp16" else 32):
-            pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 one fp16 only")
+    elif ksplit in ("large", "large128", "dma128"):
+        if (dtype != "fp16" and ksplit in ("dma128", "large128")) or Cin % (64 if dtype == "fp16" else 32):
+            pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 / 256x128 ones fp16 only")
         old_nk = call("mdx_conv_set_narrow_kmax", 0)
-        old = call("mdx_conv_set_large_tiles", 2 if ksplit == "large" else 0)
+        old = call("mdx_conv_set_large_tiles", {"large": 2, "large128": 3}.get(ksplit, 0))
         old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
         old_i = call("mdx_conv_set_mfma_prio", int(case[0] % 2 == 0))  # both DMA schedules across the cases
         old_da = call("mdx_conv_set_dma_after", int(case[1] % 2 == 0))
@@ -146,7 +146,7 @@ def test_conv2d(mdx, dtype, case, ksplit):
             if dtype == "fp32" and Cout > 64:
                 assert kid.value == (3 if f32_mode == 1 else 2)
             elif dtype == "fp16":
-                assert kid.value == (2 if ksplit == "large" else 3)
+                assert kid.value == (2 if ksplit in ("large", "large128") else 3)
         finally:
             call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_large_tiles", old)
