@@ -182,3 +182,32 @@ def test_native_tsv_rows_match_python_repr(RS):
     cells = [RS._tsv_cells(c) for c in cols]
     want = "".join("\t".join(r) + "\n" for r in zip(*cells)).encode()
     assert native == want
+
+
+def test_chunk_writer_abort_leaves_no_results(mdx, tmp_path):
+    """A failed extraction stops the writer thread without finishing the
+    results file and without raising over the extraction's own exception
+    (extract.extract_session -> _ChunkWriter.abort): here the writer thread
+    itself fails on a malformed chunk, and abort() neither raises nor writes
+    results_00.npz; close() on a healthy writer does."""
+    import numpy as np
+    from moseq2_detectron_extract_amd.extract import _ChunkWriter
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig
+
+    class Src:
+        path = str(tmp_path / "depth.dat")
+        last_frame_idx = 4
+
+        def read(self, idx):
+            return np.zeros((len(idx), 424, 512), np.int16)
+
+    args = (Src(), np.full((424, 512), 670.0), np.ones((424, 512), bool), 670.0, ExtractConfig(), None, None)
+    w = _ChunkWriter(str(tmp_path / "bad"), *args)
+    w.write({"frame_idxs": np.arange(2), "offset": 0, "scalars": {"no_such_scalar": np.zeros(2)}, "keypoints": {},
+             "depth_frames": np.zeros((2, 80, 80), np.uint8), "mask_frames": np.zeros((2, 80, 80), np.uint8),
+             "features": {"flips": np.zeros(2, bool), "features": {}}})
+    w.abort()
+    assert not (tmp_path / "bad" / "results_00.npz").exists()
+    ok = _ChunkWriter(str(tmp_path / "good"), *args)
+    ok.close()
+    assert (tmp_path / "good" / "results_00.npz").exists()

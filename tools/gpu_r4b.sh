@@ -17,3 +17,9 @@ tail -8 $O/t$T.log
 bash tools/gpu_fc1_pmc.sh B0 || exit 1
 MDX_PACE=4,1 bash tools/gpu_fc1_pmc.sh B4 || exit 1
 MDX_PACE=2,1 bash tools/gpu_fc1_pmc.sh B2 || exit 1
+# fp16 256x128 tile: conv tests, then the fp16 loop A/B (256x256 vs 256x128)
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -k "test_conv2d and large" > $O/tconv_$T.log 2>&1; echo "conv tests rc=$?"; tail -2 $O/tconv_$T.log
+for lt in 1 4 1 4; do
+  timeout -k 10 300 python3 -u bench.py --dtype fp16 --steps 40 --no-roofline --no-cpu-baseline --no-secondary --set mdx_conv_set_large_tiles=$lt > $O/b16_${T}_lt$lt.json 2>/dev/null || { echo "bench lt$lt failed"; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('$O/b16_${T}_lt$lt.json').read().strip().splitlines()[-1]); print('fp16 large_tiles=$lt', d['value'])"
+done
