@@ -60,11 +60,30 @@ int main(int argc, char **argv) {
         s = s * 1664525u + 1013904223u;
         hx[i] = (_Float16)(((s >> 8) & 0xffff) / 65536.0f * 8.0f - 3.0f);
     }
-    _Float16 *x;
-    float *part, *stats, *bgout;
+    _Float16 *x, *up, *y;
+    float *part, *stats, *bgout, *gamma, *beta;
     float4 *bsrc, *bdst;
     const long long nbg = 64ll << 20;  // 1 GiB each way
     CK(hipMalloc(&x, nx * 2));
+    // the FPN top-down form of the apply kernel: y = (GN(x) + up2(up)) / 2
+    const size_t nup = nx / 4;
+    std::vector<_Float16> hu(nup);
+    for (size_t i = 0; i < nup; ++i) {
+        s = s * 1664525u + 1013904223u;
+        hu[i] = (_Float16)(((s >> 8) & 0xffff) / 65536.0f * 6.0f - 2.0f);
+    }
+    std::vector<float> hg(C), hb(C);
+    for (int c = 0; c < C; ++c) {
+        hg[c] = 0.8f + 0.001f * c;
+        hb[c] = -0.1f + 0.0005f * c;
+    }
+    CK(hipMalloc(&up, nup * 2));
+    CK(hipMalloc(&y, nx * 2));
+    CK(hipMalloc(&gamma, C * 4));
+    CK(hipMalloc(&beta, C * 4));
+    CK(hipMemcpy(up, hu.data(), nup * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(gamma, hg.data(), C * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(beta, hb.data(), C * 4, hipMemcpyHostToDevice));
     CK(hipMalloc(&part, (size_t)N * G * nch * 3 * 4));
     CK(hipMalloc(&stats, (size_t)N * G * 2 * 4));
     CK(hipMalloc(&bgout, 4096));
@@ -77,7 +96,8 @@ int main(int argc, char **argv) {
     CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
     const size_t npart = (size_t)N * G * nch * 3, nstat = (size_t)N * G * 2;
     std::vector<float> p0(npart), s0(nstat), p1(npart), s1(nstat);
-    int bad_part = 0, bad_stat = 0;
+    std::vector<uint16_t> y0(nx), y1(nx);
+    int bad_part = 0, bad_stat = 0, bad_y = 0;
     for (int r = 0; r <= reps; ++r) {
         CK(hipMemsetAsync(part, 0xff, npart * 4, sa));  // stale partials would show as NaN
         if (r > 0 && (bg & 1))
@@ -85,12 +105,30 @@ int main(int argc, char **argv) {
         if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
         hipLaunchKernelGGL(mdx::k_gn_partial<_Float16>, dim3(nch, N), dim3(256), 0, sa, x, HW, C, G, part);
         hipLaunchKernelGGL(mdx::k_gn_final, dim3((N * G + 3) / 4), dim3(256), 0, sa, part, N * G, nch, 1e-5f, stats);
+        hipLaunchKernelGGL(mdx::k_gn_apply<_Float16>, dim3(2048), dim3(256), 0, sa, x, N, H, W, C, G, stats, gamma, beta,
+                           up, 2, y);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         std::vector<float> &pp = r == 0 ? p0 : p1, &ss = r == 0 ? s0 : s1;
         CK(hipMemcpy(pp.data(), part, npart * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(ss.data(), stats, nstat * 4, hipMemcpyDeviceToHost));
+        std::vector<uint16_t> &yy = r == 0 ? y0 : y1;
+        CK(hipMemcpy(yy.data(), y, nx * 2, hipMemcpyDeviceToHost));
         if (r == 0) continue;
+        if (memcmp(y0.data(), y1.data(), nx * 2)) {
+            ++bad_y;
+            if (bad_y <= 3) {
+                size_t nd = 0, first = (size_t)-1;
+                for (size_t i = 0; i < nx; ++i)
+                    if (y0[i] != y1[i]) {
+                        if (first == (size_t)-1) first = i;
+                        ++nd;
+                    }
+                const size_t c = first % C, pix = first / C;
+                printf("rep %d: %zu outputs differ; first: image %zu pixel %zu channel %zu\n", r, nd, pix / HW,
+                       pix % HW, c);
+            }
+        }
         if (memcmp(p0.data(), p1.data(), npart * 4)) {
             ++bad_part;
             if (bad_part <= 3) {
@@ -108,7 +146,7 @@ int main(int argc, char **argv) {
         }
         if (memcmp(s0.data(), s1.data(), nstat * 4)) ++bad_stat;
     }
-    printf("{\"reps\": %d, \"background\": %d, \"partials_differ\": %d, \"stats_differ\": %d}\n", reps, bg, bad_part,
-           bad_stat);
+    printf("{\"reps\": %d, \"background\": %d, \"partials_differ\": %d, \"stats_differ\": %d, \"apply_differ\": %d}\n",
+           reps, bg, bad_part, bad_stat, bad_y);
     return 0;
 }

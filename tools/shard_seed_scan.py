@@ -31,16 +31,19 @@ def main():
                           ExtractConfig(chunk_size=chunk, batch_size=16, use_tracking=True, select_instances=True))
         raw = torch.from_numpy(s.frames(0, nfr)).cuda()
         tr = InstanceTracker(1)
-        cen_ok, cross, nk_all, changes = 0, 0, [], 0
+        cen_ok, cross, nk_all, changes, trk_ok = 0, 0, [], 0, 0
         for a in range(0, nfr, chunk):
             st, host = ex.features_pass(raw[a:a + chunk])
             cen_ok += int(np.isfinite(host["centroid"][:, 0]).sum())
             nk = st["nkeep"]
             nk_all.extend(nk.tolist())
             ch = select_chunk(tr, nk, host["centers"], a)
+            cen_t = ex.host_angles(host)[0]  # the Kalman tracking branch (pre-selection features)
+            trk_ok += int(np.isfinite(cen_t[:, 0]).sum())
             changes += len(ch)
             cross += sum(1 for f, sel in ch.items() if a + f >= bnd and any(g < bnd for g, _ in sel))
         print(json.dumps({"seed": seed, "wseed": wseed, "centroid_frac": round(cen_ok / nfr, 3),
+                          "tracked_centroid_frac": round(trk_ok / nfr, 3),
                           "nkeep_hist": np.bincount(nk_all, minlength=5).tolist(), "changed_frames": changes,
                           "cross_boundary_picks": cross}), flush=True)
 
