@@ -2237,12 +2237,9 @@ extern "C" int mdx_conv_set_single_stage(int on) {
 }
 // LDS of a k_conv launch: stage buffers (one when the whole K is one step or
 // the single-stage instance, else two) or the half-tile fp32 epilogue image
-// the persistent single-stage pointwise GEMM (k_conv_sbp) for fp32 launches
-// of k_conv_sb (A/B while measured: MDX_PERSIST=1); ctr: 8 ints of scratch
-static int g_persist = [] {
-    const char *e = getenv("MDX_PERSIST");
-    return e ? atoi(e) : 0;
-}();
+// the persistent single-stage pointwise GEMM (k_conv_sbp) for the fp32
+// residual-free stride-1 launches of k_conv_sb: single-stage mode 5
+// (mdx_conv_set_single_stage); ctr: 8 ints of scratch
 template <int BN_>
 static void launch_sbp(ConvArgs a, int batches, int *ctr, size_t lds, hipStream_t s) {
     a.pace = ctr;
@@ -2621,9 +2618,9 @@ general:
     // (mode 4: as 3, plus the fp16 KxK layers the LDS-DMA kernels do not take)
     const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 3 && in_dtype == 1 && out_dtype == 1));
     const bool sbg = g_conv_sb >= 2 && !pw &&
-                     ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb == 4 && in_dtype == 1 && out_dtype == 1));
-    if (g_persist && pw && sb && in_dtype == 0 && out_dtype == 0 && a.ksplit == 1 && workspace &&
-        workspace_bytes >= 64) {
+                     ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 4 && in_dtype == 1 && out_dtype == 1));
+    if (g_conv_sb == 5 && pw && sb && in_dtype == 0 && out_dtype == 0 && a.ksplit == 1 && stride == 1 && !residual &&
+        workspace && workspace_bytes >= 64) {
         if (narrow)
             launch_sbp<64>(a, 1, reinterpret_cast<int *>(workspace), conv_lds(64, a.ksteps, true), s);
         else
@@ -3020,7 +3017,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64) {
-        if (g_pw && g_conv_sb && g_persist) {
+        if (g_pw && g_conv_sb == 5) {
             launch_sbp<64>(a, NB, wino_ctr, conv_lds(64, a.ksteps, true), s);
             gemm_kernel = MDX_CONV_KERNEL_SB64;
         } else if (g_pw && g_conv_sb) {
@@ -3035,7 +3032,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             gemm_kernel = MDX_CONV_KERNEL_REG64;
         }
     } else {
-        if (g_pw && g_conv_sb && g_persist) {
+        if (g_pw && g_conv_sb == 5) {
             launch_sbp<128>(a, NB, wino_ctr, conv_lds(128, a.ksteps, true), s);
             gemm_kernel = MDX_CONV_KERNEL_SB128;
         } else if (g_pw && g_conv_sb) {
