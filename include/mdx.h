@@ -369,10 +369,7 @@ int mdx_conv_set_pointwise(int on);
  * instance k_conv_sb (three workgroups per CU, two barriers per K-step, the
  * same sums bit for bit as the two-stage instance): 1 fp32, 2 also the
  * fp32 KxK layers (k_conv_sbg), 3 also the fp16 register-staged pointwise
- * layers, 4 also the fp16 register-staged KxK layers (default), 5 as 4 with
- * the fp32 residual-free stride-1 pointwise layers and Winograd GEMMs on the
- * persistent k_conv_sbp (per-XCD work-item counters, each tile's first K-step
- * loaded during the previous tile's last; same sums bit for bit), 0 the
+ * layers, 4 also the fp16 register-staged KxK layers (default), 0 the
  * two-stage instances.  Returns the old value. */
 int mdx_conv_set_single_stage(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);

@@ -96,10 +96,6 @@ struct ConvArgs {
     // projection shortcut concatenated onto its conv3 GEMM)
     const void *x2;
     int K1, H2, W2, Cin2, stride2, x2bytes;
-    // k_conv_sbp (persistent): 8 per-XCD work-item counters (zeroed before
-    // the launch) and the batch entries of the launch (0 = 1)
-    int *pace;
-    int batches;
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -154,10 +150,10 @@ __device__ __forceinline__ void finish8(const ConvArgs &a, int gm, int gn0, floa
 // store (out and res may alias as far as the compiler knows, so a per-item
 // load -> store sequence would serialise every load behind the previous
 // store).  item(q, gm, gn0, src): row (-1 = skip), first channel, fp32 values.
-template <typename TO, int NQ, typename F, bool RES = true>
+template <typename TO, int NQ, typename F>
 __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
     TO *O = reinterpret_cast<TO *>(a.out);
-    const TO *RS = RES ? reinterpret_cast<const TO *>(a.res) : nullptr;
+    const TO *RS = reinterpret_cast<const TO *>(a.res);
     const int Co = a.out_mode == 1 ? a.Cout / 4 : a.Cout;
     const bool vec_ok = (a.Cout % 8) == 0 && (Co % 8) == 0 && a.out_mode == 0;
     constexpr int RW = sizeof(TO) == 2 ? 1 : 2;  // 16-B words of 8 residual values
@@ -514,198 +510,6 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sb(Con
 template <typename T, typename TO, int BN_>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sbg(ConvArgs a) {
     conv_body<T, TO, BN_, false, false, true>(a);
-}
-
-// ---------------------------------------------------------------------------
-// k_conv_sbp: k_conv_sb (fp32 pointwise, one LDS stage, three workgroups per
-// CU) as a persistent kernel.  Work items = (batch entry z, output tile) of
-// the launch, dealt per XCD: XCD x owns the contiguous item range
-// [x Q, (x + 1) Q) and its workgroups take the next item from that XCD's
-// counter (then from the other XCDs' ranges), so the tiles in flight on an
-// XCD share their A row panels in its L2.  While a tile's last K-step is
-// multiplied, the first K-step of the workgroup's NEXT tile is already
-// loaded into the register stage: the global-load latency of each tile's
-// first step, which the one-shot grid pays once per tile, is hidden behind
-// the previous tile (the short-K Winograd GEMMs have 2-16 K-steps per tile).
-// The sums are those of k_conv_sb bit for bit (same MFMA order per
-// accumulator).  a.pace: 8 int counters (zeroed before the launch).
-// ---------------------------------------------------------------------------
-template <int BN_>
-__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sbp(ConvArgs a) {
-    using T = float;
-    constexpr int BK = 32, VEC = 4;
-    constexpr int TI = BM / 32, TJ = BN_ / 32;
-    constexpr int A_TILE = BM * PITCH;
-    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ int s_item[2];
-    char *As = smem;
-    char *Bs = smem + A_TILE;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    const int kc = tid & 7, lrow = tid >> 3;
-    const int items = a.tiles_total * (a.batches > 0 ? a.batches : 1);
-    const int xcd = blockIdx.x % 8;
-    const int Q = (items + 7) / 8;
-    constexpr unsigned OOB = 0xFFFFFFF0u;
-    const int nk = (a.K + BK - 1) / BK;
-    // next item of this workgroup: its XCD's range first, then the others'
-    auto grab = [&]() -> int {
-        for (int d = 0; d < 8; ++d) {
-            const int x = (xcd + d) & 7;
-            const int lo = x * Q, hi = lo + Q < items ? lo + Q : items;
-            if (lo >= hi) continue;
-            const int i = __hip_atomic_fetch_add(a.pace + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (lo + i < hi) return lo + i;
-        }
-        return -1;
-    };
-    // item -> (batch entry, first row, first channel) (stride-1 pointwise
-    // layers only: row m's A bytes start at m * Cin * 4)
-    auto coords = [&](int it, int &m0, int &n0, int &z) {
-        z = it / a.tiles_total;
-        const int t = it - z * a.tiles_total;
-        const int tm = t / a.tiles_n;
-        m0 = tm * BM;
-        n0 = (t - tm * a.tiles_n) * BN_;
-    };
-    uint4 ra[4], rb[BLOADS];
-    const unsigned rowb = (unsigned)a.Cin * (unsigned)sizeof(T);
-    auto load = [&](int m0, int n0, int z, int kt) {
-        const int kglob = kt * BK + kc * VEC;
-        const bool kok = kglob < a.K;
-        const unsigned kb = (unsigned)(kglob * (int)sizeof(T));
-        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(reinterpret_cast<const char *>(a.x) + (long long)z * a.bsx), (short)0, a.xbytes, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(reinterpret_cast<const char *>(a.w) + (long long)z * a.bsw), (short)0, a.wbytes, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int gm = m0 + lrow + 32 * i;
-            ra[i] = __builtin_bit_cast(
-                uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && gm < a.M) ? (unsigned)gm * rowb + kb : OOB, 0, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i) {
-            const int gn = n0 + lrow + 32 * i;
-            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * (long long)sizeof(T));
-            rb[i] = __builtin_bit_cast(uint4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
-        }
-    };
-    const int wpiece = (kc ^ ((lrow >> 1) & 7)) * 16;
-    auto store_lds = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(As + (lrow + 32 * i) * PITCH + wpiece) = ra[i];
-#pragma unroll
-        for (int i = 0; i < BLOADS; ++i) *reinterpret_cast<uint4 *>(Bs + (lrow + 32 * i) * PITCH + wpiece) = rb[i];
-    };
-
-    void *const out0 = a.out;
-    if (tid == 0) s_item[0] = grab();
-    __syncthreads();
-    // (workgroup-uniform: readfirstlane, so the tile coordinates and the
-    // buffer descriptors built from them stay scalar)
-    int cur = __builtin_amdgcn_readfirstlane(s_item[0]);
-    if (cur < 0) return;
-    int m0, n0, z;
-    coords(cur, m0, n0, z);
-    load(m0, n0, z, 0);
-    int slot = 0;
-    while (true) {
-        // the next item, grabbed now so that its first K-step can be loaded
-        // during this one's last (s_item double-buffered)
-        if (tid == 0) s_item[slot ^ 1] = grab();
-        float4v acc[TI][TJ];
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-        __syncthreads();  // the previous epilogue is done with the LDS; s_item[slot ^ 1] visible
-        const int nxt = __builtin_amdgcn_readfirstlane(s_item[slot ^ 1]);
-        store_lds();  // step 0 of this item
-        if (nk > 1) {
-            load(m0, n0, z, 1);
-        } else if (nxt >= 0) {
-            int nm0, nn0, nz;
-            coords(nxt, nm0, nn0, nz);
-            load(nm0, nn0, nz, 0);
-        }
-        __syncthreads();
-        for (int kt = 0; kt < nk; ++kt) {
-            const char *Ab = As + (wm * (BM / 2) + (lane & 15)) * PITCH;
-            const char *Bb = Bs + (wn * (BN_ / 2) + (lane & 15)) * PITCH;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int koff = ((4 * s + (lane >> 4)) ^ ((lane & 15) >> 1)) * 16;
-                float4v af[TI], bf[TJ];
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
-#pragma unroll
-                for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * PITCH + koff);
-                constexpr int IG = TJ >= 4 ? 1 : 4 / TJ;
-#pragma unroll
-                for (int i0 = 0; i0 < TI; i0 += IG)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-#pragma unroll
-                        for (int i = i0; i < i0 + IG; ++i)
-#pragma unroll
-                            for (int j = 0; j < TJ; ++j)
-                                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-            }
-            __syncthreads();  // every wave is done reading the stage
-            if (kt + 1 < nk) {
-                store_lds();
-                if (kt + 2 < nk) {
-                    load(m0, n0, z, kt + 2);
-                } else if (nxt >= 0) {  // the next item's first K-step
-                    int nm0, nn0, nz;
-                    coords(nxt, nm0, nn0, nz);
-                    load(nm0, nn0, nz, 0);
-                }
-                __syncthreads();
-            }
-        }
-        // epilogue (as conv_body): two halves of BM / 2 rows through LDS
-        constexpr int CP = BN_ + 4;
-        constexpr int HM = BM / 2;
-        float *Cs = reinterpret_cast<float *>(smem);
-        constexpr int CPR = BN_ / 8;
-        constexpr int NQ = HM * CPR / CONV_THREADS;
-        a.out = reinterpret_cast<char *>(out0) + (long long)z * a.bso;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (wm == h) {
-#pragma unroll
-                for (int i = 0; i < TI; ++i)
-#pragma unroll
-                    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int row = i * 16 + (lane >> 4) * 4 + r;
-                            const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
-                            Cs[row * CP + col] = acc[i][j][r];
-                        }
-            }
-            __syncthreads();
-            const int mh = m0 + h * HM;
-            auto item = [&](int q, int &gm, int &gn0, const float *&src) {
-                const int c = tid + q * CONV_THREADS;
-                const int row = c / CPR, ch = c - row * CPR;
-                gm = mh + row;
-                gn0 = n0 + ch * 8;
-                src = Cs + row * CP + ch * 8;
-                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
-            };
-            finish_batch<float, NQ, decltype(item), false>(a, item);
-            if (h == 0) __syncthreads();
-        }
-        if (nxt < 0) break;
-        cur = nxt;
-        coords(cur, m0, n0, z);
-        slot ^= 1;
-    }
 }
 
 // split-K reduction: sum the slices (fixed order) and apply the epilogue
@@ -2237,20 +2041,6 @@ extern "C" int mdx_conv_set_single_stage(int on) {
 }
 // LDS of a k_conv launch: stage buffers (one when the whole K is one step or
 // the single-stage instance, else two) or the half-tile fp32 epilogue image
-// the persistent single-stage pointwise GEMM (k_conv_sbp) for the fp32
-// residual-free stride-1 launches of k_conv_sb: single-stage mode 5
-// (mdx_conv_set_single_stage); ctr: 8 ints of scratch
-template <int BN_>
-static void launch_sbp(ConvArgs a, int batches, int *ctr, size_t lds, hipStream_t s) {
-    a.pace = ctr;
-    a.batches = batches;
-    const long long items = (long long)a.tiles_total * batches;
-    const long long slots = 256ll * (BN_ == 64 ? 4 : 3);
-    const unsigned grid = (unsigned)(items < slots ? items : slots);
-    (void)hipMemsetAsync(ctr, 0, 8 * sizeof(int), s);
-    hipLaunchKernelGGL((k_conv_sbp<BN_>), dim3(grid), dim3(CONV_THREADS), lds, s, a);
-}
-
 static size_t conv_lds(int bn, int ksteps, bool sb) {
     const size_t main_ = (ksteps == 1 || sb ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
     const size_t epi = (size_t)(BM / 2) * (bn + 4) * 4;
@@ -2619,17 +2409,6 @@ general:
     const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 3 && in_dtype == 1 && out_dtype == 1));
     const bool sbg = g_conv_sb >= 2 && !pw &&
                      ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 4 && in_dtype == 1 && out_dtype == 1));
-    if (g_conv_sb == 5 && pw && sb && in_dtype == 0 && out_dtype == 0 && a.ksplit == 1 && stride == 1 && !residual &&
-        workspace && workspace_bytes >= 64) {
-        if (narrow)
-            launch_sbp<64>(a, 1, reinterpret_cast<int *>(workspace), conv_lds(64, a.ksteps, true), s);
-        else
-            launch_sbp<128>(a, 1, reinterpret_cast<int *>(workspace), conv_lds(128, a.ksteps, true), s);
-        t_plan_kernel = narrow ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_SB128;
-        t_plan_ksplit = 1;
-        MDX_CHECK_LAUNCH("mdx_conv2d");
-        return MDX_OK;
-    }
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
@@ -2888,8 +2667,12 @@ static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
 // split-plane Winograd GEMMs on k_gemm_x6 when the batch gives it at least
-// this many 256 x 256 workgroups (below: k_conv_x3)
-static int g_wino_x6_min_wgs = 384;
+// this many 256 x 256 workgroups (below: k_conv_x3); MDX_WINO_X6_MIN_WGS
+// overrides it for A/B runs (a huge value: every layer on k_conv_x3)
+static const int g_wino_x6_min_wgs = [] {
+    const char *e = getenv("MDX_WINO_X6_MIN_WGS");
+    return e ? atoi(e) : 384;
+}();
 
 static int winograd_impl(const float *x, int N, int H, int W, int Cin, const float *U, const void *Up,
                          const float *bias, int Cout, int relu, int m, float *out, void *workspace,
@@ -2933,9 +2716,6 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     float *V = reinterpret_cast<float *>(workspace);
     float *Mx = planes ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + NB * T * Cin * 6)
                        : V + NB * T * Cin;
-    // scratch counters of the persistent GEMM: the workspace's last 64 B
-    // (past V and M: mdx_winograd_workspace_bytes keeps 256 B spare)
-    int *wino_ctr = reinterpret_cast<int *>(reinterpret_cast<char *>(workspace) + ((workspace_bytes - 64) & ~63ll));
     WinoProbe *probe = t_wino_probe;
     auto mark = [&](int i) {
         if (probe) (void)hipEventRecord(probe->ev[i], s);
@@ -3017,10 +2797,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64) {
-        if (g_pw && g_conv_sb == 5) {
-            launch_sbp<64>(a, NB, wino_ctr, conv_lds(64, a.ksteps, true), s);
-            gemm_kernel = MDX_CONV_KERNEL_SB64;
-        } else if (g_pw && g_conv_sb) {
+        if (g_pw && g_conv_sb) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 64>), grid, dim3(CONV_THREADS),
                                conv_lds(64, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB64;
@@ -3032,10 +2809,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             gemm_kernel = MDX_CONV_KERNEL_REG64;
         }
     } else {
-        if (g_pw && g_conv_sb == 5) {
-            launch_sbp<128>(a, NB, wino_ctr, conv_lds(128, a.ksteps, true), s);
-            gemm_kernel = MDX_CONV_KERNEL_SB128;
-        } else if (g_pw && g_conv_sb) {
+        if (g_pw && g_conv_sb) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 128>), grid, dim3(CONV_THREADS),
                                conv_lds(128, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB128;

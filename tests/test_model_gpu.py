@@ -869,16 +869,6 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     got = out.cpu().double()
     err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
     assert err < 1e-4, err
-    if split == 0:
-        # the batched GEMMs on the persistent k_conv_sbp: the same sums bit for bit
-        old_ss = call("mdx_conv_set_single_stage", 5)
-        try:
-            out5 = torch.full_like(out, float("nan"))
-            call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out5), P(ws), nb,
-                 None)
-        finally:
-            call("mdx_conv_set_single_stage", old_ss)
-        assert torch.equal(out5, out)
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,m", [(8, 112, 128, 256, 256, 6), (16, 56, 64, 128, 128, 4),
@@ -1090,9 +1080,7 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
     try:
         for ks in ((1, 3) if Cout % 8 == 0 else (1,)):
             outs = []
-            # 5: the persistent k_conv_sbp where it applies (stride 1, no
-            # residual, no split-K), else the same kernels as 1
-            for single in (0, 1, 5):
+            for single in (0, 1):
                 call("mdx_conv_set_single_stage", single)
                 out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
                 call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0, 0,
@@ -1103,7 +1091,7 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
                 err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
                 assert err < 1e-4, (ks, single, err)
                 outs.append(out)
-            assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), ks
+            assert torch.equal(outs[0], outs[1]), ks
     finally:
         for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
                          "mdx_conv_set_stream1x1_f32"), olds):

@@ -67,7 +67,11 @@ MIN_POSES = 8           # non-NaN poses (both sides) per case
 MIN_SEL_EXACT = 0.9     # fp32: fraction of frames whose selected mask is the oracle's, pixel for pixel
 ANGLE_ULPS = 2          # fp32: angle agreement (deg) in units in the last place when the masks agree
 FP16_FRAMES = 0.8       # fp16: fraction of frames passing the detection checks / the pose bounds
-FP16_CROP_EXACT = 0.1   # fp16: fraction of non-NaN-pose frames whose crop equals the oracle chain's
+FP16_CROP_EXACT = 0.12  # fp16: fraction of non-NaN-pose frames whose crop equals the oracle chain's
+                        # (round-4 records: R50 B=32 4 / 21, R101 B=64 8 / 63)
+MIXED_CROP_EXACT = 0.9  # config 5 as stated (fp32 trunk / box head, fp16 mask + keypoint heads): the same
+                        # fraction (round-4 record: R101 B=64 62 / 64), and every frame passes the
+                        # detection and pose checks
 SEED = 77               # synthetic session of the batch
 # seeded synthetic weights per depth: R101 with seed 0 selects detections off
 # the animal on 61 of 64 frames (NaN poses on both sides, nothing compared
@@ -322,6 +326,9 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
     assert n_pose >= MIN_POSES, stats["summary"]
     if dtype == "fp32":
         assert n_sel >= MIN_SEL_EXACT * B, stats["summary"]
+    elif dtype == "mixed":
+        assert det_ok == B and pose_ok == B, stats["summary"]
+        assert sum(exact_vs) >= MIXED_CROP_EXACT * len(exact_vs), stats["summary"]
     else:
         assert det_ok >= FP16_FRAMES * B and pose_ok >= FP16_FRAMES * B, stats["summary"]
         assert sum(exact_vs) >= FP16_CROP_EXACT * len(exact_vs), stats["summary"]

@@ -22,7 +22,11 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-NFR, CHUNK, BATCH, WORLD = 192, 48, 16, 2   # 4 chunks: rank 0 owns frames 0-95, rank 1 96-191
+# 4 chunks of 96: rank 0 owns frames 0-191, rank 1 192-383.  Session seed 77
+# with weight seed 0 (tools/shard_seed_scan.py, profiles/r04_experiments.json):
+# the tracked centroid is finite on every frame and one of rank 1's frames
+# picks a detection of rank 0's shard through the tail hand-off
+NFR, CHUNK, BATCH, WORLD, SEED = 384, 96, 32, 2, 77
 
 
 def _cfg():
@@ -94,7 +98,7 @@ def sharded_vs_single(mdx, tmp_path_factory):
     import torch.multiprocessing as mp
     from moseq2_detectron_extract_amd import synth
     from moseq2_detectron_extract_amd.extract import extract_session
-    seed = 31
+    seed = SEED
     d = tmp_path_factory.mktemp("config4")
     s = synth.SyntheticSession(NFR, seed=seed)
     s.write(str(d / "sess"))
@@ -138,9 +142,11 @@ def test_sharded_session_equals_one_process(sharded_vs_single):
     for k in single:
         cat = np.concatenate([r[k] for r in ranks])
         np.testing.assert_array_equal(cat, single[k], err_msg=k)
-    # the session is not degenerate: the animal is found and the angles move
-    assert np.isfinite(single["scalars/centroid_x_px"]).mean() > 0.5
+    # the session is not degenerate: the animal is tracked, the angles move,
+    # the crops carry depth
+    assert np.isfinite(single["scalars/centroid_x_px"]).mean() > 0.9
     assert np.nanstd(single["scalars/angle"]) > 1.0
+    assert (single["frames"].reshape(NFR, -1).max(1) > 0).mean() > 0.9
 
 
 def test_sharded_writers_equal_one_process(sharded_vs_single):

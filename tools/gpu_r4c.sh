@@ -4,9 +4,12 @@ export TMPDIR=/tmp
 T=${1:-x}
 O=gpurun_out; mkdir -p $O
 for v in nopk pk; do
-  for bg in 0 3; do
-    timeout -k 10 120 ./tools/native/gn_repro_$v 300 $bg > $O/gn_${T}_${v}_bg$bg.log 2>&1 || { echo "gn_repro_$v bg$bg failed: $?"; exit 1; }
-    echo "$v bg$bg: $(tail -1 $O/gn_${T}_${v}_bg$bg.log)"
+  for hw in "112 128" "14 16" "28 32"; do
+    for bg in 0 3; do
+      tag=${v}_bg${bg}_${hw// /x}
+      timeout -k 10 120 ./tools/native/gn_repro_$v 300 $bg $hw > $O/gn_${T}_$tag.log 2>&1 || { echo "gn_repro $tag failed: $?"; exit 1; }
+      echo "$tag: $(tail -1 $O/gn_${T}_$tag.log)"
+    done
   done
 done
 timeout -k 10 400 python3 -u tools/shard_seed_scan.py 384 96 192 9 77 31 9:1 77:1 5 > $O/scan_$T.log 2>&1 || { echo scan failed; tail -5 $O/scan_$T.log; exit 1; }

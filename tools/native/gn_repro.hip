@@ -12,7 +12,8 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I. -munsafe-fp-atomics \
 //     tools/native/gn_repro.hip -o gn_repro_pk
 //   ... -Xclang -target-feature -Xclang -packed-fp32-ops ... -o gn_repro_nopk
-// Run: gn_repro_<v> REPS BG (BG: 0 none, 1 VALU loop, 2 HBM copy, 3 both)
+// Run: gn_repro_<v> REPS BG [H W] (BG: 0 none, 1 VALU loop, 2 HBM copy, 3 both;
+// the FPN level maps of a 448x512 input: 112x128, 56x64, 28x32, 14x16)
 #include "moseq2-detectron-extract_amd/csrc/model_ops.hip"
 namespace mdx {
 void set_error(const char *, ...) {}
@@ -51,7 +52,8 @@ __global__ __launch_bounds__(256) void k_bg_copy(const float4 *src, float4 *dst,
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 200;
     const int bg = argc > 2 ? atoi(argv[2]) : 3;
-    const int N = 4, H = 112, W = 128, C = 256, G = 32, HW = H * W;
+    const int H = argc > 3 ? atoi(argv[3]) : 112, W = argc > 4 ? atoi(argv[4]) : 128;
+    const int N = 4, C = 256, G = 32, HW = H * W;
     const int nch = (HW + mdx::GN_CHUNK_PIX - 1) / mdx::GN_CHUNK_PIX;
     const size_t nx = (size_t)N * HW * C;
     std::vector<_Float16> hx(nx);
