@@ -88,6 +88,7 @@ for r in range(reps):
         inter = {k: m.tensor(k) for k in order}
     torch.cuda.synchronize()
     first = None
+    diffs = []
     for k in order:
         a, b = ref["intermediates"][k], inter[k]
         if k in ("proposals", "proposal_scores", "box_pred"):
@@ -100,8 +101,15 @@ for r in range(reps):
             b = b.reshape(a.shape)
         if not torch.equal(torch.nan_to_num(a.float(), nan=7e7), torch.nan_to_num(b.float(), nan=7e7)):
             d = (a.float() - b.float()).abs()
+            diffs.append(k)
+            if first is not None:
+                continue
             first = (k, int((d != 0).sum()), float(d.max()))
-            if os.environ.get("DBG_DETAIL") and d.dim() == 4:
+            if k.endswith("gnws5"):
+                # level-5 GN workspace: [stats 2*N*G][partials 3*N*G*nch]
+                idx = (d.flatten() != 0).nonzero().flatten()
+                print("   gnws5 differing floats:", idx.numel(), "first indices", idx[:12].tolist(), flush=True)
+            if os.environ.get("DBG_DETAIL") and d.dim() == 4 and d.shape[1] > 1 and d.shape[3] % 32 == 0:
                 Bn, Hh, Ww, Cc = d.shape
                 grp = (d != 0).reshape(Bn, Hh * Ww, 32, Cc // 32)  # GN groups of C/32 channels
                 per = grp.float().mean(dim=(1, 3))                # fraction differing per (image, group)
@@ -109,8 +117,8 @@ for r in range(reps):
                 pix = (d != 0).any(dim=3).reshape(Bn, -1).sum(1).tolist()
                 print("   detail", k, "img/grp with diffs:", len(bad), bad[:12], "frac", [round(float(per[i, j]), 3) for i, j in bad[:12]],
                       "pixels differing per image", pix, "ref max", float(a.float().abs().max()), flush=True)
-            break
-    print(dt, mode, "rep", r, first or "identical", "boxes_equal", bool(torch.equal(oa["boxes"], ref["boxes"])), flush=True)
+    print(dt, mode, "rep", r, first or "identical", "all differing:", diffs[:12],
+          "boxes_equal", bool(torch.equal(oa["boxes"], ref["boxes"])), flush=True)
     hist[first[0] if first else None] = hist.get(first[0] if first else None, 0) + 1
 print("summary", dt, mode, hist, flush=True)
 if os.environ.get("MDX_DEBUG_SHADOW"):

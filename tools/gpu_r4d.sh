@@ -5,8 +5,8 @@ T=${1:-x}
 O=gpurun_out; mkdir -p $O
 # where the packed-FP32 GroupNorm difference starts: shadow copies of the
 # level-5 GN workspace (stats | partials) and of the GN outputs
-MDX_LIB_VARIANT=pk MDX_DEBUG_SHADOW=1 DBG_DETAIL=1 timeout -k 10 300 python3 -u tools/dbg_race.py fp16 24 same > $O/race_shadow_$T.log 2>&1 || { echo race failed; tail -5 $O/race_shadow_$T.log; exit 1; }
-tail -6 $O/race_shadow_$T.log
+MDX_LIB_VARIANT=pk MDX_DEBUG_SHADOW=1 timeout -k 10 300 python3 -u tools/dbg_race.py fp16 30 same > $O/race_shadow_$T.log 2>&1 || { echo race failed; tail -5 $O/race_shadow_$T.log; exit 1; }
+grep -c identical $O/race_shadow_$T.log; grep -v identical $O/race_shadow_$T.log | tail -12
 # fc1 on the 256x256 LDS-DMA kernel (2.7 GB) vs k_conv_sb (14 GB) in the pipelined loop
 for d in 0 2 0 2; do
   timeout -k 10 300 python3 -u bench.py --steps 60 --no-roofline --no-cpu-baseline --no-secondary --set mdx_conv_set_dma_f32=$d > $O/bd_${T}_$d.json 2>/dev/null || { echo "bench dma $d failed"; exit 1; }
