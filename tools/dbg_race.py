@@ -109,6 +109,14 @@ for r in range(reps):
                 # level-5 GN workspace: [stats 2*N*G][partials 3*N*G*nch]
                 idx = (d.flatten() != 0).nonzero().flatten()
                 print("   gnws5 differing floats:", idx.numel(), "first indices", idx[:12].tolist(), flush=True)
+                dump = os.environ.get("DBG_DUMP")
+                if dump and not os.path.exists(dump):
+                    # the GN's input and both workspaces, for the CPU restatement
+                    # of the partial / final kernels (tools/gn_emulate.py)
+                    import numpy as np
+                    np.savez(dump, lat_ref=ref["intermediates"]["fpn_lateral5"].cpu().numpy(),
+                             lat_rep=inter["fpn_lateral5"].cpu().numpy(),
+                             ws_ref=a.cpu().numpy(), ws_rep=b.cpu().numpy(), rep=r)
             if os.environ.get("DBG_DETAIL") and d.dim() == 4 and d.shape[1] > 1 and d.shape[3] % 32 == 0:
                 Bn, Hh, Ww, Cc = d.shape
                 grp = (d != 0).reshape(Bn, Hh * Ww, 32, Cc // 32)  # GN groups of C/32 channels
