@@ -273,8 +273,9 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
 /* Split-plane mode (mdx_conv_set_fp32_split(6)): the same layer with U also
  * split once into bf16 planes (mdx_split_x6 of U as NB*Cout rows of Cin):
  * the input transform writes V as planes and the NB GEMMs run on the 256x256
- * LDS-DMA plane kernel (k_gemm_x6) when they give it >= 384 workgroups;
- * otherwise as mdx_conv3x3_winograd.  Cin % 16 == 0 for the plane path. */
+ * LDS-DMA plane kernel (k_gemm_x6); outside split mode, or with Cin % 16 != 0,
+ * as mdx_conv3x3_winograd.  Model handles use it only with MDX_WINO_X6 set in
+ * the environment (4 % slower end to end than k_conv_x3 on every layer). */
 int mdx_conv3x3_winograd_x6(const float *x, int N, int H, int W, int Cin, const float *U, const void *U_planes,
                             const float *bias, int Cout, int relu, int m, float *out, void *workspace,
                             int64_t workspace_bytes, mdx_stream_t stream);

@@ -52,5 +52,6 @@ struct WinoProbe {
     int gemm_kernel;
 };
 void wino_probe(WinoProbe *p);
+bool winograd_planes_enabled();  // the model packs Winograd weight planes (MDX_WINO_X6 set)
 
 }  // namespace mdx

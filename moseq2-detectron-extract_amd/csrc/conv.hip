@@ -2666,13 +2666,13 @@ extern "C" int mdx_winograd_tile(int H, int W, int mode) {
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
-// split-plane Winograd GEMMs on k_gemm_x6 when the batch gives it at least
-// this many 256 x 256 workgroups (below: k_conv_x3); MDX_WINO_X6_MIN_WGS
-// overrides it for A/B runs (a huge value: every layer on k_conv_x3)
-static const int g_wino_x6_min_wgs = [] {
-    const char *e = getenv("MDX_WINO_X6_MIN_WGS");
-    return e ? atoi(e) : 384;
-}();
+// the model packs Winograd weight planes (and so runs the split-plane
+// Winograd GEMMs on k_gemm_x6) only when MDX_WINO_X6 is set: the split-plane
+// loop measured 4 % slower with them (1481 / 1494 vs 1543 / 1574 frames/s,
+// profiles/r04_experiments.json), the plane input transform writing 6 B per
+// value against 4
+static const bool g_wino_x6_model = getenv("MDX_WINO_X6") != nullptr;
+bool mdx::winograd_planes_enabled() { return g_wino_x6_model; }
 
 static int winograd_impl(const float *x, int N, int H, int W, int Cin, const float *U, const void *Up,
                          const float *bias, int Cout, int relu, int m, float *out, void *workspace,
@@ -2709,9 +2709,8 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
                 "mdx_conv3x3_winograd: layer too large");
     hipStream_t s = as_stream(stream);
     // split-plane mode with the U planes: V written as planes, the NB GEMMs on
-    // the 256 x 256 LDS-DMA plane kernel (if the batch fills the chip)
-    const long long x6_wgs = ceil_div(T, X6_BM) * ceil_div(Cout, X6_BN) * NB;
-    const bool planes = Up && g_fp32_split == 6 && Cin % 16 == 0 && x6_wgs >= g_wino_x6_min_wgs &&
+    // the 256 x 256 LDS-DMA plane kernel
+    const bool planes = Up && g_fp32_split == 6 && Cin % 16 == 0 &&
                         T * Cin * 6 < (1ll << 31) && (long long)Cout * Cin * 6 < (1ll << 31);
     float *V = reinterpret_cast<float *>(workspace);
     float *Mx = planes ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + NB * T * Cin * 6)

@@ -298,7 +298,7 @@ struct Packer {
                 float *ud = upload_f32(u);
                 (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = ud;
                 // split-plane handles: U as bf16 planes too (k_gemm_x6's B operand)
-                if (mdx_conv_fp32_split() == 6 && ci % 16 == 0 && ud && err.empty()) {
+                if (mdx_conv_fp32_split() == 6 && mdx::winograd_planes_enabled() && ci % 16 == 0 && ud && err.empty()) {
                     void *d = nullptr;
                     if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes((int64_t)nb * co, ci)) != hipSuccess) {
                         err = "device allocation of Winograd weight planes failed";

@@ -876,10 +876,9 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
 def test_conv3x3_winograd_planes(mdx, N, H, W, Cin, Cout, m):
     """Split-plane Winograd (mdx_conv3x3_winograd_x6): V written as bf16
     planes by the input transform, U split once (mdx_split_x6), the (m+2)^2
-    GEMMs on k_gemm_x6 when they give it >= 384 workgroups (the first two
-    shapes; the third, 128 workgroups, falls back to k_conv_x3) -- against
-    the fp64 direct convolution within the fp32 tolerance (the kernels
-    launched show in the rocprof traces under profiles/)."""
+    GEMMs on k_gemm_x6 -- against the fp64 direct convolution within the
+    fp32 tolerance.  (The model uses it only with MDX_WINO_X6 set: slower
+    end to end, profiles/r04_experiments.json.)"""
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
     g = torch.Generator().manual_seed(N * 1000 + H + m)

@@ -12,12 +12,16 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I. -munsafe-fp-atomics \
 //     tools/native/gn_repro.hip -o gn_repro_pk
 //   ... -Xclang -target-feature -Xclang -packed-fp32-ops ... -o gn_repro_nopk
-// Run: gn_repro_<v> REPS BG [H W] (BG: 0 none, 1 VALU loop, 2 HBM copy, 3 both;
-// the FPN level maps of a 448x512 input: 112x128, 56x64, 28x32, 14x16)
+// Run: gn_repro_<v> REPS BG [H W] (BG bits: 1 VALU loop, 2 HBM copy, 4 the
+// library's fp16 3x3 conv (LDS-DMA k_convg), 8 its fp32 3x3 conv (k_conv_sb),
+// both from libmdx.so through dlopen; the FPN level maps of a 448x512 input:
+// 112x128, 56x64, 28x32, 14x16)
 #include "moseq2-detectron-extract_amd/csrc/model_ops.hip"
 namespace mdx {
 void set_error(const char *, ...) {}
 }
+
+#include <dlfcn.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -93,6 +97,25 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&bdst, nbg * 16));
     CK(hipMemset(bsrc, 0, nbg * 16));
     CK(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+    // background convs: the library's own kernels (fp16 and fp32 3x3, 8 x 112 x 128 x 256)
+    typedef int (*conv_fn)(const void *, int, int, int, int, const void *, const float *, int, int, int, int, int,
+                           const void *, int, int, int, int, void *, void *);
+    conv_fn conv = nullptr;
+    void *cx = nullptr, *cw = nullptr, *co = nullptr;
+    if (bg & 12) {
+        void *lib = dlopen("moseq2-detectron-extract_amd/libmdx.so", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) {
+            fprintf(stderr, "dlopen: %s\n", dlerror());
+            return 2;
+        }
+        conv = (conv_fn)dlsym(lib, "mdx_conv2d");
+        const size_t nin = 8ull * 112 * 128 * 256;
+        CK(hipMalloc(&cx, nin * 4));
+        CK(hipMalloc(&co, nin * 4));
+        CK(hipMalloc(&cw, 256ull * 2304 * 4));
+        CK(hipMemset(cx, 0x3c, nin * 4));
+        CK(hipMemset(cw, 0x1c, 256ull * 2304 * 4));
+    }
     hipStream_t sa, sb;
     CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
@@ -105,6 +128,13 @@ int main(int argc, char **argv) {
         if (r > 0 && (bg & 1))
             hipLaunchKernelGGL(k_bg_valu, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
         if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
+        for (int k = 0; r > 0 && (bg & 12) && k < 1 + r % 3; ++k) {
+            const int f16 = (bg & 4) ? 1 : 0;
+            if (conv(cx, 8, 112, 128, 256, cw, nullptr, 256, 3, 3, 1, 1, nullptr, 0, 0, f16, f16, co, sb) != 0) {
+                fprintf(stderr, "background conv failed\n");
+                return 2;
+            }
+        }
         hipLaunchKernelGGL(mdx::k_gn_partial<_Float16>, dim3(nch, N), dim3(256), 0, sa, x, HW, C, G, part);
         hipLaunchKernelGGL(mdx::k_gn_final, dim3((N * G + 3) / 4), dim3(256), 0, sa, part, N * G, nch, 1e-5f, stats);
         hipLaunchKernelGGL(mdx::k_gn_apply<_Float16>, dim3(2048), dim3(256), 0, sa, x, N, H, W, C, G, stats, gamma, beta,
