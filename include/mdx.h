@@ -223,9 +223,6 @@ int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const
  * the fp16 layers on the 256x128 tile (two workgroups per CU) instead.
  * Returns the old mode. */
 int mdx_conv_set_large_tiles(int mode);
-/* Layers with KH*KW*Cin <= kmax use the 64-wide output-channel tile (more
- * workgroups per CU for HBM-bound small-K layers).  Returns the old value. */
-int mdx_conv_set_narrow_kmax(int kmax);
 /* Policy for the 128x128 LDS-DMA fp16 kernel (Cin % 64 == 0): 0 never, 1 when
  * the layer has >= min_tiles 128x128 tiles, 2 whenever eligible (default 0:
  * slower than the 256x256 / split-K kernels inside the full forward).

@@ -48,7 +48,6 @@ SIGNATURES = {
     "mdx_finalize_angles": (I32, [P, P, P, P, I64, I32, P, P]),
     "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
     "mdx_conv_set_large_tiles": (I32, [I32]),
-    "mdx_conv_set_narrow_kmax": (I32, [I32]),
     "mdx_conv_set_dma128": (I32, [I32, I32]),
     "mdx_conv_set_mfma_prio": (I32, [I32]),
     "mdx_conv_set_mfma_prio256": (I32, [I32]),
