@@ -52,6 +52,9 @@ struct WinoProbe {
     int gemm_kernel;
 };
 void wino_probe(WinoProbe *p);
-bool winograd_planes_enabled();  // the model packs Winograd weight planes (MDX_WINO_X6 set)
+bool winograd_planes_enabled();  // the model runs Winograd GEMMs on k_gemm_x6 (MDX_WINO_X6 set)
+// weights of the next split-plane conv launch on this thread as bf16 planes
+// (mdx_split_x6 layout), or null; the model handle sets it around a layer
+void x3_weight_planes(const void *planes);
 
 }  // namespace mdx

@@ -571,12 +571,17 @@ __device__ __forceinline__ void split3_store(const uint4 &v, char *p0, int plane
     *reinterpret_cast<bf16x4 *>(p0 + 2 * plane_bytes) = l;
 }
 
-template <typename TO, int BN_, int NP>
+// BP: the weights (B operand) arrive already split, as bf16 planes in the
+// mdx_split_x6 layout (per row, 96 B per 16 K = hi | mid | lo; a.w, a.wbytes
+// and a.bsw in plane bytes, K % 32 == 0): each 16-B piece is copied to its
+// plane row in LDS, and only the activations are split in the kernel.
+template <typename TO, int BN_, int NP, bool BP = false>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(ConvArgs a) {
     static_assert(NP == 6 || NP == 9, "x6 or x9 plane products");
     constexpr int BK = 32, VEC = 4;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
-    constexpr int BLOADS = BN_ * 8 / CONV_THREADS;
+    // B loads per thread and K-step: 16-B fp32 chunks, or 16-B plane pieces (12 per row)
+    constexpr int BLOADS = BP ? BN_ * 12 / CONV_THREADS : BN_ * 8 / CONV_THREADS;
     constexpr int APL = BM * X3_ROWB, BPL = BN_ * X3_ROWB;  // bytes of one plane
     constexpr int STAGE = 3 * (APL + BPL);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -633,12 +638,24 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
             const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
             A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
         }
+        if constexpr (BP) {
+            const int kb = kglob - kc * VEC;  // the K-step's first K value
 #pragma unroll
-        for (int i = 0; i < BLOADS; ++i) {
-            const int gn = n0 + lrow + 32 * i;
-            const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * 4ll);
-            Bv[i] = __builtin_bit_cast(uint4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
+            for (int i = 0; i < BLOADS; ++i) {
+                const int c = tid + CONV_THREADS * i, row = c / 12, piece = c - row * 12;
+                const int gn = n0 + row;
+                const unsigned off = (unsigned)(((long long)gn * a.K + kb) * 6ll + piece * 16);
+                Bv[i] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, (kb < a.K && gn < a.Cout) ? off : OOB, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < BLOADS; ++i) {
+                const int gn = n0 + lrow + 32 * i;
+                const unsigned off = (unsigned)(((long long)gn * a.K + kglob) * 4ll);
+                Bv[i] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && gn < a.Cout) ? off : OOB, 0, 0));
+            }
         }
     };
     auto advance_k = [&]() {
@@ -657,8 +674,19 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
         char *st = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < 4; ++i) split3_store(A[i], st + (lrow + 32 * i) * X3_ROWB + kc * 8, APL);
+        if constexpr (BP) {
+            // piece = 16-K group g (0, 1), plane p, half h: plane p, row, bytes 32 g + 16 h
 #pragma unroll
-        for (int i = 0; i < BLOADS; ++i) split3_store(Bv[i], st + 3 * APL + (lrow + 32 * i) * X3_ROWB + kc * 8, BPL);
+            for (int i = 0; i < BLOADS; ++i) {
+                const int c = tid + CONV_THREADS * i, row = c / 12, piece = c - row * 12;
+                const int g = piece / 6, p = (piece - g * 6) >> 1, h = piece & 1;
+                *reinterpret_cast<uint4 *>(st + 3 * APL + p * BPL + row * X3_ROWB + g * 32 + h * 16) = Bv[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < BLOADS; ++i)
+                split3_store(Bv[i], st + 3 * APL + (lrow + 32 * i) * X3_ROWB + kc * 8, BPL);
+        }
     };
 
     float4v acc_h[TI][TJ], acc_x[TI][TJ];
@@ -2064,12 +2092,29 @@ extern "C" int mdx_conv_set_x3_narrow(int on) {
     g_x3_narrow = on;
     return old;
 }
+// weight planes for the next split-plane launch on this thread (set by the
+// model handle around a layer's conv call; see mdx::x3_weight_planes)
+static thread_local const void *t_x3_wplanes = nullptr;
+void mdx::x3_weight_planes(const void *planes) { t_x3_wplanes = planes; }
+
 // launch of the split-plane fp32 kernel (LDS: double-buffered planes or the epilogue image)
-static void launch_x3(const ConvArgs &a, int bn, dim3 grid, hipStream_t s) {
+// (with weight planes pending and K % 32 == 0: the pre-split-B instance; a.w,
+// a.wbytes and a.bsw switch to the planes)
+static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
     const size_t stage = 3 * ((size_t)BM * X3_ROWB + (size_t)bn * X3_ROWB);
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * stage;
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+    if (t_x3_wplanes && g_fp32_split == 6 && a.K % 32 == 0 && (long long)a.Cout * a.K * 6 < (1ll << 31)) {
+        a.bsw = a.bsw / 4 * 6;
+        a.w = t_x3_wplanes;
+        a.wbytes = a.Cout * a.K * 6;
+        if (bn == 64)
+            hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        return;
+    }
     if (bn == 64) {
         if (g_fp32_split == 9)
             hipLaunchKernelGGL((k_conv_x3<float, 64, 9>), grid, dim3(CONV_THREADS), lds, s, a);

@@ -59,6 +59,9 @@ struct ConvW {
     // fp32 Linear layers: the weights split once into bf16 planes for
     // mdx_gemm_x6 (used while mdx_conv_fp32_split() != 0)
     void *x6 = nullptr;
+    // fp32 conv layers of split-plane handles (KH*KW*Cin % 32 == 0): the OHWI
+    // weights as bf16 planes, k_conv_x3's pre-split B operand
+    void *wp = nullptr;
 };
 
 struct GnW {
@@ -246,6 +249,20 @@ struct Packer {
         return d;
     }
     float *upload_f32(const std::vector<float> &v) { return (float *)upload(v, false); }
+    // device fp32 rows x K (K % 16 == 0) -> bf16 planes (mdx_split_x6 layout), owned by the model
+    void *split_planes(const float *w, int64_t rows, int K) {
+        void *d = nullptr;
+        if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes(rows, K)) != hipSuccess) {
+            err = "device allocation of weight planes failed";
+            return nullptr;
+        }
+        m.allocs.push_back(d);
+        if (mdx_split_x6(w, rows, K, K, d, nullptr) != MDX_OK || hipDeviceSynchronize() != hipSuccess) {
+            err = "weight plane split failed";
+            return nullptr;
+        }
+        return d;
+    }
 
     // Winograd tile sizes to pack for the next 3x3 layers: the ones the
     // policy current at create time can pick (mdx_winograd_tile); the heads
@@ -284,6 +301,10 @@ struct Packer {
         c.stride = stride;
         c.pad = pad;
         c.dt = cur_dt;
+        if (cur_dt == 0 && mdx_conv_fp32_split() == 6 && ((size_t)kh * kw * ci) % 32 == 0 && c.w && err.empty()) {
+            c.wp = split_planes((const float *)c.w, co, kh * kw * ci);
+            if (!c.wp) return c;
+        }
         if (cur_dt == 0 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && ci >= 64 && ci % 4 == 0 && co % 8 == 0 &&
             err.empty()) {
             std::vector<float> oihw((size_t)co * ci * 9), u;
@@ -297,18 +318,11 @@ struct Packer {
                 mdx_winograd_weights(oihw.data(), co, ci, m_, u.data());
                 float *ud = upload_f32(u);
                 (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = ud;
-                // split-plane handles: U as bf16 planes too (k_gemm_x6's B operand)
-                if (mdx_conv_fp32_split() == 6 && mdx::winograd_planes_enabled() && ci % 16 == 0 && ud && err.empty()) {
-                    void *d = nullptr;
-                    if (hipMalloc(&d, (size_t)mdx_x6_plane_bytes((int64_t)nb * co, ci)) != hipSuccess) {
-                        err = "device allocation of Winograd weight planes failed";
-                        break;
-                    }
-                    m.allocs.push_back(d);
-                    if (mdx_split_x6(ud, (int64_t)nb * co, ci, ci, d, nullptr) != MDX_OK ||
-                        hipDeviceSynchronize() != hipSuccess)
-                        err = "Winograd weight plane split failed";
-                    c.winox6[m_ / 2 - 1] = d;
+                // split-plane handles: U as bf16 planes too (the pre-split B
+                // operand of k_conv_x3, or k_gemm_x6's with MDX_WINO_X6)
+                if (mdx_conv_fp32_split() == 6 && ci % 16 == 0 && ud && err.empty()) {
+                    c.winox6[m_ / 2 - 1] = split_planes(ud, (int64_t)nb * co, ci);
+                    if (!c.winox6[m_ / 2 - 1]) break;
                 }
             }
         }
@@ -670,12 +684,15 @@ struct Fwd {
                             (float *)out, s));
         } else if (wino) {
             const void *wx6 = mdx_conv_fp32_split() == 6 ? cw.winox6[wm / 2 - 1] : nullptr;
-            if (wx6)
+            if (wx6 && mdx::winograd_planes_enabled())
                 chk(mdx_conv3x3_winograd_x6((const float *)x, N, H, W, cw.cin, wu, wx6, cw.b, cw.cout, relu ? 1 : 0,
                                             wm, (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
-            else
+            else {
+                mdx::x3_weight_planes(wx6);  // the split-plane GEMMs take U's planes (K = Cin % 32 == 0)
                 chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
                                          (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
+                mdx::x3_weight_planes(nullptr);
+            }
             if (m.profile) {
                 wino_probe(nullptr);
                 // three records: input transform, batched GEMM, output transform
@@ -693,9 +710,12 @@ struct Fwd {
                     p.r = rs[q];
                 }
             }
-        } else
+        } else {
+            mdx::x3_weight_planes(cw.wp);  // split-plane mode: the pre-split weights
             chk(mdx_conv2d_splitk(x, N, H, W, cw.cin, cw.w, cw.b, cw.cout, cw.k, cw.k, cw.stride, cw.pad, residual,
                                   relu ? 1 : 0, out_mode, cw.dt, out_f32 ? 0 : cw.dt, out, 0, splitk, SPLITK_WS, s));
+            mdx::x3_weight_planes(nullptr);
+        }
         if (pe) {
             (void)hipEventRecord(pe->e1, s);
             int kid = -1, ks = 0;

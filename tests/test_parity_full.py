@@ -177,6 +177,7 @@ def _oracle(depth, B):
 @pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 6, 0),
                                                       (50, 32, "fp32", 2, 0),
                                                       (50, 32, "fp32", 0, 0), (50, 32, "fp32", 4, 6),
+                                                      (50, 32, "fp32", 6, 6),
                                                       (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0),
                                                       (101, 64, "mixed", 6, 0), (101, 64, "fp32", 6, 0)])
 def test_forward_full_frame(mdx, depth, B, dtype, wino, split):
