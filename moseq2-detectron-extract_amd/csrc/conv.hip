@@ -554,28 +554,37 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int X3_ROWB = 64;
 
+// two values at a time: one v_cvt_pk_bf16_f32 per plane, the bf16 pair back
+// to fp32 by a shift and a mask, the exact remainder by one v_pk_add_f32
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 bf2_to_f2(unsigned u) {
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3_pair(f32x2 x, unsigned &h, unsigned &m, unsigned &l) {
+    h = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+    const f32x2 r1 = x - bf2_to_f2(h);
+    m = __builtin_bit_cast(unsigned, __builtin_convertvector(r1, bf16x2));
+    const f32x2 r2 = r1 - bf2_to_f2(m);
+    l = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, bf16x2));
+}
 __device__ __forceinline__ void split3_store(const uint4 &v, char *p0, int plane_bytes) {
-    const float f[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
-    bf16x4 h, m, l;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const __bf16 hb = (__bf16)f[e];
-        const float r1 = f[e] - (float)hb;
-        const __bf16 mb = (__bf16)r1;
-        h[e] = hb;
-        m[e] = mb;
-        l[e] = (__bf16)(r1 - (float)mb);
-    }
-    *reinterpret_cast<bf16x4 *>(p0) = h;
-    *reinterpret_cast<bf16x4 *>(p0 + plane_bytes) = m;
-    *reinterpret_cast<bf16x4 *>(p0 + 2 * plane_bytes) = l;
+    uint2 h, m, l;
+    split3_pair(f32x2{__uint_as_float(v.x), __uint_as_float(v.y)}, h.x, m.x, l.x);
+    split3_pair(f32x2{__uint_as_float(v.z), __uint_as_float(v.w)}, h.y, m.y, l.y);
+    *reinterpret_cast<uint2 *>(p0) = h;
+    *reinterpret_cast<uint2 *>(p0 + plane_bytes) = m;
+    *reinterpret_cast<uint2 *>(p0 + 2 * plane_bytes) = l;
 }
 
 // BP: the weights (B operand) arrive already split, as bf16 planes in the
 // mdx_split_x6 layout (per row, 96 B per 16 K = hi | mid | lo; a.w, a.wbytes
 // and a.bsw in plane bytes, K % 32 == 0): each 16-B piece is copied to its
 // plane row in LDS, and only the activations are split in the kernel.
-template <typename TO, int BN_, int NP, bool BP = false>
+// PW: 1x1 / stride 1 / unpadded layers and the Winograd GEMMs -- row m of A is
+// pixel m, so a lane's A address is its row's offset + the K offset (no
+// per-K-step tap / bounds arithmetic on the VALU the split already loads).
+template <typename TO, int BN_, int NP, bool BP = false, bool PW = false>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(ConvArgs a) {
     static_assert(NP == 6 || NP == 9, "x6 or x9 plane products");
     constexpr int BK = 32, VEC = 4;
@@ -629,14 +638,25 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
     constexpr unsigned OOB = 0xFFFFFFF0u;
+    // PW: byte offset of each A row (pixel m0 + lrow + 32 i), OOB for rows past M
+    unsigned a_rowoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a_rowoff[i] = a_ok[i] ? (unsigned)((long long)(m0 + lrow + 32 * i) * a.Cin * 4) : OOB;
     auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
         const bool kok = kglob < a.K;
+        if constexpr (PW) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
-            const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
-            A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+            for (int i = 0; i < 4; ++i)
+                A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rx, (kok && a_rowoff[i] != OOB) ? a_rowoff[i] + kglob * 4 : OOB, 0, 0));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int iy = a_iy0[i] + kky, ix = a_ix0[i] + kkx;
+                const bool ok = kok && a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                const unsigned off = (unsigned)((a_base[i] + ((long long)iy * a.W + ix) * a.Cin + kci) * 4ll);
+                A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : OOB, 0, 0));
+            }
         }
         if constexpr (BP) {
             const int kb = kglob - kc * VEC;  // the K-step's first K value
@@ -660,6 +680,7 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     };
     auto advance_k = [&]() {
         kglob += BK;
+        if constexpr (PW) return;  // one tap: the K offset is kglob itself
         kci += BK;
         while (kci >= a.Cin) {
             kci -= a.Cin;
@@ -2105,14 +2126,23 @@ static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * stage;
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+    const bool pw = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && (long long)a.M * a.Cin * 4 < (1ll << 31);
     if (t_x3_wplanes && g_fp32_split == 6 && a.K % 32 == 0 && (long long)a.Cout * a.K * 6 < (1ll << 31)) {
         a.bsw = a.bsw / 4 * 6;
         a.w = t_x3_wplanes;
         a.wbytes = a.Cout * a.K * 6;
-        if (bn == 64)
+        if (bn == 64 && pw)
+            hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        else if (bn == 64)
             hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        else if (pw)
+            hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         else
             hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true>), grid, dim3(CONV_THREADS), lds, s, a);
+        return;
+    }
+    if (bn == 64 && pw && g_fp32_split == 6) {
+        hipLaunchKernelGGL((k_conv_x3<float, 64, 6, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
         return;
     }
     if (bn == 64) {

@@ -1052,6 +1052,32 @@ def test_forward_fused_shortcut_matches_unfused(small_case):
         assert err < 2e-4, f"{k}: rel err {err:.2e}"
 
 
+def test_split_plane_preplit_weights_bit_equal(small_case):
+    """Split-plane mode (mdx_conv_set_fp32_split(6)): a handle created in that
+    mode carries its conv weights and Winograd U as bf16 planes (split once,
+    mdx_split_x6) and k_conv_x3 copies them instead of splitting the weights
+    per tile; a handle created outside it splits them in the kernel.  The
+    split is the same (RNE hi, mid of the exact remainder, lo) and the MFMA
+    order is the same, so the backbone and FPN features agree bit for bit --
+    with the pointwise (PW) instance on the 1x1 layers and Winograd GEMMs."""
+    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd.model import MaskRCNN
+    cfg, sd, _, imgs = small_case
+    old = call("mdx_conv_set_fp32_split", 0)
+    try:
+        m_kernel_split = MaskRCNN(cfg, sd, dtype="fp32")
+        call("mdx_conv_set_fp32_split", 6)
+        m_planes = MaskRCNN(cfg, sd, dtype="fp32")
+        x = torch.from_numpy(imgs[..., 0]).cuda()
+        a = m_kernel_split.forward(x, intermediates=True)["intermediates"]
+        b = m_planes.forward(x, intermediates=True)["intermediates"]
+        torch.cuda.synchronize()
+    finally:
+        call("mdx_conv_set_fp32_split", old)
+    for k in ("res2", "res3", "res4", "res5", "p2", "p3", "p4", "p5", "p6"):
+        assert torch.equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 1 and c[7] == 0])
 def test_conv2d_fp32_pointwise_instances(mdx, case):
     """fp32 pointwise layers (1x1, unpadded, stride 1 or 2) on k_conv's PW
