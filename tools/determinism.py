@@ -1,7 +1,9 @@
 """Soak test of the stream-pipelined loop: every output of OverlappedExtractor
 (5 streams, two forwards in flight, frame stages beside them) compared bit
 for bit with the serial step on the same batch, over many steps.
-Usage: python tools/determinism.py [fp32|fp16] [steps] [batch] [model_streams]"""
+Usage: python tools/determinism.py [fp32|fp16] [steps] [batch] [model_streams]
+(DET_SPLIT=6: the fp32 layers as bf16 plane products, set before the handle
+is created so it carries the weight planes)"""
 import json
 import os
 import sys
@@ -26,6 +28,9 @@ def main():
     s = synth.SyntheticSession(nb * B, seed=21)
     raw = torch.from_numpy(s.frames(0, nb * B)).cuda()
     batches = [raw[i * B:(i + 1) * B] for i in range(nb)]
+    if os.environ.get("DET_SPLIT"):
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_fp32_split", int(os.environ["DET_SPLIT"]))
     pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype, weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=B))
     keys = ("depth_frames", "mask_frames", "centroid", "angle", "keypoints", "ndet")

@@ -2,7 +2,7 @@
 written as depth.dat, then extract.extract_session chunk by chunk (frame
 source -> device hot path -> host angle / tracking step -> crops, scalars,
 keypoints).  Prints frames/s with tracking off and on.
-Usage: python tools/extract_bench.py [nframes] [chunk] [fp32|fp16]"""
+Usage: python tools/extract_bench.py [nframes] [chunk] [fp32|fp16] [model_streams]"""
 import json
 import os
 import sys
@@ -17,6 +17,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
     chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
     dtype = sys.argv[3] if len(sys.argv) > 3 else "fp32"
+    streams = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     import numpy as np
     import torch
     import mdx_pkg
@@ -27,7 +28,7 @@ def main():
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig
     s = synth.SyntheticSession(n, seed=9)
     pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype, weights="synthetic")
-    res = {"nframes": n, "chunk": chunk, "dtype": dtype}
+    res = {"nframes": n, "chunk": chunk, "dtype": dtype, "model_streams": streams}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         t0 = time.perf_counter()
         s.write(td)
@@ -42,7 +43,8 @@ def main():
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     out = extract_session(path, s.bground_im, s.roi, pred,
-                                          ExtractConfig(chunk_size=chunk, use_tracking=tracking, overlap_host=overlap),
+                                          ExtractConfig(chunk_size=chunk, use_tracking=tracking, overlap_host=overlap,
+                                                        model_streams=streams),
                                           true_depth=s.true_depth)
                     torch.cuda.synchronize()
                     dt = time.perf_counter() - t0
