@@ -115,7 +115,8 @@ def test_conv2d(mdx, dtype, case, ksplit):
             pytest.skip("256x256 split-K: Cin % 64 (fp16) / 32 (fp32) == 0, Cout % 256 == 0")
         nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
         ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
-        old_nk = call("mdx_conv_set_narrow_kmax", 0)
+        if Cin * k * k <= 128:
+            pytest.skip("K <= 128 layers stay on the 64-wide register-staged tile (the policy's narrow-K rule)")
         old = call("mdx_conv_set_split256", 2, 1)
         old_f = call("mdx_conv_set_dma_f32", 2)
         try:
@@ -127,11 +128,11 @@ def test_conv2d(mdx, dtype, case, ksplit):
         finally:
             call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_split256", old, 18)
-            call("mdx_conv_set_narrow_kmax", old_nk)
     elif ksplit in ("large", "large128", "dma128"):
         if (dtype != "fp16" and ksplit in ("dma128", "large128")) or Cin % (64 if dtype == "fp16" else 32):
             pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 / 256x128 ones fp16 only")
-        old_nk = call("mdx_conv_set_narrow_kmax", 0)
+        if Cin * k * k <= 128:
+            pytest.skip("K <= 128 layers stay on the 64-wide register-staged tile (the policy's narrow-K rule)")
         old = call("mdx_conv_set_large_tiles", {"large": 2, "large128": 3}.get(ksplit, 0))
         old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
         old_i = call("mdx_conv_set_mfma_prio", int(case[0] % 2 == 0))  # both DMA schedules across the cases
@@ -150,7 +151,6 @@ def test_conv2d(mdx, dtype, case, ksplit):
         finally:
             call("mdx_conv_set_dma_f32", old_f)
             call("mdx_conv_set_large_tiles", old)
-            call("mdx_conv_set_narrow_kmax", old_nk)
             call("mdx_conv_set_dma128", old_d, 1536)
             call("mdx_conv_set_mfma_prio", old_i)
             call("mdx_conv_set_dma_after", old_da)

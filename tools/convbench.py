@@ -59,9 +59,8 @@ def main():
         flops = 2.0 * M * Cout * k * k * Cin
         byts = 2.0 * (x.numel() + w.numel() + out.numel() + (r.numel() if res else 0))
         line = f"M={M:7d} N={Cout:5d} K={k * k * Cin:6d} res={int(res)}:"
-        for mode, nk in ((0, 0), (2, 0), (0, 1 << 20)):
+        for mode, nk in ((0, 0), (2, 0)):
             old = call("mdx_conv_set_large_tiles", mode)
-            oldk = call("mdx_conv_set_narrow_kmax", nk)
 
             def go():
                 call("mdx_conv2d_splitk", P(x), N, H, W, Cin, P(w), P(b), Cout, k, k, s, p, P(r), 1, 0, 1, 1,
@@ -74,7 +73,6 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             call("mdx_conv_set_large_tiles", old)
-            call("mdx_conv_set_narrow_kmax", oldk)
             t = e0.elapsed_time(e1) / 10 * 1e-3
             line += f"  [{'64' if nk else ('128' if mode == 0 else '256')}] {t * 1e6:7.1f}us {flops / t / 1e12:6.1f}TF {byts / t / 1e12:5.2f}TB/s"
         print(line, flush=True)
