@@ -625,11 +625,13 @@ def main():
             "value": round(frames_done / dtx, 2), "unit": "frames/s", "ms_per_step": round(dtx / args.steps * 1e3, 3),
             "dtype": "fp32 operands split exactly into 3 bf16 planes, 6 plane products on the bf16 matrix cores, "
                      "fp32 accumulation",
-            "note": "mdx_conv_set_fp32_split(6): conv layers on k_conv_x3 (split in registers), box head FCs on "
+            "note": "mdx_conv_set_fp32_split(6): conv layers and Winograd GEMMs on k_conv_x3 (weights split into "
+                    "planes once when the handle is created, activations split in registers), box head FCs on "
                     "k_gemm_x6 (256x256 LDS-DMA over planes written by the box pooler / mdx_split_x6); per product the "
                     "dropped terms are below one fp32 rounding; "
                     "full-frame parity vs the fp32 oracle at least as close as the f32-MFMA kernels' "
-                    "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6], DESIGN.md section 3)"}
+                    "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6] and [50-32-fp32-6-6], "
+                    "DESIGN.md section 3)"}
         del exx
 
     if world == 1 and not args.no_secondary and not args.no_extract_loop and args.dtype == "fp32":
