@@ -27,7 +27,9 @@ x = prep(torch.from_numpy(s.frames(0, 8)).cuda())
 xa, xb = x[:4].contiguous(), x[4:].contiguous()
 lut = proc.scale_lut(0, 100)
 m = pred.model
-mb = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dt, weights="synthetic").model if mode == "other" else m
+# other: a second handle on stream B (DBG_OTHER_DT: its dtype, default the same)
+mb = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=os.environ.get("DBG_OTHER_DT", dt),
+                           weights="synthetic").model if mode == "other" else m
 import ctypes
 from moseq2_detectron_extract_amd._lib import call
 P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
