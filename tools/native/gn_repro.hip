@@ -14,8 +14,10 @@
 //   ... -Xclang -target-feature -Xclang -packed-fp32-ops ... -o gn_repro_nopk
 // Run: gn_repro_<v> REPS BG [H W] (BG bits: 1 VALU loop, 2 HBM copy, 4 the
 // library's fp16 3x3 conv (LDS-DMA k_convg), 8 its fp32 3x3 conv (k_conv_sb),
-// both from libmdx.so through dlopen; the FPN level maps of a 448x512 input:
-// 112x128, 56x64, 28x32, 14x16)
+// both from libmdx.so through dlopen, 16 a packed-FP32 VALU loop (two-lane
+// vector FMAs / adds with lane swaps), 32 the GN statistics kernels on a
+// second 8 x 112 x 128 map; the FPN level maps of a 448x512 input: 112x128,
+// 56x64, 28x32, 14x16)
 #include "moseq2-detectron-extract_amd/csrc/model_ops.hip"
 namespace mdx {
 void set_error(const char *, ...) {}
@@ -45,6 +47,19 @@ __global__ __launch_bounds__(256) void k_bg_valu(float *out, int iters) {
         b = fmaf(b, c, a);
     }
     if (a == 12345.f) out[threadIdx.x] = a + b;  // keep the loop
+}
+
+// background packed-FP32 load: two-lane vectors (v_pk_fma_f32 / v_pk_add_f32
+// with op_sel lane swaps in the packed build, scalar FMAs in the other)
+typedef float f2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_bg_pk(float *out, int iters) {
+    f2v a = {threadIdx.x * 1e-3f, 0.5f}, b = {blockIdx.x * 1e-4f, 0.25f}, c = {1.0001f, 0.9999f};
+    for (int i = 0; i < iters; ++i) {
+        a = a * c + b;
+        b = b * c + a.yx;
+        a = a + b.xx;
+    }
+    if (a.x == 12345.f) out[threadIdx.x] = a.y + b.x + b.y;  // keep the loop
 }
 
 // background HBM load: streaming copy
@@ -116,6 +131,22 @@ int main(int argc, char **argv) {
         CK(hipMemset(cx, 0x3c, nin * 4));
         CK(hipMemset(cw, 0x1c, 256ull * 2304 * 4));
     }
+    // background GN: the same kernels over a second, larger map
+    const int BH = 112, BW = 128, BN_ = 8, bnch = (BH * BW + mdx::GN_CHUNK_PIX - 1) / mdx::GN_CHUNK_PIX;
+    _Float16 *bx = nullptr;
+    float *bpart = nullptr, *bstats = nullptr;
+    if (bg & 32) {
+        const size_t nb = (size_t)BN_ * BH * BW * C;
+        std::vector<_Float16> hb2(nb);
+        for (size_t i = 0; i < nb; ++i) {
+            s = s * 1664525u + 1013904223u;
+            hb2[i] = (_Float16)(((s >> 8) & 0xffff) / 65536.0f * 4.0f - 1.0f);
+        }
+        CK(hipMalloc(&bx, nb * 2));
+        CK(hipMemcpy(bx, hb2.data(), nb * 2, hipMemcpyHostToDevice));
+        CK(hipMalloc(&bpart, (size_t)BN_ * G * bnch * 3 * 4));
+        CK(hipMalloc(&bstats, (size_t)BN_ * G * 2 * 4));
+    }
     hipStream_t sa, sb;
     CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
@@ -128,6 +159,13 @@ int main(int argc, char **argv) {
         if (r > 0 && (bg & 1))
             hipLaunchKernelGGL(k_bg_valu, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
         if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
+        if (r > 0 && (bg & 16))
+            hipLaunchKernelGGL(k_bg_pk, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
+        for (int k = 0; r > 0 && (bg & 32) && k < 4 + r % 5; ++k) {
+            hipLaunchKernelGGL(mdx::k_gn_partial<_Float16>, dim3(bnch, BN_), dim3(256), 0, sb, bx, BH * BW, C, G, bpart);
+            hipLaunchKernelGGL(mdx::k_gn_final, dim3((BN_ * G + 3) / 4), dim3(256), 0, sb, bpart, BN_ * G, bnch, 1e-5f,
+                               bstats);
+        }
         for (int k = 0; r > 0 && (bg & 12) && k < 1 + r % 3; ++k) {
             const int f16 = (bg & 4) ? 1 : 0;
             if (conv(cx, 8, 112, 128, 256, cw, nullptr, 256, 3, 3, 1, 1, nullptr, 0, 0, f16, f16, co, sb) != 0) {
