@@ -132,7 +132,10 @@ int main(int argc, char **argv) {
         CK(hipMemset(cw, 0x1c, 256ull * 2304 * 4));
     }
     // background GN: the same kernels over a second, larger map
-    const int BH = 112, BW = 128, BN_ = 8, bnch = (BH * BW + mdx::GN_CHUNK_PIX - 1) / mdx::GN_CHUNK_PIX;
+    // (GN_BG="H W N": another map size, e.g. "14 16 4" = the level-5 map of a 4-image batch)
+    int BH = 112, BW = 128, BN_ = 8;
+    if (const char *e = getenv("GN_BG")) sscanf(e, "%d %d %d", &BH, &BW, &BN_);
+    const int bnch = (BH * BW + mdx::GN_CHUNK_PIX - 1) / mdx::GN_CHUNK_PIX;
     _Float16 *bx = nullptr;
     float *bpart = nullptr, *bstats = nullptr;
     if (bg & 32) {
@@ -161,7 +164,8 @@ int main(int argc, char **argv) {
         if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
         if (r > 0 && (bg & 16))
             hipLaunchKernelGGL(k_bg_pk, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
-        for (int k = 0; r > 0 && (bg & 32) && k < 4 + r % 5; ++k) {
+        const int gn_bg_launches = getenv("GN_BG_LAUNCHES") ? atoi(getenv("GN_BG_LAUNCHES")) : 4;
+        for (int k = 0; r > 0 && (bg & 32) && k < gn_bg_launches + r % 5; ++k) {
             hipLaunchKernelGGL(mdx::k_gn_partial<_Float16>, dim3(bnch, BN_), dim3(256), 0, sb, bx, BH * BW, C, G, bpart);
             hipLaunchKernelGGL(mdx::k_gn_final, dim3((BN_ * G + 3) / 4), dim3(256), 0, sb, bpart, BN_ * G, bnch, 1e-5f,
                                bstats);
