@@ -29,6 +29,8 @@ def main():
             for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                 if n in c:
                     d[n.lower() + "_frac"] = c[n] / wc
+        if c.get("SQ_INSTS_LDS"):
+            d["lds_bank_conflict_cycles_per_lds_inst"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_INSTS_LDS"]
         d["dispatch_records"] = len(disp[k])
         out[k[:90]] = d
     for k, d in sorted(out.items(), key=lambda kv: -kv[1].get("GRBM_GUI_ACTIVE", 0))[:12]:
