@@ -577,6 +577,13 @@ __device__ __forceinline__ void split3_store(const uint4 &v, char *p0, int plane
     *reinterpret_cast<uint2 *>(p0 + 2 * plane_bytes) = l;
 }
 
+// LDS rows of 64 B, four 16-B chunks: chunk c of row r lives at position
+// c ^ x3_swz(r), so that each 16-lane group of a fragment ds_read_b128 (rows
+// 0-15 x one chunk, groups {0-3,12-15,20-27}, ...) hits 16 distinct 16-B bank
+// slots; unswizzled, rows r and r + 4 of a group share banks (2-way: the
+// kernel measured 3.7 conflict cycles per LDS instruction, SQ_LDS_BANK_CONFLICT)
+__device__ __forceinline__ int x3_swz(int r) { return ((r >> 3) & 1) << 1; }
+
 // BP: the weights (B operand) arrive already split, as bf16 planes in the
 // mdx_split_x6 layout (per row, 96 B per 16 K = hi | mid | lo; a.w, a.wbytes
 // and a.bsw in plane bytes, K % 32 == 0): each 16-B piece is copied to its
@@ -662,9 +669,12 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
             const int kb = kglob - kc * VEC;  // the K-step's first K value
 #pragma unroll
             for (int i = 0; i < BLOADS; ++i) {
-                const int c = tid + CONV_THREADS * i, row = c / 12, piece = c - row * 12;
+                // piece c = (plane p, row, chunk q = 2 g + h): 8 consecutive
+                // lanes fill two whole 64-B rows of one plane (conflict-free stores)
+                const int c = tid + CONV_THREADS * i, p = c / (BN_ * 4), rem = c - p * (BN_ * 4);
+                const int row = rem >> 2, q = rem & 3;
                 const int gn = n0 + row;
-                const unsigned off = (unsigned)(((long long)gn * a.K + kb) * 6ll + piece * 16);
+                const unsigned off = (unsigned)(((long long)gn * a.K + kb) * 6ll + (q >> 1) * 96 + p * 32 + (q & 1) * 16);
                 Bv[i] = __builtin_bit_cast(
                     uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, (kb < a.K && gn < a.Cout) ? off : OOB, 0, 0));
             }
@@ -694,19 +704,24 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     auto store_lds = [&](int buf, const uint4 (&A)[4], const uint4 (&Bv)[BLOADS]) {
         char *st = smem + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) split3_store(A[i], st + (lrow + 32 * i) * X3_ROWB + kc * 8, APL);
+        for (int i = 0; i < 4; ++i) {
+            const int row = lrow + 32 * i;
+            split3_store(A[i], st + row * X3_ROWB + (((kc >> 1) ^ x3_swz(row)) << 4) + (kc & 1) * 8, APL);
+        }
         if constexpr (BP) {
-            // piece = 16-K group g (0, 1), plane p, half h: plane p, row, bytes 32 g + 16 h
 #pragma unroll
             for (int i = 0; i < BLOADS; ++i) {
-                const int c = tid + CONV_THREADS * i, row = c / 12, piece = c - row * 12;
-                const int g = piece / 6, p = (piece - g * 6) >> 1, h = piece & 1;
-                *reinterpret_cast<uint4 *>(st + 3 * APL + p * BPL + row * X3_ROWB + g * 32 + h * 16) = Bv[i];
+                const int c = tid + CONV_THREADS * i, p = c / (BN_ * 4), rem = c - p * (BN_ * 4);
+                const int row = rem >> 2, q = rem & 3;
+                *reinterpret_cast<uint4 *>(st + 3 * APL + p * BPL + row * X3_ROWB + ((q ^ x3_swz(row)) << 4)) = Bv[i];
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < BLOADS; ++i)
-                split3_store(Bv[i], st + 3 * APL + (lrow + 32 * i) * X3_ROWB + kc * 8, BPL);
+            for (int i = 0; i < BLOADS; ++i) {
+                const int row = lrow + 32 * i;
+                split3_store(Bv[i], st + 3 * APL + row * X3_ROWB + (((kc >> 1) ^ x3_swz(row)) << 4) + (kc & 1) * 8,
+                             BPL);
+            }
         }
     };
 
@@ -741,8 +756,9 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
             load_global(Ai, Bi);
             advance_k();
         }
-        const char *Ab = smem + cur * STAGE + (wm * (BM / 2) + (lane & 15)) * X3_ROWB + (lane >> 4) * 16;
-        const char *Bb = smem + cur * STAGE + 3 * APL + (wn * (BN_ / 2) + (lane & 15)) * X3_ROWB + (lane >> 4) * 16;
+        const int fo = ((lane >> 4) ^ x3_swz(lane & 15)) << 4;  // (row bits 0-3 = lane & 15)
+        const char *Ab = smem + cur * STAGE + (wm * (BM / 2) + (lane & 15)) * X3_ROWB + fo;
+        const char *Bb = smem + cur * STAGE + 3 * APL + (wn * (BN_ / 2) + (lane & 15)) * X3_ROWB + fo;
         bf16x8 af[3][TI], bf[3][TJ];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
