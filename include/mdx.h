@@ -273,6 +273,11 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
  * LDS-DMA plane kernel (k_gemm_x6); outside split mode, or with Cin % 16 != 0,
  * as mdx_conv3x3_winograd.  Model handles use it only with MDX_WINO_X6 set in
  * the environment (4 % slower end to end than k_conv_x3 on every layer). */
+/* Split-plane launches with pre-split weights (model handles in mode 6) on
+ * the single-stage k_conv_x3 (one LDS stage, one accumulator set, three
+ * workgroups per CU): 1 (default) or 0 (two LDS stages, separate hi*hi and
+ * cross-product accumulators).  Returns the old value. */
+int mdx_conv_set_x3_single_stage(int on);
 int mdx_conv3x3_winograd_x6(const float *x, int N, int H, int W, int Cin, const float *U, const void *U_planes,
                             const float *bias, int Cout, int relu, int m, float *out, void *workspace,
                             int64_t workspace_bytes, mdx_stream_t stream);

@@ -591,8 +591,11 @@ __device__ __forceinline__ int x3_swz(int r) { return ((r >> 3) & 1) << 1; }
 // PW: 1x1 / stride 1 / unpadded layers and the Winograd GEMMs -- row m of A is
 // pixel m, so a lane's A address is its row's offset + the K offset (no
 // per-K-step tap / bounds arithmetic on the VALU the split already loads).
-template <typename TO, int BN_, int NP, bool BP = false, bool PW = false>
-__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(ConvArgs a) {
+// SB: one LDS stage and one register stage (36 KB of LDS at BN 64), the
+// plane products of all six pairs summed in one accumulator set -- three
+// workgroups per CU instead of two; two barriers per K-step (as k_conv_sb).
+template <typename TO, int BN_, int NP, bool BP = false, bool PW = false, bool SB = false>
+__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? (SB ? 3 : 2) : 1) void k_conv_x3(ConvArgs a) {
     static_assert(NP == 6 || NP == 9, "x6 or x9 plane products");
     constexpr int BK = 32, VEC = 4;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     int kci = kglob % a.Cin;
     int kr = kglob / a.Cin;
     int kkx = kr % a.KW, kky = kr / a.KW;
-    uint4 ra[2][4], rb[2][BLOADS];
+    uint4 ra[SB ? 1 : 2][4], rb[SB ? 1 : 2][BLOADS];
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
     constexpr unsigned OOB = 0xFFFFFFF0u;
@@ -725,13 +728,18 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
         }
     };
 
-    float4v acc_h[TI][TJ], acc_x[TI][TJ];
+    // (SB: acc_x is acc_h -- one accumulator set)
+    float4v acc_h[TI][TJ], acc_xs[SB ? 1 : TI][SB ? 1 : TJ];
+    auto acc_x = [&](int i, int j) -> float4v & {
+        if constexpr (SB) return acc_h[i][j];
+        else return acc_xs[i][j];
+    };
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
             acc_h[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-            acc_x[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+            if constexpr (!SB) acc_xs[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
         }
 
     const int nk_all = (a.K + BK - 1) / BK;
@@ -740,7 +748,7 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     advance_k();
     store_lds(0, ra[0], rb[0]);
     if (nk > 1) {
-        load_global(ra[1], rb[1]);
+        load_global(ra[SB ? 0 : 1], rb[SB ? 0 : 1]);
         advance_k();
     }
     __syncthreads();
@@ -751,8 +759,8 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
     constexpr int P0 = NP == 9 ? 0 : 3;
     auto kstep = [&](int kt, uint4 (&Ai)[4], uint4 (&Bi)[BLOADS], const uint4 (&As_)[4],
                      const uint4 (&Bs_)[BLOADS]) {
-        const int cur = kt & 1;
-        if (kt + 2 < nk) {
+        const int cur = SB ? 0 : (kt & 1);
+        if (!SB && kt + 2 < nk) {
             load_global(Ai, Bi);
             advance_k();
         }
@@ -773,21 +781,35 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
             for (int i = 0; i < TI; ++i)
 #pragma unroll
                 for (int j = 0; j < TJ; ++j)
-                    acc_x[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[PA[q]][i], bf[PB[q]][j], acc_x[i][j], 0, 0, 0);
+                    acc_x(i, j) = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[PA[q]][i], bf[PB[q]][j], acc_x(i, j), 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
                 acc_h[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bf[0][j], acc_h[i][j], 0, 0, 0);
-        if (kt + 1 < nk) store_lds(cur ^ 1, As_, Bs_);
+        if constexpr (SB) {
+            // [MFMAs of kt] barrier [store kt + 1, load kt + 2 into the same registers] barrier
+            __syncthreads();
+            if (kt + 1 < nk) store_lds(0, Ai, Bi);
+            if (kt + 2 < nk) {
+                load_global(Ai, Bi);
+                advance_k();
+            }
+        } else if (kt + 1 < nk) {
+            store_lds(cur ^ 1, As_, Bs_);
+        }
         __syncthreads();
     };
     int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-        kstep(kt, ra[0], rb[0], ra[1], rb[1]);
-        kstep(kt + 1, ra[1], rb[1], ra[0], rb[0]);
+    if constexpr (SB) {
+        for (; kt < nk; ++kt) kstep(kt, ra[0], rb[0], ra[0], rb[0]);
+    } else {
+        for (; kt + 1 < nk; kt += 2) {
+            kstep(kt, ra[0], rb[0], ra[SB ? 0 : 1], rb[SB ? 0 : 1]);
+            kstep(kt + 1, ra[SB ? 0 : 1], rb[SB ? 0 : 1], ra[0], rb[0]);
+        }
+        if (kt < nk) kstep(kt, ra[0], rb[0], ra[SB ? 0 : 1], rb[SB ? 0 : 1]);
     }
-    if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
 
     // ---- epilogue: as k_conv, in two halves of BM/2 rows
     constexpr int CP = BN_ + 4;
@@ -806,7 +828,7 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 2 : 1) void k_conv_x3(Con
                     for (int r = 0; r < 4; ++r) {
                         const int row = i * 16 + (lane >> 4) * 4 + r;
                         const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
-                        Cs[row * CP + col] = acc_h[i][j][r] + acc_x[i][j][r];
+                        Cs[row * CP + col] = SB ? acc_h[i][j][r] : acc_h[i][j][r] + acc_x(i, j)[r];
                     }
         }
         __syncthreads();
@@ -2134,6 +2156,13 @@ extern "C" int mdx_conv_set_x3_narrow(int on) {
 static thread_local const void *t_x3_wplanes = nullptr;
 void mdx::x3_weight_planes(const void *planes) { t_x3_wplanes = planes; }
 
+// the single-stage split-plane instance (k_conv_x3<..., SB>) for the pre-split-weight launches
+static int g_x3_sb = 1;
+extern "C" int mdx_conv_set_x3_single_stage(int on) {
+    const int old = g_x3_sb;
+    g_x3_sb = on;
+    return old;
+}
 // launch of the split-plane fp32 kernel (LDS: double-buffered planes or the epilogue image)
 // (with weight planes pending and K % 32 == 0: the pre-split-B instance; a.w,
 // a.wbytes and a.bsw switch to the planes)
@@ -2147,6 +2176,15 @@ static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
         a.bsw = a.bsw / 4 * 6;
         a.w = t_x3_wplanes;
         a.wbytes = a.Cout * a.K * 6;
+        if (bn == 64 && g_x3_sb) {
+            // one LDS stage: the stage or the epilogue image
+            const size_t lds1 = stage > lds_epi ? stage : lds_epi;
+            if (pw)
+                hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, true, true>), grid, dim3(CONV_THREADS), lds1, s, a);
+            else
+                hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, false, true>), grid, dim3(CONV_THREADS), lds1, s, a);
+            return;
+        }
         if (bn == 64 && pw)
             hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, true>), grid, dim3(CONV_THREADS), lds, s, a);
         else if (bn == 64)

@@ -1059,11 +1059,15 @@ def test_split_plane_preplit_weights_bit_equal(small_case):
     per tile; a handle created outside it splits them in the kernel.  The
     split is the same (RNE hi, mid of the exact remainder, lo) and the MFMA
     order is the same, so the backbone and FPN features agree bit for bit --
-    with the pointwise (PW) instance on the 1x1 layers and Winograd GEMMs."""
+    with the pointwise (PW) instance on the 1x1 layers and Winograd GEMMs.
+    The single-stage instance those launches take by default
+    (mdx_conv_set_x3_single_stage) sums all six products in one accumulator
+    set: within fp32 rounding of the two-stage kernel."""
     from moseq2_detectron_extract_amd._lib import call
     from moseq2_detectron_extract_amd.model import MaskRCNN
     cfg, sd, _, imgs = small_case
     old = call("mdx_conv_set_fp32_split", 0)
+    old_sb = call("mdx_conv_set_x3_single_stage", 0)
     try:
         m_kernel_split = MaskRCNN(cfg, sd, dtype="fp32")
         call("mdx_conv_set_fp32_split", 6)
@@ -1071,11 +1075,17 @@ def test_split_plane_preplit_weights_bit_equal(small_case):
         x = torch.from_numpy(imgs[..., 0]).cuda()
         a = m_kernel_split.forward(x, intermediates=True)["intermediates"]
         b = m_planes.forward(x, intermediates=True)["intermediates"]
+        b = {k: v.clone() for k, v in b.items()}
+        call("mdx_conv_set_x3_single_stage", 1)
+        c = m_planes.forward(x, intermediates=True)["intermediates"]
         torch.cuda.synchronize()
     finally:
         call("mdx_conv_set_fp32_split", old)
+        call("mdx_conv_set_x3_single_stage", old_sb)
     for k in ("res2", "res3", "res4", "res5", "p2", "p3", "p4", "p5", "p6"):
         assert torch.equal(a[k], b[k]), k
+        gb, gc = b[k].double(), c[k].double()
+        assert (gb - gc).abs().max().item() <= 2e-5 * gb.abs().max().item(), k
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 1 and c[7] == 0])
