@@ -124,6 +124,14 @@ int main(int argc, char **argv) {
             return 2;
         }
         conv = (conv_fn)dlsym(lib, "mdx_conv2d");
+        // BG_CONV_REG=1: the register-staged fp16 kernels (k_conv_sb / k_conv_sbg)
+        // instead of the LDS-DMA tiles (large tiles and the 256x256 split-K off)
+        if (getenv("BG_CONV_REG")) {
+            typedef int (*set1_fn)(int);
+            typedef int (*set2_fn)(int, int);
+            ((set1_fn)dlsym(lib, "mdx_conv_set_large_tiles"))(0);
+            ((set2_fn)dlsym(lib, "mdx_conv_set_split256"))(0, 18);
+        }
         const size_t nin = 8ull * 112 * 128 * 256;
         CK(hipMalloc(&cx, nin * 4));
         CK(hipMalloc(&co, nin * 4));
