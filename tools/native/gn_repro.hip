@@ -15,7 +15,8 @@
 // Run: gn_repro_<v> REPS BG [H W] (BG bits: 1 VALU loop, 2 HBM copy, 4 the
 // library's fp16 3x3 conv (LDS-DMA k_convg), 8 its fp32 3x3 conv (k_conv_sb),
 // both from libmdx.so through dlopen, 16 a packed-FP32 VALU loop (two-lane
-// vector FMAs / adds with lane swaps), 32 the GN statistics kernels on a
+// vector FMAs / adds with lane swaps), 128 / 256 / 512 f16 / bf16 / f32
+// MFMA loops, 32 the GN statistics kernels on a
 // second 8 x 112 x 128 map; the FPN level maps of a 448x512 input: 112x128,
 // 56x64, 28x32, 14x16)
 #include "moseq2-detectron-extract_amd/csrc/model_ops.hip"
@@ -60,6 +61,35 @@ __global__ __launch_bounds__(256) void k_bg_pk(float *out, int iters) {
         a = a + b.xx;
     }
     if (a.x == 12345.f) out[threadIdx.x] = a.y + b.x + b.y;  // keep the loop
+}
+
+// background matrix-core loads: chains of 16x16x32 f16 / bf16 or 16x16x4 f32
+// MFMAs on register operands (4 independent accumulators per wave)
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int KIND>
+__global__ __launch_bounds__(256) void k_bg_mfma(float *out, int iters) {
+    f4v acc[4] = {};
+    const float s = threadIdx.x * 1e-3f;
+    h8v ha, hb;
+    b8v ba, bb;
+    for (int e = 0; e < 8; ++e) {
+        ha[e] = (_Float16)(s + e);
+        hb[e] = (_Float16)(1.f - s);
+        ba[e] = (__bf16)(s + e);
+        bb[e] = (__bf16)(1.f - s);
+    }
+    for (int i = 0; i < iters; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr (KIND == 0) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[q], 0, 0, 0);
+            else if constexpr (KIND == 1) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba, bb, acc[q], 0, 0, 0);
+            else acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(s, s + 1.f, acc[q], 0, 0, 0);
+        }
+    float t = 0.f;
+    for (int q = 0; q < 4; ++q) t += acc[q][0] + acc[q][3];
+    if (t == 12345.f) out[threadIdx.x] = t;  // keep the loop
 }
 
 // background HBM load: streaming copy
@@ -170,6 +200,13 @@ int main(int argc, char **argv) {
         if (r > 0 && (bg & 1))
             hipLaunchKernelGGL(k_bg_valu, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
         if (r > 0 && (bg & 2)) hipLaunchKernelGGL(k_bg_copy, dim3(4096), dim3(256), 0, sb, bsrc, bdst, nbg);
+        // 128 / 256 / 512: f16 / bf16 / f32 MFMA loops
+        if (r > 0 && (bg & 128))
+            hipLaunchKernelGGL(k_bg_mfma<0>, dim3(2048), dim3(256), 0, sb, bgout, 2000 + 97 * (r % 7));
+        if (r > 0 && (bg & 256))
+            hipLaunchKernelGGL(k_bg_mfma<1>, dim3(2048), dim3(256), 0, sb, bgout, 2000 + 97 * (r % 7));
+        if (r > 0 && (bg & 512))
+            hipLaunchKernelGGL(k_bg_mfma<2>, dim3(2048), dim3(256), 0, sb, bgout, 2000 + 97 * (r % 7));
         if (r > 0 && (bg & 16))
             hipLaunchKernelGGL(k_bg_pk, dim3(2048), dim3(256), 0, sb, bgout, 20000 + 997 * (r % 7));
         const int gn_bg_launches = getenv("GN_BG_LAUNCHES") ? atoi(getenv("GN_BG_LAUNCHES")) : 4;
