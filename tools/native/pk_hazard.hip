@@ -1,0 +1,166 @@
+// Which packed-FP32 instruction forms change their results while another
+// kernel's waves run 16-bit matrix instructions on the same CUs.
+//
+// tools/native/gn_repro.hip showed the library's GroupNorm statistics kernel,
+// built with packed-FP32 forms, giving different results run to run beside a
+// bare loop of v_mfma_f32_16x16x32_bf16 / _f16 (register operands only, no
+// memory traffic) and never beside v_mfma_f32_16x16x4f32, nor when built
+// without the packed forms.  Here each victim kernel runs one packed-FP32
+// instruction form (inline asm, so the form is exactly the one named) in a
+// dependent chain over per-lane inputs, and every rep's output is compared
+// bit for bit with the first rep's (run alone).  The victims' arithmetic is a
+// pure function of the inputs: any difference is an execution fault.
+//
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/native/pk_hazard.hip -o tools/native/pk_hazard
+// Run:   pk_hazard REPS BG   (BG: 0 none, 1 bf16 MFMA loop, 2 f16, 3 f32)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));         \
+            exit(2);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// the forms: 0 v_pk_add_f32 (plain), 1 v_pk_add_f32 op_sel:[0,1] op_sel_hi:[1,0]
+// (the GN partial's cross-half accumulate), 2 v_pk_add_f32 op_sel_hi:[1,0]
+// neg_lo:[0,1] neg_hi:[0,1] (its broadcast subtract), 3 v_pk_mul_f32 (plain),
+// 4 v_pk_fma_f32 (plain), 5 scalar v_add_f32 pair (control)
+constexpr int NFORMS = 6;
+
+template <int F>
+__global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *__restrict__ out, int iters) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    f2 a = in[i], b = in[i + gridDim.x * 256];
+    const f2 c = f2{0.9990234375f, 1.0009765625f};
+    for (int k = 0; k < iters; ++k) {
+        if constexpr (F == 0) {
+            asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+        } else if constexpr (F == 1) {
+            asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "+v"(a) : "v"(b));
+        } else if constexpr (F == 2) {
+            f2 d;
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+            a = d;
+        } else if constexpr (F == 3) {
+            asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a) : "v"(c));
+        } else if constexpr (F == 4) {
+            asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(a) : "v"(c), "v"(b));
+        } else {
+            float x = a.x, y = a.y;
+            asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(b.y));
+            asm volatile("v_add_f32 %0, %0, %1" : "+v"(y) : "v"(b.x));
+            a = f2{x, y};
+        }
+        // b drifts so the chain is not periodic; scalar multiplies (inline asm,
+        // so no packed form appears outside the one under test)
+        float bx = b.x, by = b.y;
+        asm volatile("v_mul_f32 %0, %0, %1" : "+v"(bx) : "v"(c.x));
+        asm volatile("v_mul_f32 %0, %0, %1" : "+v"(by) : "v"(c.y));
+        b = f2{bx, by};
+    }
+    out[i] = a;
+}
+
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int KIND>
+__global__ __launch_bounds__(256) void k_bg_mfma(float *out, int iters) {
+    f4v acc[4] = {};
+    const float s = threadIdx.x * 1e-3f;
+    b8v ba, bb;
+    h8v ha, hb;
+    for (int e = 0; e < 8; ++e) {
+        ba[e] = (__bf16)(s + e);
+        bb[e] = (__bf16)(1.f - s);
+        ha[e] = (_Float16)(s + e);
+        hb[e] = (_Float16)(1.f - s);
+    }
+    for (int i = 0; i < iters; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr (KIND == 1) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba, bb, acc[q], 0, 0, 0);
+            else if constexpr (KIND == 2) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[q], 0, 0, 0);
+            else acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(s, s + 1.f, acc[q], 0, 0, 0);
+        }
+    float t = 0.f;
+    for (int q = 0; q < 4; ++q) t += acc[q][0] + acc[q][3];
+    if (t == 12345.f) out[threadIdx.x] = t;  // keep the loop
+}
+
+template <int F>
+static void launch(const f2 *in, f2 *out, int blocks, int iters, hipStream_t s) {
+    hipLaunchKernelGGL(k_victim<F>, dim3(blocks), dim3(256), 0, s, in, out, iters);
+}
+static void launch_form(int f, const f2 *in, f2 *out, int blocks, int iters, hipStream_t s) {
+    switch (f) {
+        case 0: launch<0>(in, out, blocks, iters, s); break;
+        case 1: launch<1>(in, out, blocks, iters, s); break;
+        case 2: launch<2>(in, out, blocks, iters, s); break;
+        case 3: launch<3>(in, out, blocks, iters, s); break;
+        case 4: launch<4>(in, out, blocks, iters, s); break;
+        default: launch<5>(in, out, blocks, iters, s); break;
+    }
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    const int bg = argc > 2 ? atoi(argv[2]) : 1;
+    const int blocks = 512, iters = 256, n = blocks * 256;
+    std::vector<f2> hin(2 * n);
+    unsigned s = 777u;
+    for (auto &v : hin) {
+        s = s * 1664525u + 1013904223u;
+        const float a = ((s >> 8) & 0xffff) / 65536.0f - 0.5f;
+        s = s * 1664525u + 1013904223u;
+        const float b = ((s >> 8) & 0xffff) / 65536.0f - 0.5f;
+        v = f2{a, b};
+    }
+    f2 *in, *out;
+    float *bgout;
+    CK(hipMalloc(&in, 2 * n * sizeof(f2)));
+    CK(hipMalloc(&out, n * sizeof(f2)));
+    CK(hipMalloc(&bgout, 4096));
+    CK(hipMemcpy(in, hin.data(), 2 * n * sizeof(f2), hipMemcpyHostToDevice));
+    hipStream_t sa, sb;
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    std::vector<f2> ref(n), got(n);
+    printf("{\"reps\": %d, \"background\": %d", reps, bg);
+    for (int f = 0; f < NFORMS; ++f) {
+        int bad = 0, lanes_hi = 0, lanes_lo = 0;
+        for (int r = 0; r <= reps; ++r) {
+            if (r > 0 && bg == 1) hipLaunchKernelGGL(k_bg_mfma<1>, dim3(2048), dim3(256), 0, sb, bgout, 400 + 37 * (r % 5));
+            if (r > 0 && bg == 2) hipLaunchKernelGGL(k_bg_mfma<2>, dim3(2048), dim3(256), 0, sb, bgout, 400 + 37 * (r % 5));
+            if (r > 0 && bg == 3) hipLaunchKernelGGL(k_bg_mfma<3>, dim3(2048), dim3(256), 0, sb, bgout, 400 + 37 * (r % 5));
+            launch_form(f, in, out, blocks, iters, sa);
+            CK(hipGetLastError());
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(r == 0 ? ref.data() : got.data(), out, n * sizeof(f2), hipMemcpyDeviceToHost));
+            if (r == 0) continue;
+            if (memcmp(ref.data(), got.data(), n * sizeof(f2))) {
+                ++bad;
+                const unsigned *ru = reinterpret_cast<const unsigned *>(ref.data());
+                const unsigned *gu = reinterpret_cast<const unsigned *>(got.data());
+                for (int i = 0; i < n; ++i) {
+                    lanes_lo += ru[2 * i] != gu[2 * i];
+                    lanes_hi += ru[2 * i + 1] != gu[2 * i + 1];
+                }
+            }
+        }
+        printf(", \"form%d\": {\"reps_differing\": %d, \"lo_values_differing\": %d, \"hi_values_differing\": %d}", f, bad,
+               lanes_lo, lanes_hi);
+    }
+    printf("}\n");
+    return 0;
+}
