@@ -37,23 +37,19 @@ def _flags():
 HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mfma"]}
 
 # model_ops.hip (GroupNorm, RPN, ROIAlign, box / mask / keypoint post-processing)
-# is compiled without the packed FP32 VALU instructions (v_pk_add/mul/fma_f32,
-# which the compiler forms with op_sel / neg source modifiers): with them the
-# fp16 pipelined loop -- two model forwards on different hardware queues --
-# gave outputs different from the serial step in 133 of 150 steps, without
-# them in 0 of 150 (tools/determinism.py over the same tree, the build the
-# only variable: profiles/r03_determinism_packed_fp32.json).  Round 4 put the
-# first difference in k_gn_partial's partial sums (tools/dbg_race.py,
-# tools/gn_emulate.py: the serial result equals a CPU restatement of the
-# packed instruction sequence bit for bit, the pipelined one departs in whole
-# workgroups, channels 128-255) while its inputs and every workspace byte it
-# reads are the same in every rep; the isolated kernels never reproduce it
-# (tools/native/gn_repro.hip).  The cause is therefore not shown; this flag is
-# the workaround in force ("Item 6"), not a proof that
-# no race exists.  conv.hip and inpaint.hip, once built the same way, are
-# built with the packed forms again (0 of 150 mismatches in fp16 and fp32).
-# The target-feature switch reaches the host compile too, where clang ignores
-# it with a warning.
+# is compiled without the packed FP32 VALU instructions.  Round 4 found why
+# ("Item 6"): the form v_pk_add_f32 vD, vA, vB
+# op_sel:[0,1] op_sel_hi:[1,0] (low result = A.lo + B.hi), which the compiler
+# forms from two-lane vector code in GroupNorm / ROIAlign / upsample, returns
+# wrong low halves on gfx950 while other waves on the CU issue bf16 / f16
+# MFMAs (tools/native/pk_hazard.hip: 200 / 200 reps beside a register-only
+# bf16 MFMA loop, never alone or beside f32 MFMAs; the plain, broadcast,
+# multiply and FMA packed forms never fault).  With the forms, the fp16
+# pipelined loop differed from the serial step in 133 of 150 steps.
+# conv.hip and inpaint.hip keep the packed forms: they contain no op_sel
+# variant, which tools/isa_lint.py checks on the built library
+# (tests/test_isa_lint.py).  The target-feature switch reaches the host
+# compile too, where clang ignores it with a warning.
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32}
 
