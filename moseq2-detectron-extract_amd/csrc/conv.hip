@@ -595,7 +595,7 @@ __device__ __forceinline__ int x3_swz(int r) { return ((r >> 3) & 1) << 1; }
 // plane products of all six pairs summed in one accumulator set -- three
 // workgroups per CU instead of two; two barriers per K-step (as k_conv_sb).
 template <typename TO, int BN_, int NP, bool BP = false, bool PW = false, bool SB = false>
-__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? (SB ? 3 : 2) : (SB ? 2 : 1)) void k_conv_x3(ConvArgs a) {
+__global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? (SB ? 3 : 2) : 1) void k_conv_x3(ConvArgs a) {
     static_assert(NP == 6 || NP == 9, "x6 or x9 plane products");
     constexpr int BK = 32, VEC = 4;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -2176,18 +2176,13 @@ static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
         a.bsw = a.bsw / 4 * 6;
         a.w = t_x3_wplanes;
         a.wbytes = a.Cout * a.K * 6;
-        if (g_x3_sb) {
-            // one LDS stage: the stage or the epilogue image (the 128-wide
-            // tile -- mdx_conv_set_x3_narrow(0) -- at two workgroups per CU)
+        if (bn == 64 && g_x3_sb) {
+            // one LDS stage: the stage or the epilogue image
             const size_t lds1 = stage > lds_epi ? stage : lds_epi;
-            if (bn == 64 && pw)
+            if (pw)
                 hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, true, true>), grid, dim3(CONV_THREADS), lds1, s, a);
-            else if (bn == 64)
-                hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, false, true>), grid, dim3(CONV_THREADS), lds1, s, a);
-            else if (pw)
-                hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true, true, true>), grid, dim3(CONV_THREADS), lds1, s, a);
             else
-                hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true, false, true>), grid, dim3(CONV_THREADS), lds1, s, a);
+                hipLaunchKernelGGL((k_conv_x3<float, 64, 6, true, false, true>), grid, dim3(CONV_THREADS), lds1, s, a);
             return;
         }
         if (bn == 64 && pw)
