@@ -49,10 +49,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # HIP hardware queues: at least 8 (HIP's default is 4), set before the runtime
-# initialises, so that the loop's streams -- H2D, front, three model forwards,
+# initialises, so that the loop's streams -- H2D, front, four model forwards,
 # tail, the gather -- each get a queue of their own: with 4 queues a third
-# model stream shares a queue with another stage and lost 2 %, with 8 it gained
-# 2.5 % over two streams (1348 -> 1382 fps, profiles/r03_experiments.json).
+# model stream shared a queue with another stage and lost 2 %, with 8 it gained
+# 2.5 % over two streams (1348 -> 1382 fps, profiles/r03_experiments.json), and
+# a fourth 0.7-1.0 % over three (profiles/r04_experiments.json).
 # Recorded in the line.  (The illegal-address faults once seen with 8 queues
 # and three model streams were the inpaint set-up race, fixed: DESIGN.md §3.)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
@@ -93,7 +94,7 @@ def parse():
     ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_conv_set_winograd_min_cin")
     ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT[,INT]",
                     help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
-    ap.add_argument("--model-streams", type=int, default=3,
+    ap.add_argument("--model-streams", type=int, default=4,
                     help="forwards in flight at once (one HIP stream each)")
     ap.add_argument("--chunk-batches", type=int, default=8,
                     help="batches per chunk in the default loop (the chunk's forwards alternate over the streams)")
