@@ -55,12 +55,12 @@ class ExtractConfig:
     mask_iou_threshold: float = 0.5
     fix_invalid_pixels: bool = True
     use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
-    # forwards of consecutive batches in flight within a chunk: 3, as in the
-    # hot loop (config-3 loop, 6000 frames: 1293 / 1313 frames/s against
-    # 1266 / 1293 with 2, tracking off / on; profiles/r04_experiments.json);
-    # give the process GPU_MAX_HW_QUEUES=8 (bench.py does) so each forward
-    # gets a hardware queue of its own
-    model_streams: int = 3
+    # forwards of consecutive batches in flight within a chunk: 4, as in the
+    # hot loop (config-3 loop, 6000 frames, tracking off / on: 2 streams 1266 /
+    # 1293 frames/s, 3 streams 1293 / 1313 and 1294 / 1314, 4 streams 1315 /
+    # 1332; profiles/r04_experiments.json); give the process
+    # GPU_MAX_HW_QUEUES=8 (bench.py does) so each forward gets a hardware queue
+    model_streams: int = 4
     overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
