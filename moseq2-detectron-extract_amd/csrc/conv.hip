@@ -450,28 +450,17 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
     if constexpr (sizeof(TO) == 4 && !DUAL) {
         if (a.direct) {
             // each lane holds rows 4 (lane >> 4) + r of column lane & 15 of
-            // every 16 x 16 tile: 16 lanes store 64 contiguous bytes per row;
-            // bias, residual and ReLU in finish8's order (NHWC, ksplit 1)
+            // every 16 x 16 tile: 16 lanes store 64 contiguous bytes per row
             float *O = reinterpret_cast<float *>(a.out);
-            const float *RS = reinterpret_cast<const float *>(a.res);
 #pragma unroll
             for (int i = 0; i < TI; ++i)
 #pragma unroll
                 for (int j = 0; j < TJ; ++j) {
                     const int gn = n0 + wn * (BN_ / 2) + j * 16 + (lane & 15);
-                    const bool nok = gn < a.Cout;
-                    const float bv = a.bias && nok ? a.bias[gn] : 0.f;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int gm = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-                        if (gm < a.M && nok) {
-                            const long long oi = (long long)gm * a.Cout + gn;
-                            float x = acc[i][j][r];
-                            if (a.bias) x += bv;
-                            if (RS) x += RS[oi];
-                            if (a.relu) x = x > 0.f ? x : 0.f;
-                            O[oi] = x;
-                        }
+                        if (gm < a.M && gn < a.Cout) O[(long long)gm * a.Cout + gn] = acc[i][j][r];
                     }
                 }
             return;
@@ -2174,15 +2163,6 @@ extern "C" int mdx_conv_set_fp32_split(int mode) {
     return old;
 }
 extern "C" int mdx_conv_fp32_split(void) { return g_fp32_split; }
-// fp32 GEMM epilogue straight from the MFMA register layout (ConvArgs::direct)
-// instead of through LDS: 0 off, 1 the Winograd GEMMs, 2 also the fp32 conv /
-// FC layers on the register-staged kernels (NHWC output, no split-K)
-static int g_direct_epi = 0;
-extern "C" int mdx_conv_set_direct_epilogue(int mode) {
-    const int old = g_direct_epi;
-    g_direct_epi = mode;
-    return old;
-}
 // 64-wide N tile for every split-plane launch (72 KB of LDS and <= 256
 // registers: two workgroups per CU, measured 6-25 % faster per layer than the
 // 128-wide tile's one workgroup per CU, whose single wave per SIMD serialises
@@ -2568,8 +2548,6 @@ general:
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
-    // fp32 layers: the epilogue straight from the MFMA layout (mode 2)
-    a.direct = g_direct_epi >= 2 && in_dtype == 0 && out_dtype == 0 && out_mode == 0 && a.ksplit == 1;
     const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
     // (mode 3: the fp16 register-staged PW layers too; the fp16 model's big
     // layers stay on the LDS-DMA kernels)
@@ -2834,6 +2812,14 @@ extern "C" int mdx_winograd_tile(int H, int W, int mode) {
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
+// Winograd GEMMs (f32 MFMA kernels) store their raw accumulators straight
+// from registers (ConvArgs::direct) instead of through the LDS epilogue
+static int g_wino_direct = 0;
+extern "C" int mdx_conv_set_wino_direct(int on) {
+    const int old = g_wino_direct;
+    g_wino_direct = on;
+    return old;
+}
 
 // the model packs Winograd weight planes (and so runs the split-plane
 // Winograd GEMMs on k_gemm_x6) only when MDX_WINO_X6 is set: the split-plane
@@ -2919,7 +2905,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     int gemm_kernel;
     // NB GEMMs M[xi] (T x Cout) = V[xi] (T x Cin) U[xi]^T in one launch (grid.z)
     ConvArgs a{};
-    a.direct = g_direct_epi >= 1;
+    a.direct = g_wino_direct;
     a.x = V; a.w = U; a.bias = nullptr; a.res = nullptr; a.out = Mx;
     a.H = (int)T; a.W = 1; a.Cin = Cin; a.Cout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
     a.OH = (int)T; a.OW = 1; a.M = (int)T; a.K = Cin; a.relu = 0; a.out_mode = 0;

@@ -876,7 +876,7 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
                                            (2, 56, 64, 128, 128)])
 def test_conv3x3_winograd_direct_epilogue(mdx, N, H, W, Cin, Cout, m):
     """The Winograd GEMMs' raw accumulators stored straight from the MFMA
-    register layout (mdx_conv_set_direct_epilogue(1)) equal the LDS-epilogue
+    register layout (mdx_conv_set_wino_direct(1)) equal the LDS-epilogue
     stores bit for bit, ragged tiles included."""
     from moseq2_detectron_extract_amd._lib import call
     import ctypes
@@ -892,49 +892,17 @@ def test_conv3x3_winograd_direct_epilogue(mdx, N, H, W, Cin, Cout, m):
     nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout, m)
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
     outs = []
-    old = call("mdx_conv_set_direct_epilogue", 0)
+    old = call("mdx_conv_set_wino_direct", 0)
     old_s = call("mdx_conv_set_fp32_split", 0)
     try:
         for d in (0, 1):
-            call("mdx_conv_set_direct_epilogue", d)
+            call("mdx_conv_set_wino_direct", d)
             out = torch.empty(N, H, W, Cout, device="cuda")
             call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, 1, m, P(out), P(ws), nb, None)
             torch.cuda.synchronize()
             outs.append(out)
     finally:
-        call("mdx_conv_set_direct_epilogue", old)
-        call("mdx_conv_set_fp32_split", old_s)
-    assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_fp32_direct_epilogue(mdx, case):
-    """fp32 conv layers with the epilogue straight from the MFMA layout
-    (mdx_conv_set_direct_epilogue(2): bias, residual and ReLU applied per
-    element in the LDS epilogue's order) equal the LDS epilogue bit for bit."""
-    from moseq2_detectron_extract_amd._lib import call
-    import ctypes
-    N, H, W, Cin, Cout, k, s, p, res, relu = case
-    g = torch.Generator().manual_seed(sum(case[:8]))
-    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    x = torch.randn(N, H, W, Cin, generator=g).cuda()
-    w = (torch.randn(Cout, k, k, Cin, generator=g) / (k * k * Cin) ** 0.5).cuda()
-    b = torch.randn(Cout, generator=g).cuda()
-    r = torch.randn(N, OH, OW, Cout, generator=g).cuda() if res else None
-    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-    outs = []
-    old = call("mdx_conv_set_direct_epilogue", 0)
-    old_s = call("mdx_conv_set_fp32_split", 0)
-    try:
-        for d in (0, 2):
-            call("mdx_conv_set_direct_epilogue", d)
-            out = torch.empty(N, OH, OW, Cout, device="cuda")
-            call("mdx_conv2d", P(x), N, H, W, Cin, P(w), P(b), Cout, k, k, s, p, P(r), int(relu), 0, 0, 0, P(out),
-                 None)
-            torch.cuda.synchronize()
-            outs.append(out)
-    finally:
-        call("mdx_conv_set_direct_epilogue", old)
+        call("mdx_conv_set_wino_direct", old)
         call("mdx_conv_set_fp32_split", old_s)
     assert torch.equal(outs[0], outs[1])
 
