@@ -273,10 +273,6 @@ int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const flo
  * LDS-DMA plane kernel (k_gemm_x6); outside split mode, or with Cin % 16 != 0,
  * as mdx_conv3x3_winograd.  Model handles use it only with MDX_WINO_X6 set in
  * the environment (4 % slower end to end than k_conv_x3 on every layer). */
-/* Winograd GEMMs on the f32 MFMA kernels: 1 stores the raw accumulators
- * straight from the MFMA register layout, 0 (default) through the LDS
- * epilogue.  Returns the old value. */
-int mdx_conv_set_wino_direct(int on);
 /* Split-plane launches with pre-split weights (model handles in mode 6) on
  * the single-stage k_conv_x3 (one LDS stage, one accumulator set, three
  * workgroups per CU): 1 (default) or 0 (two LDS stages, separate hi*hi and

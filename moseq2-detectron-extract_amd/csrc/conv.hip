@@ -96,9 +96,6 @@ struct ConvArgs {
     // projection shortcut concatenated onto its conv3 GEMM)
     const void *x2;
     int K1, H2, W2, Cin2, stride2, x2bytes;
-    // raw fp32 GEMM output (no bias / residual / ReLU, ksplit 1: the Winograd
-    // GEMMs): accumulators stored straight from the MFMA layout, no LDS pass
-    int direct;
 };
 
 // bias / residual / ReLU on 8 consecutive output channels gn0.. of row gm and
@@ -447,25 +444,6 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
     if (kt < nk) kstep(kt, ra[0], rb[0], ra[1], rb[1]);
     }
 
-    if constexpr (sizeof(TO) == 4 && !DUAL) {
-        if (a.direct) {
-            // each lane holds rows 4 (lane >> 4) + r of column lane & 15 of
-            // every 16 x 16 tile: 16 lanes store 64 contiguous bytes per row
-            float *O = reinterpret_cast<float *>(a.out);
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) {
-                    const int gn = n0 + wn * (BN_ / 2) + j * 16 + (lane & 15);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int gm = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-                        if (gm < a.M && gn < a.Cout) O[(long long)gm * a.Cout + gn] = acc[i][j][r];
-                    }
-                }
-            return;
-        }
-    }
     // ---- epilogue, in two halves of BM/2 rows (the LDS image is half the
     // tile, so a one-step-K launch fits 4 workgroups per CU): the waves owning
     // the half write their accumulators to LDS (fp32, row-major), then all
@@ -2812,15 +2790,6 @@ extern "C" int mdx_winograd_tile(int H, int W, int mode) {
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
 
-// Winograd GEMMs (f32 MFMA kernels) store their raw accumulators straight
-// from registers (ConvArgs::direct) instead of through the LDS epilogue
-static int g_wino_direct = 0;
-extern "C" int mdx_conv_set_wino_direct(int on) {
-    const int old = g_wino_direct;
-    g_wino_direct = on;
-    return old;
-}
-
 // the model packs Winograd weight planes (and so runs the split-plane
 // Winograd GEMMs on k_gemm_x6) only when MDX_WINO_X6 is set: the split-plane
 // loop measured 4 % slower with them (1481 / 1494 vs 1543 / 1574 frames/s,
@@ -2905,7 +2874,6 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     int gemm_kernel;
     // NB GEMMs M[xi] (T x Cout) = V[xi] (T x Cin) U[xi]^T in one launch (grid.z)
     ConvArgs a{};
-    a.direct = g_wino_direct;
     a.x = V; a.w = U; a.bias = nullptr; a.res = nullptr; a.out = Mx;
     a.H = (int)T; a.W = 1; a.Cin = Cin; a.Cout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
     a.OH = (int)T; a.OW = 1; a.M = (int)T; a.K = Cin; a.relu = 0; a.out_mode = 0;

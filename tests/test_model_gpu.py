@@ -871,42 +871,6 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     assert err < 1e-4, err
 
 
-@pytest.mark.parametrize("m", [4, 6])
-@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 13, 17, 256, 256), (1, 14, 16, 256, 64), (4, 6, 5, 260, 136),
-                                           (2, 56, 64, 128, 128)])
-def test_conv3x3_winograd_direct_epilogue(mdx, N, H, W, Cin, Cout, m):
-    """The Winograd GEMMs' raw accumulators stored straight from the MFMA
-    register layout (mdx_conv_set_wino_direct(1)) equal the LDS-epilogue
-    stores bit for bit, ragged tiles included."""
-    from moseq2_detectron_extract_amd._lib import call
-    import ctypes
-    g = torch.Generator().manual_seed(N * 100 + H + m)
-    x = torch.randn(N, H, W, Cin, generator=g).clamp_min(0)
-    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
-    b = torch.randn(Cout, generator=g)
-    U = np.empty(((m + 2) ** 2, Cout, Cin), np.float32)
-    wn = np.ascontiguousarray(w.numpy())
-    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, m, U.ctypes.data_as(ctypes.c_void_p))
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    xd, Ud, bd = x.cuda(), torch.from_numpy(U).cuda(), b.cuda()
-    nb = call("mdx_winograd_workspace_bytes", N, H, W, Cin, Cout, m)
-    ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
-    outs = []
-    old = call("mdx_conv_set_wino_direct", 0)
-    old_s = call("mdx_conv_set_fp32_split", 0)
-    try:
-        for d in (0, 1):
-            call("mdx_conv_set_wino_direct", d)
-            out = torch.empty(N, H, W, Cout, device="cuda")
-            call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, 1, m, P(out), P(ws), nb, None)
-            torch.cuda.synchronize()
-            outs.append(out)
-    finally:
-        call("mdx_conv_set_wino_direct", old)
-        call("mdx_conv_set_fp32_split", old_s)
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("N,H,W,Cin,Cout,m", [(8, 112, 128, 256, 256, 6), (16, 56, 64, 128, 128, 4),
                                                (4, 61, 67, 64, 96, 6)])
 def test_conv3x3_winograd_planes(mdx, N, H, W, Cin, Cout, m):
