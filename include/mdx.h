@@ -66,6 +66,12 @@ int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, in
  * the last reset; such a frame is left un-inpainted.  Synchronous (reads a
  * device counter); reset != 0 clears it.  Expected 0: tests assert it. */
 int mdx_inpaint_errors(int reset);
+/* mdx_inpaint_ns that also adds its unconverged frames to the caller's device
+ * counter `errors` (one uint32, stream-ordered): a per-session count that
+ * other users of the library in the same process do not touch.  NULL = the
+ * process-wide counter only. */
+int mdx_inpaint_ns_counted(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
+                           void *workspace, unsigned int *errors, mdx_stream_t stream);
 
 /* scale_raw_frames(frames, vmin, vmax, 'uint8') as a 256-entry LUT built on
  * the host in float64 (M/proc/proc.py:214-234).  int_vmin != 0 reproduces

@@ -46,23 +46,25 @@ HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mf
 # bf16 MFMA loop, never alone or beside f32 MFMAs; the plain, broadcast,
 # multiply and FMA packed forms never fault).  With the forms, the fp16
 # pipelined loop differed from the serial step in 133 of 150 steps.
-# conv.hip and inpaint.hip keep the packed forms: they contain no op_sel
-# variant, which tools/isa_lint.py checks on the built library
-# (tests/test_isa_lint.py).  The target-feature switch reaches the host
-# compile too, where clang ignores it with a warning.
+# conv.hip and inpaint.hip keep the packed forms: every packed instruction
+# they compile to is one of the forms tools/native/pk_hazard.hip cleared
+# beside 16-bit MFMAs, which build() checks on every library it links
+# (_isa_lint.py, a whitelist; the build fails on anything else).  The
+# target-feature switch reaches the host compile too, where clang ignores it
+# with a warning.
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32}
 
 
-def sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+def sources(csrc: str = CSRC):
+    return sorted(glob.glob(os.path.join(csrc, "*.hip")))
 
 
-def _deps_newer(target: str, srcs) -> bool:
+def _deps_newer(target: str, srcs, csrc: str = CSRC) -> bool:
     if not os.path.exists(target):
         return True
     t = os.path.getmtime(target)
-    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(os.path.dirname(HERE), "include", "*.h"))
+    hdrs = glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(os.path.dirname(HERE), "include", "*.h"))
     return any(os.path.getmtime(s) > t for s in list(srcs) + hdrs)
 
 
@@ -79,16 +81,20 @@ def _flags_changed(obj: str, flags: list) -> bool:
         return True
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, jobs: int = 8, csrc: str = CSRC, obj: str = OBJ,
+          lib: str = LIB) -> str:
+    """Compile every csrc/*.hip for gfx950, link `lib`, then refuse it (delete
+    and raise) if it has undefined symbols of its own or any packed
+    instruction outside the whitelist of cleared forms (_isa_lint)."""
+    os.makedirs(obj, exist_ok=True)
     cc = hipcc()
-    srcs = sources()
+    srcs = sources(csrc)
     objs = []
     todo = []
     for s in srcs:
-        o = os.path.join(OBJ, os.path.basename(s)[:-4] + ".o")
+        o = os.path.join(obj, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
-        if force or _deps_newer(o, [s]) or _flags_changed(o, _cmd_flags(os.path.basename(s))):
+        if force or _deps_newer(o, [s], csrc) or _flags_changed(o, _cmd_flags(os.path.basename(s))):
             todo.append((s, o))
 
     def comp(so):
@@ -107,29 +113,50 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
             list(ex.map(comp, todo))
-    if force or todo or _deps_newer(LIB, objs):
-        cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+    if force or todo or _deps_newer(lib, objs, csrc):
+        cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"link of libmdx.so failed:\n{r.stderr[-6000:]}")
-        check_symbols()
-    return LIB
+            raise RuntimeError(f"link of {os.path.basename(lib)} failed:\n{r.stderr[-6000:]}")
+        check_symbols(lib)
+        check_isa(lib)
+    return lib
 
 
-def check_symbols() -> None:
+def check_symbols(lib: str = LIB) -> None:
     """A shared link does not reject undefined symbols; a kernel whose host
     stub was not emitted only fails at dlopen on the GPU box.  Refuse the
     library here instead."""
     nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
-    r = subprocess.run([nm, "-u", "-C", LIB], capture_output=True, text=True)
+    r = subprocess.run([nm, "-u", "-C", lib], capture_output=True, text=True)
     if r.returncode != 0:
         return
     bad = [ln.strip() for ln in r.stdout.splitlines() if "mdx::" in ln]
     if bad:
-        os.remove(LIB)
-        raise RuntimeError("libmdx.so has undefined symbols of its own:\n" + "\n".join(bad[:20]))
+        os.remove(lib)
+        raise RuntimeError(f"{os.path.basename(lib)} has undefined symbols of its own:\n" + "\n".join(bad[:20]))
+
+
+def check_isa(lib: str = LIB) -> None:
+    """The packed-instruction whitelist (_isa_lint.py) on the linked
+    library's device code: a form pk_hazard.hip has not cleared beside 16-bit
+    MFMAs deletes the library and fails the build, so it never reaches the
+    GPU box."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mdx_isa_lint", os.path.join(HERE, "_isa_lint.py"))
+    lint = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lint)
+    if not lint.available():
+        raise RuntimeError("ROCm LLVM tools (llvm-objcopy, clang-offload-bundler, llvm-objdump) absent: "
+                           "cannot check the library's packed instruction forms")
+    hits = lint.scan(lib)
+    if hits:
+        os.remove(lib)
+        raise RuntimeError(f"{os.path.basename(lib)}: {len(hits)} packed instruction(s) outside the forms "
+                           "cleared by tools/native/pk_hazard.hip (_isa_lint.CLEARED), e.g.\n" +
+                           "\n".join(f"  {s}: {i}" for s, i in hits[:10]))
 
 
 if __name__ == "__main__":

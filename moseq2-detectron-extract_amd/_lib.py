@@ -35,6 +35,7 @@ SIGNATURES = {
     "mdx_inpaint_workspace_bytes": (I64, [I64, I32, I32]),
     "mdx_inpaint_ns": (I32, [P, P, I64, I32, I32, I32, P, P]),
     "mdx_inpaint_errors": (I32, [I32]),
+    "mdx_inpaint_ns_counted": (I32, [P, P, I64, I32, I32, I32, P, P, P]),
     "mdx_build_scale_lut": (I32, [F64, F64, I32, P]),
     "mdx_scale_frames": (I32, [P, I64, P, P, P]),
     "mdx_clean_workspace_bytes": (I64, [I64, I32, I32]),

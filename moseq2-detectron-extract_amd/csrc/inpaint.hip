@@ -233,7 +233,8 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_compact(const uint8_t
 __device__ unsigned int g_inp_errors = 0;
 
 __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *__restrict__ invalid, int H, int W,
-                                                                 int range, int *__restrict__ ws, InpLayout L) {
+                                                                 int range, int *__restrict__ ws, InpLayout L,
+                                                                 unsigned int *__restrict__ errors) {
     __shared__ int sh[INP_SETUP_THREADS];
     __shared__ int s_flag[2], s_bad;
     const int tid = threadIdx.x;
@@ -325,6 +326,7 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(const uint8_t *
             if (tid == 0) {
                 hdr[0] = hdr[1] = 0;
                 atomicAdd(&g_inp_errors, 1u);
+                if (errors) atomicAdd(errors, 1u);  // the caller's own count (mdx_inpaint_ns_counted)
             }
             return;
         }
@@ -552,8 +554,8 @@ extern "C" int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W) {
     return n * inp_layout(H, W).total * 4;
 }
 
-extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
-                              void *workspace, mdx_stream_t stream) {
+extern "C" int mdx_inpaint_ns_counted(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
+                                      void *workspace, unsigned int *errors, mdx_stream_t stream) {
     MDX_REQUIRE(frames && invalid, "mdx_inpaint_ns: null frames/invalid");
     MDX_REQUIRE(radius >= 0 && radius <= 7, "mdx_inpaint_ns: radius must be in [0, 7] (got %d)", radius);
     MDX_REQUIRE(H > 0 && W > 0, "mdx_inpaint_ns: bad shape");
@@ -571,9 +573,14 @@ extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n
     hipLaunchKernelGGL(k_inp_compact, dim3(L.nch, (unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W,
                        (int *)workspace, L);
     hipLaunchKernelGGL(k_inp_setup, dim3((unsigned)n), dim3(INP_SETUP_THREADS), 0, s, invalid, H, W, radius,
-                       (int *)workspace, L);
+                       (int *)workspace, L, errors);
     hipLaunchKernelGGL(k_inp_march, dim3(INP_MARCH_BLOCKS, (unsigned)n), dim3(64 * MARCH_WAVES), 0, s, frames, H, W,
                        radius, (int *)workspace, L);
     MDX_CHECK_LAUNCH("mdx_inpaint_ns");
     return MDX_OK;
+}
+
+extern "C" int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
+                              void *workspace, mdx_stream_t stream) {
+    return mdx_inpaint_ns_counted(frames, invalid, n, H, W, radius, workspace, nullptr, stream);
 }

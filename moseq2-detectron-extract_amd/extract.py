@@ -3,11 +3,21 @@ without its control plane): frame source -> GPUExtractor.process_chunk per
 chunk -> results in the writer's layout (M/io/result.py:106-130), optionally
 restricted to this rank's chunk-aligned shard.
 
-With tracking on and more than one rank the chunk loop runs in two device
-passes around the exchange step (shard.tracking_exchange): pass 1 keeps each
-chunk's prepped / mask / cleaned frames resident in HBM (3 x 216 KB per frame:
-a 1M-frame session over 8 GPUs holds ~81 GB per GPU, well inside 288 GB) and
-ships its feature records to rank 0; pass 2 crops at the tracked values.
+Sharded sessions (world > 1).  Each rank runs its contiguous block of whole
+chunks.  With tracking or instance selection on (the reference's defaults)
+the chunk loop runs in two device passes around the exchange step
+(shard.instance_exchange / tracking_exchange): pass 1 runs the whole hot path
+per chunk and keeps only a compact host record per frame (the kept
+detections' mask logits and boxes, keypoints, keep indices: ~13 KB per
+frame; GPUExtractor.features_pass_compact), so device memory stays one
+chunk's working set however long the shard is; pass 2 re-runs each chunk's
+front (prep + inpaint + clean, a few % of the forward) from its raw frames,
+re-pastes the selected masks and crops at the exchanged pose.  The ranks'
+finished chunks are gathered to rank 0 round by round over the process group
+(shard.gather_chunk_results: RCCL over xGMI for nccl), where one writer fills
+the session's single results_00 file and keypoints TSV -- the files one
+process writes, byte for byte (ResultWriterStep's single writer,
+M/pipeline/write_results_step.py:31-36).
 
 The h5 writer itself is not rebuilt (h5py is absent from this image); the
 results are returned as arrays keyed like the h5 datasets and can be saved as
@@ -22,10 +32,10 @@ from typing import Dict, Optional
 import numpy as np
 
 from .pipeline import ExtractConfig, GPUExtractor
-from .results import (KeypointsTSVWriter, MemoryH5, check_completion_status, create_extract_h5, open_results,
-                      status_filename, write_extracted_chunk_to_h5, write_status)
+from .results import (KeypointsTSVWriter, MemoryH5, check_completion_status, create_extract_h5, join_tsv_parts,
+                      open_results, status_filename, write_extracted_chunk_to_h5, write_status)
 from .session import RawDepthSource
-from .shard import instance_exchange, pass_tail_forward, tracking_exchange
+from .shard import gather_chunk_results, instance_exchange, pass_tail_forward, tracking_exchange
 
 
 def shard_chunk_range(nchunks: int, world: int, rank: int):
@@ -44,12 +54,13 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     """Extract every chunk of the session (or of this rank's shard).  Returns
     {'frames': uint8 (n,80,80), 'frames_mask': uint8 (n,80,80),
     'scalars/<name>': (n,), 'keypoints/<name>': (n,), 'flips': bool (n,),
-    'frame_idxs': (n,)} in frame order."""
+    'frame_idxs': (n,)} in frame order, this rank's frames.  With
+    `output_dir` the session's results_00 file, keypoints_00.tsv and status
+    file are written there once (by rank 0 of a sharded session)."""
     status_path = None
     if output_dir:  # status file first, as M/extract.py:47-62 (skip a completed session)
-        out_dir = output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}")
-        os.makedirs(out_dir, exist_ok=True)
-        status_path = status_filename(out_dir)
+        os.makedirs(output_dir, exist_ok=True)
+        status_path = status_filename(output_dir)
         done = skip_completed and check_completion_status(status_path)
         if world > 1:  # every rank must agree, or a skipping rank would leave the others in the exchange
             done = _all_ranks(done)
@@ -58,17 +69,24 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         status = status or {"complete": False, "skip": False, "uuid": str(uuid.uuid4()),
                             "metadata": _load_metadata(path), "parameters": dict(vars(config))}
         status["complete"] = False
-        write_status(status_path, status)
+        if rank == 0:
+            write_status(status_path, status)
     src = RawDepthSource(path, frame_trim=frame_trim)
     ex = GPUExtractor(bground_im, roi, predictor, config)
     batches = src.batches(config.chunk_size, config.chunk_overlap)
+    nrounds = len(batches)
     if world > 1:  # contiguous block of whole chunks per rank, as shard.shard_chunks deals them
         c0, c1 = shard_chunk_range(len(batches), world, rank)
+        nrounds = len(range(*shard_chunk_range(len(batches), world, 0)))  # rank 0 owns the most chunks
         batches = batches[c0:c1]
     # the results file and keypoints TSV are written chunk by chunk as chunks
-    # finish (ResultWriterStep, its own process in the reference)
-    writer = _ChunkWriter(output_dir if world == 1 else os.path.join(output_dir, f"rank{rank}"), src, bground_im,
-                          roi, true_depth, config, first_frame, status) if output_dir else None
+    # finish (ResultWriterStep, its own process in the reference): one writer,
+    # on rank 0, fed by the result gather when the session is sharded
+    writer = None
+    if output_dir:
+        local = _ChunkWriter(output_dir, src, bground_im, roi, true_depth, config, first_frame, status,
+                             parts=world) if rank == 0 else None
+        writer = local if world == 1 else _GatherWriter(local, nrounds)
 
     def finished(d):
         if writer is not None:
@@ -81,20 +99,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     ok = False
     try:
         if exchange:
-            states = []
-            for idx, raw in src.iterate(device=True, batches=batches):
-                st, host = ex.features_pass(raw)
-                states.append((np.asarray(idx), st, host))
-            if config.select_instances:  # the instance tracker is sequential over the session too
-                _select_exchange(ex, states)
-            if config.use_tracking:
-                tracked = tracking_exchange([h for _, _, h in states], ex.point_tracker, ex.angle_tracker)
-            else:  # per-chunk angle filtering: no sequential state across chunks
-                tracked = [ex.host_angles(h) for _, _, h in states]
-            for (idx, st, host), (cen, kp, ang, fl) in zip(states, tracked):
-                parts.append(finished(ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0,
-                                                      true_depth)))
-            states.clear()
+            parts = _run_two_pass(src, batches, ex, config, true_depth, finished)
         elif config.overlap_host:
             parts = _run_overlapped(src, batches, ex, true_depth, finished)
         else:
@@ -109,8 +114,11 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
             else:  # the extraction's own exception propagates; the results file is left unfinished
                 writer.abort()
     if output_dir:
-        status["complete"] = True  # M/extract.py:129-131
-        write_status(status_path, status)
+        if rank == 0:
+            status["complete"] = True  # M/extract.py:129-131
+            write_status(status_path, status)
+        if world > 1:  # no rank returns before the status file says complete
+            _all_ranks(True)
     out: Dict[str, np.ndarray] = {}
     if not parts:
         return out
@@ -125,6 +133,38 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     if out_npz:
         np.savez_compressed(out_npz, **out)
     return out
+
+
+def _run_two_pass(src, batches, ex, config, true_depth, finished):
+    """The sharded session's chunk loop around the exchange step.  Pass 1:
+    each chunk's hot path up to the host step, kept as a compact host record
+    (GPUExtractor.features_pass_compact; the chunk's device frames are
+    released).  Exchanges: the instance tracker's picks (instance_exchange +
+    the tail hand-off, changed frames' moments recomputed), then the Kalman
+    tracking (tracking_exchange).  Pass 2: each chunk's front again from its
+    raw frames, the selected masks re-pasted, crops at the exchanged pose."""
+    comps = []
+    for idx, raw in src.iterate(device=True, batches=batches):
+        comp, host = ex.features_pass_compact(raw)
+        comps.append((np.asarray(idx), comp, host))
+    if config.select_instances:  # the instance tracker is sequential over the session too
+        _select_exchange_compact(ex, comps, src)
+    else:
+        for _, comp, host in comps:
+            ex.apply_selection_compact(comp, host, {}, 0, {}, None)
+    if config.use_tracking:
+        tracked = tracking_exchange([h for _, _, h in comps], ex.point_tracker, ex.angle_tracker)
+    else:  # per-chunk angle filtering: no sequential state across chunks
+        tracked = [ex.host_angles(h) for _, _, h in comps]
+    parts = []
+    for (idx, comp, host), (cen, kp, ang, fl), (idx2, raw) in zip(comps, tracked,
+                                                                 src.iterate(device=True, batches=batches)):
+        if not np.array_equal(np.asarray(idx2), idx):
+            raise RuntimeError("second pass: the frame source returned another chunk")
+        parts.append(finished(ex.finish_chunk_compact(comp, raw, cen, kp, ang, fl, host["axis_length"], idx, 0,
+                                                      true_depth)))
+    comps.clear()
+    return parts
 
 
 def _all_ranks(flag: bool) -> bool:
@@ -157,7 +197,7 @@ class _ChunkWriter:
     which fills the datasets, deflates the completed crop rows and appends
     the TSV; close() drains it and finishes the file."""
 
-    def __init__(self, output_dir, src, bground_im, roi, true_depth, config, first_frame, status):
+    def __init__(self, output_dir, src, bground_im, roi, true_depth, config, first_frame, status, parts: int = 1):
         os.makedirs(output_dir, exist_ok=True)
         ts_file = os.path.join(os.path.dirname(os.path.abspath(src.path)), "depth_ts.txt")
         nframes = src.last_frame_idx
@@ -169,6 +209,11 @@ class _ChunkWriter:
                             "metadata": {}}
         self.h5 = open_results(output_dir)
         self.tsv = KeypointsTSVWriter(output_dir)
+        # a sharded session's TSV: one headerless part per rank, joined in
+        # rank (= session) order at close
+        self.tsv_parts = [KeypointsTSVWriter(output_dir, path=f"{self.tsv.path}.part{r}", header=False)
+                          for r in range(parts)] if parts > 1 else None
+        self._cols = None
         create_extract_h5(self.h5, cfg, status)
         import queue
         import threading
@@ -184,25 +229,33 @@ class _ChunkWriter:
                 return
             if self._err:  # keep draining after an error so write() / close() never block
                 continue
+            d, part = d
             try:
                 write_extracted_chunk_to_h5(self.h5, d)
-                self.tsv.write(d)
+                if self.tsv_parts is None:
+                    self.tsv.write(d)
+                else:
+                    if self._cols is None:
+                        self._cols = list(KeypointsTSVWriter.columns(d))
+                    self.tsv_parts[part].write(d)
             except BaseException as e:  # surfaced by write() / close()
                 self._err.append(e)
 
-    def write(self, d: dict) -> None:
+    def write(self, d: dict, part: int = 0) -> None:
         if self._err:
             raise self._err[0]
         f = d["features"]
-        self._q.put({"frame_idxs": d["frame_idxs"], "offset": d["offset"], "scalars": d["scalars"],
-                     "keypoints": d["keypoints"], "depth_frames": d["depth_frames"], "mask_frames": d["mask_frames"],
-                     "features": {"flips": f["flips"], "features": f["features"]}})
+        self._q.put(({"frame_idxs": d["frame_idxs"], "offset": d["offset"], "scalars": d["scalars"],
+                      "keypoints": d["keypoints"], "depth_frames": d["depth_frames"], "mask_frames": d["mask_frames"],
+                      "features": {"flips": f["flips"], "features": f["features"]}}, part))
 
     def close(self) -> None:
         self._q.put(None)
         self._t.join()
         if self._err:
             raise self._err[0]
+        if self.tsv_parts is not None and self._cols is not None:
+            join_tsv_parts(self.tsv.path, self._cols, [w.path for w in self.tsv_parts])
         self.h5.close()
 
     def abort(self) -> None:
@@ -222,32 +275,68 @@ class _ChunkWriter:
                 pass
 
 
-def _select_exchange(ex, states):
+def _select_exchange_compact(ex, comps, src):
     """Instance selection of a sharded session: rank 0 runs the tracker over
     every rank's frames in session order (shard.instance_exchange); each rank
-    gathers its picks, taking a pick at its shard's start from the preceding
-    rank's last frames (shard.pass_tail_forward)."""
+    applies its picks to its compact chunk records, taking a pick at its
+    shard's start from the preceding rank's last frames
+    (shard.pass_tail_forward, compact logit records)."""
     import torch.distributed as dist
     tracker = ex.instance_tracker if dist.get_rank() == 0 else None
-    off, changes = instance_exchange([h for _, _, h in states], [st["nkeep"] for _, st, _ in states], tracker)
+    off, changes = instance_exchange([h for _, _, h in comps], [c["nkeep"] for _, c, _ in comps], tracker)
     f0s, f = [], off
-    for _, st, _ in states:
+    for _, c, _ in comps:
         f0s.append(f)
-        f += len(st["nkeep"])
+        f += len(c["nkeep"])
+
     # this shard's tail for the next rank, chained from the preceding shard's
     # through its own chunks: a shard shorter than POINTWISE_HIT_COUNTER_MAX
     # frames still forwards the session's last frames
     def own_tail(got):
         t = got
-        for (_, st, _), f0 in zip(states, f0s):
-            t = ex.chunk_tail(st, f0, t)
+        for (_, c, _), f0 in zip(comps, f0s):
+            t = ex.chunk_tail_compact(c, f0, t)
         return t
 
     prev = pass_tail_forward(own_tail)
-    for (_, st, host), ch, f0 in zip(states, changes, f0s):
-        tail = ex.chunk_tail(st, f0, prev)
-        ex.apply_selection(st, host, ch, f0, prev)
+    for (idx, c, host), ch, f0 in zip(comps, changes, f0s):
+        tail = ex.chunk_tail_compact(c, f0, prev)
+        ex.apply_selection_compact(c, host, ch, f0, prev, lambda fr, idx=idx: src.read(idx[np.asarray(fr)]))
         prev = tail
+
+
+class _GatherWriter:
+    """The writer end of a sharded session: every rank hands its finished
+    chunks here in order; each call is one round of
+    shard.gather_chunk_results, after which rank 0's _ChunkWriter writes the
+    round's chunks (one per rank, rank order; rows land at their frame
+    indices, TSV rows in per-rank part files joined at close).  `nrounds`
+    is the most chunks any rank owns: close() runs the rounds this rank has
+    no chunk for."""
+
+    def __init__(self, local, nrounds: int):
+        self.local, self.nrounds, self.done = local, nrounds, 0
+
+    def _round(self, d) -> None:
+        got = gather_chunk_results(d)
+        self.done += 1
+        if self.local is not None:
+            for r, x in enumerate(got):
+                if x is not None:
+                    self.local.write(x, part=r)
+
+    def write(self, d: dict) -> None:
+        self._round(d)
+
+    def close(self) -> None:
+        while self.done < self.nrounds:
+            self._round(None)
+        if self.local is not None:
+            self.local.close()
+
+    def abort(self) -> None:
+        if self.local is not None:
+            self.local.abort()
 
 
 def _lighten(d: dict) -> dict:

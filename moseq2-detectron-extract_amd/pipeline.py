@@ -41,6 +41,17 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def default_model_streams(hw_queues: Optional[int] = None) -> int:
+    """Model streams for the hardware queues this process has (package
+    HW_QUEUES, from GPU_MAX_HW_QUEUES): the front, tail and copy streams share
+    two queues and every forward keeps one of its own, up to 4 forwards (the
+    measured optimum at 8 queues; at HIP's default of 4 queues a third
+    forward lost 2 %)."""
+    if hw_queues is None:
+        from . import HW_QUEUES as hw_queues
+    return max(1, min(4, int(hw_queues) - 2))
+
+
 @dataclass
 class ExtractConfig:
     """The extract CLI options on the hot path (M/cli.py:333-418 defaults)."""
@@ -55,12 +66,12 @@ class ExtractConfig:
     mask_iou_threshold: float = 0.5
     fix_invalid_pixels: bool = True
     use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
-    # forwards of consecutive batches in flight within a chunk: 4, as in the
-    # hot loop (config-3 loop, 6000 frames, tracking off / on: 2 streams 1266 /
-    # 1293 frames/s, 3 streams 1293 / 1313 and 1294 / 1314, 4 streams 1315 /
-    # 1332; profiles/r04_experiments.json); give the process
-    # GPU_MAX_HW_QUEUES=8 (bench.py does) so each forward gets a hardware queue
-    model_streams: int = 4
+    # forwards of consecutive batches in flight within a chunk: 4 at 8
+    # hardware queues, as in the hot loop (config-3 loop, 6000 frames,
+    # tracking off / on: 2 streams 1266 / 1293 frames/s, 3 streams 1293 / 1313
+    # and 1294 / 1314, 4 streams 1315 / 1332; profiles/r04_experiments.json),
+    # 2 at HIP's default of 4 queues (default_model_streams)
+    model_streams: int = field(default_factory=default_model_streams)
     overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
@@ -116,10 +127,11 @@ class GPUExtractor:
         # ProcessFeaturesStep's norfair instance tracker (process_features_step.py:35-38), per session
         self.instance_tracker = INS.InstanceTracker(config.expected_instances)
         self._frames_seen = 0
-        self._inpaint_errors_seen = call("mdx_inpaint_errors", 0)  # process-wide device counter
+        self._inpaint_errors_seen = 0  # of this extractor's own counter (FramePrep.inpaint_errors)
         self._tail_dets = {}  # session frame -> (mask planes (D,h,w), keypoints (D,K,3), keep_idx row)
         self._streams = []
         self._pipe = None     # OverlappedExtractor of the pipelined features pass
+        self.keep_mask_logits = False  # set by the compact sharded passes (features_pass_compact)
 
     def infer(self, prepped: torch.Tensor):
         """Model forward over a prepped chunk in batch_size slices
@@ -143,28 +155,37 @@ class GPUExtractor:
                 st.wait_event(ready)
                 with torch.cuda.stream(st):
                     prepped.record_stream(st)
-                    o = self.predictor.run(prepped[i:i + bs], self.lut)
-                    sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
-                    o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
-                    if self.cfg.select_instances:
-                        o["centers"] = mask_centers(o, keep_idx, nkeep)
+                    o = self._infer_batch(prepped[i:i + bs])
                 for v in o.values():
                     for t in (v if isinstance(v, (list, tuple)) else (v,)):
                         if torch.is_tensor(t):
                             t.record_stream(cur)
             else:
-                o = self.predictor.run(prepped[i:i + bs], self.lut)
-                sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
-                o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
-                if self.cfg.select_instances:
-                    o["centers"] = mask_centers(o, keep_idx, nkeep)
+                o = self._infer_batch(prepped[i:i + bs])
             outs.append(o)
         if ns > 1 and n > bs:
             for st in self._streams[:ns]:
                 cur.wait_stream(st)
         keys = ("boxes", "scores", "classes", "ndet", "keypoints", "d2_mask", "sel_keypoints", "nkeep", "keep_idx")
-        keys += ("centers",) if "centers" in outs[0] else ()
+        keys += tuple(k for k in ("centers", "mask_logits") if k in outs[0])
         return {k: torch.cat([o[k] for o in outs]) for k in keys} | {"masks": [o["masks"] for o in outs]}
+
+    def _infer_batch(self, x: torch.Tensor) -> dict:
+        """One batch on the current stream: forward, mask NMS + instance 0,
+        the kept detections' centres (instance selection on) and, for the
+        compact sharded passes (keep_mask_logits), a copy of the mask head's
+        logits (B, D, M, M) -- with the boxes, all mdx_paste_masks needs to
+        re-make any detection's mask plane."""
+        o = self.predictor.run(x, self.lut)
+        sel, kp, nkeep, keep_idx = mask_nms_select(o, self.cfg.mask_iou_threshold)
+        o.update(d2_mask=sel, sel_keypoints=kp, nkeep=nkeep, keep_idx=keep_idx)
+        if self.cfg.select_instances:
+            o["centers"] = mask_centers(o, keep_idx, nkeep)
+        if self.keep_mask_logits:
+            B, D = o["boxes"].shape[:2]
+            lg = self.predictor.model.tensor("mask_logits")  # copied on this stream before the next forward
+            o["mask_logits"] = lg.view(B, D, lg.shape[1], lg.shape[2])
+        return o
 
     def select_instances(self, state: dict, host: dict):
         """ProcessFeaturesStep.__select_instances (process_features_step.py:
@@ -298,8 +319,11 @@ class GPUExtractor:
         host = {"centroid": feats["centroid"].cpu().numpy(), "orientation": feats["orientation"].cpu().numpy(),
                 "axis_length": feats["axis_length"].cpu().numpy(), "keypoints": inf["sel_keypoints"].cpu().numpy()}
         state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": inf["nkeep"].cpu().numpy()}
-        if self.cfg.select_instances:  # inputs of the host instance-selection step (select_instances)
+        if self.keep_mask_logits:  # features_pass_compact's inputs (no mask planes)
+            state["inf"] = {k: inf[k] for k in ("keypoints", "keep_idx", "mask_logits", "boxes")}
+        elif self.cfg.select_instances:  # inputs of the host instance-selection step (select_instances)
             state["inf"] = {k: inf[k] for k in ("masks", "keypoints", "keep_idx", "sel_keypoints")}
+        if self.cfg.select_instances:
             host["centers"] = inf["centers"].cpu().numpy()
         return state, host
 
@@ -330,13 +354,19 @@ class GPUExtractor:
         """One chunk's pipeline results -> (device state, host features)."""
         cat = lambda key: torch.cat([o[key] for o in outs])  # noqa: E731
         icat = lambda key: torch.cat([o["inf"][key] for o in outs])  # noqa: E731
-        prepped, cleaned, d2 = cat("prepped"), cat("cleaned"), icat("d2_mask")
+        if self.keep_mask_logits:  # the compact pass keeps no device frames
+            prepped = cleaned = d2 = None
+        else:
+            prepped, cleaned, d2 = cat("prepped"), cat("cleaned"), icat("d2_mask")
         host = {"centroid": cat("centroid").cpu().numpy(), "orientation": cat("orientation").cpu().numpy(),
                 "axis_length": cat("axis_length").cpu().numpy(), "keypoints": icat("sel_keypoints").cpu().numpy()}
         state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": icat("nkeep").cpu().numpy()}
-        if self.cfg.select_instances:
+        if self.keep_mask_logits:  # features_pass_compact's inputs (no mask planes)
+            state["inf"] = {k: icat(k) for k in ("keypoints", "keep_idx", "mask_logits", "boxes")}
+        elif self.cfg.select_instances:
             state["inf"] = {"masks": [m for o in outs for m in o["inf"]["masks"]], "keypoints": icat("keypoints"),
                             "keep_idx": icat("keep_idx"), "sel_keypoints": icat("sel_keypoints")}
+        if self.cfg.select_instances:
             host["centers"] = icat("centers").cpu().numpy()
         return state, host
 
@@ -367,12 +397,149 @@ class GPUExtractor:
             "depth_frames": depth.cpu().numpy(), "mask_frames": mask.cpu().numpy(),
         }
 
+    # ------------------------------------------------------------------
+    # compact chunk state of the sharded two-pass session (extract.py)
+    # ------------------------------------------------------------------
+    def features_pass_compact(self, raw):
+        """features_pass for the sharded session's first pass, keeping O(1)
+        device memory across chunks: the chunk's prepped / cleaned / d2 frames
+        and mask planes are released when this returns, and what the
+        exchanges and the second pass need is kept on the host in compact
+        form -- per frame the kept detections' mask logits (D x M x M fp32)
+        and boxes (re-pasted on the device by mdx_paste_masks, bit-identical
+        to the forward's planes), their keypoints, keep_idx and nkeep:
+        ~13 KB per frame against ~1.5 MB of device planes.  Returns
+        (compact, host features)."""
+        raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+        self.keep_mask_logits = True
+        try:
+            state, host = self.features_pass(raw)
+        finally:
+            self.keep_mask_logits = False
+        inf = state.pop("inf")
+        comp = {"nkeep": state["nkeep"].astype(np.int64), "keep_idx": inf["keep_idx"].cpu().numpy(),
+                "det_kp": inf["keypoints"].cpu().numpy(), "logits": inf["mask_logits"].cpu().numpy(),
+                "boxes": inf["boxes"].cpu().numpy(), "device": raw.device}
+        return comp, host
+
+    def _sel_default(self, comp) -> None:
+        """Instance 0 of every frame (mask_nms_select's choice): the record
+        the second pass pastes as the frame's d2 mask."""
+        n = len(comp["nkeep"])
+        j = np.maximum(comp["keep_idx"][:, 0], 0)
+        comp["sel_logits"] = comp["logits"][np.arange(n), j].copy()
+        comp["sel_box"] = comp["boxes"][np.arange(n), j].copy()
+        comp["sel_has"] = (comp["nkeep"] > 0).astype(np.int32)
+
+    def chunk_tail_compact(self, comp, f0: int, prev_tail: Optional[dict] = None) -> dict:
+        """chunk_tail over a compact chunk: {session frame: (record float32
+        (D, 1, M*M + 4) = logits | box per detection, keypoints (D,K,3), keep
+        row (D,))} of the session's last POINTWISE_HIT_COUNTER_MAX frames up
+        to the end of this chunk (shard.pass_tail_forward ships these)."""
+        n = len(comp["nkeep"])
+        lo = f0 + n - INS.POINTWISE_HIT_COUNTER_MAX
+        a = max(0, n - INS.POINTWISE_HIT_COUNTER_MAX)
+        out = {g: v for g, v in (prev_tail or {}).items() if lo <= g < f0}
+        D = comp["logits"].shape[1]
+        for f in range(a, n):
+            rec = np.concatenate([comp["logits"][f].reshape(D, -1), comp["boxes"][f]], axis=1)
+            out[f0 + f] = (torch.from_numpy(np.ascontiguousarray(rec, np.float32)).view(D, 1, -1),
+                           comp["det_kp"][f], comp["keep_idx"][f])
+        return out
+
+    def apply_selection_compact(self, comp, host: dict, changes: dict, f0: int, prev_tail: dict, raw_reader):
+        """apply_selection over a compact chunk: the picked detection's logits
+        and box become the frame's d2 record (pasted in the second pass), its
+        keypoints the frame's, num_instances the number picked; the changed
+        frames' moments are recomputed on the device from their raw frames
+        (raw_reader(chunk frame indices) -> int16 (k,H,W); prep, inpaint and
+        clean are per-frame, so equal to the chunk's) and the re-pasted mask.
+        Drops the chunk's all-detection records afterwards."""
+        self._sel_default(comp)
+        if changes:
+            nkeep, kph = comp["nkeep"], host["keypoints"]
+            M2 = comp["logits"].shape[2] * comp["logits"].shape[3]
+            fr = sorted(changes)
+            for f in fr:
+                sel = changes[f]
+                nkeep[f] = len(sel)
+                if not sel:
+                    comp["sel_has"][f] = 0
+                    kph[f] = np.nan
+                    continue
+                g, slot = sel[0]
+                comp["sel_has"][f] = 1
+                if g >= f0:
+                    j = int(comp["keep_idx"][g - f0, slot])
+                    comp["sel_logits"][f] = comp["logits"][g - f0, j]
+                    comp["sel_box"][f] = comp["boxes"][g - f0, j]
+                    kph[f] = comp["det_kp"][g - f0, j]
+                else:  # a detection of the preceding chunk's last frames (any rank)
+                    rec, kps, krow = prev_tail[g]
+                    j = int(krow[slot])
+                    r = np.asarray(rec[j].reshape(-1).cpu().numpy() if torch.is_tensor(rec) else rec[j]).reshape(-1)
+                    comp["sel_logits"][f] = r[:M2].reshape(comp["sel_logits"].shape[1:])
+                    comp["sel_box"][f] = r[M2:M2 + 4]
+                    kph[f] = kps[j]
+            raw = raw_reader(fr)
+            raw = raw if torch.is_tensor(raw) else torch.from_numpy(np.ascontiguousarray(raw))
+            raw = raw.to(comp["device"])
+            prepped = self.prep(raw)
+            cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
+            d2 = self._paste_selected(comp, fr, prepped.shape[1:])
+            feats = proc.frame_moments(cleaned, d2, float(self.cfg.frame_threshold))
+            idx = np.asarray(fr)
+            for k in ("centroid", "orientation", "axis_length"):
+                host[k][idx] = feats[k].cpu().numpy()
+        for k in ("logits", "boxes", "det_kp"):  # only the selected records travel to the second pass
+            comp.pop(k, None)
+
+    def _paste_selected(self, comp, frames, hw) -> torch.Tensor:
+        """d2 masks (k, h, w) of `frames` (chunk indices) from their selected
+        records: mdx_paste_masks with one detection per frame, the model's
+        mask threshold -- the kernel and inputs of the forward's own paste."""
+        dev = comp["device"]
+        fr = np.asarray(frames, dtype=np.int64)
+        k = len(fr)
+        h, w = int(hw[0]), int(hw[1])
+        d2 = torch.empty((k, h, w), dtype=torch.uint8, device=dev)
+        if k == 0:
+            return d2
+        M = comp["sel_logits"].shape[1]
+        lg = torch.from_numpy(np.ascontiguousarray(comp["sel_logits"][fr], np.float32)).to(dev)
+        bx = torch.from_numpy(np.ascontiguousarray(comp["sel_box"][fr], np.float32)).to(dev)
+        has = torch.from_numpy(np.ascontiguousarray(comp["sel_has"][fr], np.int32)).to(dev)
+        thr = float(self.predictor.model.cfg.mask_threshold)
+        for a in range(0, k, 65535):  # grid.y = frames per launch
+            b = min(k, a + 65535)
+            call("mdx_paste_masks", _p(lg[a:b]), _p(bx[a:b]), _p(has[a:b]), b - a, 1, M, h, w, h * w, thr,
+                 _p(d2[a:b]), _stream())
+        return d2
+
+    def finish_chunk_compact(self, comp, raw, centroid, keypoints, angles, flips, axis_length, frame_idxs=None,
+                             offset: int = 0, true_depth: float = 673.1) -> dict:
+        """Second pass of a compact chunk: the chunk's front (prep + inpaint +
+        clean) re-run from its raw frames -- deterministic, so equal to the
+        first pass's -- the d2 masks re-pasted from the selected records, then
+        finish_chunk."""
+        raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else \
+            torch.from_numpy(np.ascontiguousarray(raw)).to(comp["device"])
+        prepped, cleaned = self.front(raw)
+        if "sel_logits" not in comp:
+            self._sel_default(comp)
+        d2 = self._paste_selected(comp, np.arange(len(comp["nkeep"])), prepped.shape[1:])
+        state = {"prepped": prepped, "d2": d2, "cleaned": cleaned, "nkeep": comp["nkeep"]}
+        return self.finish_chunk(state, centroid, keypoints, angles, flips, axis_length, frame_idxs, offset,
+                                 true_depth)
+
     def _check_inpaint(self) -> None:
         """Once per chunk: frames whose inpaint cluster labelling did not
         converge are left un-inpainted by k_inp_setup and counted on the
-        device (mdx_inpaint_errors); such frames would differ from the
-        reference's, so a new count is raised here rather than written."""
-        n = call("mdx_inpaint_errors", 0)
+        device in this extractor's own counter (mdx_inpaint_ns_counted);
+        such frames would differ from the reference's, so a new count is
+        raised here rather than written.  Another extractor of the same
+        process does not touch the count."""
+        n = self.prep.inpaint_errors()
         if n > self._inpaint_errors_seen:
             self._inpaint_errors_seen = n
             raise proc.MdxError(f"inpaint: {n} frame(s) whose invalid-pixel labelling did not converge "

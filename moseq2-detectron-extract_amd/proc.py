@@ -124,6 +124,13 @@ class FramePrep:
         self.vmin, self.vmax = vmin, vmax
         self.fix_invalid_pixels = fix_invalid_pixels
         self._ws = None
+        self._errors = None  # this prep's device count of unconverged inpaint frames (inpaint_errors)
+
+    def inpaint_errors(self) -> int:
+        """Frames of THIS prep's calls whose inpaint labelling did not
+        converge (left un-inpainted; mdx_inpaint_ns_counted).  Synchronises
+        the current stream."""
+        return 0 if self._errors is None else int(self._errors.item())
 
     def crop(self, H, W):
         if self.bbox is None:
@@ -192,7 +199,12 @@ def fill_invalid_pixels(frames, invalid_mask, _workspace_owner=None):
         ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=f.device)
         if owner is not None:
             owner._ws = ws
-    call("mdx_inpaint_ns", _ptr(f), _ptr(m), n, H, W, 3, _ptr(ws), _stream())
+    err = None
+    if owner is not None:  # the owner's own non-convergence counter (FramePrep.inpaint_errors)
+        if getattr(owner, "_errors", None) is None:
+            owner._errors = torch.zeros((1,), dtype=torch.int32, device=f.device)
+        err = owner._errors
+    call("mdx_inpaint_ns_counted", _ptr(f), _ptr(m), n, H, W, 3, _ptr(ws), _ptr(err), _stream())
     return _ret(f, as_np)
 
 

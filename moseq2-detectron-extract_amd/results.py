@@ -175,9 +175,12 @@ def _npy_header(a: np.ndarray) -> bytes:
 
 class _DeflateStream:
     """The ``<key>.npy`` member of a C-contiguous array as one raw deflate
-    stream built row range by row range: the header and every range are
-    independently deflated pieces ending on a sync flush (pigz's layout), the
-    stream closed by an empty final block; CRC-32 and size run along."""
+    stream built as rows complete: the header, then the body in
+    independently deflated pieces cut at ABSOLUTE multiples of _PIECE bytes
+    (each ends on a sync flush, the last one finishes the stream -- pigz's
+    layout), so the compressed bytes do not depend on the order or the
+    grouping in which rows arrive (one process or the ranks of a sharded
+    session write the same file); CRC-32 and size run along."""
 
     def __init__(self, arr: np.ndarray, level: int, pool):
         self.arr, self.level, self.pool = arr, level, pool
@@ -186,21 +189,36 @@ class _DeflateStream:
         self.pieces = [c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)]
         self.crc = zlib.crc32(head)
         self.size = len(head)
-        self.rows = 0
+        self.rowbytes = arr[0].nbytes if arr.ndim and arr.shape[0] else 0
+        self.off = 0   # body bytes deflated so far (a multiple of _PIECE until finish)
+        self.rows = 0  # rows whose bytes are complete
+
+    def _body(self) -> memoryview:
+        return memoryview(self.arr.reshape(-1).view(np.uint8))
 
     def feed(self, upto: int) -> None:
+        """Rows [0, upto) are final: deflate the whole pieces they complete."""
         if upto <= self.rows:
             return
-        body = memoryview(self.arr[self.rows:upto].reshape(-1).view(np.uint8))
-        self.pieces += _deflate_pieces(body, self.level, self.pool, final=False)
-        self.crc = zlib.crc32(body, self.crc)
-        self.size += len(body)
         self.rows = upto
+        end = (upto * self.rowbytes) // _PIECE * _PIECE
+        if end > self.off:
+            body = self._body()[self.off:end]
+            self.pieces += _deflate_pieces(body, self.level, self.pool, final=False)
+            self.crc = zlib.crc32(body, self.crc)
+            self.size += len(body)
+            self.off = end
 
     def finish(self):
-        self.feed(self.arr.shape[0] if self.arr.ndim else 0)
-        return self.pieces + [zlib.compressobj(self.level, zlib.DEFLATED, -15).flush(zlib.Z_FINISH)], self.crc, \
-            self.size
+        body = self._body()[self.off:] if self.arr.ndim else memoryview(b"")
+        if len(body):
+            self.pieces += _deflate_pieces(body, self.level, self.pool, final=True)
+            self.crc = zlib.crc32(body, self.crc)
+            self.size += len(body)
+        else:
+            self.pieces.append(zlib.compressobj(self.level, zlib.DEFLATED, -15).flush(zlib.Z_FINISH))
+        self.off += len(body)
+        return self.pieces, self.crc, self.size
 
 
 def save_npz(path: str, arrays: Dict[str, np.ndarray], level: int = 4, workers: int = 0,
@@ -370,13 +388,17 @@ def write_extracted_chunk_to_h5(h5_file, results: dict) -> None:
 
 class KeypointsTSVWriter:
     """keypoints_XX.tsv: Frame_Idx, Flip, Centroid_X, Centroid_Y, Angle, then
-    every keypoint field, one row per frame, appended per chunk."""
+    every keypoint field, one row per frame, appended per chunk.  `path` /
+    `header=False`: a headerless part file (one per rank of a sharded
+    session, joined by join_tsv_parts)."""
 
-    def __init__(self, output_dir: str, bg_roi_index: int = 0):
-        self.path = os.path.join(output_dir, f"keypoints_{bg_roi_index:02d}.tsv")
-        self._header = True
+    def __init__(self, output_dir: str, bg_roi_index: int = 0, path: Optional[str] = None, header: bool = True):
+        self.path = path or os.path.join(output_dir, f"keypoints_{bg_roi_index:02d}.tsv")
+        self._header = header
+        self._fresh = True  # the first write truncates the file
 
-    def write(self, data: dict) -> None:
+    @staticmethod
+    def columns(data: dict) -> dict:
         feats = data["features"]
         cen = np.asarray(feats["features"]["centroid"])
         cols = {"Frame_Idx": np.asarray(data["frame_idxs"]), "Flip": np.asarray(feats["flips"]),
@@ -384,6 +406,10 @@ class KeypointsTSVWriter:
                 "Angle": np.asarray(feats["features"]["orientation"])}
         for k, v in data["keypoints"].items():
             cols[k] = np.asarray(v)
+        return cols
+
+    def write(self, data: dict) -> None:
+        cols = self.columns(data)
         # the bytes of pandas.DataFrame(cols).to_csv(sep="\t", index=False)
         # (shortest round-trip floats, NaN as an empty field): formatted in
         # libmdx's host code (no GIL held) when every column is float64 /
@@ -392,11 +418,27 @@ class KeypointsTSVWriter:
         if body is None:
             cells = [_tsv_cells(v) for v in cols.values()]
             body = "".join("\t".join(r) + "\n" for r in zip(*cells)).encode()
-        with open(self.path, "wb" if self._header else "ab") as fh:
-            if self._header:
+        with open(self.path, "wb" if self._fresh else "ab") as fh:
+            if self._header and self._fresh:
                 fh.write(("\t".join(cols) + "\n").encode())
             fh.write(body)
-        self._header = False
+        self._fresh = False
+
+
+def join_tsv_parts(path: str, header_cols, parts) -> None:
+    """keypoints_XX.tsv of a sharded session: the header, then the ranks'
+    headerless part files in rank (= session) order; the parts are removed."""
+    with open(path, "wb") as out:
+        out.write(("\t".join(header_cols) + "\n").encode())
+        for p in parts:
+            if os.path.exists(p):
+                with open(p, "rb") as fh:
+                    while True:
+                        b = fh.read(1 << 24)
+                        if not b:
+                            break
+                        out.write(b)
+                os.remove(p)
 
 
 def _tsv_rows_native(columns) -> Optional[bytes]:

@@ -223,9 +223,17 @@ def instance_exchange(host_chunks: List[Dict[str, np.ndarray]], nkeeps: List[np.
     return offset, res
 
 
+def _tail_dtypes():
+    """Tail payload dtype by header code: 0 uint8 mask planes, 1 float32
+    compact records (GPUExtractor.chunk_tail_compact)."""
+    import torch
+    return (torch.uint8, torch.float32)
+
+
 def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
     """Chain rank r-1 -> rank r of the last frames' kept detections (mask
-    planes, keypoints, keep rows; instances.POINTWISE_HIT_COUNTER_MAX frames):
+    planes or compact logit records, keypoints, keep rows;
+    instances.POINTWISE_HIT_COUNTER_MAX frames):
     a pick at the start of rank r's shard can be a detection of the previous
     shard's last frames.  `tail` is {session frame: (planes (D,h,w) uint8,
     keypoints (D,K,3), keep row (D,))}, a callable mapping the received tail
@@ -241,9 +249,9 @@ def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
     if rank > 0:
         hdr = torch.zeros(6, dtype=torch.int64, device=device)
         dist.recv(hdr, rank - 1, group=group)
-        nf, D, h, w, K = (int(v) for v in hdr[:5].tolist())
+        nf, D, h, w, K, code = (int(v) for v in hdr.tolist())
         if nf:
-            planes = torch.empty((nf, D, h, w), dtype=torch.uint8, device=device)
+            planes = torch.empty((nf, D, h, w), dtype=_tail_dtypes()[code], device=device)
             meta = torch.empty((nf, 1 + D + D * K * 3), dtype=torch.float64, device=device)
             dist.recv(planes, rank - 1, group=group)
             dist.recv(meta, rank - 1, group=group)
@@ -254,13 +262,15 @@ def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
     send = got if tail is None else (tail(got) if callable(tail) else tail)
     if rank < world - 1:
         keys = sorted(send)
+        code = 0
         if keys:
             p0, k0, _ = send[keys[0]]
             D, h, w = (int(v) for v in p0.shape)
             K = int(np.asarray(k0).shape[1])
+            code = _tail_dtypes().index(p0.dtype)
         else:
             D = h = w = K = 0
-        hdr = torch.tensor([len(keys), D, h, w, K, 0], dtype=torch.int64, device=device)
+        hdr = torch.tensor([len(keys), D, h, w, K, code], dtype=torch.int64, device=device)
         dist.send(hdr, rank + 1, group=group)
         if keys:
             planes = torch.stack([send[g][0].to(device) for g in keys]).contiguous()
@@ -270,3 +280,93 @@ def pass_tail_forward(tail: Optional[Dict], group=None, device=None):
             dist.send(planes, rank + 1, group=group)
             dist.send(torch.from_numpy(np.ascontiguousarray(meta)).to(device), rank + 1, group=group)
     return got
+
+
+# ----------------------------------------------------------------------------
+# the result gather of a sharded session (one results file, written by rank 0)
+# ----------------------------------------------------------------------------
+def _result_columns(d: Dict) -> List[Tuple[str, np.ndarray]]:
+    """The writer's fields of a finished chunk (_ChunkWriter.write), as
+    per-frame columns in a fixed order (scalar / keypoint dict order kept:
+    it is the TSV's column order)."""
+    off = int(d.get("offset", 0))
+    f = d["features"]
+    cols = [("frame_idxs", np.asarray(d["frame_idxs"])), ("depth_frames", np.asarray(d["depth_frames"])[off:]),
+            ("mask_frames", np.asarray(d["mask_frames"])[off:]), ("flips", np.asarray(f["flips"])[off:]),
+            ("centroid", np.asarray(f["features"]["centroid"])[off:]),
+            ("orientation", np.asarray(f["features"]["orientation"])[off:])]
+    cols += [("scalars/" + k, np.asarray(v)[off:]) for k, v in d["scalars"].items()]
+    cols += [("keypoints/" + k, np.asarray(v)[off:]) for k, v in d["keypoints"].items()]
+    return cols
+
+
+def pack_chunk_results(d: Dict):
+    """A finished chunk's writer fields -> (schema JSON bytes, rows uint8
+    (n, rowbytes)): every per-frame value's bytes side by side, so one byte
+    tensor per chunk crosses the process group."""
+    import json
+    cols = _result_columns(d)
+    n = len(cols[0][1])
+    schema, parts = [], []
+    for name, a in cols:
+        a = np.ascontiguousarray(a)
+        if len(a) != n:
+            raise ValueError(f"pack_chunk_results: column {name} has {len(a)} rows, expected {n}")
+        schema.append([name, a.dtype.str, list(a.shape[1:])])
+        parts.append(a.reshape(n, -1).view(np.uint8) if a.size else np.zeros((n, 0), np.uint8))
+    rows = np.concatenate(parts, axis=1) if parts else np.zeros((n, 0), np.uint8)
+    return json.dumps(schema).encode(), np.ascontiguousarray(rows)
+
+
+def unpack_chunk_results(schema: bytes, rows: np.ndarray) -> Dict:
+    """Inverse of pack_chunk_results: the data dict _ChunkWriter.write
+    consumes (offset 0)."""
+    import json
+    sch = json.loads(schema.decode())
+    n = rows.shape[0]
+    out, o = {}, 0
+    for name, dt, shp in sch:
+        dt = np.dtype(dt)
+        w = dt.itemsize * int(np.prod(shp, dtype=np.int64))
+        out[name] = np.ascontiguousarray(rows[:, o:o + w]).view(dt).reshape((n,) + tuple(shp))
+        o += w
+    d = {"frame_idxs": out["frame_idxs"], "offset": 0, "depth_frames": out["depth_frames"],
+         "mask_frames": out["mask_frames"],
+         "features": {"flips": out["flips"], "features": {"centroid": out["centroid"],
+                                                          "orientation": out["orientation"]}},
+         "scalars": {k[8:]: v for k, v in out.items() if k.startswith("scalars/")},
+         "keypoints": {k[10:]: v for k, v in out.items() if k.startswith("keypoints/")}}
+    return d
+
+
+def gather_chunk_results(d: Optional[Dict], group=None, device=None, dst: int = 0):
+    """One round of the sharded session's result gather: every rank passes
+    its next finished chunk (None when it has no chunk left); rank `dst`
+    gets [chunk dict or None per rank] in rank order, the others None.  The
+    bytes travel as flat uint8 tensors through dist.gather (RCCL over xGMI
+    with the nccl backend, gloo on the CPU)."""
+    import torch
+    import torch.distributed as dist
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    if d is None:
+        sch, rows = b"", np.zeros((0, 0), np.uint8)
+    else:
+        sch, rows = pack_chunk_results(d)
+    t_sch = torch.from_numpy(np.frombuffer(sch, np.uint8).copy()).to(device)
+    t_rows = torch.from_numpy(rows.reshape(-1)).to(device)
+    t_n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=device)
+    all_n = gather_ragged_to_rank0(t_n, group, dst)
+    all_sch = gather_ragged_to_rank0(t_sch, group, dst)
+    all_rows = gather_ragged_to_rank0(t_rows, group, dst)
+    if all_rows is None:
+        return None
+    res = []
+    for n, s, r in zip(all_n, all_sch, all_rows):
+        if s.numel() == 0:
+            res.append(None)
+            continue
+        n = int(n.item())
+        b = r.cpu().numpy()
+        res.append(unpack_chunk_results(s.cpu().numpy().tobytes(), b.reshape(n, -1) if n else b.reshape(0, 0)))
+    return res

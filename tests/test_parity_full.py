@@ -41,8 +41,9 @@ Tolerances (written here, stated in DESIGN.md §4):
       non-NaN-pose frames give the oracle's depth crop byte for byte (the
       rest differ because fp16 moves the small seeded-weight masks by a few
       near-threshold pixels, and with them the pose); recorded per frame.
-  coverage: at least MIN_POSES frames per case carry a non-NaN pose on both
-    sides (the chain is compared on real contours, not NaN against NaN).
+  coverage: at least MIN_POSES frames per case (30 / 32 for R50, 60 / 64 for
+    R101) carry a non-NaN pose on both sides (the chain is compared on real
+    contours, not NaN against NaN).
 The measured numbers are written to gpurun_out/parity_full_<case>.json when
 that directory exists (evidence for DESIGN.md)."""
 import json
@@ -63,7 +64,7 @@ TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, c
        # keypoint and pose bounds)
        "mixed": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05)}
 MASK_PX_FLOOR = 4       # pixels: the seeded-weight masks can be a handful of pixels
-MIN_POSES = 8           # non-NaN poses (both sides) per case
+MIN_POSES = {50: 30, 101: 60}  # non-NaN poses (both sides) per case, by depth
 MIN_SEL_EXACT = 0.9     # fp32: fraction of frames whose selected mask is the oracle's, pixel for pixel
 ANGLE_ULPS = 2          # fp32: angle agreement (deg) in units in the last place when the masks agree
 FP16_FRAMES = 0.8       # fp16: fraction of frames passing the detection checks / the pose bounds
@@ -73,10 +74,13 @@ MIXED_CROP_EXACT = 0.9  # config 5 as stated (fp32 trunk / box head, fp16 mask +
                         # fraction (round-4 record: R101 B=64 62 / 64), and every frame passes the
                         # detection and pose checks
 SEED = 77               # synthetic session of the batch
-# seeded synthetic weights per depth: R101 with seed 0 selects detections off
+# seeded synthetic weights per depth, chosen so the downstream chain is
+# compared on (nearly) every frame: R101 with seed 0 selects detections off
 # the animal on 61 of 64 frames (NaN poses on both sides, nothing compared
-# downstream); seed 1 selects on-animal masks on every frame
-WEIGHT_SEED = {50: 0, 101: 1}
+# downstream), seed 1 selects on-animal masks on every frame; R50 with seed 0
+# gave 22 / 32 non-NaN oracle poses, seed 3 gives 31 / 32
+# (tools/pose_seed_scan.py 50 32 0..7: 22, 25, 26, 31, 21, 1, 26, 26)
+WEIGHT_SEED = {50: 3, 101: 1}
 ORACLE_CHUNK = 8        # frames per oracle forward (its intermediates of a whole batch would not fit)
 
 _ORACLE = {}
@@ -324,7 +328,7 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
                 assert rec["centroid_bit_exact"] and rec["angle_ulps"] <= ANGLE_ULPS, rec
                 assert rec["crop_bit_exact_vs_oracle"], rec
     stats["summary"].update(detections_ok=det_ok, pose_ok=pose_ok)
-    assert n_pose >= MIN_POSES, stats["summary"]
+    assert n_pose >= MIN_POSES[orc["cfg"].depth], stats["summary"]
     if dtype == "fp32":
         assert n_sel >= MIN_SEL_EXACT * B, stats["summary"]
     elif dtype == "mixed":

@@ -270,3 +270,130 @@ def test_host_pipeline_order_and_errors(mdx):
 
     with pytest.raises(OSError, match="no stream"):
         host_pipeline(gen(6), lambda i: i, setup=bad_setup)
+
+
+# ------------------------------------------------- one results file per session
+class _FakeSrc:
+    """What _ChunkWriter reads from the frame source."""
+
+    def __init__(self, d, n):
+        self.path = os.path.join(d, "depth.dat")
+        self.last_frame_idx = n
+
+    def read(self, idx):
+        return np.full((len(idx), 424, 512), 7, np.int16)
+
+
+def _fake_chunks(n, chunk, seed=3):
+    """Writer data dicts of a synthetic session (float32 / float64 columns,
+    NaNs, the reference's scalar and keypoint names)."""
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.features import keypoint_attributes, scalar_attributes
+    rng = np.random.default_rng(seed)
+    out = []
+    for a in range(0, n, chunk):
+        idx = np.arange(a, min(n, a + chunk))
+        k = len(idx)
+        cen = rng.normal(200, 30, (k, 2))
+        cen[rng.random(k) < 0.1] = np.nan
+        out.append({"frame_idxs": idx, "offset": 0,
+                    "scalars": {s: rng.normal(0, 1, k).astype(np.float32) for s in scalar_attributes()},
+                    "keypoints": {s: rng.normal(0, 50, k) for s in keypoint_attributes()},
+                    "depth_frames": rng.integers(0, 255, (k, 80, 80), dtype=np.uint8),
+                    "mask_frames": (rng.random((k, 80, 80)) < 0.3).astype(np.uint8),
+                    "features": {"flips": rng.random(k) < 0.5,
+                                 "features": {"centroid": cen, "orientation": rng.uniform(0, 360, k)}}})
+    return out
+
+
+def _writer_args(d, n):
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig
+    cfg = ExtractConfig(chunk_size=50, model_streams=2)
+    status = {"uuid": "0f0f", "parameters": dict(vars(cfg)), "metadata": {"SerialNumber": "x"}}
+    roi = np.zeros((424, 512), np.uint8)
+    roi[100:300, 100:400] = 1
+    return (_FakeSrc(d, n), np.full((424, 512), 670.0), roi, 673.1, cfg, None, status)
+
+
+def _gather_writer_worker(rank, world, port, q, out_dir, n, chunk):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.extract import _ChunkWriter, _GatherWriter, shard_chunk_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    chunks = _fake_chunks(n, chunk)
+    c0, c1 = shard_chunk_range(len(chunks), world, rank)
+    nrounds = len(range(*shard_chunk_range(len(chunks), world, 0)))
+    local = _ChunkWriter(out_dir, *_writer_args(out_dir, n), parts=world) if rank == 0 else None
+    w = _GatherWriter(local, nrounds)
+    for d in chunks[c0:c1]:
+        w.write(d)
+    w.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, "ok"))
+
+
+@pytest.mark.parametrize("world,n,chunk", [(2, 230, 50), (3, 100, 50)])
+def test_sharded_writer_one_file_equals_one_process(mdx, tmp_path, world, n, chunk):
+    """The ranks' chunks gathered round by round to rank 0 (gloo) make ONE
+    results_00 file and keypoints_00.tsv equal to one process's, byte for
+    byte: uneven shards (padding rounds) and a rank without chunks; rows
+    arrive out of session order, and the crop stacks' deflate pieces are cut
+    at absolute offsets, so the file does not depend on arrival order."""
+    from moseq2_detectron_extract_amd.extract import _ChunkWriter
+    from moseq2_detectron_extract_amd import results as RS
+    one = tmp_path / "one"
+    one.mkdir()
+    w = _ChunkWriter(str(one), *_writer_args(str(one), n))
+    for d in _fake_chunks(n, chunk):
+        w.write(d)
+    w.close()
+    sh = tmp_path / "sharded"
+    sh.mkdir()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_writer_worker, args=(r, world, port, q, str(sh), n, chunk))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert set(got.values()) == {"ok"}
+    assert sorted(os.listdir(sh)) == sorted(os.listdir(one))  # no part files left behind
+    assert (sh / "keypoints_00.tsv").read_bytes() == (one / "keypoints_00.tsv").read_bytes()
+    assert (sh / "results_00.npz").read_bytes() == (one / "results_00.npz").read_bytes()
+    z = np.load(str(one / "results_00.npz"))
+    assert z["frames"].shape == (n, 80, 80) and z["frames"].any()
+
+
+def test_deflate_stream_independent_of_arrival(mdx, tmp_path, monkeypatch):
+    """The streamed crop member's bytes are the same whatever groups of rows
+    arrive in which order (pieces cut at absolute _PIECE offsets), and equal
+    to the member save_npz writes for the whole array at once."""
+    from moseq2_detectron_extract_amd import results as RS
+    monkeypatch.setattr(RS, "_PIECE", 4096)
+    rng = np.random.default_rng(0)
+    arr = rng.integers(0, 4, (300, 80, 80), dtype=np.uint8)
+    outs = []
+    for order in ([range(0, 300)], [range(200, 300), range(0, 120), range(120, 200)],
+                  [range(i, min(300, i + 7)) for i in range(0, 300, 7)][::-1]):
+        h = RS.MemoryH5(str(tmp_path / "a.npz"))
+        ds = h.create_dataset("frames", (300, 80, 80), "uint8")
+        for rows in order:
+            ds[np.asarray(rows)] = arr[np.asarray(rows)]
+            h.rows_written(np.asarray(rows))
+        h.close()
+        outs.append((tmp_path / "a.npz").read_bytes())
+    assert outs[0] == outs[1] == outs[2]
+    RS.save_npz(str(tmp_path / "b.npz"), {"frames": arr}, level=4)
+    np.testing.assert_array_equal(np.load(str(tmp_path / "a.npz"))["frames"], arr)

@@ -5,13 +5,17 @@ gloo for the collectives), over a synthetic .dat session of several chunks,
 tracking on, instance selection on, the result writers on.
 
 The sharded run goes through everything the host-only tests in
-test_shard.py stand in for: the device feature pass per chunk with the
-chunk's frames kept resident, the rank-0 instance and tracking exchanges,
-the mask-plane hand-off of a shard's last detections to the next rank
-(shard.pass_tail_forward: device planes -> host -> the next rank's device,
-then the gather kernel), the device finish (crops at the tracked pose) and
-the MIN all-reduce completion check.  Everything it returns and writes must
-equal the one-process session bit for bit.
+test_shard.py stand in for: the compact first pass per chunk (the chunk's
+device frames released, mask logits + boxes kept on the host), the rank-0
+instance and tracking exchanges, the hand-off of a shard's last detections
+to the next rank as compact logit records (shard.pass_tail_forward, re-pasted
+on the receiving device), the second pass (the chunk's front re-run from its
+raw frames, the selected masks re-pasted, crops at the tracked pose), the
+round-by-round result gather to rank 0's single writer, and the MIN
+all-reduce completion check.  Everything it returns must equal the
+one-process session bit for bit, the one results file and keypoints TSV it
+writes must equal the one-process files byte for byte, and each rank's peak
+device memory must not grow with the number of chunks it owns.
 """
 import os
 import socket
@@ -27,13 +31,30 @@ pytestmark = pytest.mark.gpu
 # the tracked centroid is finite on every frame and one of rank 1's frames
 # picks a detection of rank 0's shard through the tail hand-off
 NFR, CHUNK, BATCH, WORLD, SEED = 384, 96, 32, 2, 77
+# the memory check: the same ranks over a session of 6 chunks per rank
+NFR_LONG, SEED_LONG = 1152, 78
+# one chunk's device working set: prepped + cleaned + d2 frames (3 x 216,153
+# B) and four mask planes (4 x 216,160 B) per frame
+CHUNK_BYTES = CHUNK * (3 * 216153 + 4 * 216160)
 
 
 def _cfg():
     import mdx_pkg
     mdx_pkg.load()
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig
-    return ExtractConfig(chunk_size=CHUNK, batch_size=BATCH, use_tracking=True, select_instances=True)
+    return ExtractConfig(chunk_size=CHUNK, batch_size=BATCH, use_tracking=True, select_instances=True,
+                         model_streams=2)
+
+
+def _status(sess_dir):
+    """One status for every run, so the one-process and the sharded results
+    files carry the same uuid / parameters and can be compared byte for
+    byte."""
+    import json
+    with open(os.path.join(sess_dir, "metadata.json")) as fh:
+        meta = json.load(fh)
+    return {"complete": False, "skip": False, "uuid": "00000000-r5-config4", "metadata": meta,
+            "parameters": dict(vars(_cfg()))}
 
 
 def _predictor():
@@ -77,19 +98,31 @@ def _rank_main(rank, port, sess_dir, out_dir, seed, q):
 
         E.instance_exchange = spy
         pred = _predictor()
+        torch.cuda.reset_peak_memory_stats()
         out = E.extract_session(os.path.join(sess_dir, "depth.dat"), s.bground_im, s.roi, pred, _cfg(),
-                                true_depth=s.true_depth, world=WORLD, rank=rank, output_dir=out_dir)
-        np.savez(os.path.join(out_dir, f"ret_rank{rank}.npz"), **out)
+                                true_depth=s.true_depth, world=WORLD, rank=rank, output_dir=out_dir,
+                                status=_status(sess_dir))
+        torch.cuda.synchronize()
+        peak2 = torch.cuda.max_memory_allocated()
+        np.savez(os.path.join(os.path.dirname(out_dir), f"ret_rank{rank}.npz"), **out)
         # a completed sharded session is skipped by every rank (MIN all-reduce)
         again = E.extract_session(os.path.join(sess_dir, "depth.dat"), s.bground_im, s.roi, pred, _cfg(),
                                   true_depth=s.true_depth, world=WORLD, rank=rank, output_dir=out_dir)
+        # 6 chunks per rank instead of 2: the same peak device memory
+        long_dir = os.path.join(os.path.dirname(sess_dir), "sess_long")
+        sl = synth.SyntheticSession(NFR_LONG, seed=SEED_LONG)
+        torch.cuda.reset_peak_memory_stats()
+        E.extract_session(os.path.join(long_dir, "depth.dat"), sl.bground_im, sl.roi, pred, _cfg(),
+                          true_depth=sl.true_depth, world=WORLD, rank=rank,
+                          output_dir=os.path.join(os.path.dirname(out_dir), "shard_long"))
         torch.cuda.synchronize()
+        peak6 = torch.cuda.max_memory_allocated()
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, "ok", len(cross), again == {}))
+        q.put((rank, "ok", len(cross), again == {}, (peak2, peak6)))
     except BaseException as e:  # reported to the parent, which fails the test
         import traceback
-        q.put((rank, "error", traceback.format_exc()[-3000:], False))
+        q.put((rank, "error", traceback.format_exc()[-3000:], False, None))
         raise
 
 
@@ -102,6 +135,7 @@ def sharded_vs_single(mdx, tmp_path_factory):
     d = tmp_path_factory.mktemp("config4")
     s = synth.SyntheticSession(NFR, seed=seed)
     s.write(str(d / "sess"))
+    synth.SyntheticSession(NFR_LONG, seed=SEED_LONG).write(str(d / "sess_long"))
     # the two ranks first, in fresh processes (each takes its own HIP context)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -113,9 +147,9 @@ def sharded_vs_single(mdx, tmp_path_factory):
     got = {}
     try:
         for _ in range(WORLD):
-            r, status, info, skipped = q.get(timeout=300)
+            r, status, info, skipped, peaks = q.get(timeout=300)
             assert status == "ok", f"rank {r} failed:\n{info}"
-            got[r] = (info, skipped)
+            got[r] = (info, skipped, peaks)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -125,8 +159,8 @@ def sharded_vs_single(mdx, tmp_path_factory):
         assert p.exitcode == 0
     # the same session in this process, one rank
     single = extract_session(str(d / "sess" / "depth.dat"), s.bground_im, s.roi, _predictor(), _cfg(),
-                             true_depth=s.true_depth, output_dir=str(d / "single"))
-    ranks = [dict(np.load(str(d / "shard" / f"ret_rank{r}.npz"))) for r in range(WORLD)]
+                             true_depth=s.true_depth, output_dir=str(d / "single"), status=_status(str(d / "sess")))
+    ranks = [dict(np.load(str(d / f"ret_rank{r}.npz"))) for r in range(WORLD)]
     return d, single, ranks, got
 
 
@@ -150,22 +184,29 @@ def test_sharded_session_equals_one_process(sharded_vs_single):
 
 
 def test_sharded_writers_equal_one_process(sharded_vs_single):
-    """Each rank's results file holds its shard's rows of the one-process
-    file, byte for byte; the keypoint TSVs of the ranks concatenate to the
-    one-process TSV; both ranks skip the completed session on a rerun."""
+    """The sharded session writes ONE results_00 file and ONE keypoints_00.tsv
+    (rank 0's writer, fed by the result gather), equal to the one-process
+    files byte for byte, and no per-rank files; both ranks skip the completed
+    session on a rerun."""
     d, _, _, got = sharded_vs_single
+    assert sorted(os.listdir(d / "shard")) == sorted(os.listdir(d / "single"))
+    for name in ("results_00.npz", "keypoints_00.tsv"):
+        assert (d / "shard" / name).read_bytes() == (d / "single" / name).read_bytes(), name
     one = np.load(str(d / "single" / "results_00.npz"))
-    tsv = []
+    assert one["frames"].shape == (NFR, 80, 80)
     for r in range(WORLD):
-        part = np.load(str(d / "shard" / f"rank{r}" / "results_00.npz"))
-        lo, hi = r * NFR // 2, (r + 1) * NFR // 2
-        for k in ("frames", "frames_mask", "scalars/angle", "scalars/centroid_x_px", "scalars/area_px"):
-            np.testing.assert_array_equal(part[k][lo:hi], one[k][lo:hi], err_msg=f"rank {r} {k}")
-        tsv.append((d / "shard" / f"rank{r}" / "keypoints_00.tsv").read_text().splitlines())
         assert got[r][1], f"rank {r} re-ran a completed session"
-    want = (d / "single" / "keypoints_00.tsv").read_text().splitlines()
-    assert tsv[0][0] == want[0]  # header
-    assert tsv[0] + tsv[1][1:] == want
+
+
+def test_sharded_peak_memory_flat(sharded_vs_single):
+    """Per rank, the peak device memory of a 6-chunk shard exceeds that of a
+    2-chunk shard by less than one chunk's working set: nothing per chunk
+    stays resident until the exchange (compact first pass)."""
+    _, _, _, got = sharded_vs_single
+    for r in range(WORLD):
+        peak2, peak6 = got[r][2]
+        print({"rank": r, "peak_2_chunks_MB": peak2 / 2**20, "peak_6_chunks_MB": peak6 / 2**20})
+        assert peak6 <= peak2 + CHUNK_BYTES, (r, peak2, peak6, CHUNK_BYTES)
 
 
 def test_sharded_session_crossed_the_rank_boundary(sharded_vs_single):

@@ -34,11 +34,19 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // the forms: 0 v_pk_add_f32 (plain), 1 v_pk_add_f32 op_sel:[0,1] op_sel_hi:[1,0]
 // (the GN partial's cross-half accumulate), 2 v_pk_add_f32 op_sel_hi:[1,0]
 // neg_lo:[0,1] neg_hi:[0,1] (its broadcast subtract), 3 v_pk_mul_f32 (plain),
-// 4 v_pk_fma_f32 (plain), 5 scalar v_add_f32 pair (control)
-constexpr int NFORMS = 6;
+// 4 v_pk_fma_f32 (plain), 5 scalar v_add_f32 pair (control); round 5, the
+// other forms the shipped library holds (tools/isa_lint.py lists them):
+// 6 v_pk_add_f32 neg_lo:[0,1] neg_hi:[0,1] (subtract), 7 v_pk_add_f32 with an
+// inline constant op_sel_hi:[1,0], 8 v_pk_fma_f32 constant op_sel_hi:[1,0,1],
+// 9 v_pk_fma_f32 SGPR pair op_sel_hi:[1,0,1], 10 v_pk_mul_f32 SGPR pair,
+// 11 v_pk_mul_f32 constant op_sel_hi:[1,0], 12 v_pk_mul_f32 SGPR pair
+// op_sel_hi:[1,0], 13 v_pk_min_u16 / v_pk_max_u16 (plain, and an SGPR with
+// op_sel_hi:[1,0])
+constexpr int NFORMS = 14;
 
 template <int F>
-__global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *__restrict__ out, int iters) {
+__global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *__restrict__ out, int iters,
+                                                unsigned long long sc) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     f2 a = in[i], b = in[i + gridDim.x * 256];
     const f2 c = f2{0.9990234375f, 1.0009765625f};
@@ -55,6 +63,38 @@ __global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *_
             asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a) : "v"(c));
         } else if constexpr (F == 4) {
             asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(a) : "v"(c), "v"(b));
+        } else if constexpr (F == 6) {
+            asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(a) : "v"(b));
+        } else if constexpr (F == 7) {
+            asm volatile("v_pk_add_f32 %0, %0, 0.5 op_sel_hi:[1,0]" : "+v"(a));
+            float x = a.x, y = a.y;
+            asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(b.x));
+            asm volatile("v_sub_f32 %0, %0, %1" : "+v"(y) : "v"(b.y));
+            a = f2{x, y};
+        } else if constexpr (F == 8) {
+            asm volatile("v_pk_fma_f32 %0, %0, 0.5, %1 op_sel_hi:[1,0,1]" : "+v"(a) : "v"(b));
+        } else if constexpr (F == 9) {
+            asm volatile("v_pk_fma_f32 %0, %0, %1, %2 op_sel_hi:[1,0,1]" : "+v"(a) : "s"(sc), "v"(b));
+        } else if constexpr (F == 10 || F == 11 || F == 12) {
+            if constexpr (F == 10) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a) : "s"(sc));
+            if constexpr (F == 11) asm volatile("v_pk_mul_f32 %0, %0, 2.0 op_sel_hi:[1,0]" : "+v"(a));
+            if constexpr (F == 12) asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(a) : "s"(sc));
+            float x = a.x, y = a.y;  // keep the magnitude and feed b in, scalar forms only
+            asm volatile("v_mul_f32 %0, 0.5, %0" : "+v"(x));
+            asm volatile("v_mul_f32 %0, 0.5, %0" : "+v"(y));
+            asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(b.y));
+            asm volatile("v_add_f32 %0, %0, %1" : "+v"(y) : "v"(b.x));
+            a = f2{x, y};
+        } else if constexpr (F == 13) {
+            unsigned x = __builtin_bit_cast(unsigned, a.x), y = __builtin_bit_cast(unsigned, a.y);
+            const unsigned bx = __builtin_bit_cast(unsigned, b.x), by = __builtin_bit_cast(unsigned, b.y);
+            const unsigned su = (unsigned)sc;
+            asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(x) : "v"(by));
+            asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(y) : "v"(bx));
+            asm volatile("v_pk_min_u16 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(y) : "s"(su));
+            asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(by));
+            asm volatile("v_xor_b32 %0, %0, %1" : "+v"(y) : "v"(bx));
+            a = f2{__builtin_bit_cast(float, x), __builtin_bit_cast(float, y)};
         } else {
             float x = a.x, y = a.y;
             asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(b.y));
@@ -100,7 +140,11 @@ __global__ __launch_bounds__(256) void k_bg_mfma(float *out, int iters) {
 
 template <int F>
 static void launch(const f2 *in, f2 *out, int blocks, int iters, hipStream_t s) {
-    hipLaunchKernelGGL(k_victim<F>, dim3(blocks), dim3(256), 0, s, in, out, iters);
+    // SGPR operand: (0.9990234375f, 1.0009765625f) as one 64-bit pair
+    const float c2[2] = {0.9990234375f, 1.0009765625f};
+    unsigned long long sc;
+    memcpy(&sc, c2, 8);
+    hipLaunchKernelGGL(k_victim<F>, dim3(blocks), dim3(256), 0, s, in, out, iters, sc);
 }
 static void launch_form(int f, const f2 *in, f2 *out, int blocks, int iters, hipStream_t s) {
     switch (f) {
@@ -109,7 +153,15 @@ static void launch_form(int f, const f2 *in, f2 *out, int blocks, int iters, hip
         case 2: launch<2>(in, out, blocks, iters, s); break;
         case 3: launch<3>(in, out, blocks, iters, s); break;
         case 4: launch<4>(in, out, blocks, iters, s); break;
-        default: launch<5>(in, out, blocks, iters, s); break;
+        case 5: launch<5>(in, out, blocks, iters, s); break;
+        case 6: launch<6>(in, out, blocks, iters, s); break;
+        case 7: launch<7>(in, out, blocks, iters, s); break;
+        case 8: launch<8>(in, out, blocks, iters, s); break;
+        case 9: launch<9>(in, out, blocks, iters, s); break;
+        case 10: launch<10>(in, out, blocks, iters, s); break;
+        case 11: launch<11>(in, out, blocks, iters, s); break;
+        case 12: launch<12>(in, out, blocks, iters, s); break;
+        default: launch<13>(in, out, blocks, iters, s); break;
     }
 }
 

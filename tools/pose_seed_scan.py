@@ -1,0 +1,51 @@
+"""Pick the seeded synthetic weights of tests/test_parity_full.py: per weight
+seed, the number of the batch's frames whose ORACLE chain carries a non-NaN
+pose (selected mask -> clean -> moments), i.e. frames the full-frame parity
+test compares downstream.  CPU only (oracle/), the test's session seed.
+Usage: python tools/pose_seed_scan.py DEPTH B wseed [wseed ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, synthetic_state_dict
+    from oracle import features_ref as FR
+    from oracle import frameops as O
+    from oracle import model_ref as R
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    depth, B = int(sys.argv[1]), int(sys.argv[2])
+    s = synth.SyntheticSession(B, seed=77)
+    raw = s.frames(0, B)
+    prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
+    scaled = O.scale_raw_frames(prepped, 0, 100)
+    cl = O.clean_frames(prepped, iters_tail=3)
+    for ws in (int(v) for v in sys.argv[3:]):
+        cfg = ModelConfig(depth=depth, score_thresh_test=0.0)
+        sd = synthetic_state_dict(cfg, ws)
+        d2 = np.zeros(prepped.shape, np.uint8)
+        nkeep = []
+        for a in range(0, B, 8):
+            w, _ = R.forward(sd, cfg, scaled[a:a + 8, ..., None])
+            for j, x in enumerate(w):
+                keep = FR.nms_mask_instances(x["pred_masks"].numpy(), x["scores"].numpy())
+                nkeep.append(len(keep))
+                if keep:
+                    d2[a + j] = x["pred_masks"][keep[0]].numpy()
+        fw = O.get_frame_features(cl, 3, mask=d2)
+        ok = np.isfinite(fw["centroid"][:, 0])
+        print(json.dumps({"depth": depth, "B": B, "wseed": ws, "non_nan_poses": int(ok.sum()),
+                          "nkeep_hist": np.bincount(nkeep, minlength=5).tolist(),
+                          "mask_px": [int(v) for v in d2.reshape(B, -1).sum(1)]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
