@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--no-h2d", action="store_true", help="raw batches already resident in HBM (no H2D in the loop)")
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
     ap.add_argument("--no-extract-loop", action="store_true", help="skip the config-3 extract-loop secondary")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the config-5 secondary (R101-FPN B=64, fp16 mask + keypoint heads)")
     ap.add_argument("--extract-frames", type=int, default=10000)
     ap.add_argument("--extract-chunk", type=int, default=1000)
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
@@ -181,7 +183,7 @@ PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
 PMC_FILE = {"fp16": "r04_pmc_kernels_fp16.json", "fp32": "r04_pmc_kernels_fp32.json"}
 # frame kernels per stage (rocprofv3 symbol substrings) for the PMC bytes
-FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k_morph"),
+FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k_morph", "k_clean_stream"),
                  "moments": ("k_moments",), "crop": ("k_crop",)}
 
 
@@ -442,14 +444,14 @@ def cpu_baseline(nframes: int, dtype_cfg, chunk: int = 16):
                       f"restated in C, mask NMS, C clean/moments/crop; SCORE_THRESH_TEST=0), {dt:.1f} s"}
 
 
-def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs):
+def measure(args, dtype, B, world, rank, raw_host, sess, dist, gather_bufs, depth=None):
     """Warm up, then time args.steps batches of the overlapped hot path with
     the H2D copy of every raw batch from pinned host memory inside the timed
     region.  Returns (seconds (max over ranks), extractor)."""
     import torch
     from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor, OverlappedExtractor
-    cfg = ModelConfig(depth=args.depth, score_thresh_test=0.0)
+    cfg = ModelConfig(depth=depth or args.depth, score_thresh_test=0.0)
     pred = Predictor.from_config(cfg, dtype=dtype, seed=0, weights="synthetic")
     ns = 1 if args.no_overlap else max(1, args.model_streams)
     ex = GPUExtractor(sess.bground_im, sess.roi, pred, ExtractConfig(batch_size=B, model_streams=ns))
@@ -634,6 +636,36 @@ def main():
                     "(tests/test_parity_full.py::test_forward_full_frame[50-32-fp32-4-6] and [50-32-fp32-6-6], "
                     "DESIGN.md section 3)"}
         del exx
+
+    if not args.no_secondary and not args.no_config5 and args.dtype == "fp32" and args.depth == 50:
+        # BASELINE config 5 as stated: R101-FPN, batch 64, fp32 trunk / RPN /
+        # box head with the keypoint + mask heads in fp16 ("mixed"), the same
+        # loop, its own roofline
+        torch.cuda.synchronize()
+        secondary = secondary or {}
+        try:
+            B5 = 64
+            sess5 = synth.SyntheticSession(2 * B5, seed=2000 + rank)
+            f5 = sess5.frames(0, 2 * B5)
+            raw5 = [torch.from_numpy(f5[i * B5:(i + 1) * B5]).pin_memory() for i in range(2)]
+            gb5 = None if gather_bufs is None else \
+                [torch.empty((B5, 2, 80, 80), dtype=torch.uint8, device=gather_bufs[0].device) for _ in range(world)]
+            dt5, ex5, cfg5 = measure(args, "mixed", B5, world, rank, raw5, sess5, dist, gb5, depth=101)
+            c5 = {"value": round(world * args.steps * B5 / dt5, 2), "unit": "frames/s",
+                  "ms_per_step": round(dt5 / args.steps * 1e3, 3), "dtype": "mixed",
+                  "config": {"workload": "BASELINE config 5: R101-FPN Mask/Keypoint R-CNN, batch 64, fp32 backbone / "
+                                         "FPN / RPN / box head, fp16 mask + keypoint heads, same hot path and loop",
+                             "global_batch": B5 * world, "model_gflop_per_frame": round(flops_per_image(cfg5) / 1e9, 2)},
+                  "note": "parity: tests/test_parity_full.py::test_forward_full_frame[101-64-mixed-6-0]"}
+            if not args.no_roofline:
+                per5 = conv_roofline(ex5, raw5[0].cuda())
+                r5 = roofline_line(per5, "fp32", flops_per_image(cfg5) * B5)
+                c5["roofline"] = {k: r5[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernels",
+                                                     "all_conv")}
+            secondary["config5"] = c5
+            del ex5
+        except Exception as e:  # a secondary must never sink the bench line
+            secondary["config5"] = {"value": None, "error": repr(e)[:300]}
 
     if world == 1 and not args.no_secondary and not args.no_extract_loop and args.dtype == "fp32":
         torch.cuda.synchronize()

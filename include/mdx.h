@@ -91,6 +91,12 @@ int64_t mdx_clean_workspace_bytes(int64_t n, int H, int W);
 int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k,
                      const uint8_t *strel, int kh, int kw, int iters, uint8_t *out,
                      uint8_t *workspace, mdx_stream_t stream);
+/* clean_frames kernel choice: 0 = one launch per pass, 1 = the fused streaming
+ * kernel over 256-column strips (default), 2 = over 512-column strips.  The
+ * fused kernel serves median 3 + opening with the 9x9 ellipse, 3 iterations
+ * (the extract path); other parameters run the per-pass kernels.  Returns the
+ * previous mode. */
+int mdx_clean_set_mode(int mode);
 
 /* get_frame_features(frames, frame_threshold=thr, mask=mask, use_cc=*) +
  * im_moment_features -- M/proc/proc.py:237-302, :518-549.  Largest contour
@@ -101,6 +107,16 @@ int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k,
 int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W,
                       double thr, double *centroid, double *orientation, double *axis_length,
                       double *area, mdx_stream_t stream);
+/* mdx_frame_moments with a caller workspace of
+ * mdx_frame_moments_workspace_bytes(n, H, W) bytes: the threshold / mask
+ * bit-packing runs as its own launch over every CU (one wave per 64 pixels),
+ * the contour following per frame reads the packed words (the path the
+ * Python layer takes).  workspace NULL = packing inside the per-frame
+ * kernel. */
+int64_t mdx_frame_moments_workspace_bytes(int64_t n, int H, int W);
+int mdx_frame_moments_ws(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W, double thr,
+                         double *centroid, double *orientation, double *axis_length, double *area,
+                         void *workspace, mdx_stream_t stream);
 
 /* crop_and_rotate_frame(frame, center, angle, crop_size=(cw, ch)) for every
  * frame of src0 (and of src1 when not NULL, same centers/angles) --
@@ -295,6 +311,11 @@ int mdx_winograd_tile(int H, int W, int mode);
  * transformed weights of the fp32 3x3 layers with Cin >= 64). */
 int mdx_conv_set_winograd_min_cin(int cin);
 int mdx_conv_winograd_min_cin(void);
+/* Model handle: run each fp32 Winograd layer in image slices whose transformed
+ * input (or output) is at most `mb` MB, so the transforms' intermediate
+ * tensors stay in the Infinity Cache between the three launches; 0 (default)
+ * = one pass over the batch.  Returns the previous value. */
+int mdx_model_set_wino_slice(int mb);
 /* Winograd GEMMs with Cout % 256 == 0 and Cin % 32 == 0 on the 256x256
  * LDS-DMA fp32 kernel: mode 0 never (default: measured no faster), 1 when the
  * batched launch has at least min_wgs workgroups, 2 whenever eligible; returns

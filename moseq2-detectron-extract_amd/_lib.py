@@ -40,7 +40,10 @@ SIGNATURES = {
     "mdx_scale_frames": (I32, [P, I64, P, P, P]),
     "mdx_clean_workspace_bytes": (I64, [I64, I32, I32]),
     "mdx_clean_frames": (I32, [P, I64, I32, I32, I32, P, I32, I32, I32, P, P, P]),
+    "mdx_clean_set_mode": (I32, [I32]),
     "mdx_frame_moments": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P]),
+    "mdx_frame_moments_workspace_bytes": (I64, [I64, I32, I32]),
+    "mdx_frame_moments_ws": (I32, [P, P, I64, I32, I32, F64, P, P, P, P, P, P]),
     "mdx_crop_rotate": (I32, [P, P, I64, I32, I32, P, P, I32, I32, P, P, P, P]),
     "mdx_frame_scalars": (I32, [P, P, I64, I32, I32, F64, F64, P, I32, P, P, P, P, P]),
     "mdx_bground_median": (I32, [P, I64, I32, I32, I32, P, P, P]),
@@ -86,6 +89,7 @@ SIGNATURES = {
     "mdx_format_tsv_rows": (I64, [P, P, I32, I64, P, I64]),
     "mdx_conv2d_dual": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_model_set_fuse_shortcut": (I32, [I32]),
+    "mdx_model_set_wino_slice": (I32, [I32]),
     "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),
     "mdx_preprocess_s2d": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, P, P]),
     "mdx_preprocess_s2d_folded": (I32, [P, I32, I32, I32, P, I32, I32, I32, P, P]),

@@ -253,6 +253,275 @@ __global__ __launch_bounds__(CT_THREADS) void k_morph(const uint8_t *__restrict_
 }
 
 // ---------------------------------------------------------------------------
+// clean_frames fused: the extract path's exact chain -- medianBlur(3)
+// (replicate border), erode x3 and dilate x3 with the 9x9 ellipse (OpenCV's
+// neutral border per pass) -- as ONE streaming kernel (M/proc/proc.py:480-515).
+//
+// One workgroup per (frame, strip of SW output columns) walks the frame from
+// top to bottom, one row per step, as a 7-stage line-buffer pipeline: every
+// stage consumes the row its predecessor produced in the previous step and
+// emits one row, so each pixel of each pass is computed once (no vertical
+// halo; the horizontal halo is the 25-column strip margin) and the frame is
+// read once and written once.  Stage inputs travel through double-buffered
+// LDS rows (u16 per pixel, one barrier per step); each stage's vertical
+// window lives in registers (a 9-row ring, the step loop unrolled by 9).
+//
+//   stage 0 (waves MW..): median of the 3x3 window -- columns sorted with
+//     v_min3 / v_med3 / v_max3, median = med3(max3(lows), med3(mids),
+//     min3(highs)) (exact); these lanes also stream the raw rows in, 9
+//     steps ahead (registers -> LDS).
+//   stages 1..6 (waves 0..MW-1), 4 output columns per lane as two u16 pairs:
+//     the ellipse rows are spans of half-width 0 / 3 / 4 (rows 0,8 / 1,2,6,7
+//     / 3,4,5), so per input row the lane computes the three span minima
+//     (v_pk_min_u16, shared between its two pairs) and per output row the
+//     min over the 9 ring rows.  Dilation runs as erosion of the inverted
+//     image (max(a,b) = 255 - min(255-a, 255-b)): stage 3 writes 255 - v, the
+//     last stage inverts back, so all six stages share one instruction stream
+//     and one neutral value (255) for pixels outside the frame.
+// Rows / columns outside the frame are written as the neutral value, which
+// is exactly OpenCV's per-pass border handling.
+// ---------------------------------------------------------------------------
+template <int SW>
+struct CleanStream {
+    static constexpr int E(int s) { return 4 * (6 - s); }            // stage s: extra columns each side
+    static constexpr int NQ(int s) { return SW / 4 + E(s) / 2; }      // quads (4 columns) of stage s
+    static constexpr int MORPH_LANES = 6 * (SW / 4) + 30;              // stages 1..6
+    static constexpr int MW = (MORPH_LANES + 63) / 64;                 // morph waves
+    static constexpr int DW = (NQ(0) + 63) / 64;                       // median / loader waves
+    static constexpr int THREADS = 64 * (MW + DW);
+    static constexpr int PU = SW + 64;                                 // u16 per LDS row
+    static constexpr int PB = SW + 64;                                 // raw bytes per LDS row
+    static constexpr int RAWB = SW + 50;                               // raw columns per row: X0-25 .. X0+SW+24
+    static constexpr int LB = (RAWB + 64 * DW - 1) / (64 * DW);        // raw bytes per loader lane per row
+    // step t: the median consumes raw row t - 26 and emits row t - 27; stage
+    // s >= 1 consumes row t - IN(s) and emits row t - OUT(s)
+    static constexpr int IN(int s) { return 28 + 5 * (s - 1); }
+    static constexpr int OUT(int s) { return IN(s) + 4; }
+};
+
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) { return pk_op<false>(a, b); }
+// one VALU instruction each (written out: the compiler shares min(a, b)
+// between a min3 and a med3 of the same operands and then emits neither)
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+template <int SW>
+__global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const uint8_t *__restrict__ src, int H,
+                                                                             int W, int strips,
+                                                                             uint8_t *__restrict__ out) {
+    using C = CleanStream<SW>;
+    __shared__ __attribute__((aligned(16))) uint16_t stg[6][2][C::PU];  // stage 0..5 outputs, by step parity
+    __shared__ __attribute__((aligned(16))) uint8_t raw[2][C::PB];      // raw rows, by step parity
+    const long long frame = blockIdx.x / strips;
+    const int X0 = (int)(blockIdx.x % strips) * SW, BX = X0 - 28;      // LDS column 0 = image column BX
+    const uint8_t *s = src + frame * H * W;
+    uint8_t *o = out + frame * H * W;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const bool med = wave >= C::MW;
+    const int NSTEP = H + C::OUT(6) + 1;
+    constexpr uint32_t NEUT = 0x00FF00FFu;
+
+    // ---- per-lane role ----
+    int stage = 0, q = -1, x0 = 0;
+    if (!med) {
+        int l = tid, st = 1;
+        while (st <= 6 && l >= C::NQ(st)) l -= C::NQ(st++);
+        if (st <= 6) {
+            stage = st;
+            q = l;
+            x0 = X0 - C::E(st) + 4 * l;
+        }
+    } else {
+        const int l = tid - 64 * C::MW;
+        if (l < C::NQ(0)) {
+            q = l;
+            x0 = X0 - C::E(0) + 4 * l;
+        }
+    }
+    // outside-column masks of this lane's two pairs (0xFF in the outside halves)
+    uint32_t cm[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int c0 = x0 + 2 * p, c1 = c0 + 1;
+        cm[p] = ((c0 < 0 || c0 >= W) ? 0xFFu : 0u) | ((c1 < 0 || c1 >= W) ? 0xFF0000u : 0u);
+    }
+    const uint32_t inv = stage == 3 || stage == 6 ? NEUT : 0u;  // dilation: work on 255 - v
+    const int idx = x0 - BX;                                      // u16 / byte column of this lane's quad
+    const int out_off = stage >= 1 ? C::OUT(stage) : 27;
+
+    // ---- register file shared by the two roles (one array, so the compiler
+    // allocates it once): morph lanes hold their 9-row ring of span minima
+    // (slot k: R[6k .. 6k+5] = span-0 pair 0/1, span-3 pair 0/1, span-4 pair
+    // 0/1); median lanes hold their 3-row window of raw columns (R[0..17])
+    // and the 9-deep raw-row prefetch queue (R[18..44]) ----
+    static_assert(C::LB <= 3, "loader queue exceeds its register share");
+    uint32_t R[54];
+#pragma unroll
+    for (int k = 0; k < 54; ++k) R[k] = NEUT;
+#define MV(kk, c) R[(kk) * 6 + (c)]
+#define QV(k, m) R[18 + (k) * 3 + (m)]
+#define R0(k, p) R[(k) * 6 + (p)]
+#define R3(k, p) R[(k) * 6 + 2 + (p)]
+#define R4(k, p) R[(k) * 6 + 4 + (p)]
+    const int ll = tid - 64 * C::MW;
+    uint32_t s3p[2] = {NEUT, NEUT};  // morph lanes: the previous input row's span-3 minima
+    // raw row r, clamped (replicate border), into queue slot k
+    auto load_row = [&](int k, int r) {
+        const int gy = min(max(r, 0), H - 1);
+#pragma unroll
+        for (int m = 0; m < C::LB; ++m) {
+            const int c = ll + 64 * C::DW * m;
+            const int gx = min(max(BX + 3 + c, 0), W - 1);
+            QV(k, m) = c < C::RAWB ? (uint32_t)s[(long long)gy * W + gx] : 0u;
+        }
+    };
+    auto store_row = [&](int k, int par) {
+#pragma unroll
+        for (int m = 0; m < C::LB; ++m) {
+            const int c = ll + 64 * C::DW * m;
+            if (c < C::RAWB) raw[par][3 + c] = (uint8_t)QV(k, m);
+        }
+    };
+    if (med) {
+        load_row(0, -26);  // consumed by the median at step 0
+        store_row(0, 1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) load_row(k, k - 25);
+#pragma unroll
+        for (int k = 0; k < 18; ++k) R[k] = 255u;
+    }
+    __syncthreads();
+
+    for (int t0 = 0; t0 < NSTEP; t0 += 9) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int t = t0 + k;
+            if (t >= NSTEP) continue;  // uniform (no break: the ring indices must stay compile-time)
+            const int rd = (t - 1) & 1, wr = t & 1;
+            if (med) {
+                // raw row t - 25 for the next step, then prefetch row t - 16
+                store_row(k, wr);
+                load_row(k, t - 16);
+                if (q >= 0) {
+                    const uint32_t *rw = reinterpret_cast<const uint32_t *>(raw[rd]);
+                    const uint32_t d0 = rw[idx / 4 - 1], d1 = rw[idx / 4], d2 = rw[idx / 4 + 1];
+                    const int kk = k % 3;
+                    MV(kk, 0) = d0 >> 24;
+                    MV(kk, 1) = d1 & 255u;
+                    MV(kk, 2) = (d1 >> 8) & 255u;
+                    MV(kk, 3) = (d1 >> 16) & 255u;
+                    MV(kk, 4) = d1 >> 24;
+                    MV(kk, 5) = d2 & 255u;
+                    uint32_t lo[6], mi[6], hi[6];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        lo[c] = umin3(MV(0, c), MV(1, c), MV(2, c));
+                        mi[c] = umed3(MV(0, c), MV(1, c), MV(2, c));
+                        hi[c] = umax3(MV(0, c), MV(1, c), MV(2, c));
+                    }
+                    uint32_t m4[4];
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+                        m4[p] = umed3(umax3(lo[p], lo[p + 1], lo[p + 2]), umed3(mi[p], mi[p + 1], mi[p + 2]),
+                                      umin3(hi[p], hi[p + 1], hi[p + 2]));
+                    const int row = t - out_off;
+                    uint32_t a = m4[0] | (m4[1] << 16), b = m4[2] | (m4[3] << 16);
+                    if (row < 0 || row >= H) {
+                        a = b = NEUT;
+                    } else {
+                        a |= cm[0];
+                        b |= cm[1];
+                    }
+                    *reinterpret_cast<uint2 *>(&stg[0][wr][idx]) = make_uint2(a, b);
+                }
+            } else if (q >= 0) {
+                const uint16_t *in = stg[stage - 1][rd];
+                const uint2 u0 = *reinterpret_cast<const uint2 *>(in + idx - 4);
+                const uint2 u1 = *reinterpret_cast<const uint2 *>(in + idx);
+                const uint2 u2 = *reinterpret_cast<const uint2 *>(in + idx + 4);
+                // pairs (x + s, x + s + 1) for s = -4 .. 6
+                const uint32_t qm4 = u0.x, qm2 = u0.y, q0 = u1.x, q2 = u1.y, q4 = u2.x, q6 = u2.y;
+                const uint32_t qm3 = __builtin_amdgcn_alignbyte(qm2, qm4, 2);
+                const uint32_t qm1 = __builtin_amdgcn_alignbyte(q0, qm2, 2);
+                const uint32_t q1 = __builtin_amdgcn_alignbyte(q2, q0, 2);
+                const uint32_t q3 = __builtin_amdgcn_alignbyte(q4, q2, 2);
+                const uint32_t q5 = __builtin_amdgcn_alignbyte(q6, q4, 2);
+                const uint32_t u = pmin(pmin(pmin(qm1, q0), pmin(q1, q2)), q3);
+                const uint32_t s3a = pmin(u, pmin(qm3, qm2)), s3b = pmin(u, pmin(q4, q5));
+                // the ring keeps, per row r, the span-3 minimum of rows r-1 and r
+                // (the ellipse's half-width-3 rows come in adjacent pairs)
+                R3(k, 0) = pmin(s3a, s3p[0]);
+                R3(k, 1) = pmin(s3b, s3p[1]);
+                s3p[0] = s3a;
+                s3p[1] = s3b;
+                R4(k, 0) = pmin(s3a, pmin(qm4, q4));
+                R4(k, 1) = pmin(s3b, pmin(qm2, q6));
+                R0(k, 0) = q0;
+                R0(k, 1) = q2;
+                // ellipse rows 0..8 of the output row = ring slots k+1 .. k+9:
+                // row 0 span 0, rows 1-2 (pair at slot k+3), rows 3-5 span 4,
+                // rows 6-7 (pair at slot k+8), row 8 span 0
+                uint32_t v[2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const uint32_t a = pmin(R0((k + 1) % 9, p), R0(k, p));
+                    const uint32_t b = pmin(R3((k + 3) % 9, p), R3((k + 8) % 9, p));
+                    const uint32_t c = pmin(pmin(R4((k + 4) % 9, p), R4((k + 5) % 9, p)), R4((k + 6) % 9, p));
+                    v[p] = pmin(pmin(a, b), c);
+                }
+                const int row = t - out_off;
+                if (stage < 6) {
+                    uint32_t a = (v[0] ^ inv) | cm[0], b = (v[1] ^ inv) | cm[1];
+                    if (row < 0 || row >= H) a = b = NEUT;
+                    *reinterpret_cast<uint2 *>(&stg[stage][wr][idx]) = make_uint2(a, b);
+                } else if (row >= 0 && row < H) {
+                    const uint32_t a = v[0] ^ inv, b = v[1] ^ inv;
+                    const uint32_t packed = __builtin_amdgcn_perm(b, a, 0x06040200u);  // bytes 0, 2 of a, b
+                    uint8_t *dst = o + (long long)row * W + x0;
+                    if (x0 >= 0 && x0 + 4 <= W && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+                        *reinterpret_cast<uint32_t *>(dst) = packed;
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            if (x0 + c >= 0 && x0 + c < W) dst[c] = (uint8_t)(packed >> (8 * c));
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+#undef MV
+#undef QV
+#undef R0
+#undef R3
+#undef R4
+}
+
+// the ellipse 9x9 (cv2.getStructuringElement(MORPH_ELLIPSE, (9, 9))) row spans
+// the fused kernel hard-codes
+__host__ inline bool is_ellipse9(const uint8_t *strel, int kh, int kw) {
+    static const int hw[9] = {0, 3, 3, 4, 4, 4, 3, 3, 0};
+    if (kh != 9 || kw != 9) return false;
+    for (int r = 0; r < 9; ++r)
+        for (int c = 0; c < 9; ++c)
+            if ((strel[r * 9 + c] != 0) != (c >= 4 - hw[r] && c <= 4 + hw[r])) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // moments: one workgroup per frame.
 // The blob mask (frame > thr) & mask is bit-packed into LDS with a 1-pixel
 // zero frame (findContours pads the image with zeros).  Every pixel that can
@@ -418,13 +687,46 @@ __device__ void moments_to_features(const Green &g, double *cen, double *ori, do
     ax[1] = k * sqrt((mu20 + mu02 - common) / m00);
 }
 
-// ithr: the threshold as an integer, v > thr <=> (int)v > ithr for uint8 v
-template <bool SMALL>
+// The blob mask bit-packed by every CU (the threshold / mask pass is
+// embarrassingly parallel; only the contour following is per frame): one
+// wave per 64 padded pixels of a row, one byte of frame and mask per lane,
+// the predicate gathered by one ballot into two words of the padded layout
+// k_moments uses (bit b of word (py, wx) = pixel (py - 1, 32 wx + b - 1)).
+// Per frame PH * pww words + one zero slack word.
+__global__ __launch_bounds__(256) void k_moments_pack(const uint8_t *__restrict__ frames,
+                                                      const uint8_t *__restrict__ mask, int H, int W, int ithr,
+                                                      int pww, int chunks, long long nwaves,
+                                                      uint32_t *__restrict__ bits) {
+    const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gw >= nwaves) return;  // whole waves
+    const int lane = threadIdx.x & 63;
+    const int PH = H + 2;
+    const int c = (int)(gw % chunks);
+    const long long rowg = gw / chunks;
+    const int py = (int)(rowg % PH);
+    const long long f = rowg / PH;
+    const int x = 64 * c - 1 + lane;
+    bool b = false;
+    if (py >= 1 && py <= H && x >= 0 && x < W) {
+        const long long i = f * (long long)H * W + (long long)(py - 1) * W + x;
+        b = (int)frames[i] > ithr && (!mask || mask[i]);
+    }
+    const unsigned long long m = __ballot(b);
+    uint32_t *o = bits + f * ((long long)PH * pww + 1) + (long long)py * pww;
+    if (lane == 0) o[2 * c] = (uint32_t)m;
+    if (lane == 1 && 2 * c + 1 < pww) o[2 * c + 1] = (uint32_t)(m >> 32);
+    if (lane == 2 && c == 0 && py == PH - 1) o[pww] = 0u;  // the slack word after the last row
+}
+
+// ithr: the threshold as an integer, v > thr <=> (int)v > ithr for uint8 v.
+// PRE: the bits come packed from k_moments_pack (`pre`), else packed here.
+template <bool SMALL, bool PRE>
 __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restrict__ frames,
                                                          const uint8_t *__restrict__ mask, int H, int W,
                                                          int ithr, double *__restrict__ cen,
                                                          double *__restrict__ ori, double *__restrict__ axl,
-                                                         double *__restrict__ area, int pww) {
+                                                         double *__restrict__ area, int pww,
+                                                         const uint32_t *__restrict__ pre) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
     __shared__ unsigned long long s_best;
     __shared__ Green s_g;
@@ -434,6 +736,10 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
     const int PH = H + 2, PW = W + 2;
     const int nwords = PH * pww;
     if (threadIdx.x == 0) s_best = 0ull;
+    if constexpr (PRE) {
+        const uint32_t *src = pre + f * ((int64_t)nwords + 1);
+        for (int w = threadIdx.x; w <= nwords; w += MOM_THREADS) bits[w] = src[w];
+    } else
     // bit-pack (frame > thr) & mask into LDS, one padded 32-pixel word per
     // lane: bit b of word (py, wx) is unpadded pixel (py - 1, 32 wx + b - 1).
     // Interior words read their 32 pixels [32 wx, 32 wx + 32) with two 16-B
@@ -527,19 +833,24 @@ __global__ __launch_bounds__(MOM_THREADS) void k_moments(const uint8_t *__restri
 // ---------------------------------------------------------------------------
 // crop_and_rotate_frame: one workgroup per frame, both sources share the map.
 // ---------------------------------------------------------------------------
+// (blockIdx.y: a block of output rows, so a batch's crops spread over
+// several workgroups per frame; each recomputes the 6-double map)
+constexpr int CROP_RB = 4;
+
 __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, const uint8_t *__restrict__ src1,
                                               int H, int W, const double *__restrict__ center,
                                               const double *__restrict__ angle, int cw, int ch,
                                               uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,
                                               int *__restrict__ window) {
     const int64_t f = blockIdx.x;
+    const bool lead = blockIdx.y == 0 && threadIdx.x == 0;  // writes the window
     const double cxc = center[2 * f], cyc = center[2 * f + 1], ang_deg = angle[f];
     uint8_t *o0 = out0 + f * (int64_t)cw * ch;
     uint8_t *o1 = out1 ? out1 + f * (int64_t)cw * ch : nullptr;
     bool zero = isnan(ang_deg) || isnan(cxc) || isnan(cyc) || cxc < 0 || cyc < 0;
     int xmin = 0, ymin = 0, pw = 0, ph = 0;
     double M[6] = {0, 0, 0, 0, 0, 0};
-    if (window && threadIdx.x == 0) {  // -1 x4: the reference returns zeros before computing a window
+    if (window && lead) {  // -1 x4: the reference returns zeros before computing a window
         window[4 * f] = window[4 * f + 1] = window[4 * f + 2] = window[4 * f + 3] = -1;
     }
     if (!zero) {
@@ -547,7 +858,7 @@ __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, 
         const int xmax = (int)(cxc + cw / 2) + cw;
         ymin = (int)(cyc - ch / 2) + ch;
         const int ymax = (int)(cyc + ch / 2) + ch;
-        if (window && threadIdx.x == 0) {
+        if (window && lead) {
             window[4 * f] = xmin;
             window[4 * f + 1] = xmax;
             window[4 * f + 2] = ymin;
@@ -582,7 +893,9 @@ __global__ __launch_bounds__(256) void k_crop(const uint8_t *__restrict__ src0, 
     const int round_delta = AB_SCALE / TAB / 2;
     const uint8_t *s0 = src0 + f * (int64_t)H * W;
     const uint8_t *s1 = src1 ? src1 + f * (int64_t)H * W : nullptr;
-    for (int i = threadIdx.x; i < cw * ch; i += 256) {
+    const int rows = (ch + CROP_RB - 1) / CROP_RB;
+    const int i0 = (int)blockIdx.y * rows * cw, i1 = min(ch, ((int)blockIdx.y + 1) * rows) * cw;
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
         if (zero) {
             o0[i] = 0;
             if (o1) o1[i] = 0;
@@ -751,6 +1064,18 @@ extern "C" int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t 
 
 extern "C" int64_t mdx_clean_workspace_bytes(int64_t n, int H, int W) { return n * H * W; }
 
+// clean_frames kernel choice: 0 = one launch per pass (k_median3, k_morph),
+// 1 = the fused streaming kernel over 256-column strips (default), 2 = over
+// 512-column strips.  The fused kernel serves the extract path's chain
+// (median 3, opening with the 9x9 ellipse, 3 iterations); anything else runs
+// the per-pass kernels.  Returns the previous mode.
+static int g_clean_mode = 1;
+extern "C" int mdx_clean_set_mode(int mode) {
+    const int old = g_clean_mode;
+    if (mode >= 0 && mode <= 2) g_clean_mode = mode;
+    return old;
+}
+
 extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k, const uint8_t *strel,
                                 int kh, int kw, int iters, uint8_t *out, uint8_t *workspace, mdx_stream_t stream) {
     MDX_REQUIRE(src && out && src != out, "mdx_clean_frames: null or aliased buffers");
@@ -797,6 +1122,19 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
     MDX_REQUIRE(n <= 65535, "mdx_clean_frames: n > 65535 per call");
     MDX_REQUIRE((long long)H * W < (1ll << 31), "mdx_clean_frames: frame too large");
     hipStream_t s = as_stream(stream);
+    if (g_clean_mode != 0 && median_k == 3 && iters == 3 && is_ellipse9(strel, kh, kw)) {
+        if (g_clean_mode == 2) {
+            const int strips = (int)ceil_div(W, 512);
+            hipLaunchKernelGGL(k_clean_stream<512>, dim3((unsigned)(n * strips)), dim3(CleanStream<512>::THREADS), 0,
+                               s, src, H, W, strips, out);
+        } else {
+            const int strips = (int)ceil_div(W, 256);
+            hipLaunchKernelGGL(k_clean_stream<256>, dim3((unsigned)(n * strips)), dim3(CleanStream<256>::THREADS), 0,
+                               s, src, H, W, strips, out);
+        }
+        MDX_CHECK_LAUNCH("mdx_clean_frames");
+        return MDX_OK;
+    }
     const int tiles_x = (int)ceil_div(W, CT_W), tiles_y = (int)ceil_div(H, CT_H);
     const dim3 grid(tiles_x * tiles_y, (unsigned)n);
     const int LW = CT_W + kw - 1, LH = CT_H + kh - 1, LP = (LW + 7) & ~3;
@@ -821,9 +1159,14 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
     return MDX_OK;
 }
 
-extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W, double thr,
-                                 double *centroid, double *orientation, double *axis_length, double *area,
-                                 mdx_stream_t stream) {
+extern "C" int64_t mdx_frame_moments_workspace_bytes(int64_t n, int H, int W) {
+    if (n <= 0 || H <= 0 || W <= 0) return 0;
+    return n * ((int64_t)(H + 2) * ceil_div(W + 2, 32) + 1) * 4;
+}
+
+extern "C" int mdx_frame_moments_ws(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W, double thr,
+                                    double *centroid, double *orientation, double *axis_length, double *area,
+                                    void *workspace, mdx_stream_t stream) {
     MDX_REQUIRE(frames && centroid && orientation && axis_length, "mdx_frame_moments: null pointer");
     MDX_REQUIRE(H > 0 && W > 0, "mdx_frame_moments: bad shape");
     if (n == 0) return MDX_OK;
@@ -833,14 +1176,37 @@ extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int
     MDX_REQUIRE(n <= 0x7fffffff, "mdx_frame_moments: n too large");
     // v > thr for uint8 v <=> v > floor(thr) (NaN: never)
     const int ithr = thr != thr ? 255 : thr < 0 ? -1 : thr >= 255 ? 255 : (int)floor(thr);
-    if (H <= 512 && W <= 512)
-        hipLaunchKernelGGL(k_moments<true>, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask,
-                           H, W, ithr, centroid, orientation, axis_length, area, pww);
+    hipStream_t s = as_stream(stream);
+    const uint32_t *pre = static_cast<const uint32_t *>(workspace);
+    if (pre) {
+        const int chunks = (pww + 1) / 2;
+        const long long nwaves = n * (long long)(H + 2) * chunks;
+        MDX_REQUIRE(ceil_div(nwaves, 4) < (1ll << 31), "mdx_frame_moments: too many frames per call");
+        hipLaunchKernelGGL(k_moments_pack, dim3((unsigned)ceil_div(nwaves, 4)), dim3(256), 0, s, frames, mask, H, W,
+                           ithr, pww, chunks, nwaves, (uint32_t *)workspace);
+    }
+    const bool small = H <= 512 && W <= 512;
+    if (pre && small)
+        hipLaunchKernelGGL((k_moments<true, true>), dim3((unsigned)n), dim3(MOM_THREADS), lds, s, frames, mask, H, W,
+                           ithr, centroid, orientation, axis_length, area, pww, pre);
+    else if (pre)
+        hipLaunchKernelGGL((k_moments<false, true>), dim3((unsigned)n), dim3(MOM_THREADS), lds, s, frames, mask, H, W,
+                           ithr, centroid, orientation, axis_length, area, pww, pre);
+    else if (small)
+        hipLaunchKernelGGL((k_moments<true, false>), dim3((unsigned)n), dim3(MOM_THREADS), lds, s, frames, mask, H, W,
+                           ithr, centroid, orientation, axis_length, area, pww, pre);
     else
-        hipLaunchKernelGGL(k_moments<false>, dim3((unsigned)n), dim3(MOM_THREADS), lds, as_stream(stream), frames, mask,
-                           H, W, ithr, centroid, orientation, axis_length, area, pww);
+        hipLaunchKernelGGL((k_moments<false, false>), dim3((unsigned)n), dim3(MOM_THREADS), lds, s, frames, mask, H,
+                           W, ithr, centroid, orientation, axis_length, area, pww, pre);
     MDX_CHECK_LAUNCH("mdx_frame_moments");
     return MDX_OK;
+}
+
+extern "C" int mdx_frame_moments(const uint8_t *frames, const uint8_t *mask, int64_t n, int H, int W, double thr,
+                                 double *centroid, double *orientation, double *axis_length, double *area,
+                                 mdx_stream_t stream) {
+    return mdx_frame_moments_ws(frames, mask, n, H, W, thr, centroid, orientation, axis_length, area, nullptr,
+                                stream);
 }
 
 extern "C" int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t n, int H, int W,
@@ -850,7 +1216,7 @@ extern "C" int mdx_crop_rotate(const uint8_t *src0, const uint8_t *src1, int64_t
     MDX_REQUIRE(!src1 == !out1, "mdx_crop_rotate: src1/out1 must both be set or both NULL");
     MDX_REQUIRE(cw > 0 && ch > 0 && H > 0 && W > 0, "mdx_crop_rotate: bad shape");
     if (n == 0) return MDX_OK;
-    hipLaunchKernelGGL(k_crop, dim3((unsigned)n), dim3(256), 0, as_stream(stream), src0, src1, H, W, center,
+    hipLaunchKernelGGL(k_crop, dim3((unsigned)n, CROP_RB), dim3(256), 0, as_stream(stream), src0, src1, H, W, center,
                        angle_deg, cw, ch, out0, out1, (int *)window);
     MDX_CHECK_LAUNCH("mdx_crop_rotate");
     return MDX_OK;

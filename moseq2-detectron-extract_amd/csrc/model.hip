@@ -18,6 +18,7 @@
 // captured into a HIP graph.  Every intermediate lives in a per-stream arena:
 // one allocation sized by a dry run of the same code, bump-allocated per
 // forward, so forwards on different streams run concurrently.
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -114,6 +115,11 @@ struct Model {
     int hdt = 0;       // mask + keypoint heads (cfg.head_dtype; = dt unless mixed)
     bool stem_fold = false;  // stem over the 2-channel (value, inside) s2d input (fp32 handles)
     bool fuse_sc = false;    // projection shortcuts fused into conv3 (Block::c3sc)
+    // the Winograd policy and fp32 split mode the weights were prepared for
+    // (Winograd U tiles, bf16 planes): a later switch runs the layers it did
+    // not prepare on the fallback kernels, reported once
+    int create_wino = 0, create_split = 0;
+    std::atomic<bool> policy_warned{false};
     size_t es = 4;     // activation element size
     std::vector<void *> allocs;
     ConvW stem;
@@ -606,6 +612,25 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
 }
 
 // ------------------------------------------------------------ forward
+// Winograd layers in image slices (knob, MB of transformed input per slice;
+// 0 = the whole batch in one pass): the input transform, batched GEMM and
+// output transform of a slice then move V and M through the 256 MB Infinity
+// Cache instead of HBM.  Profiled forwards keep one pass (the probe times
+// the three launches of one call).
+static int g_wino_slice_mb = 0;
+extern "C" int mdx_model_set_wino_slice(int mb) {
+    const int old = g_wino_slice_mb;
+    if (mb >= 0) g_wino_slice_mb = mb;
+    return old;
+}
+static int wino_slice_images(int N, int H, int W, int cin, int cout, int m, bool profile) {
+    if (g_wino_slice_mb <= 0 || profile) return N;
+    const double tiles = (double)((H + m - 1) / m) * ((W + m - 1) / m);
+    const double v = tiles * (m + 2) * (m + 2) * 4.0 * (cin > cout ? cin : cout);  // V or M bytes per image
+    const int per = (int)((double)g_wino_slice_mb * (1 << 20) / v);
+    return per < 1 ? 1 : (per >= N ? N : per);
+}
+
 struct Fwd {
     Model &m;
     Ctx &c;
@@ -689,8 +714,15 @@ struct Fwd {
                                             wm, (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
             else {
                 mdx::x3_weight_planes(wx6);  // the split-plane GEMMs take U's planes (K = Cin % 32 == 0)
-                chk(mdx_conv3x3_winograd((const float *)x, N, H, W, cw.cin, wu, cw.b, cw.cout, relu ? 1 : 0, wm,
-                                         (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
+                // image slices whose transformed tensors stay in the Infinity
+                // Cache between the three launches (mdx_model_set_wino_slice)
+                const int ns = wino_slice_images(N, H, W, cw.cin, cw.cout, wm, m.profile);
+                for (int i0 = 0; i0 < N; i0 += ns) {
+                    const int n = std::min(ns, N - i0);
+                    chk(mdx_conv3x3_winograd((const float *)x + (size_t)i0 * H * W * cw.cin, n, H, W, cw.cin, wu, cw.b,
+                                             cw.cout, relu ? 1 : 0, wm, (float *)out + (size_t)i0 * OH * OW * cw.cout,
+                                             c.wino_base, (int64_t)c.wino_cap, s));
+                }
                 mdx::x3_weight_planes(nullptr);
             }
             if (m.profile) {
@@ -1058,6 +1090,8 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     m->es = cfg->dtype == 1 ? 2 : 4;
     m->stem_fold = cfg->dtype == 0 && g_stem_fold;
     m->fuse_sc = g_fuse_sc == 2 || (g_fuse_sc == 1 && cfg->dtype == 0);
+    m->create_wino = mdx_conv_winograd_enabled();
+    m->create_split = mdx_conv_fp32_split();
     std::string err;
     if (!pack(*m, sd, err)) {
         set_error("mdx_model_create: %s", err.c_str());
@@ -1092,6 +1126,13 @@ extern "C" int mdx_model_forward(mdx_model_t model, const uint8_t *frames, int B
     MDX_REQUIRE(!out->masks || out->mask_plane_stride >= (int64_t)h * w,
                 "mdx_model_forward: mask_plane_stride < h*w");
     hipStream_t s = as_stream(stream);
+    if (m.dt == 0 && (mdx_conv_winograd_enabled() != m.create_wino || mdx_conv_fp32_split() != m.create_split) &&
+        !m.policy_warned.exchange(true))
+        fprintf(stderr,
+                "mdx_model_forward: this handle's weights were prepared for Winograd policy %d / fp32 split %d, "
+                "now %d / %d: layers without prepared weights run on the fallback kernels (create the handle "
+                "after setting the policy)\n",
+                m.create_wino, m.create_split, mdx_conv_winograd_enabled(), mdx_conv_fp32_split());
     Ctx &c = *get_ctx(m, s);
     const int r = reserve(m, c, B, h, w, s);
     if (r != MDX_OK) return r;
@@ -1139,6 +1180,13 @@ extern "C" int mdx_model_debug_fill(mdx_model_t model, int B, int h, int w, int 
     MDX_REQUIRE(model && byte >= 0 && byte <= 255, "mdx_model_debug_fill: bad arguments");
     Model &m = *(Model *)model;
     hipStream_t s = as_stream(stream);
+    if ((mdx_conv_winograd_enabled() != m.create_wino || mdx_conv_fp32_split() != m.create_split) &&
+        !m.policy_warned.exchange(true))
+        fprintf(stderr,
+                "mdx_model_forward: this handle's weights were prepared for Winograd policy %d / fp32 split %d, "
+                "now %d / %d: layers without prepared weights run on the fallback kernels (create the handle "
+                "after setting the policy)\n",
+                m.create_wino, m.create_split, mdx_conv_winograd_enabled(), mdx_conv_fp32_split());
     Ctx &c = *get_ctx(m, s);
     const int r = reserve(m, c, B, h, w, s);
     if (r != MDX_OK) return r;

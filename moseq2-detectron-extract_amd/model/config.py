@@ -98,7 +98,11 @@ class ModelConfig:
 
     @property
     def in_channels(self) -> int:
-        return 1 if self.input_format == "L" else 3
+        """Stem input channels: Detectron2 builds the backbone for
+        ShapeSpec(channels=len(MODEL.PIXEL_MEAN)); an 'L' model with the base
+        config's three means has a 3-channel stem (its 1-channel image is
+        broadcast over the three normalisations in preprocess_image)."""
+        return len(self.pixel_mean) if self.input_format == "L" else 3
 
     @classmethod
     def from_yaml(cls, path, **overrides) -> "ModelConfig":
@@ -150,12 +154,12 @@ class ModelConfig:
         need(len(self.keypoint_conv_dims) <= 16, "MODEL.ROI_KEYPOINT_HEAD.CONV_DIMS", self.keypoint_conv_dims,
              "at most 16 convs")
         need(self.input_format in ("RGB", "BGR", "L"), "INPUT.FORMAT", self.input_format, "'RGB', 'BGR' or 'L'")
-        nch = 1 if self.input_format == "L" else 3
-        for key, v in (("MODEL.PIXEL_MEAN", self.pixel_mean), ("MODEL.PIXEL_STD", self.pixel_std)):
-            # one value per input channel (a 1-channel model may carry the
-            # base config's three equal values)
-            need(len(v) == nch or (nch == 1 and len(set(v)) == 1), key, v,
-                 f"{nch} value(s) for INPUT.FORMAT {self.input_format!r}")
+        # one value per stem input channel: 3 for 'RGB' / 'BGR', 1 or 3 for
+        # 'L' (a 3-value 'L' model has a 3-channel stem, see in_channels)
+        need(len(self.pixel_mean) in ((1, 3) if self.input_format == "L" else (3,)), "MODEL.PIXEL_MEAN",
+             self.pixel_mean, f"1 or 3 values for INPUT.FORMAT 'L', 3 otherwise")
+        need(len(self.pixel_std) == len(self.pixel_mean), "MODEL.PIXEL_STD", self.pixel_std,
+             "one value per MODEL.PIXEL_MEAN entry")
         for k in ("rpn_bbox_reg_weights", "box_reg_weights"):
             w = getattr(self, k)
             need(len(w) == 4 and all(v > 0 for v in w), k, w, "four positive weights")

@@ -287,8 +287,10 @@ def frame_moments(frames, mask=None, frame_threshold=10.0):
     ori = torch.empty((n,), dtype=torch.float64, device=src.device)
     ax = torch.empty((n, 2), dtype=torch.float64, device=src.device)
     area = torch.empty((n,), dtype=torch.float64, device=src.device)
-    call("mdx_frame_moments", _ptr(src), _ptr(m), n, H, W, float(frame_threshold), _ptr(cen), _ptr(ori), _ptr(ax),
-         _ptr(area), _stream())
+    ws = torch.empty(max(1, call("mdx_frame_moments_workspace_bytes", n, H, W)), dtype=torch.uint8,
+                     device=src.device)  # the bit-packed blob masks (packed over every CU)
+    call("mdx_frame_moments_ws", _ptr(src), _ptr(m), n, H, W, float(frame_threshold), _ptr(cen), _ptr(ori), _ptr(ax),
+         _ptr(area), _ptr(ws), _stream())
     return {"centroid": cen, "orientation": ori, "axis_length": ax, "area": area}
 
 

@@ -82,6 +82,36 @@ def test_clean_random_edges(mdx):
     np.testing.assert_array_equal(proc.clean_frames(x, iters_tail=2), O.clean_frames(x, iters_tail=2))
 
 
+@pytest.mark.parametrize("mode", [1, 2, 0])
+def test_clean_fused_streaming_kernel(mdx, session, raw, mode):
+    """The extract path's chain (median 3, opening with the 9x9 ellipse, 3
+    iterations) on the fused streaming kernel (mdx_clean_set_mode 1: 256-
+    column strips, 2: 512) and on the per-pass kernels (0), bit for bit vs
+    the oracle: full frames, random bytes on ragged shapes (one strip, strip
+    + 1 column, tiny and 1-row / 1-column frames, an image narrower than the
+    25-column halo), the extreme values 0 / 255 everywhere."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    from moseq2_detectron_extract_amd._lib import call
+    old = call("mdx_clean_set_mode", mode)
+    try:
+        prepped, _ = O.prep_raw_frames(raw[:8], session.bground_im, session.roi, 0, 100, fix_invalid_pixels=False)
+        np.testing.assert_array_equal(proc.clean_frames(prepped, iters_tail=3), O.clean_frames(prepped, iters_tail=3))
+        rng = np.random.default_rng(17)
+        for shape in [(2, 423, 511), (2, 64, 256), (2, 37, 257), (1, 9, 513), (3, 1, 40), (2, 30, 1), (2, 5, 7),
+                      (1, 200, 1030)]:
+            x = rng.integers(0, 256, size=shape, dtype=np.uint8)
+            # sparse blobs as well as noise: long constant runs exercise the borders
+            x[0] = np.where(rng.random(shape[1:]) < 0.7, 0, x[0])
+            np.testing.assert_array_equal(proc.clean_frames(x, iters_tail=3), O.clean_frames(x, iters_tail=3),
+                                          err_msg=str(shape))
+        for v in (0, 255):
+            x = np.full((2, 50, 300), v, np.uint8)
+            np.testing.assert_array_equal(proc.clean_frames(x, iters_tail=3), O.clean_frames(x, iters_tail=3))
+    finally:
+        call("mdx_clean_set_mode", old)
+
+
 def test_frame_features(mdx, session, raw):
     from oracle import frameops as O
     from moseq2_detectron_extract_amd import proc

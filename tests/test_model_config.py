@@ -84,6 +84,16 @@ def test_every_cfg_key_reaches_the_abi(mdx):
                                  ).aspect_ratios == (0.5, 1.0, 2.0)
     assert ModelConfig.from_yaml(d2_config(**{"INPUT.FORMAT": "L", "MODEL.PIXEL_MEAN": [1.12],
                                               "MODEL.PIXEL_STD": [5.79]})).in_channels == 1
+    # 'L' with the base config's three means: Detectron2's stem takes len(PIXEL_MEAN) = 3 channels
+    # (ADVICE r4), so the state dict must carry a (64, 3, 7, 7) stem and does
+    from moseq2_detectron_extract_amd.model.weights import state_dict_spec
+    c3 = ModelConfig.from_yaml(d2_config(**{"INPUT.FORMAT": "L", "MODEL.PIXEL_MEAN": [1.12] * 3,
+                                            "MODEL.PIXEL_STD": [5.79] * 3}))
+    assert c3.in_channels == 3
+    assert [shape for name, shape, _ in state_dict_spec(c3) if name.endswith("stem.conv1.weight")] == [(64, 3, 7, 7)]
+    with pytest.raises(NotImplementedError, match="PIXEL_STD"):
+        ModelConfig.from_yaml(d2_config(**{"INPUT.FORMAT": "L", "MODEL.PIXEL_MEAN": [1.12] * 3,
+                                           "MODEL.PIXEL_STD": [5.79]}))
 
 
 @pytest.mark.parametrize("key,val", [

@@ -35,7 +35,31 @@ def main():
     prep_noinp = proc.FramePrep(sess.bground_im, sess.roi, 0, 100, False)
     p0, inv = prep_noinp(raw, return_invalid=True)
 
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+
+    def clean_mode(m):
+        def f():
+            old = call("mdx_clean_set_mode", m)
+            try:
+                proc.clean_frames(prepped, iters_tail=3)
+            finally:
+                call("mdx_clean_set_mode", old)
+        return f
+
+    def moments_nows():
+        n, H, W = cleaned.shape
+        out = [torch.empty((n, 2), dtype=torch.float64, device="cuda"), torch.empty((n,), dtype=torch.float64,
+               device="cuda"), torch.empty((n, 2), dtype=torch.float64, device="cuda")]
+        call("mdx_frame_moments", ctypes.c_void_p(cleaned.data_ptr()), ctypes.c_void_p(mask.data_ptr()), n, H, W, 3.0,
+             *[ctypes.c_void_p(t.data_ptr()) for t in out], None,
+             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
     ops = {
+        "clean_perpass": clean_mode(0),
+        "clean_stream256": clean_mode(1),
+        "clean_stream512": clean_mode(2),
+        "moments_in_kernel_pack": moments_nows,
         "prep_noinpaint": lambda: prep_noinp(raw),
         "prep_inpaint": lambda: prep(raw),
         "inpaint_only": lambda: proc.fill_invalid_pixels(p0.clone(), inv),
