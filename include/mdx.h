@@ -92,10 +92,10 @@ int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int median_k,
                      const uint8_t *strel, int kh, int kw, int iters, uint8_t *out,
                      uint8_t *workspace, mdx_stream_t stream);
 /* clean_frames kernel choice: 0 = one launch per pass, 1 = the fused streaming
- * kernel over 256-column strips (default), 2 = over 512-column strips.  The
- * fused kernel serves median 3 + opening with the 9x9 ellipse, 3 iterations
- * (the extract path); other parameters run the per-pass kernels.  Returns the
- * previous mode. */
+ * kernel with the strip width chosen by batch size (default), 2 = 256-column
+ * strips, 3 = 512-column strips.  The fused kernel serves median 3 + opening
+ * with the 9x9 ellipse, 3 iterations (the extract path); other parameters run
+ * the per-pass kernels.  Returns the previous mode. */
 int mdx_clean_set_mode(int mode);
 
 /* get_frame_features(frames, frame_threshold=thr, mask=mask, use_cc=*) +

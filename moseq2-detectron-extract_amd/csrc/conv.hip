@@ -217,7 +217,7 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
 // SB: one LDS stage instead of two (a second barrier per K-step before the
 // next stage overwrites it), so three workgroups fit a CU instead of two
 // (launched as k_conv_sb).
-template <typename T, typename TO, int BN_, bool DUAL, bool PW, bool SB>
+template <typename T, typename TO, int BN_, bool DUAL, bool PW, bool SB, bool AFP = false>
 __device__ __forceinline__ void conv_body(ConvArgs &a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -395,6 +395,30 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            } else if constexpr (AFP && TJ >= 4) {
+                // A fragments double-buffered: row tile i + 1's fragment is
+                // read while tile i's 4 TJ MFMAs issue (the plain form below
+                // compiles to one register quad reloaded per tile behind an
+                // lgkmcnt(0)); same MFMA order per accumulator: bit-identical
+                float4v bf[TJ];
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
+                float4v a_cur = *reinterpret_cast<const float4v *>(Ab + koff);
+#pragma unroll
+                for (int i = 0; i < TI; ++i) {
+                    const float4v a_nxt =
+                        i + 1 < TI ? *reinterpret_cast<const float4v *>(Ab + (i + 1) * 16 * PITCH + koff) : a_cur;
+                    // keep the read above the MFMAs (the scheduler would sink it
+                    // below them to save the four registers)
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[e], bf[j][e], acc[i][j], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    a_cur = a_nxt;
+                }
             } else {
                 // B fragments first and the row tile outermost: the MFMAs of
                 // tile i start once bf and af[i] have arrived (per accumulator
@@ -501,9 +525,9 @@ template <typename T, typename TO, int BN_, bool DUAL = false, bool PW = false>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     conv_body<T, TO, BN_, DUAL, PW, false>(a);
 }
-template <typename T, typename TO, int BN_, bool DUAL = false>
+template <typename T, typename TO, int BN_, bool DUAL = false, bool AFP = false>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sb(ConvArgs a) {
-    conv_body<T, TO, BN_, DUAL, true, true>(a);
+    conv_body<T, TO, BN_, DUAL, true, true, AFP>(a);
 }
 // the single-stage schedule for general layers (padded / KxK: the stem, the
 // Cin < 128 3x3 layers)
@@ -2121,6 +2145,14 @@ extern "C" int mdx_conv_set_pointwise(int on) {
 // the fp16 register-staged PW layers (default: fp16 loop 3924 -> 4009 fps,
 // config 5 3310 -> 3320), 0 the two-stage k_conv instances
 static int g_conv_sb = 4;
+// k_conv_sb's fp32 A fragments double-buffered in registers (1) or reloaded
+// per row tile (0, default) -- mdx_conv_set_sb_afp; bit-identical sums
+static int g_sb_afp = 0;
+extern "C" int mdx_conv_set_sb_afp(int on) {
+    const int old = g_sb_afp;
+    if (on >= 0) g_sb_afp = on ? 1 : 0;
+    return old;
+}
 extern "C" int mdx_conv_set_single_stage(int on) {
     const int old = g_conv_sb;
     g_conv_sb = on;
@@ -2536,7 +2568,13 @@ general:
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
-        if (narrow && pw && sb)                                                                             \
+        if (narrow && pw && sb && g_sb_afp)                                                                 \
+            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS),             \
+                               conv_lds(64, a.ksteps, true), s, a);                                         \
+        else if (!narrow && pw && sb && g_sb_afp)                                                           \
+            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 128, false, true>), grid, dim3(CONV_THREADS),            \
+                               conv_lds(128, a.ksteps, true), s, a);                                        \
+        else if (narrow && pw && sb)                                                                        \
             hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64>), grid, dim3(CONV_THREADS),          \
                                conv_lds(64, a.ksteps, true), s, a);                                         \
         else if (!narrow && pw && sb)                                                                       \
@@ -2920,7 +2958,11 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
     } else if (bn == 64) {
-        if (g_pw && g_conv_sb) {
+        if (g_pw && g_conv_sb && g_sb_afp) {
+            hipLaunchKernelGGL((k_conv_sb<float, float, 64, false, true>), grid, dim3(CONV_THREADS),
+                               conv_lds(64, a.ksteps, true), s, a);
+            gemm_kernel = MDX_CONV_KERNEL_SB64;
+        } else if (g_pw && g_conv_sb) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 64>), grid, dim3(CONV_THREADS),
                                conv_lds(64, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB64;
@@ -2932,7 +2974,11 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             gemm_kernel = MDX_CONV_KERNEL_REG64;
         }
     } else {
-        if (g_pw && g_conv_sb) {
+        if (g_pw && g_conv_sb && g_sb_afp) {
+            hipLaunchKernelGGL((k_conv_sb<float, float, 128, false, true>), grid, dim3(CONV_THREADS),
+                               conv_lds(128, a.ksteps, true), s, a);
+            gemm_kernel = MDX_CONV_KERNEL_SB128;
+        } else if (g_pw && g_conv_sb) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 128>), grid, dim3(CONV_THREADS),
                                conv_lds(128, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB128;

@@ -324,7 +324,7 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
                                                                              uint8_t *__restrict__ out) {
     using C = CleanStream<SW>;
     __shared__ __attribute__((aligned(16))) uint16_t stg[6][2][C::PU];  // stage 0..5 outputs, by step parity
-    __shared__ __attribute__((aligned(16))) uint8_t raw[2][C::PB];      // raw rows, by step parity
+    __shared__ __attribute__((aligned(16))) uint8_t raw[9][C::PB];      // raw rows of the current 9-step block
     const long long frame = blockIdx.x / strips;
     const int X0 = (int)(blockIdx.x % strips) * SW, BX = X0 - 28;      // LDS column 0 = image column BX
     const uint8_t *s = src + frame * H * W;
@@ -358,6 +358,9 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
         const int c0 = x0 + 2 * p, c1 = c0 + 1;
         cm[p] = ((c0 < 0 || c0 >= W) ? 0xFFu : 0u) | ((c1 < 0 || c1 >= W) ? 0xFF0000u : 0u);
     }
+    bool cok[4];  // this lane's output columns inside the frame
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cok[c] = x0 + c >= 0 && x0 + c < W;
     const uint32_t inv = stage == 3 || stage == 6 ? NEUT : 0u;  // dilation: work on 255 - v
     const int idx = x0 - BX;                                      // u16 / byte column of this lane's quad
     const int out_off = stage >= 1 ? C::OUT(stage) : 27;
@@ -365,58 +368,61 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
     // ---- register file shared by the two roles (one array, so the compiler
     // allocates it once): morph lanes hold their 9-row ring of span minima
     // (slot k: R[6k .. 6k+5] = span-0 pair 0/1, span-3 pair 0/1, span-4 pair
-    // 0/1); median lanes hold their 3-row window of raw columns (R[0..17])
-    // and the 9-deep raw-row prefetch queue (R[18..44]) ----
-    static_assert(C::LB <= 3, "loader queue exceeds its register share");
+    // 0/1); median lanes hold their 3-row window of raw columns (R[0..17]) ----
     uint32_t R[54];
 #pragma unroll
     for (int k = 0; k < 54; ++k) R[k] = NEUT;
 #define MV(kk, c) R[(kk) * 6 + (c)]
-#define QV(k, m) R[18 + (k) * 3 + (m)]
 #define R0(k, p) R[(k) * 6 + (p)]
 #define R3(k, p) R[(k) * 6 + 2 + (p)]
 #define R4(k, p) R[(k) * 6 + 4 + (p)]
     const int ll = tid - 64 * C::MW;
     uint32_t s3p[2] = {NEUT, NEUT};  // morph lanes: the previous input row's span-3 minima
-    // raw row r, clamped (replicate border), into queue slot k
+    // raw rows stream in a 9-step block ahead: at the start of block b the
+    // median lanes store block b's 9 rows (loaded at the start of block b-1)
+    // into LDS and load block b+1's into registers of their own (not shared
+    // with the ring: no wait on these loads anywhere but the next block's
+    // store, 9 steps later).  Columns past the strip read a clamped, valid
+    // byte that the store skips.
+    uint32_t qv[9][C::LB];
     auto load_row = [&](int k, int r) {
         const int gy = min(max(r, 0), H - 1);
 #pragma unroll
         for (int m = 0; m < C::LB; ++m) {
             const int c = ll + 64 * C::DW * m;
             const int gx = min(max(BX + 3 + c, 0), W - 1);
-            QV(k, m) = c < C::RAWB ? (uint32_t)s[(long long)gy * W + gx] : 0u;
-        }
-    };
-    auto store_row = [&](int k, int par) {
-#pragma unroll
-        for (int m = 0; m < C::LB; ++m) {
-            const int c = ll + 64 * C::DW * m;
-            if (c < C::RAWB) raw[par][3 + c] = (uint8_t)QV(k, m);
+            qv[k][m] = (uint32_t)s[(long long)gy * W + gx];
         }
     };
     if (med) {
-        load_row(0, -26);  // consumed by the median at step 0
-        store_row(0, 1);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) load_row(k, k - 25);
+        for (int k = 0; k < 9; ++k) load_row(k, k - 26);  // block 0: steps 0..8 consume raw rows -26 .. -18
 #pragma unroll
         for (int k = 0; k < 18; ++k) R[k] = 255u;
     }
-    __syncthreads();
 
     for (int t0 = 0; t0 < NSTEP; t0 += 9) {
+        if (med) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+#pragma unroll
+                for (int m = 0; m < C::LB; ++m) {
+                    const int c = ll + 64 * C::DW * m;
+                    if (c < C::RAWB) raw[k][3 + c] = (uint8_t)qv[k][m];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) load_row(k, t0 + 9 + k - 26);
+        }
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
             const int t = t0 + k;
             if (t >= NSTEP) continue;  // uniform (no break: the ring indices must stay compile-time)
             const int rd = (t - 1) & 1, wr = t & 1;
             if (med) {
-                // raw row t - 25 for the next step, then prefetch row t - 16
-                store_row(k, wr);
-                load_row(k, t - 16);
                 if (q >= 0) {
-                    const uint32_t *rw = reinterpret_cast<const uint32_t *>(raw[rd]);
+                    const uint32_t *rw = reinterpret_cast<const uint32_t *>(raw[k]);  // raw row t - 26
                     const uint32_t d0 = rw[idx / 4 - 1], d1 = rw[idx / 4], d2 = rw[idx / 4 + 1];
                     const int kk = k % 3;
                     MV(kk, 0) = d0 >> 24;
@@ -489,22 +495,18 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
                     *reinterpret_cast<uint2 *>(&stg[stage][wr][idx]) = make_uint2(a, b);
                 } else if (row >= 0 && row < H) {
                     const uint32_t a = v[0] ^ inv, b = v[1] ^ inv;
-                    const uint32_t packed = __builtin_amdgcn_perm(b, a, 0x06040200u);  // bytes 0, 2 of a, b
                     uint8_t *dst = o + (long long)row * W + x0;
-                    if (x0 >= 0 && x0 + 4 <= W && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
-                        *reinterpret_cast<uint32_t *>(dst) = packed;
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < 4; ++c)
-                            if (x0 + c >= 0 && x0 + c < W) dst[c] = (uint8_t)(packed >> (8 * c));
-                    }
+                    // byte stores (rows of an odd-width frame are not 4-B aligned)
+                    if (cok[0]) dst[0] = (uint8_t)a;
+                    if (cok[1]) dst[1] = (uint8_t)(a >> 16);
+                    if (cok[2]) dst[2] = (uint8_t)b;
+                    if (cok[3]) dst[3] = (uint8_t)(b >> 16);
                 }
             }
             __syncthreads();
         }
     }
 #undef MV
-#undef QV
 #undef R0
 #undef R3
 #undef R4
@@ -1065,14 +1067,16 @@ extern "C" int mdx_scale_frames(const uint8_t *in, int64_t count, const uint8_t 
 extern "C" int64_t mdx_clean_workspace_bytes(int64_t n, int H, int W) { return n * H * W; }
 
 // clean_frames kernel choice: 0 = one launch per pass (k_median3, k_morph),
-// 1 = the fused streaming kernel over 256-column strips (default), 2 = over
-// 512-column strips.  The fused kernel serves the extract path's chain
-// (median 3, opening with the 9x9 ellipse, 3 iterations); anything else runs
-// the per-pass kernels.  Returns the previous mode.
+// 1 = the fused streaming kernel, strip width by batch size (default: 512
+// columns from 16 strips per launch on, else 256), 2 = 256-column strips,
+// 3 = 512-column strips.  The fused kernel
+// serves the extract path's chain (median 3, opening with the 9x9 ellipse,
+// 3 iterations); anything else runs the per-pass kernels.  Returns the
+// previous mode.
 static int g_clean_mode = 1;
 extern "C" int mdx_clean_set_mode(int mode) {
     const int old = g_clean_mode;
-    if (mode >= 0 && mode <= 2) g_clean_mode = mode;
+    if (mode >= 0 && mode <= 3) g_clean_mode = mode;
     return old;
 }
 
@@ -1123,7 +1127,12 @@ extern "C" int mdx_clean_frames(const uint8_t *src, int64_t n, int H, int W, int
     MDX_REQUIRE((long long)H * W < (1ll << 31), "mdx_clean_frames: frame too large");
     hipStream_t s = as_stream(stream);
     if (g_clean_mode != 0 && median_k == 3 && iters == 3 && is_ellipse9(strel, kh, kw)) {
-        if (g_clean_mode == 2) {
+        // auto: the 512-column strips (least halo work per frame: the kernel is
+        // VALU-issue bound, and in the extract loop its CU time, not its
+        // latency, is what the concurrent forwards feel) unless the batch is
+        // too small to give a few dozen CUs work
+        const bool wide = g_clean_mode == 3 || (g_clean_mode == 1 && n * ceil_div(W, 512) >= 16);
+        if (wide) {
             const int strips = (int)ceil_div(W, 512);
             hipLaunchKernelGGL(k_clean_stream<512>, dim3((unsigned)(n * strips)), dim3(CleanStream<512>::THREADS), 0,
                                s, src, H, W, strips, out);

@@ -108,6 +108,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         ok = True
     finally:
         src.close()
+        ex.close()
         if writer is not None:
             if ok:
                 writer.close()
@@ -144,9 +145,11 @@ def _run_two_pass(src, batches, ex, config, true_depth, finished):
     tracking (tracking_exchange).  Pass 2: each chunk's front again from its
     raw frames, the selected masks re-pasted, crops at the exchanged pose."""
     comps = []
+    trace = _mem_trace()
     for idx, raw in src.iterate(device=True, batches=batches):
         comp, host = ex.features_pass_compact(raw)
         comps.append((np.asarray(idx), comp, host))
+        trace(f"pass1 chunk {len(comps)}")
     if config.select_instances:  # the instance tracker is sequential over the session too
         _select_exchange_compact(ex, comps, src)
     else:
@@ -163,8 +166,24 @@ def _run_two_pass(src, batches, ex, config, true_depth, finished):
             raise RuntimeError("second pass: the frame source returned another chunk")
         parts.append(finished(ex.finish_chunk_compact(comp, raw, cen, kp, ang, fl, host["axis_length"], idx, 0,
                                                       true_depth)))
+        trace(f"pass2 chunk {len(parts)}")
     comps.clear()
     return parts
+
+
+def _mem_trace():
+    """MDX_MEM_TRACE=1: device memory (torch allocator) after each chunk of
+    the two-pass loop, on stderr (the sharded memory test reads it)."""
+    if not os.environ.get("MDX_MEM_TRACE"):
+        return lambda what: None
+    import sys
+    import torch
+
+    def trace(what):
+        torch.cuda.synchronize()
+        print(f"[mdx mem] {what}: allocated {torch.cuda.memory_allocated() / 2**20:.1f} MB, "
+              f"peak {torch.cuda.max_memory_allocated() / 2**20:.1f} MB", file=sys.stderr, flush=True)
+    return trace
 
 
 def _all_ranks(flag: bool) -> bool:

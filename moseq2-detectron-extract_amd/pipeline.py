@@ -294,6 +294,30 @@ class GPUExtractor:
         cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
         return prepped, cleaned
 
+    def front_chunk(self, raw: torch.Tensor):
+        """front() over a chunk in batch_size slices (the same per-frame
+        results): the inpaint / clean workspaces stay one batch's size."""
+        n = raw.shape[0]
+        B = max(1, int(self.cfg.batch_size))
+        if n <= B:
+            return self.front(raw)
+        y0, y1, x0, x1 = self.prep.crop(raw.shape[1], raw.shape[2])
+        prepped = torch.empty((n, y1 - y0, x1 - x0), dtype=torch.uint8, device=raw.device)
+        cleaned = torch.empty_like(prepped)
+        for i in range(0, n, B):
+            p, c = self.front(raw[i:i + B])
+            prepped[i:i + B].copy_(p)
+            cleaned[i:i + B].copy_(c)
+        return prepped, cleaned
+
+    def close(self) -> None:
+        """Release the extractor's device state now (the pipeline, its
+        streams and results, the prep workspaces) rather than when the
+        cyclic garbage collector gets to the extractor <-> pipeline cycle."""
+        self._pipe = None
+        self._streams = []
+        self.prep._ws = None
+
     def tail(self, prepped: torch.Tensor, cleaned: torch.Tensor, inf: dict):
         """Moments of the selected mask, angle, crops."""
         feats = proc.frame_moments(cleaned, inf["d2_mask"], float(self.cfg.frame_threshold))
@@ -484,8 +508,7 @@ class GPUExtractor:
             raw = raw_reader(fr)
             raw = raw if torch.is_tensor(raw) else torch.from_numpy(np.ascontiguousarray(raw))
             raw = raw.to(comp["device"])
-            prepped = self.prep(raw)
-            cleaned = proc.clean_frames(prepped, iters_tail=self.cfg.iters_tail, strel_tail=self.strel)
+            prepped, cleaned = self.front_chunk(raw)
             d2 = self._paste_selected(comp, fr, prepped.shape[1:])
             feats = proc.frame_moments(cleaned, d2, float(self.cfg.frame_threshold))
             idx = np.asarray(fr)
@@ -524,7 +547,7 @@ class GPUExtractor:
         finish_chunk."""
         raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else \
             torch.from_numpy(np.ascontiguousarray(raw)).to(comp["device"])
-        prepped, cleaned = self.front(raw)
+        prepped, cleaned = self.front_chunk(raw)
         if "sel_logits" not in comp:
             self._sel_default(comp)
         d2 = self._paste_selected(comp, np.arange(len(comp["nkeep"])), prepped.shape[1:])

@@ -82,11 +82,12 @@ def test_clean_random_edges(mdx):
     np.testing.assert_array_equal(proc.clean_frames(x, iters_tail=2), O.clean_frames(x, iters_tail=2))
 
 
-@pytest.mark.parametrize("mode", [1, 2, 0])
+@pytest.mark.parametrize("mode", [1, 2, 3, 0])
 def test_clean_fused_streaming_kernel(mdx, session, raw, mode):
     """The extract path's chain (median 3, opening with the 9x9 ellipse, 3
-    iterations) on the fused streaming kernel (mdx_clean_set_mode 1: 256-
-    column strips, 2: 512) and on the per-pass kernels (0), bit for bit vs
+    iterations) on the fused streaming kernel (mdx_clean_set_mode 1: strip
+    width by batch, 2: 256-column strips, 3: 512) and on the per-pass kernels
+    (0), bit for bit vs
     the oracle: full frames, random bytes on ragged shapes (one strip, strip
     + 1 column, tiny and 1-row / 1-column frames, an image narrower than the
     25-column halo), the extreme values 0 / 255 everywhere."""

@@ -57,8 +57,9 @@ def main():
 
     ops = {
         "clean_perpass": clean_mode(0),
-        "clean_stream256": clean_mode(1),
-        "clean_stream512": clean_mode(2),
+        "clean_stream_auto": clean_mode(1),
+        "clean_stream256": clean_mode(2),
+        "clean_stream512": clean_mode(3),
         "moments_in_kernel_pack": moments_nows,
         "prep_noinpaint": lambda: prep_noinp(raw),
         "prep_inpaint": lambda: prep(raw),

@@ -32,18 +32,31 @@ def main():
         cfg = ModelConfig(depth=depth, score_thresh_test=0.0)
         sd = synthetic_state_dict(cfg, ws)
         d2 = np.zeros(prepped.shape, np.uint8)
-        nkeep = []
-        for a in range(0, B, 8):
-            w, _ = R.forward(sd, cfg, scaled[a:a + 8, ..., None])
-            for j, x in enumerate(w):
-                keep = FR.nms_mask_instances(x["pred_masks"].numpy(), x["scores"].numpy())
-                nkeep.append(len(keep))
-                if keep:
-                    d2[a + j] = x["pred_masks"][keep[0]].numpy()
+        nkeep, near = [], []
+        try:
+            for a in range(0, B, 8):
+                w, _ = R.forward(sd, cfg, scaled[a:a + 8, ..., None])
+                for j, x in enumerate(w):
+                    keep = FR.nms_mask_instances(x["pred_masks"].numpy(), x["scores"].numpy()) \
+                        if len(x["scores"]) else []
+                    nkeep.append(len(keep))
+                    if keep:
+                        d2[a + j] = x["pred_masks"][keep[0]].numpy()
+                        # pixels of the selected mask's pasted probability this close to the
+                        # 0.5 threshold: where an fp32 rounding difference can flip a pixel
+                        p = x["pred_mask_probs"][keep[0]].numpy()
+                        near.append(int((np.abs(p - 0.5) < 1e-5).sum()))
+                    else:
+                        near.append(0)
+        except Exception as e:  # a seed the oracle chain cannot run (e.g. no detection at all)
+            print(json.dumps({"depth": depth, "B": B, "wseed": ws, "error": repr(e)[:200]}), flush=True)
+            continue
         fw = O.get_frame_features(cl, 3, mask=d2)
         ok = np.isfinite(fw["centroid"][:, 0])
         print(json.dumps({"depth": depth, "B": B, "wseed": ws, "non_nan_poses": int(ok.sum()),
                           "nkeep_hist": np.bincount(nkeep, minlength=5).tolist(),
+                          "frames_with_near_threshold_px": int((np.asarray(near) > 0).sum()),
+                          "near_threshold_px": near,
                           "mask_px": [int(v) for v in d2.reshape(B, -1).sum(1)]}), flush=True)
 
 
