@@ -311,6 +311,11 @@ int mdx_winograd_tile(int H, int W, int mode);
  * transformed weights of the fp32 3x3 layers with Cin >= 64). */
 int mdx_conv_set_winograd_min_cin(int cin);
 int mdx_conv_winograd_min_cin(void);
+/* fp32 single-stage GEMM (k_conv_sb): 1 = the A fragments of the next row
+ * tile are read from LDS while the current tile's MFMAs issue (two register
+ * quads), 0 = one quad reloaded per tile.  Same MFMA order: bit-identical.
+ * Returns the previous value. */
+int mdx_conv_set_sb_afp(int on);
 /* Model handle: run each fp32 Winograd layer in image slices whose transformed
  * input (or output) is at most `mb` MB, so the transforms' intermediate
  * tensors stay in the Infinity Cache between the three launches; 0 (default)

@@ -60,6 +60,7 @@ SIGNATURES = {
     "mdx_conv_set_single_stage": (I32, [I32]),
     "mdx_conv_set_fp32_split": (I32, [I32]),
     "mdx_conv_set_x3_single_stage": (I32, [I32]),
+    "mdx_conv_set_sb_afp": (I32, [I32]),
     "mdx_conv_fp32_split": (I32, []),
     "mdx_roi_align_get_mode": (I32, []),
     "mdx_conv_set_x3_narrow": (I32, [I32]),

@@ -1115,18 +1115,23 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
     try:
         for ks in ((1, 3) if Cout % 8 == 0 else (1,)):
             outs = []
-            for single in (0, 1):
+            # single-stage with the A-fragment prefetch (mdx_conv_set_sb_afp) too
+            for single, afp in ((0, 0), (1, 0), (1, 1)):
                 call("mdx_conv_set_single_stage", single)
-                out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
-                call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0, 0,
-                     0, P(out), ks, P(ws), nb, None)
+                old_afp = call("mdx_conv_set_sb_afp", afp)
+                try:
+                    out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
+                    call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0,
+                         0, 0, P(out), ks, P(ws), nb, None)
+                finally:
+                    call("mdx_conv_set_sb_afp", old_afp)
                 kid, ks_ = ctypes.c_int(), ctypes.c_int()
                 call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
                 assert kid.value in ((18, 19) if single else (14, 15)), kid.value
                 err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
                 assert err < 1e-4, (ks, single, err)
                 outs.append(out)
-            assert torch.equal(outs[0], outs[1]), ks
+            assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2]), ks
     finally:
         for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
                          "mdx_conv_set_stream1x1_f32"), olds):

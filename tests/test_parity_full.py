@@ -77,15 +77,18 @@ SEED = 77               # synthetic session of the batch
 # seeded synthetic weights per depth, chosen so the downstream chain is
 # compared on (nearly) every frame: R101 with seed 0 selects detections off
 # the animal on 61 of 64 frames (NaN poses on both sides, nothing compared
-# downstream), seed 1 selects on-animal masks on every frame; R50 with seed 0
+# downstream), seed 1 selects on-animal masks on every frame.  R50 with seed 0
 # gave 22 / 32 non-NaN oracle poses.  tools/pose_seed_scan.py 50 32 over
-# seeds 0-30 (non-NaN oracle poses / frames whose selected mask has pixels
-# within 1e-5 of the 0.5 paste threshold, where an fp32 rounding difference
-# flips a pixel): 0: 22 / 1, 3: 31 / 22, 11: 32 / 5, 14: 30 / 1, 21: 32 / 15,
-# the rest < 30 poses.  Seed 3 ran on the MI355X with 20-24 / 32 identical
-# selected masks (its masks are large, ~4.7k px), below MIN_SEL_EXACT;
-# seed 14 keeps both bars (30 poses, 1 near-threshold frame)
-WEIGHT_SEED = {50: 14, 101: 1}
+# seeds 0-50 measures per seed the non-NaN oracle poses, the frames whose
+# selected mask has pixels within 1e-5 of the 0.5 paste threshold (where an
+# fp32 rounding difference flips a pixel) and the frames where flipping one
+# such pixel moves the oracle's own pose past the fp32 bounds.  Candidates
+# with >= 30 poses: 3 (31 poses, 22 near-threshold frames: 20-24 / 32
+# identical selected masks on the MI355X, below MIN_SEL_EXACT), 14 (30, 1,
+# but that frame's flip turns the angle 1.36 deg: failed the pose bound),
+# 11 (32, 5: 28-31 / 32 identical), 34 (31, 2), 35 (32, 0).  Seed 35: every
+# frame posed, no pixel near the threshold.
+WEIGHT_SEED = {50: 35, 101: 1}
 ORACLE_CHUNK = 8        # frames per oracle forward (its intermediates of a whole batch would not fit)
 
 _ORACLE = {}

@@ -53,9 +53,34 @@ def main():
             continue
         fw = O.get_frame_features(cl, 3, mask=d2)
         ok = np.isfinite(fw["centroid"][:, 0])
+        # pose sensitivity: flip each near-threshold pixel of the selected mask
+        # alone and re-measure the oracle pose (a frame whose angle moves by
+        # more than the fp32 tolerance of tests/test_parity_full.py -- 1 deg --
+        # or whose centroid moves by more than 0.5 px fails there as soon as
+        # the GPU rounds that pixel the other way)
+        risky = []
+        for f in range(B):
+            if not near[f] or not ok[f]:
+                continue
+            ang0 = np.rad2deg(fw["orientation"][f])
+            worst = 0.0
+            # the near pixels of frame f (recomputed from its oracle probabilities)
+            w, _ = R.forward(sd, cfg, scaled[f:f + 1, ..., None])
+            keep = FR.nms_mask_instances(w[0]["pred_masks"].numpy(), w[0]["scores"].numpy())
+            p = w[0]["pred_mask_probs"][keep[0]].numpy()
+            for yx in np.argwhere(np.abs(p - 0.5) < 1e-5)[:16]:
+                m = d2[f:f + 1].copy()
+                m[0, yx[0], yx[1]] ^= 1
+                g = O.get_frame_features(cl[f:f + 1], 3, mask=m)
+                da = abs(((np.rad2deg(g["orientation"][0]) - ang0) + 90) % 180 - 90)
+                dc = float(np.abs(g["centroid"][0] - fw["centroid"][f]).max())
+                worst = max(worst, da if dc <= 0.5 else 999.0)
+            if worst > 1.0:
+                risky.append([f, round(worst, 3)])
         print(json.dumps({"depth": depth, "B": B, "wseed": ws, "non_nan_poses": int(ok.sum()),
                           "nkeep_hist": np.bincount(nkeep, minlength=5).tolist(),
                           "frames_with_near_threshold_px": int((np.asarray(near) > 0).sum()),
+                          "pose_risky_frames": risky,
                           "near_threshold_px": near,
                           "mask_px": [int(v) for v in d2.reshape(B, -1).sum(1)]}), flush=True)
 
