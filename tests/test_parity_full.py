@@ -86,9 +86,13 @@ SEED = 77               # synthetic session of the batch
 # with >= 30 poses: 3 (31 poses, 22 near-threshold frames: 20-24 / 32
 # identical selected masks on the MI355X, below MIN_SEL_EXACT), 14 (30, 1,
 # but that frame's flip turns the angle 1.36 deg: failed the pose bound),
-# 11 (32, 5: 28-31 / 32 identical), 34 (31, 2), 35 (32, 0).  Seed 35: every
-# frame posed, no pixel near the threshold.
-WEIGHT_SEED = {50: 35, 101: 1}
+# 11 (32, 5: 28-31 / 32 identical), 34 (31, 2), 35 (32, 0).  Seed 35 passed
+# every fp32 case but its fp16 case had 25 / 32 frames within the fp16
+# detection bounds (tools/parity_seed_check.py fp16 0: seeds 3, 11, 21, 34
+# pass, 33 and 35 fail); seed 34 passes all seven R50 cases: 31 / 32 poses,
+# 29-30 / 32 identical selected masks in fp32, 32 / 32 fp16 detections
+# (profiles/r05_parity_full_R50_*).
+WEIGHT_SEED = {50: 34, 101: 1}
 ORACLE_CHUNK = 8        # frames per oracle forward (its intermediates of a whole batch would not fit)
 
 _ORACLE = {}
