@@ -326,6 +326,22 @@ int mdx_model_set_wino_slice(int mb);
  * batched launch has at least min_wgs workgroups, 2 whenever eligible; returns
  * the old mode. */
 int mdx_conv_set_winograd_dma(int mode, int min_wgs);
+/* Fused Winograd F(4x4,3x3), fp32 (k_wino_f4): the input transform, the 36
+ * tile-point GEMMs and the output transform + bias + ReLU in one launch, no
+ * workspace.  Weights: U of mdx_winograd_weights(m = 4) repacked by the host
+ * function mdx_winograd_pack_f4 (same size, 36 * Cout * Cin floats).
+ * Cin % 8 == 0, Cout % 32 == 0, x / U under 2 GiB. */
+int mdx_winograd_pack_f4(const float *U, int Cout, int Cin, float *U_packed);
+int mdx_conv3x3_winograd_fused(const float *x, int N, int H, int W, int Cin, const float *U_packed,
+                               const float *bias, int Cout, int relu, float *out, mdx_stream_t stream);
+/* Policy for fused F(4,3): mode 0 never (default; measured slower than the
+ * three-launch path except on 64-channel layers), 1 when the
+ * launch has at least min_wgs workgroups (32 tiles x 32 channels each;
+ * min_wgs <= 0 keeps the current threshold), 2 whenever the shape allows (not
+ * in split-plane mode).  Returns the old mode.  mdx_winograd_fused_eligible:
+ * 1 if the policy takes the fused kernel for this layer. */
+int mdx_conv_set_winograd_fused(int mode, int min_wgs);
+int mdx_winograd_fused_eligible(int N, int H, int W, int Cin, int Cout);
 /* fp32 1x1 layers with Cout <= 16 (the RPN / mask / box predictors) on the
  * narrow-output kernel k_head_f32 (1, default) or the general kernels (0);
  * returns the old value. */
@@ -368,6 +384,8 @@ enum {
     MDX_CONV_KERNEL_SBDUAL64 = 21,
     MDX_CONV_KERNEL_SBG128 = 22, /* REG128 / REG64 on the single-stage k_conv_sbg (mdx_conv_set_single_stage(2)) */
     MDX_CONV_KERNEL_SBG64 = 23,
+    MDX_CONV_KERNEL_WINO_FUSED = 24, /* fused Winograd F(4,3) (mdx_conv_set_winograd_fused): both transforms
+                                        and the 36 GEMMs in one launch */
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

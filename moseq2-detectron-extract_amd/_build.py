@@ -53,7 +53,7 @@ HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mf
 # target-feature switch reaches the host compile too, where clang ignores it
 # with a warning.
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32}
+DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32, "wino_fused.hip": NO_PACKED_FP32}
 
 
 def sources(csrc: str = CSRC):

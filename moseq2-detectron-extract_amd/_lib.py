@@ -75,6 +75,10 @@ SIGNATURES = {
     "mdx_conv_set_winograd_min_cin": (I32, [I32]),
     "mdx_conv_winograd_min_cin": (I32, []),
     "mdx_conv_set_winograd_dma": (I32, [I32, I32]),
+    "mdx_conv_set_winograd_fused": (I32, [I32, I32]),
+    "mdx_winograd_fused_eligible": (I32, [I32, I32, I32, I32, I32]),
+    "mdx_winograd_pack_f4": (I32, [P, I32, I32, P]),
+    "mdx_conv3x3_winograd_fused": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, P, P]),
     "mdx_conv_set_head_f32": (I32, [I32]),
     "mdx_x6_plane_bytes": (I64, [I64, I32]),
     "mdx_split_x6": (I32, [P, I64, I32, I64, P, P]),

@@ -52,6 +52,9 @@ struct WinoProbe {
     int gemm_kernel;
 };
 void wino_probe(WinoProbe *p);
+WinoProbe *wino_probe_current();
+// the kernel id / K slices mdx_conv2d_last_plan reports for this thread
+void set_last_plan(int kernel, int ksplit);
 bool winograd_planes_enabled();  // the model runs Winograd GEMMs on k_gemm_x6 (MDX_WINO_X6 set)
 // weights of the next split-plane conv launch on this thread as bf16 planes
 // (mdx_split_x6 layout), or null; the model handle sets it around a layer

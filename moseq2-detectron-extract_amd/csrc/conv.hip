@@ -2827,6 +2827,11 @@ extern "C" int mdx_winograd_tile(int H, int W, int mode) {
 
 static thread_local WinoProbe *t_wino_probe = nullptr;
 void mdx::wino_probe(WinoProbe *p) { t_wino_probe = p; }
+WinoProbe *mdx::wino_probe_current() { return t_wino_probe; }
+void mdx::set_last_plan(int kernel, int ksplit) {
+    t_plan_kernel = kernel;
+    t_plan_ksplit = ksplit;
+}
 
 // the model packs Winograd weight planes (and so runs the split-plane
 // Winograd GEMMs on k_gemm_x6) only when MDX_WINO_X6 is set: the split-plane
@@ -2874,10 +2879,10 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     // the 256 x 256 LDS-DMA plane kernel
     const bool planes = Up && g_fp32_split == 6 && Cin % 16 == 0 &&
                         T * Cin * 6 < (1ll << 31) && (long long)Cout * Cin * 6 < (1ll << 31);
+    WinoProbe *probe = t_wino_probe;
     float *V = reinterpret_cast<float *>(workspace);
     float *Mx = planes ? reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + NB * T * Cin * 6)
                        : V + NB * T * Cin;
-    WinoProbe *probe = t_wino_probe;
     auto mark = [&](int i) {
         if (probe) (void)hipEventRecord(probe->ev[i], s);
     };

@@ -734,7 +734,14 @@ struct Fwd {
                     {MDX_CONV_KERNEL_WINO_IN, 1, T, cw.cin, A * A, 4.0 * (px + (double)A * A * T) * cw.cin, 0.0},
                     {probe.gemm_kernel, 1, A * A * T, cw.cout, cw.cin, 2.0 * (double)A * A * T * cw.cout * cw.cin, 0.0},
                     {MDX_CONV_KERNEL_WINO_OUT, 1, T, cw.cout, A * A, 4.0 * ((double)A * A * T + px) * cw.cout, 0.0}};
+                // the fused kernel (one launch, timed by ev[2] / ev[3]) is one record
+                const bool fused = probe.gemm_kernel == MDX_CONV_KERNEL_WINO_FUSED;
                 for (int q = 0; q < 3; ++q) {
+                    if (fused && q != 1) {
+                        (void)hipEventDestroy(probe.ev[2 * q]);
+                        (void)hipEventDestroy(probe.ev[2 * q + 1]);
+                        continue;
+                    }
                     c.prof.emplace_back();
                     ProfEv &p = c.prof.back();
                     p.e0 = probe.ev[2 * q];

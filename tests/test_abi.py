@@ -91,3 +91,39 @@ def test_winograd_weight_transform_host(mdx, m):
     assert call("mdx_winograd_tile", 112, 128, 6) == 6 and call("mdx_winograd_tile", 56, 64, 6) == 6
     assert call("mdx_winograd_tile", 28, 32, 6) == 4 and call("mdx_winograd_tile", 7, 7, 6) == 4
     assert call("mdx_winograd_tile", 112, 128, 4) == 4 and call("mdx_winograd_tile", 5, 5, 2) == 2
+
+
+def test_winograd_fused_pack_and_policy_host(mdx):
+    """mdx_winograd_pack_f4 (host): the consumer B-fragment layout of the fused
+    F(4,3) kernel -- piece (channel block, K-step, point) of 64 lanes x 4, lane
+    (n = l & 15, k-pair kp = l >> 4) holding U at (n, 2 kp), (n, 2 kp + 1),
+    (n + 16, 2 kp), (n + 16, 2 kp + 1); a permutation of U (same multiset of
+    values).  Policy: off by default, eligibility needs Cin % 8 == 0 and
+    Cout % 32 == 0, shape errors are refused."""
+    import ctypes
+    import numpy as np
+    from moseq2_detectron_extract_amd._lib import MdxError, call
+    Cout, Cin = 64, 16
+    U = np.random.default_rng(3).standard_normal((36, Cout, Cin)).astype(np.float32)
+    Up = np.empty_like(U)
+    call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), Cout, Cin, Up.ctypes.data_as(ctypes.c_void_p))
+    KS = Cin // 8
+    pieces = Up.reshape(Cout // 32, KS, 36, 64, 4)
+    for nb, ks, xi, lane in [(0, 0, 0, 0), (1, 1, 35, 63), (0, 1, 17, 21), (1, 0, 5, 40)]:
+        n, kp = lane & 15, lane >> 4
+        want = [U[xi, nb * 32 + n + 16 * (e >> 1), ks * 8 + 2 * kp + (e & 1)] for e in range(4)]
+        np.testing.assert_array_equal(pieces[nb, ks, xi, lane], want)
+    np.testing.assert_array_equal(np.sort(Up, axis=None), np.sort(U, axis=None))
+    with pytest.raises(MdxError):
+        call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), 48, Cin, Up.ctypes.data_as(ctypes.c_void_p))
+    assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 0  # default policy: off
+    old = call("mdx_conv_set_winograd_fused", 2, 0)
+    try:
+        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 1
+        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 260, 256) == 0  # Cin % 8
+        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 48) == 0   # Cout % 32
+        call("mdx_conv_set_winograd_fused", 1, 384)
+        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 1  # 896 blocks x 8
+        assert call("mdx_winograd_fused_eligible", 32, 7, 8, 256, 256) == 0      # 4 blocks x 8 < 384
+    finally:
+        call("mdx_conv_set_winograd_fused", old, 384)

@@ -871,6 +871,46 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     assert err < 1e-4, err
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,relu,bias", [(2, 13, 17, 256, 256, True, True), (3, 7, 7, 512, 512, True, True),
+                                                      (1, 14, 16, 256, 64, False, True), (4, 6, 5, 264, 96, True, False),
+                                                      (2, 56, 64, 256, 256, True, True), (2, 112, 128, 64, 64, True, True),
+                                                      (1, 3, 3, 8, 32, False, True), (5, 29, 31, 128, 160, True, True)])
+def test_conv3x3_winograd_fused(mdx, N, H, W, Cin, Cout, relu, bias):
+    """Fused Winograd F(4x4,3x3) (k_wino_f4: input transform, 36 tile-point
+    GEMMs and output transform + bias + ReLU in one launch, no workspace
+    traffic) against the fp64 direct convolution, within the unfused
+    kernels' tolerance (1e-4 of the output scale); ragged maps exercise
+    partial tiles, padding rows / columns and a partial last tile block,
+    Cin % 16 == 8 a half K-step pair, bias=False the null-bias path."""
+    from moseq2_detectron_extract_amd._lib import call
+    import ctypes
+    g = torch.Generator().manual_seed(N * 1000 + H + Cin)
+    x = torch.randn(N, H, W, Cin, generator=g).clamp_min(0)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
+    b = torch.randn(Cout, generator=g) if bias else torch.zeros(Cout)
+    want = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1)
+    if relu:
+        want = want.clamp_min(0)
+    want = want.permute(0, 2, 3, 1)
+    U = np.empty((36, Cout, Cin), np.float32)
+    wn = np.ascontiguousarray(w.numpy())
+    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, 4, U.ctypes.data_as(ctypes.c_void_p))
+    Up = np.empty_like(U)
+    call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), Cout, Cin, Up.ctypes.data_as(ctypes.c_void_p))
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    xd, Ud, bd = x.cuda(), torch.from_numpy(Up).cuda(), b.cuda()  # (bd kept alive for the call)
+    bp = P(bd) if bias else None
+    out = torch.full((N, H, W, Cout), float("nan"), device="cuda")
+    call("mdx_conv3x3_winograd_fused", P(xd), N, H, W, Cin, P(Ud), bp, Cout, int(relu), P(out), None)
+    kid, ks_ = ctypes.c_int(), ctypes.c_int()
+    call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+    assert kid.value == 24  # MDX_CONV_KERNEL_WINO_FUSED
+    got = out.cpu().double()
+    assert torch.isfinite(got).all()  # every output pixel written
+    err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+    assert err < 1e-4, err
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cout,m", [(8, 112, 128, 256, 256, 6), (16, 56, 64, 128, 128, 4),
                                                (4, 61, 67, 64, 96, 6)])
 def test_conv3x3_winograd_planes(mdx, N, H, W, Cin, Cout, m):
