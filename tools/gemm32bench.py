@@ -25,6 +25,8 @@ DIRECT = [
     (32, 112, 128, 256, 256, 1, 1, 0, False, 1),   # fpn lateral p2
     (32, 56, 64, 512, 256, 1, 1, 0, False, 1),     # fpn lateral p3
     (32, 112, 128, 64, 64, 3, 1, 1, False, 3),     # res2 conv2 (direct 3x3)
+    (32000, 1, 1, 12544, 1024, 1, 1, 0, False, 1),  # box head fc1 (1000 ROIs x 32 frames)
+    (32000, 1, 1, 1024, 1024, 1, 1, 0, False, 1),   # box head fc2
 ]
 WINO = [  # N, H, W, Cin, Cout, count
     (32, 112, 128, 256, 256, 2),   # fpn output p2 + rpn p2
