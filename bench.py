@@ -81,6 +81,8 @@ def parse():
                     help="skip the config-5 secondary (R101-FPN B=64, fp16 mask + keypoint heads)")
     ap.add_argument("--extract-frames", type=int, default=10000)
     ap.add_argument("--extract-chunk", type=int, default=1000)
+    ap.add_argument("--extract-per-chunk", action="store_true",
+                    help="extract loop: drain the stream pipeline at every chunk (round-4 schedule, for A/B runs)")
     ap.add_argument("--dump-convs", default=None, help="write per-launch conv timings (JSON) to this path")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run batches back to back on one stream (one forward at a time)")
@@ -369,7 +371,7 @@ def extract_loop(args):
     workers = max(1, min(16, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", 16))))
     s = synth.SyntheticSession(n, seed=9)
     pred = Predictor.from_config(ModelConfig(depth=args.depth, score_thresh_test=0.0), weights="synthetic")
-    cfg = ExtractConfig(chunk_size=chunk, use_tracking=True)
+    cfg = ExtractConfig(chunk_size=chunk, use_tracking=True, stream_chunks=not args.extract_per_chunk)
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         t0 = time.perf_counter()
         s.write(td, workers=workers)

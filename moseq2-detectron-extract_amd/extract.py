@@ -383,8 +383,11 @@ def _run_overlapped(src, batches, ex, true_depth, finished=None):
         ctx["ws"] = torch.cuda.Stream()
 
     def produce():
-        for idx, raw in src.iterate(device=True, batches=batches):
-            st, host = ex.features_pass(raw)
+        # the stream pipeline runs across chunk boundaries (features_stream)
+        chunks = src.iterate(device=True, batches=batches)
+        stream = ex.features_stream(chunks) if ex.cfg.stream_chunks else \
+            ((idx, *ex.features_pass(raw)) for idx, raw in chunks)
+        for idx, st, host in stream:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             yield np.asarray(idx), st, host, ev

@@ -76,6 +76,7 @@ class ExtractConfig:
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)
     expected_instances: int = 1      # --expected-instances (M/cli.py:341)
     pipelined: bool = True           # features_pass: batches staggered over streams (OverlappedExtractor)
+    stream_chunks: bool = True       # extract loop: the stream pipeline runs across chunk boundaries
 
 
 def mask_nms_select(out: dict, iou_thresh: float = 0.5):
@@ -367,6 +368,46 @@ class GPUExtractor:
                 outs.append(r)
         outs.extend(pipe.flush())  # the current stream now waits for every stage
         return self._collect(outs)
+
+    def features_stream(self, chunks):
+        """features_pass over a sequence of (key, raw) chunks with the stream
+        pipeline running across chunk boundaries: the next chunk's first
+        batches are submitted before the current chunk's last results are
+        collected, so the streams do not drain (and refill) at every chunk.
+        Yields (key, state, host) per chunk, in order, equal to
+        features_pass(raw) of that chunk (same kernels and inputs; the
+        streams only reorder)."""
+        if not self.cfg.pipelined:
+            for key, raw in chunks:
+                yield (key, *self.features_pass(raw))
+            return
+        B = self.cfg.batch_size
+        pipe = None
+        pending = collections.deque()  # [key, nbatches, results, raw] per chunk, submission order
+
+        def done():
+            while pending and len(pending[0][2]) == pending[0][1]:
+                key, _, outs, _ = pending.popleft()
+                for o in outs:  # the caller's stream waits for exactly these batches
+                    OverlappedExtractor.wait(o)
+                yield (key, *self._collect(outs))
+
+        for key, raw in chunks:
+            raw = raw if isinstance(raw, torch.Tensor) and raw.is_cuda else \
+                torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+            if pipe is None:
+                pipe = self._pipeline(raw[:B])
+            n = raw.shape[0]
+            pending.append([key, (n + B - 1) // B, [], raw])
+            for i in range(0, n, B):
+                r = pipe.submit(raw[i:i + B])
+                if r is not None:  # results come out in submission order: the oldest open chunk's
+                    pending[0][2].append(r)
+                    yield from done()
+        if pipe is not None:
+            for r in pipe.flush():
+                pending[0][2].append(r)
+                yield from done()
 
     def _pipeline(self, first: torch.Tensor):
         if self._pipe is None:

@@ -709,6 +709,34 @@ def test_features_pass_pipelined_matches_serial(mdx):
     assert torch.equal(m1, m0)
 
 
+def test_features_stream_matches_per_chunk(mdx):
+    """features_stream (the extract loop's device pass with the stream
+    pipeline running across chunk boundaries: chunks of 40, 40 and a ragged
+    13 frames in slices of 16) yields, chunk by chunk and in order, exactly
+    what features_pass returns for each chunk alone."""
+    from moseq2_detectron_extract_amd import synth
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
+    s = synth.SyntheticSession(93, seed=8)
+    raw = torch.from_numpy(s.frames(0, 93)).cuda()
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), weights="synthetic")
+    cuts = [(0, 40), (40, 80), (80, 93)]
+    ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=16, pipelined=True))
+    streamed = list(ex.features_stream((k, raw[a:b]) for k, (a, b) in enumerate(cuts)))
+    torch.cuda.synchronize()
+    assert [k for k, _, _ in streamed] == [0, 1, 2]
+    ref = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=16, pipelined=True))
+    for (k, st, host), (a, b) in zip(streamed, cuts):
+        s0, h0 = ref.features_pass(raw[a:b])
+        torch.cuda.synchronize()
+        for key in ("centroid", "orientation", "axis_length", "keypoints", "centers"):
+            np.testing.assert_array_equal(host[key], h0[key], err_msg=f"chunk {k} {key}")
+        for key in ("prepped", "d2", "cleaned"):
+            assert torch.equal(st[key], s0[key]), (k, key)
+        np.testing.assert_array_equal(st["nkeep"], s0["nkeep"])
+        assert torch.equal(torch.cat(st["inf"]["masks"]), torch.cat(s0["inf"]["masks"]))
+
+
 @pytest.mark.parametrize("use_tracking", [False, True])
 def test_process_chunk_data_dict(mdx, use_tracking):
     """Full chunk through the device path (tracking off and on): the writer's
