@@ -57,6 +57,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     'frame_idxs': (n,)} in frame order, this rank's frames.  With
     `output_dir` the session's results_00 file, keypoints_00.tsv and status
     file are written there once (by rank 0 of a sharded session)."""
+    tl = _Timeline()
     status_path = None
     if output_dir:  # status file first, as M/extract.py:47-62 (skip a completed session)
         os.makedirs(output_dir, exist_ok=True)
@@ -72,6 +73,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         if rank == 0:
             write_status(status_path, status)
     src = RawDepthSource(path, frame_trim=frame_trim)
+    src.timeline = tl if tl.path else None
     ex = GPUExtractor(bground_im, roi, predictor, config)
     batches = src.batches(config.chunk_size, config.chunk_overlap)
     nrounds = len(batches)
@@ -87,6 +89,9 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         local = _ChunkWriter(output_dir, src, bground_im, roi, true_depth, config, first_frame, status,
                              parts=world) if rank == 0 else None
         writer = local if world == 1 else _GatherWriter(local, nrounds)
+        if local is not None and tl.path:
+            local.timeline = tl
+    tl.add("session setup", -1, tl.t0)
 
     def finished(d):
         if writer is not None:
@@ -101,12 +106,13 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         if exchange:
             parts = _run_two_pass(src, batches, ex, config, true_depth, finished)
         elif config.overlap_host:
-            parts = _run_overlapped(src, batches, ex, true_depth, finished)
+            parts = _run_overlapped(src, batches, ex, true_depth, finished, tl)
         else:
             for idx, raw in src.iterate(device=True, batches=batches):
                 parts.append(finished(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
         ok = True
     finally:
+        t0 = tl.now()
         src.close()
         ex.close()
         if writer is not None:
@@ -114,6 +120,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
                 writer.close()
             else:  # the extraction's own exception propagates; the results file is left unfinished
                 writer.abort()
+        tl.add("writer close", -1, t0)
     if output_dir:
         if rank == 0:
             status["complete"] = True  # M/extract.py:129-131
@@ -133,6 +140,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         out[f"keypoints/{k}"] = np.concatenate([np.asarray(p["keypoints"][k]) for p in parts])
     if out_npz:
         np.savez_compressed(out_npz, **out)
+    tl.dump()
     return out
 
 
@@ -233,6 +241,8 @@ class _ChunkWriter:
         self.tsv_parts = [KeypointsTSVWriter(output_dir, path=f"{self.tsv.path}.part{r}", header=False)
                           for r in range(parts)] if parts > 1 else None
         self._cols = None
+        self.timeline = None  # extract._Timeline when the extract loop is traced
+        self._nwritten = 0
         create_extract_h5(self.h5, cfg, status)
         import queue
         import threading
@@ -249,14 +259,20 @@ class _ChunkWriter:
             if self._err:  # keep draining after an error so write() / close() never block
                 continue
             d, part = d
+            tl, k = self.timeline, self._nwritten
+            self._nwritten += 1
             try:
+                t0 = tl.now() if tl else 0
                 write_extracted_chunk_to_h5(self.h5, d)
+                t1 = tl.add("results rows", k, t0) if tl else 0
                 if self.tsv_parts is None:
                     self.tsv.write(d)
                 else:
                     if self._cols is None:
                         self._cols = list(KeypointsTSVWriter.columns(d))
                     self.tsv_parts[part].write(d)
+                if tl:
+                    tl.add("keypoints tsv", k, t1)
             except BaseException as e:  # surfaced by write() / close()
                 self._err.append(e)
 
@@ -273,9 +289,12 @@ class _ChunkWriter:
         self._t.join()
         if self._err:
             raise self._err[0]
+        t0 = self.timeline.now() if self.timeline else 0
         if self.tsv_parts is not None and self._cols is not None:
             join_tsv_parts(self.tsv.path, self._cols, [w.path for w in self.tsv_parts])
         self.h5.close()
+        if self.timeline:
+            self.timeline.add("results file close", -1, t0)
 
     def abort(self) -> None:
         """Stop the writer thread after a failed extraction without finishing
@@ -367,7 +386,7 @@ def _lighten(d: dict) -> dict:
     return d
 
 
-def _run_overlapped(src, batches, ex, true_depth, finished=None):
+def _run_overlapped(src, batches, ex, true_depth, finished=None, tl=None):
     """Chunk loop with the host step off the critical path: the calling thread
     runs each chunk's device pass (prep, model, clean, moments) and hands it
     to a worker thread, which runs the sequential host step (angles / Kalman
@@ -380,31 +399,76 @@ def _run_overlapped(src, batches, ex, true_depth, finished=None):
 
     def setup():
         torch.cuda.set_device(dev)
-        ctx["ws"] = torch.cuda.Stream()
+        # high priority: the worker's few small kernels (instance selection,
+        # scalars, crops) are not queued behind the next chunk's forwards on
+        # a shared hardware queue, so the host step keeps pace with the device
+        ctx["ws"] = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+
+    tl = tl or _Timeline()
 
     def produce():
         # the stream pipeline runs across chunk boundaries (features_stream)
         chunks = src.iterate(device=True, batches=batches)
         stream = ex.features_stream(chunks) if ex.cfg.stream_chunks else \
             ((idx, *ex.features_pass(raw)) for idx, raw in chunks)
-        for idx, st, host in stream:
+        t0 = tl.now()
+        for k, (idx, st, host) in enumerate(stream):
+            tl.add("device pass", k, t0)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             yield np.asarray(idx), st, host, ev
+            t0 = tl.now()
 
     def consume(item):
         idx, st, host, ev = item
         ws = ctx["ws"]
         ws.wait_event(ev)
+        k = ctx["k"] = ctx.get("k", -1) + 1
         with torch.cuda.stream(ws):
             for t in (st["prepped"], st["d2"], st["cleaned"]):
                 t.record_stream(ws)
+            t0 = tl.now()
             ex.select_instances(st, host)
+            t1 = tl.add("instance selection", k, t0)
             cen, kp, ang, fl = ex.host_angles(host)
+            t2 = tl.add("host angles", k, t1)
             d = ex.finish_chunk(st, cen, kp, ang, fl, host["axis_length"], idx, 0, true_depth)
-        return finished(d) if finished is not None else _lighten(d)
+            t3 = tl.add("finish chunk", k, t2)
+        out = finished(d) if finished is not None else _lighten(d)
+        tl.add("writer hand-off", k, t3)
+        return out
 
     return host_pipeline(produce(), consume, setup)
+
+
+class _Timeline:
+    """MDX_EXTRACT_TRACE=<path>: wall-clock spans of the extract loop's host
+    phases per chunk (device pass on the producing thread; instance
+    selection, angles, finish and writer hand-off on the worker), written as
+    JSON at the end; no-op otherwise."""
+
+    def __init__(self):
+        import time
+        self.path = os.environ.get("MDX_EXTRACT_TRACE")
+        self.clock = time.perf_counter
+        self.t0 = self.clock()
+        self.events = []
+
+    def now(self):
+        return self.clock()
+
+    def add(self, name, chunk, t0):
+        t1 = self.clock()
+        if self.path:
+            self.events.append({"phase": name, "chunk": chunk, "start_s": round(t0 - self.t0, 4),
+                                "end_s": round(t1 - self.t0, 4)})
+        return t1
+
+    def dump(self):
+        if self.path:
+            import json
+            with open(self.path, "w") as fh:
+                json.dump({"events": self.events, "total_s": round(self.clock() - self.t0, 4)}, fh, indent=0)
 
 
 def host_pipeline(items, consume, setup=None, depth: int = 2):

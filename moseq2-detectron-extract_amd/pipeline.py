@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import threading
+import weakref
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
@@ -315,6 +317,8 @@ class GPUExtractor:
         """Release the extractor's device state now (the pipeline, its
         streams and results, the prep workspaces) rather than when the
         cyclic garbage collector gets to the extractor <-> pipeline cycle."""
+        if self._pipe is not None and self._pipe.streams is not None:
+            _checkin_streams(self.predictor, self._pipe.streams)
         self._pipe = None
         self._streams = []
         self.prep._ws = None
@@ -411,8 +415,11 @@ class GPUExtractor:
 
     def _pipeline(self, first: torch.Tensor):
         if self._pipe is None:
-            self._pipe = OverlappedExtractor(self, max(1, int(self.cfg.model_streams)), keep=True)
-            self._pipe.prime(first)
+            sset = _checkout_streams(self.predictor, max(1, int(self.cfg.model_streams)))
+            self._pipe = OverlappedExtractor(self, len(sset.models), keep=True, streams=sset)
+            if not sset.primed:
+                self._pipe.prime(first)
+                sset.primed = True
         return self._pipe
 
     def _collect(self, outs):
@@ -642,6 +649,44 @@ class GPUExtractor:
         return self.tail(prepped, cleaned, self.infer(prepped))
 
 
+class _StreamSet:
+    """The HIP streams of one OverlappedExtractor (front, model_streams model
+    streams, tail).  The native model keeps a workspace per stream
+    (mdx_model_reserve), so the extract loop of each session borrows a set
+    from its predictor's pool (_checkout_streams) instead of making new
+    streams: the workspaces, the allocator's per-stream pools and the priming
+    forward are paid once per predictor, not once per session."""
+
+    def __init__(self, model_streams: int):
+        self.device = torch.cuda.current_device()
+        self.front = torch.cuda.Stream()
+        self.models = [torch.cuda.Stream() for _ in range(model_streams)]
+        self.tail = torch.cuda.Stream()
+        self.primed = False
+
+
+_STREAM_POOLS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # predictor -> free _StreamSets
+_STREAM_POOL_LOCK = threading.Lock()
+
+
+def _checkout_streams(predictor, model_streams: int) -> _StreamSet:
+    """A free stream set of `predictor` for `model_streams` model streams on
+    the current device (a new one when every matching set is in use, e.g. by
+    a session extracting in another thread)."""
+    dev = torch.cuda.current_device()
+    with _STREAM_POOL_LOCK:
+        free = _STREAM_POOLS.setdefault(predictor, [])
+        for i, sset in enumerate(free):
+            if sset.device == dev and len(sset.models) == model_streams:
+                return free.pop(i)
+    return _StreamSet(model_streams)
+
+
+def _checkin_streams(predictor, sset: _StreamSet) -> None:
+    with _STREAM_POOL_LOCK:
+        _STREAM_POOLS.setdefault(predictor, []).append(sset)
+
+
 class OverlappedExtractor:
     """Software pipeline over consecutive batches on separate HIP streams:
     front (prep + inpaint + clean) of batch i+2, model forward + mask
@@ -657,13 +702,14 @@ class OverlappedExtractor:
     earlier (or None);
     flush() -> list of the results still in flight."""
 
-    def __init__(self, extractor: GPUExtractor, model_streams: int = 2, keep: bool = False):
+    def __init__(self, extractor: GPUExtractor, model_streams: int = 2, keep: bool = False,
+                 streams: Optional["_StreamSet"] = None):
         self.ex = extractor
         self.keep = keep  # results also carry the batch's prepped / cleaned frames and forward outputs
-        self.s_front = torch.cuda.Stream()
-        self.s_models = [torch.cuda.Stream() for _ in range(max(1, model_streams))]
+        self.streams = streams
+        sset = streams or _StreamSet(max(1, model_streams))
+        self.s_front, self.s_models, self.s_tail = sset.front, sset.models, sset.tail
         self.n_model = 0
-        self.s_tail = torch.cuda.Stream()
         self.fronted = None            # (prepped, cleaned, event) awaiting the model
         self.modeled = collections.deque()  # (prepped, cleaned, inf, event) awaiting the tail
 

@@ -147,7 +147,7 @@ class MemoryH5:
         self.close()
 
 
-_PIECE = 8 << 20  # bytes per independently deflated piece
+_PIECE = 1 << 20  # bytes per independently deflated piece (a chunk's crop rows spread over the pool)
 _ZIP64_AT = 0xFFFFFFFF  # sizes / offsets from which a member needs zip64 records (tests lower it)
 
 
@@ -157,14 +157,16 @@ def _deflate_pieces(data: memoryview, level: int, pool, final: bool = True) -> l
     finishes the stream unless final=False -- pigz's layout), compressed in
     parallel: zlib releases the GIL while it works."""
     cuts = list(range(0, len(data), _PIECE)) or [0]
+    last = len(cuts) - 1
+    return list(pool.map(lambda i: _deflate_one(data[cuts[i]:cuts[i] + _PIECE], level, final and i == last),
+                         range(len(cuts))))
 
-    def one(i):
-        c = zlib.compressobj(level, zlib.DEFLATED, -15)
-        a = cuts[i]
-        out = c.compress(data[a:a + _PIECE])
-        return out + c.flush(zlib.Z_FINISH if final and i == len(cuts) - 1 else zlib.Z_SYNC_FLUSH)
 
-    return list(pool.map(one, range(len(cuts))))
+def _deflate_one(piece, level: int, final: bool) -> bytes:
+    """One independently deflated piece, ending on a sync flush unless it
+    finishes the stream."""
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    return c.compress(piece) + c.flush(zlib.Z_FINISH if final else zlib.Z_SYNC_FLUSH)
 
 
 def _npy_header(a: np.ndarray) -> bytes:
@@ -238,22 +240,33 @@ def save_npz(path: str, arrays: Dict[str, np.ndarray], level: int = 4, workers: 
     central = []
     own = pool is None
     pool = cf.ThreadPoolExecutor(workers) if own else pool
+    def member(arr):
+        a = np.asarray(arr)
+        a = a if a.flags.c_contiguous else a.copy(order="C")  # (ascontiguousarray would make 0-d arrays 1-d)
+        head = _npy_header(a)
+        body = memoryview(a.reshape(-1).view(np.uint8)) if a.size else memoryview(b"")
+        crc = zlib.crc32(body, zlib.crc32(head))
+        size = len(head) + len(body)
+        if size <= _PIECE:
+            pieces = [_deflate_one(memoryview(head + bytes(body)), level, True)]
+        else:  # header, then the body's pieces: one deflate stream
+            c = zlib.compressobj(level, zlib.DEFLATED, -15)
+            pieces = [c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)] + _deflate_pieces(body, level, pool)
+        return pieces, crc, size
+
+    # the small members (scalars, keypoints, metadata: one piece each) are
+    # deflated concurrently, the large ones piecewise on the pool as they
+    # come; the file is written in member order either way
+    small = {k: pool.submit(member, v) for k, v in arrays.items()
+             if k not in precompressed and len(_npy_header(np.asarray(v))) + np.asarray(v).nbytes <= _PIECE}
     with open(path, "wb") as fh:
         for key, arr in arrays.items():
             if key in precompressed:  # (pieces, crc, size) of a _DeflateStream
                 pieces, crc, size = precompressed[key]
+            elif key in small:
+                pieces, crc, size = small[key].result()
             else:
-                a = np.asarray(arr)
-                a = a if a.flags.c_contiguous else a.copy(order="C")  # (ascontiguousarray would make 0-d arrays 1-d)
-                head = _npy_header(a)
-                body = memoryview(a.reshape(-1).view(np.uint8)) if a.size else memoryview(b"")
-                crc = zlib.crc32(body, zlib.crc32(head))
-                size = len(head) + len(body)
-                if size <= _PIECE:
-                    pieces = _deflate_pieces(memoryview(head + bytes(body)), level, pool)
-                else:  # header, then the body's pieces: one deflate stream
-                    c = zlib.compressobj(level, zlib.DEFLATED, -15)
-                    pieces = [c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)] + _deflate_pieces(body, level, pool)
+                pieces, crc, size = member(arr)
             csize = sum(len(x) for x in pieces)
             name = (key + ".npy").encode()
             off = fh.tell()

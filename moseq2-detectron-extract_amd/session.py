@@ -90,10 +90,47 @@ def read_frames_raw(filename: Union[str, tarfile.TarInfo], frames=None, frame_di
         raise ValueError("Could not read!")
     try:
         for first, count, dest in runs:
-            out[dest] = fetch(max(first, 0), count).reshape(count, H, W)
+            first = max(first, 0)
+            if isinstance(filename, str) and _direct_read(fh, out, first, count, dest, info["bytes_per_frame"], dt):
+                continue
+            out[dest] = fetch(first, count).reshape(count, H, W)
     finally:
         fh.close()
     return out
+
+
+_READ_PIECE = 16 << 20  # bytes per pread of a large run (pieces read by parallel threads)
+
+
+def _direct_read(fh, out: np.ndarray, first: int, count: int, dest: np.ndarray, bpf: int, dt) -> bool:
+    """A run of frames whose destination rows are consecutive in a
+    C-contiguous `out` of the file's byte order is read straight into those
+    rows (no staging copy; into a pinned buffer that is the H2D source), a
+    large run as parallel preads (the GIL is released while they read).
+    False when the run does not qualify (the caller stages it)."""
+    if not (out.flags.c_contiguous and out.dtype == dt and dt.isnative and count > 0
+            and int(dest[0]) + count - 1 == int(dest[-1]) and (count == 1 or bool(np.all(np.diff(dest) == 1)))):
+        return False
+    row0 = int(dest[0])
+    buf = memoryview(out[row0:row0 + count].reshape(-1).view(np.uint8))
+    fd, base, total = fh.fileno(), first * bpf, count * bpf
+    cuts = list(range(0, total, _READ_PIECE))
+
+    def one(a):
+        n = min(_READ_PIECE, total - a)
+        got = 0
+        while got < n:
+            r = os.preadv(fd, [buf[a + got:a + n]], base + a + got)
+            if r <= 0:
+                raise ValueError(f"raw depth file ends before frame {first + count - 1}")
+            got += r
+    if len(cuts) == 1:
+        one(0)
+    else:
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(min(4, len(cuts))) as pool:
+            list(pool.map(one, cuts))
+    return True
 
 
 class RawDepthSource:
@@ -157,7 +194,8 @@ class RawDepthSource:
         W, H = self.frame_dims
         cap = max((len(s) for s in seq), default=0)
         nbuf = prefetch + 1
-        pinned = [torch.empty((cap, H, W), dtype=torch.int16).pin_memory() for _ in range(nbuf)]
+        tl = getattr(self, "timeline", None)  # extract._Timeline when the extract loop is traced
+        pinned = [None] * nbuf  # allocated by the reader on first use: the first read starts after one
         free = queue.Queue()
         for i in range(nbuf):
             free.put(i)
@@ -169,10 +207,15 @@ class RawDepthSource:
         def reader():
             try:
                 torch.cuda.set_device(dev)
-                for idx in seq:
+                for k, idx in enumerate(seq):
                     b = free.get()
                     n = len(idx)
+                    t0 = tl.now() if tl else 0
+                    if pinned[b] is None:
+                        pinned[b] = torch.empty((cap, H, W), dtype=torch.int16).pin_memory()
                     self.read(idx, out=pinned[b][:n].numpy())
+                    if tl:
+                        tl.add("read chunk", k, t0)
                     with torch.cuda.stream(copy_stream):
                         d = torch.empty((n, H, W), dtype=torch.int16, device="cuda")
                         d.copy_(pinned[b][:n], non_blocking=True)

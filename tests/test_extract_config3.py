@@ -154,3 +154,25 @@ def test_config3_session_matches_oracle_chain(session):
             wm = w["pred_masks"][keep[0]].numpy()
             diff, union = np.logical_xor(wm, d2[i] > 0).sum(), np.logical_or(wm, d2[i] > 0).sum()
             assert diff <= max(4, 0.03 * union), (i, diff, union)
+
+
+def test_sessions_share_primed_streams(session):
+    """A second session through the same predictor borrows the first one's
+    stream set (pipeline._checkout_streams: the model's per-stream
+    workspaces, no second priming forward) and gives the same results."""
+    from moseq2_detectron_extract_amd import pipeline as P
+    from moseq2_detectron_extract_amd.extract import extract_session
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    s, d = session
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), weights="synthetic")
+    cfg = P.ExtractConfig(chunk_size=500, use_tracking=True)
+    path = str(d / "depth.dat")
+    outs = []
+    for _ in range(2):
+        outs.append(extract_session(path, s.bground_im, s.roi, pred, cfg, true_depth=s.true_depth,
+                                    frame_trim=(0, N - 1200)))
+        pool = P._STREAM_POOLS[pred]
+        assert len(pool) == 1 and pool[0].primed
+    assert outs[0].keys() == outs[1].keys()
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)

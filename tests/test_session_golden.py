@@ -46,6 +46,26 @@ def test_read_frames_raw(gio, S, files, key):
                                       gio[f"readtar_{key}"])
 
 
+def test_read_frames_raw_large_runs(S, tmp_path, monkeypatch):
+    """Runs read straight into the destination rows as parallel preads
+    (session._direct_read, pieces cut at _READ_PIECE bytes, here smaller
+    than a frame run) equal the staged read; a file that ends early raises."""
+    monkeypatch.setattr(S, "_READ_PIECE", 4096 + 24)  # pieces that cut frames mid-row
+    rng = np.random.default_rng(3)
+    raw = rng.integers(-2000, 2000, (40, 12, 16)).astype("<i2")
+    dat = str(tmp_path / "depth.dat")
+    raw.tofile(dat)
+    for sel in (list(range(40)), list(range(5, 37)), [3, 4, 5, 9, 10, 2, 30, 31, 32, 33, 0],
+                list(range(39, -1, -1))):
+        got = S.read_frames_raw(dat, sel, frame_dims=(16, 12))
+        np.testing.assert_array_equal(got, raw[sel])
+        out = np.full((len(sel), 12, 16), -1, np.int16)
+        assert S.read_frames_raw(dat, sel, frame_dims=(16, 12), out=out) is out
+        np.testing.assert_array_equal(out, raw[sel])
+    with pytest.raises(ValueError):
+        S.read_frames_raw(dat, list(range(38, 42)), frame_dims=(16, 12))
+
+
 def test_chunk_boundaries(gio, S):
     from moseq2_detectron_extract_amd.shard import gen_batch_sequence
     for k in range(5):
