@@ -386,6 +386,9 @@ enum {
     MDX_CONV_KERNEL_SBG64 = 23,
     MDX_CONV_KERNEL_WINO_FUSED = 24, /* fused Winograd F(4,3) (mdx_conv_set_winograd_fused): both transforms
                                         and the 36 GEMMs in one launch */
+    MDX_CONV_KERNEL_HB128 = 25, /* SB128 / SB64 on k_conv_hb: half K-steps, two LDS stages, four workgroups
+                                   per CU (mdx_conv_set_half_step) */
+    MDX_CONV_KERNEL_HB64 = 26,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,
@@ -399,6 +402,11 @@ int mdx_conv_set_stream1x1(int mode, int min_m);
  * M threshold: 0 never, 1 (default) Cin == 64, 2 Cin in {64,128,256}.
  * Returns the previous mode. */
 int mdx_conv_set_stream1x1_f32(int mode);
+/* fp32 pointwise GEMMs (1x1 convs, FC layers, the Winograd GEMMs) on the
+ * half-step kernel k_conv_hb instead of k_conv_sb: 0 (default) off, 1 the
+ * 128-wide N tile, 2 also the 64-wide.  Same sums bit for bit.  Returns the
+ * previous mode. */
+int mdx_conv_set_half_step(int mode);
 
 /* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
  * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1

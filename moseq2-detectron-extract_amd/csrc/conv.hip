@@ -536,6 +536,178 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sbg(Co
     conv_body<T, TO, BN_, false, false, true>(a);
 }
 
+// fp32 pointwise GEMM (1x1 convs, FC layers, the batched Winograd GEMMs) in
+// half K-steps of 16 floats: 64-B LDS rows, two LDS stages and one barrier
+// per half-step, one register stage of 2 + BN_/64 16-B loads per thread.  The
+// half-step halves the fragment and staging registers of k_conv_sb, so four
+// workgroups (16 waves) fit a CU instead of three.  Per accumulator the
+// MFMAs take the same k's in the same order as k_conv_sb's substeps (half-
+// step h = K-step h / 2, substep h % 2): bit-identical sums.
+//   iteration h: [store half-step h + 1 (registers) into the other stage,
+//   load h + 2 into the registers, fragments + MFMAs of h] barrier
+// (the other stage was last read in iteration h - 1, before its barrier).
+__device__ __forceinline__ int hb_swz(int r) { return ((r >> 3) & 1) << 1; }
+
+template <typename TO, int BN_>
+__global__ __launch_bounds__(CONV_THREADS, 4) void k_conv_hb(ConvArgs a) {
+    constexpr int RB = 64;  // LDS row bytes: 16 floats
+    constexpr int TI = BM / 32, TJ = BN_ / 32;
+    constexpr int A_TILE = BM * RB, STAGE = A_TILE + BN_ * RB;
+    constexpr int ALD = BM * 4 / CONV_THREADS, BLD = BN_ * 4 / CONV_THREADS;  // 16-B loads per thread
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (gridDim.z > 1) {  // batch entry z of a batched GEMM
+        const long long z = blockIdx.z;
+        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
+        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
+        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
+    }
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN_;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // loads: rows lrow + 64 i, 16-B piece kc of the half-step's 64 B
+    const int kc = tid & 3, lrow = tid >> 2;
+    constexpr unsigned OOB = 0xFFFFFFF0u;
+    unsigned a_off[ALD], b_off[BLD];
+    const int ohw = a.OH * a.OW;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+        const int gm = m0 + lrow + 64 * i;
+        const int b = gm / ohw, rem = gm - b * ohw;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_off[i] = gm < a.M ? (unsigned)((((long long)b * a.H + (long long)oy * a.stride) * a.W +
+                                          (long long)ox * a.stride) * a.Cin * 4)
+                            : OOB;
+    }
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) {
+        const int gn = n0 + lrow + 64 * i;
+        b_off[i] = gn < a.Cout ? (unsigned)((long long)gn * a.K * 4) : OOB;
+    }
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
+    const int k0 = (int)blockIdx.y * a.ksteps * 32;
+    const int nh = min(2 * a.ksteps, (a.K - k0 + 15) / 16);
+    int kglob = k0 + kc * 4;
+    uint4 ra[ALD], rb[BLD];
+    auto load = [&]() {
+        const bool kok = kglob < a.K;
+        const unsigned kb = (unsigned)kglob * 4u;
+#pragma unroll
+        for (int i = 0; i < ALD; ++i)
+            ra[i] = __builtin_bit_cast(
+                uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && a_off[i] != OOB) ? a_off[i] + kb : OOB, 0, 0));
+#pragma unroll
+        for (int i = 0; i < BLD; ++i)
+            rb[i] = __builtin_bit_cast(
+                uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && b_off[i] != OOB) ? b_off[i] + kb : OOB, 0, 0));
+        kglob += 16;
+    };
+    // piece kc of row R at physical piece kc ^ g_swz(R) (k_convg's 64-B row
+    // layout: the fragment reads, rows l & 15 and pieces l >> 4, are
+    // conflict-free); (lrow + 64 i) has lrow's bit 3
+    const int wpiece = (kc ^ hb_swz(lrow)) * 16;
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ALD; ++i)
+            *reinterpret_cast<uint4 *>(smem + buf * STAGE + (lrow + 64 * i) * RB + wpiece) = ra[i];
+#pragma unroll
+        for (int i = 0; i < BLD; ++i)
+            *reinterpret_cast<uint4 *>(smem + buf * STAGE + A_TILE + (lrow + 64 * i) * RB + wpiece) = rb[i];
+    };
+
+    float4v acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    const int koff = ((lane >> 4) ^ hb_swz(lane & 15)) * 16;
+    const char *Ab0 = smem + (wm * (BM / 2) + (lane & 15)) * RB + koff;
+    const char *Bb0 = smem + A_TILE + (wn * (BN_ / 2) + (lane & 15)) * RB + koff;
+
+    load();
+    store(0);
+    if (nh > 1) load();
+    __syncthreads();
+    for (int h = 0; h < nh; ++h) {
+        const int cur = h & 1;
+        if (h + 1 < nh) store(cur ^ 1);
+        if (h + 2 < nh) load();
+        const char *Ab = Ab0 + cur * STAGE, *Bb = Bb0 + cur * STAGE;
+        float4v af[TI], bf[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * RB);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * RB);
+        constexpr int IG = TJ >= 4 ? 1 : 4 / TJ;
+#pragma unroll
+        for (int i0 = 0; i0 < TI; i0 += IG)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = i0; i < i0 + IG; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        __syncthreads();
+    }
+
+    // epilogue: as conv_body's (two halves of BM/2 rows through LDS)
+    constexpr int CP = BN_ + 4;
+    constexpr int HM = BM / 2;
+    float *Cs = reinterpret_cast<float *>(smem);
+    constexpr int CPR = BN_ / 8;
+    constexpr int NQ = HM * CPR / CONV_THREADS;
+    const int kz = blockIdx.y;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        if (wm == hh) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = i * 16 + (lane >> 4) * 4 + r;
+                        const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
+                        Cs[row * CP + col] = acc[i][j][r];
+                    }
+        }
+        __syncthreads();
+        const int mh = m0 + hh * HM;
+        if (a.ksplit > 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                const int gm = mh + row, gn0 = n0 + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) continue;
+                const float *src = Cs + row * CP + ch * 8;
+                float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
+                *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
+                *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
+            }
+        } else {
+            finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+                const int c = tid + q * CONV_THREADS;
+                const int row = c / CPR, ch = c - row * CPR;
+                gm = mh + row;
+                gn0 = n0 + ch * 8;
+                src = Cs + row * CP + ch * 8;
+                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+            });
+        }
+        if (hh == 0) __syncthreads();
+    }
+}
+
 // split-K reduction: sum the slices (fixed order) and apply the epilogue
 template <typename TO>
 __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
@@ -2158,6 +2330,20 @@ extern "C" int mdx_conv_set_single_stage(int on) {
     g_conv_sb = on;
     return old;
 }
+// fp32 PW GEMMs on k_conv_hb (half K-steps, two LDS stages, four workgroups
+// per CU) instead of k_conv_sb: 0 off, 1 the 128-wide tile, 2 also the
+// 64-wide -- mdx_conv_set_half_step; bit-identical sums
+static int g_conv_hb = 0;
+extern "C" int mdx_conv_set_half_step(int mode) {
+    const int old = g_conv_hb;
+    if (mode >= 0) g_conv_hb = mode;
+    return old;
+}
+static size_t hb_lds(int bn) {
+    const size_t main_ = 2 * ((size_t)BM * 64 + (size_t)bn * 64);
+    const size_t epi = (size_t)(BM / 2) * (bn + 4) * 4;
+    return main_ > epi ? main_ : epi;
+}
 // LDS of a k_conv launch: stage buffers (one when the whole K is one step or
 // the single-stage instance, else two) or the half-tile fp32 epilogue image
 static size_t conv_lds(int bn, int ksteps, bool sb) {
@@ -2565,10 +2751,16 @@ general:
     const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 3 && in_dtype == 1 && out_dtype == 1));
     const bool sbg = g_conv_sb >= 2 && !pw &&
                      ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 4 && in_dtype == 1 && out_dtype == 1));
+    // (k_conv_hb: fp32 in and out, PW; the 64-wide tile at mode 2)
+    const bool hb = g_conv_hb && pw && sb && in_dtype == 0 && out_dtype == 0 && (!narrow || g_conv_hb >= 2);
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
-        if (narrow && pw && sb && g_sb_afp)                                                                 \
+        if (hb && narrow)                                                                                   \
+            hipLaunchKernelGGL((k_conv_hb<TO_, 64>), grid, dim3(CONV_THREADS), hb_lds(64), s, a);            \
+        else if (hb)                                                                                        \
+            hipLaunchKernelGGL((k_conv_hb<TO_, 128>), grid, dim3(CONV_THREADS), hb_lds(128), s, a);          \
+        else if (narrow && pw && sb && g_sb_afp)                                                            \
             hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS),             \
                                conv_lds(64, a.ksteps, true), s, a);                                         \
         else if (!narrow && pw && sb && g_sb_afp)                                                           \
@@ -2607,7 +2799,8 @@ general:
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
-    t_plan_kernel = narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64)
+    t_plan_kernel = hb ? (narrow ? MDX_CONV_KERNEL_HB64 : MDX_CONV_KERNEL_HB128) :
+                    narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64)
                                  : (sbg ? MDX_CONV_KERNEL_SBG64 : MDX_CONV_KERNEL_REG64))
                            : (pw ? (sb ? MDX_CONV_KERNEL_SB128 : MDX_CONV_KERNEL_PW128)
                                  : (sbg ? MDX_CONV_KERNEL_SBG128 : MDX_CONV_KERNEL_REG128));
@@ -2962,6 +3155,12 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     } else if (g_fp32_split) {
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
+    } else if (g_pw && g_conv_sb && g_conv_hb && (bn == 128 || g_conv_hb >= 2)) {
+        if (bn == 64)
+            hipLaunchKernelGGL((k_conv_hb<float, 64>), grid, dim3(CONV_THREADS), hb_lds(64), s, a);
+        else
+            hipLaunchKernelGGL((k_conv_hb<float, 128>), grid, dim3(CONV_THREADS), hb_lds(128), s, a);
+        gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_HB64 : MDX_CONV_KERNEL_HB128;
     } else if (bn == 64) {
         if (g_pw && g_conv_sb && g_sb_afp) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 64, false, true>), grid, dim3(CONV_THREADS),

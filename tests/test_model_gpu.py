@@ -852,7 +852,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1], ids=["f32-mfma", "bf16x6", "f32-dma256"])
+@pytest.mark.parametrize("split", [0, 6, -1, -2], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep"])
 @pytest.mark.parametrize("m", [2, 4, 6])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True),
@@ -884,13 +884,22 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     if split == -1 and (Cout % 256 or Cin % 32):
         pytest.skip("the 256x256 LDS-DMA GEMM needs Cout % 256 == 0 and Cin % 32 == 0")
     old = call("mdx_conv_set_fp32_split", max(split, 0))
-    # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it
+    # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it;
+    # -2: on the half-step kernel (both tiles), bit-equal to the default's
     old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
+    old_hb = call("mdx_conv_set_half_step", 2 if split == -2 else 0)
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
+        if split == -2:
+            call("mdx_conv_set_half_step", 0)
+            ref = torch.empty_like(out)
+            call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(ref), P(ws), nb,
+                 None)
+            assert torch.equal(out, ref)
     finally:
         call("mdx_conv_set_fp32_split", old)
         call("mdx_conv_set_winograd_dma", old_dma, 384)
+        call("mdx_conv_set_half_step", old_hb)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
@@ -1183,23 +1192,27 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
     try:
         for ks in ((1, 3) if Cout % 8 == 0 else (1,)):
             outs = []
-            # single-stage with the A-fragment prefetch (mdx_conv_set_sb_afp) too
-            for single, afp in ((0, 0), (1, 0), (1, 1)):
+            # single-stage with the A-fragment prefetch (mdx_conv_set_sb_afp)
+            # too, and the half-step kernel (mdx_conv_set_half_step 2: both tiles)
+            for single, afp, hb in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 2)):
                 call("mdx_conv_set_single_stage", single)
                 old_afp = call("mdx_conv_set_sb_afp", afp)
+                old_hb = call("mdx_conv_set_half_step", hb)
                 try:
                     out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
                     call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0,
                          0, 0, P(out), ks, P(ws), nb, None)
                 finally:
                     call("mdx_conv_set_sb_afp", old_afp)
+                    call("mdx_conv_set_half_step", old_hb)
                 kid, ks_ = ctypes.c_int(), ctypes.c_int()
                 call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-                assert kid.value in ((18, 19) if single else (14, 15)), kid.value
+                assert kid.value in ((25, 26) if hb else (18, 19) if single else (14, 15)), kid.value
                 err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
-                assert err < 1e-4, (ks, single, err)
+                assert err < 1e-4, (ks, single, hb, err)
                 outs.append(out)
-            assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2]), ks
+            for o in outs[1:]:
+                assert torch.equal(outs[0], o), ks
     finally:
         for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
                          "mdx_conv_set_stream1x1_f32"), olds):
