@@ -407,6 +407,10 @@ int mdx_conv_set_stream1x1_f32(int mode);
  * 128-wide N tile, 2 also the 64-wide.  Same sums bit for bit.  Returns the
  * previous mode. */
 int mdx_conv_set_half_step(int mode);
+/* fp32-out GEMMs on k_conv / k_conv_sb: the epilogue (bias, residual, ReLU,
+ * store) straight from each lane's accumulators (1, default) instead of
+ * through a half-tile LDS image (0).  Same values.  Returns the previous mode. */
+int mdx_conv_set_direct_epilogue(int on);
 
 /* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
  * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1

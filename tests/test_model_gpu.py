@@ -852,7 +852,8 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1, -2], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep"])
+@pytest.mark.parametrize("split", [0, 6, -1, -2, -3],
+                         ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep", "f32-direct-epilogue"])
 @pytest.mark.parametrize("m", [2, 4, 6])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True),
@@ -885,13 +886,16 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
         pytest.skip("the 256x256 LDS-DMA GEMM needs Cout % 256 == 0 and Cin % 32 == 0")
     old = call("mdx_conv_set_fp32_split", max(split, 0))
     # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it;
-    # -2: on the half-step kernel (both tiles), bit-equal to the default's
+    # -2: on the half-step kernel (both tiles), -3: with the direct epilogue,
+    # bit-equal to the default's
     old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
     old_hb = call("mdx_conv_set_half_step", 2 if split == -2 else 0)
+    old_de = call("mdx_conv_set_direct_epilogue", 1 if split == -3 else 0)
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
-        if split == -2:
+        if split in (-2, -3):
             call("mdx_conv_set_half_step", 0)
+            call("mdx_conv_set_direct_epilogue", 0)
             ref = torch.empty_like(out)
             call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(ref), P(ws), nb,
                  None)
@@ -900,6 +904,7 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
         call("mdx_conv_set_fp32_split", old)
         call("mdx_conv_set_winograd_dma", old_dma, 384)
         call("mdx_conv_set_half_step", old_hb)
+        call("mdx_conv_set_direct_epilogue", old_de)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
@@ -1194,10 +1199,13 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
             outs = []
             # single-stage with the A-fragment prefetch (mdx_conv_set_sb_afp)
             # too, and the half-step kernel (mdx_conv_set_half_step 2: both tiles)
-            for single, afp, hb in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 2)):
+            # and the direct epilogue (mdx_conv_set_direct_epilogue)
+            for single, afp, hb, de in ((0, 0, 0, 0), (1, 0, 0, 0), (1, 1, 0, 0), (1, 0, 2, 0), (1, 0, 0, 1),
+                                        (0, 0, 0, 1)):
                 call("mdx_conv_set_single_stage", single)
                 old_afp = call("mdx_conv_set_sb_afp", afp)
                 old_hb = call("mdx_conv_set_half_step", hb)
+                old_de = call("mdx_conv_set_direct_epilogue", de)
                 try:
                     out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
                     call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0,
@@ -1205,6 +1213,7 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
                 finally:
                     call("mdx_conv_set_sb_afp", old_afp)
                     call("mdx_conv_set_half_step", old_hb)
+                    call("mdx_conv_set_direct_epilogue", old_de)
                 kid, ks_ = ctypes.c_int(), ctypes.c_int()
                 call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
                 assert kid.value in ((25, 26) if hb else (18, 19) if single else (14, 15)), kid.value
