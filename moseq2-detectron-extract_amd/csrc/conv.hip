@@ -2529,7 +2529,12 @@ extern "C" int mdx_conv_set_dma128(int mode, int min_tiles) {
 // layers with K <= g_narrow_kmax use the 64-wide N tile (4 workgroups per CU:
 // the HBM-bound small-K 1x1 convs need the memory parallelism more than the
 // wider tile's A-operand reuse)
-static constexpr int g_narrow_kmax = 128;
+static int g_narrow_kmax = 128;
+extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
+    const int old = g_narrow_kmax;
+    if (kmax >= 0) g_narrow_kmax = kmax;
+    return old;
+}
 
 // resident workgroups the split-K model assumes for the register-staged
 // kernels (512: two per CU; 384-1024 measured neutral in round 3)

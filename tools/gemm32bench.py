@@ -16,6 +16,8 @@ sys.path.insert(0, ROOT)
 
 # N, H, W, Cin, Cout, k, stride, pad, residual, count per forward
 DIRECT = [
+    (32, 112, 128, 256, 64, 1, 1, 0, False, 2),    # res2 conv1 (blocks 2-3)
+    (32, 112, 128, 64, 256, 1, 1, 0, True, 3),     # res2 conv3
     (32, 56, 64, 512, 128, 1, 1, 0, False, 3),     # res3 conv1
     (32, 56, 64, 128, 512, 1, 1, 0, True, 4),      # res3 conv3
     (32, 28, 32, 1024, 256, 1, 1, 0, False, 5),    # res4 conv1
