@@ -399,7 +399,7 @@ enum {
  * only when Cout == 64), 2 for every eligible layer with M >= min_m. */
 int mdx_conv_set_stream1x1(int mode, int min_m);
 /* Its fp32 form (f32 MFMAs; fp32 in and out, not in split-plane mode), same
- * M threshold: 0 never, 1 (default) Cin == 64, 2 Cin in {64,128,256}.
+ * M threshold: 0 (default) never, 1 Cin == 64, 2 Cin in {64,128,256}.
  * Returns the previous mode. */
 int mdx_conv_set_stream1x1_f32(int mode);
 /* fp32 pointwise GEMMs (1x1 convs, FC layers, the Winograd GEMMs) on the

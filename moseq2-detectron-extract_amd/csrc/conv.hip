@@ -1498,11 +1498,12 @@ extern "C" int mdx_conv_set_stream1x1(int mode, int min_m) {
     g_stream_min_m = min_m;
     return old;
 }
-// fp32 streaming 1x1 kernel (k_conv1x1_stream_f32), layers with M >= g_stream_min_m: 0 never,
-// 1 Cin = 64 (default: measured 3-9 % faster than k_conv<float, float, 64> on the res2 1x1
-// layers; 8-27 % slower at Cin = 128 and 256, where the one-shot tile's 2 waves per SIMD
-// leave the f32 MFMAs idle), 2 Cin in {64, 128, 256}
-static int g_stream1x1_f32 = 1;
+// fp32 streaming 1x1 kernel (k_conv1x1_stream_f32), layers with M >= g_stream_min_m: 0 never
+// (default since the GEMMs' direct epilogue: res2 conv3 on k_conv_sb<64> 307 vs 318 us, bench
+// loop 1477 vs 1473 fps over two interleaved pairs, profiles/r05_ab_stream1x1_f32.txt),
+// 1 Cin = 64 (3-9 % faster than k_conv<float, float, 64> on the res2 1x1 layers before
+// that; 8-27 % slower at Cin = 128 and 256), 2 Cin in {64, 128, 256}
+static int g_stream1x1_f32 = 0;
 extern "C" int mdx_conv_set_stream1x1_f32(int mode) {
     const int old = g_stream1x1_f32;
     g_stream1x1_f32 = mode;
