@@ -133,10 +133,10 @@ KERNEL_DEMANGLED = {
     "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
         "void mdx::k_convg<float, float, 8, false, false, false>(mdx::ConvArgs)",
 }
-for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<float, float, BN, DUAL>
-    _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
+for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<float, float, BN, DUAL, AFP=false>
+    _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}ELb0EEEvNS_8ConvArgsE"
     KERNEL_SYMBOLS["fp32"][_k] = _m
-    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
+    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}, false>(mdx::ConvArgs)"
 for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<T, T, BN>: single stage, general layers
     for _dt, _mt, _dm in (("fp32", "ff", "float, float"), ("fp16", "DF16_DF16_", "_Float16, _Float16")):
         _m = f"_ZN3mdx10k_conv_sbgI{_mt}Li{_bn}EEEvNS_8ConvArgsE"
