@@ -255,10 +255,17 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
     unsigned a2_off[DUAL ? 4 : 1];  // DUAL: byte offset of row i's pixel in x2
     bool a_ok[4];
     const int ohw = a.OH * a.OW;
+    // stride-1 pointwise layers (the 1x1 convs without a stride, FC layers,
+    // the Winograd GEMMs): row gm's pixel is pixel gm, no index division
+    const bool pw1 = PW && !DUAL && a.stride == 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int gm = m0 + lrow + 32 * i;
         a_ok[i] = gm < a.M;
+        if (pw1) {
+            a_base[i] = a_ok[i] ? (long long)gm * a.Cin * (long long)sizeof(T) : 0xFFFFFFF0ll;
+            continue;
+        }
         const int gmc = a_ok[i] ? gm : 0;
         const int b = gmc / ohw, rem = gmc - b * ohw;
         const int oy = rem / a.OW, ox = rem - oy * a.OW;
