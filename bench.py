@@ -189,13 +189,18 @@ FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k
                  "moments": ("k_moments",), "crop": ("k_crop",)}
 
 
-def conv_roofline(extractor, raw, steps=3, dump=None):
+F16_KEY = 100  # conv_roofline(split_dtypes=True): fp16-operand launches of kernel k are keyed F16_KEY + k
+
+
+def conv_roofline(extractor, raw, steps=3, dump=None, split_dtypes=False):
     """Time every conv launch of `steps` serial steps with HIP events on the
     launch stream (mdx_model_profile: events recorded by the model handle
     around each mdx_conv2d launch; a Winograd layer as its input transform,
     batched GEMM and output transform) and tag it with the kernel the library
     chose.  Returns {kernel id: [FLOP (executed; HBM bytes for the
-    transforms), seconds, launches, ksplit]} per step."""
+    transforms), seconds, launches, ksplit]} per step; with split_dtypes
+    (config 5's fp32 trunk + fp16 heads) the fp16-operand launches of kernel
+    k are counted under F16_KEY + k, so each is priced at its own peak."""
     import torch
     model = extractor.predictor.model
     rec = []
@@ -208,7 +213,9 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
     finally:
         model.profile(False)
     per = {}
-    for kid, ks, M, N, K, fl, ms in rec:
+    for kid, ks, M, N, K, fl, ms, dt in rec:
+        if split_dtypes and dt == 1:
+            kid = F16_KEY + kid
         d = per.setdefault(kid, [0.0, 0.0, 0, 0])
         d[0] += fl / steps
         d[1] += ms * 1e-3 / steps
@@ -216,8 +223,9 @@ def conv_roofline(extractor, raw, steps=3, dump=None):
         d[3] = max(d[3], ks)
     if dump:
         n = len(rec) // steps
-        rows = [{"M": M, "N": N, "K": K, "kernel": kid, "ksplit": ks, "us": ms * 1e3,
-                 "tflops": fl / (ms * 1e-3) / 1e12 if ms > 0 else None} for kid, ks, M, N, K, fl, ms in rec[-n:]]
+        rows = [{"M": M, "N": N, "K": K, "kernel": kid, "ksplit": ks, "dtype": "fp16" if dt == 1 else "fp32",
+                 "us": ms * 1e3, "tflops": fl / (ms * 1e-3) / 1e12 if ms > 0 else None}
+                for kid, ks, M, N, K, fl, ms, dt in rec[-n:]]
         with open(dump, "w") as fh:
             json.dump(rows, fh, indent=0)
     return per
@@ -252,7 +260,7 @@ def roofline_line(per, dtype, model_flop_per_step):
     from moseq2_detectron_extract_amd._lib import call
     peak = PEAK[dtype]
     kern = _pmc(dtype)
-    mfma = [k for k in per if k not in TRANSFORMS]
+    mfma = [k for k in per if k not in TRANSFORMS and k < F16_KEY]
     ranked = sorted(per, key=lambda k: -per[k][1])
     key = max(mfma, key=lambda k: per[k][1])
     fl, sec, n, ks = per[key]
@@ -262,15 +270,17 @@ def roofline_line(per, dtype, model_flop_per_step):
 
     def row(k):
         f, t, c, _ = per[k]
-        r = {"kernel": KERNEL_NAMES.get(k, str(k)), "symbol": KERNEL_SYMBOLS[dtype].get(k),
-             "launches_per_step": round(c), "ms_per_step": round(t * 1e3, 3)}
+        f16 = k >= F16_KEY  # an fp16-operand launch in a mixed-precision run: its own peak and symbol
+        kb, dk = (k - F16_KEY, "fp16") if f16 else (k, dtype)
+        r = {"kernel": KERNEL_NAMES.get(kb, str(kb)) + (" (fp16 operands)" if f16 else ""),
+             "symbol": KERNEL_SYMBOLS[dk].get(kb), "launches_per_step": round(c), "ms_per_step": round(t * 1e3, 3)}
         if k in TRANSFORMS:
             r.update(gbytes_per_step=round(f / 1e9, 3), achieved_gbs=round(f / t / 1e9, 1),
                      frac_hbm=round(f / t / 1e9 / HBM_PEAK, 4))
         else:
             r.update(tflop_per_step=round(f / 1e12, 4), achieved_tflops=round(f / t / 1e12, 2),
-                     frac=round(f / t / 1e12 / peak, 4))
-        pb = _pmc_bytes(kern, r["symbol"]) if r["symbol"] else None
+                     frac=round(f / t / 1e12 / PEAK[dk], 4), peak=PEAK[dk])
+        pb = _pmc_bytes(_pmc(dk) if f16 else kern, r["symbol"]) if r["symbol"] else None
         if pb is not None:
             r["pmc_hbm_bytes_per_launch"] = round(pb)
         return r
@@ -604,7 +614,7 @@ def main():
     roof = None
     if not args.no_roofline:
         raw_dev = raw_host[0].cuda()
-        per = conv_roofline(ex, raw_dev, dump=args.dump_convs)
+        per = conv_roofline(ex, raw_dev, dump=args.dump_convs, split_dtypes=args.dtype == "mixed")
         roof = roofline_line(per, "fp32" if args.dtype == "mixed" else args.dtype, flops_per_image(cfg) * B)
         roof["frame_ops"] = frame_ops_line(ex, raw_dev)
     del ex
@@ -660,7 +670,7 @@ def main():
                              "global_batch": B5 * world, "model_gflop_per_frame": round(flops_per_image(cfg5) / 1e9, 2)},
                   "note": "parity: tests/test_parity_full.py::test_forward_full_frame[101-64-mixed-6-0]"}
             if not args.no_roofline:
-                per5 = conv_roofline(ex5, raw5[0].cuda())
+                per5 = conv_roofline(ex5, raw5[0].cuda(), split_dtypes=True)
                 r5 = roofline_line(per5, "fp32", flops_per_image(cfg5) * B5)
                 c5["roofline"] = {k: r5[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernels",
                                                      "all_conv")}

@@ -760,6 +760,8 @@ typedef struct mdx_conv_record {
     int kernel, ksplit;
     int64_t M, N, K;
     double flop, ms;
+    int dtype;  /* the MFMA operand type of the launch: 0 f32, 1 f16 (config 5 mixes them) */
+    int reserved;
 } mdx_conv_record;
 int mdx_model_profile(mdx_model_t model, int on);
 int mdx_model_profile_read(mdx_model_t model, mdx_conv_record *out, int max);

@@ -731,9 +731,11 @@ struct Fwd {
                 const int64_t A = wm + 2, T = (int64_t)N * ((H + wm - 1) / wm) * ((W + wm - 1) / wm);
                 const double px = (double)N * H * W;
                 const mdx_conv_record rs[3] = {
-                    {MDX_CONV_KERNEL_WINO_IN, 1, T, cw.cin, A * A, 4.0 * (px + (double)A * A * T) * cw.cin, 0.0},
-                    {probe.gemm_kernel, 1, A * A * T, cw.cout, cw.cin, 2.0 * (double)A * A * T * cw.cout * cw.cin, 0.0},
-                    {MDX_CONV_KERNEL_WINO_OUT, 1, T, cw.cout, A * A, 4.0 * ((double)A * A * T + px) * cw.cout, 0.0}};
+                    {MDX_CONV_KERNEL_WINO_IN, 1, T, cw.cin, A * A, 4.0 * (px + (double)A * A * T) * cw.cin, 0.0, 0, 0},
+                    {probe.gemm_kernel, 1, A * A * T, cw.cout, cw.cin, 2.0 * (double)A * A * T * cw.cout * cw.cin, 0.0,
+                     0, 0},
+                    {MDX_CONV_KERNEL_WINO_OUT, 1, T, cw.cout, A * A, 4.0 * ((double)A * A * T + px) * cw.cout, 0.0, 0,
+                     0}};
                 // the fused kernel (one launch, timed by ev[2] / ev[3]) is one record
                 const bool fused = probe.gemm_kernel == MDX_CONV_KERNEL_WINO_FUSED;
                 for (int q = 0; q < 3; ++q) {
@@ -761,7 +763,7 @@ struct Fwd {
             mdx_conv2d_last_plan(&kid, &ks);
             const int64_t M = (int64_t)N * OH * OW, K = (int64_t)cw.k * cw.k * cw.cin;
             pe->r = mdx_conv_record{kid + (out_f32 && cw.dt == 1 ? 10 : 0), ks, M, cw.cout, K,
-                                    2.0 * (double)M * cw.cout * (cw.kalg ? cw.kalg : K), 0.0};
+                                    2.0 * (double)M * cw.cout * (cw.kalg ? cw.kalg : K), 0.0, cw.dt, 0};
         }
         return out;
     }
@@ -784,7 +786,7 @@ struct Fwd {
             int kid = -1, ks = 0;
             mdx_conv2d_last_plan(&kid, &ks);
             const int64_t M = (int64_t)N * H * W, K = (int64_t)cw.cin + cw.kalg;
-            pe->r = mdx_conv_record{kid, ks, M, cw.cout, K, 2.0 * (double)M * cw.cout * K, 0.0};
+            pe->r = mdx_conv_record{kid, ks, M, cw.cout, K, 2.0 * (double)M * cw.cout * K, 0.0, m.dt, 0};
         }
         return out;
     }

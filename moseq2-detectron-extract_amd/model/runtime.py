@@ -75,7 +75,8 @@ class OutputsC(ctypes.Structure):
 class ConvRecordC(ctypes.Structure):
     """struct mdx_conv_record (include/mdx.h)."""
     _fields_ = [("kernel", ctypes.c_int), ("ksplit", ctypes.c_int), ("M", ctypes.c_int64), ("N", ctypes.c_int64),
-                ("K", ctypes.c_int64), ("flop", ctypes.c_double), ("ms", ctypes.c_double)]
+                ("K", ctypes.c_int64), ("flop", ctypes.c_double), ("ms", ctypes.c_double), ("dtype", ctypes.c_int),
+                ("reserved", ctypes.c_int)]
 
 
 def model_cfg_c(cfg: ModelConfig, dtype: str) -> ModelCfgC:
@@ -181,11 +182,11 @@ class MaskRCNN:
         return bool(call("mdx_model_profile", self._h, int(on)))
 
     def profile_read(self, max_records: int = 4096):
-        """[(kernel, ksplit, M, N, K, flop, ms)] of the last profiled forward
-        (the stream must be synchronised)."""
+        """[(kernel, ksplit, M, N, K, flop, ms, dtype)] of the last profiled
+        forward (the stream must be synchronised; dtype 0 f32, 1 f16)."""
         buf = (ConvRecordC * max_records)()
         n = call("mdx_model_profile_read", self._h, buf, max_records)
-        return [(r.kernel, r.ksplit, r.M, r.N, r.K, r.flop, r.ms) for r in buf[:n]]
+        return [(r.kernel, r.ksplit, r.M, r.N, r.K, r.flop, r.ms, r.dtype) for r in buf[:n]]
 
     @torch.no_grad()
     def forward(self, frames: torch.Tensor, lut: Optional[np.ndarray] = None, intermediates: bool = False):
