@@ -414,6 +414,9 @@ int mdx_conv_set_direct_epilogue(int on);
 /* fp32 / fp16 GEMM layers with K <= kmax (default 128) take the 64-wide N
  * tile (more workgroups per CU for the short-K layers).  Returns the old value. */
 int mdx_conv_set_narrow_kmax(int kmax);
+/* The fp32 Winograd input transform with two channels per thread (1) or one
+ * (0, default).  Same values.  Returns the previous mode. */
+int mdx_conv_set_wino_in2(int on);
 
 /* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
  * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1

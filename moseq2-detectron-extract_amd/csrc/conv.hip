@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "wino_tables.h"
 
 namespace mdx {
 
@@ -2106,54 +2107,6 @@ __global__ __launch_bounds__(X6_THREADS, 1) void k_gemm_x6(ConvArgs a) {
 // tiles, points 0, +-1, +-2, +-1/2 (coefficients up to 32; error ~2x F(4,3)'s),
 // used on the large maps where its 8x8 tiles waste little at the edges.
 // ---------------------------------------------------------------------------
-template <int M>
-struct WinoT;
-template <>
-struct WinoT<2> {
-    static constexpr int A = 4;
-    __device__ static constexpr float BT(int i, int j) {
-        constexpr float t[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
-        return t[i][j];
-    }
-    __device__ static constexpr float AT(int i, int j) {
-        constexpr float t[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
-        return t[i][j];
-    }
-};
-template <>
-struct WinoT<4> {
-    static constexpr int A = 6;
-    __device__ static constexpr float BT(int i, int j) {
-        constexpr float t[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0}, {0, 4, -4, -1, 1, 0},
-                                   {0, -2, -1, 2, 1, 0}, {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
-        return t[i][j];
-    }
-    __device__ static constexpr float AT(int i, int j) {
-        constexpr float t[4][6] = {{1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
-        return t[i][j];
-    }
-};
-template <>
-struct WinoT<6> {
-    static constexpr int A = 8;
-    __device__ static constexpr float BT(int i, int j) {
-        constexpr float t[8][8] = {{1, 0, -5.25f, 0, 5.25f, 0, -1, 0},       {0, 1, 1, -4.25f, -4.25f, 1, 1, 0},
-                                   {0, -1, 1, 4.25f, -4.25f, -1, 1, 0},      {0, 0.5f, 0.25f, -2.5f, -1.25f, 2, 1, 0},
-                                   {0, -0.5f, 0.25f, 2.5f, -1.25f, -2, 1, 0}, {0, 2, 4, -2.5f, -5, 0.5f, 1, 0},
-                                   {0, -2, 4, 2.5f, -5, -0.5f, 1, 0},        {0, -1, 0, 5.25f, 0, -5.25f, 0, 1}};
-        return t[i][j];
-    }
-    __device__ static constexpr float AT(int i, int j) {
-        constexpr float t[6][8] = {{1, 1, 1, 1, 1, 1, 1, 0},
-                                   {0, 1, -1, 2, -2, 0.5f, -0.5f, 0},
-                                   {0, 1, 1, 4, 4, 0.25f, 0.25f, 0},
-                                   {0, 1, -1, 8, -8, 0.125f, -0.125f, 0},
-                                   {0, 1, 1, 16, 16, 0.0625f, 0.0625f, 0},
-                                   {0, 1, -1, 32, -32, 0.03125f, -0.03125f, 1}};
-        return t[i][j];
-    }
-};
-
 // one thread per (tile, channel): workgroup (blockIdx.x = tile, blockIdx.y =
 // channel block of blockDim.x), so the tile coordinates are workgroup-uniform
 // scalars (the per-thread 64-bit div / mod of a flat index cost more than the
@@ -3032,6 +2985,14 @@ extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
 // ---------------------------------------------------------------------------
 // Winograd F(m x m, 3x3) host side
 // ---------------------------------------------------------------------------
+// Winograd input transform with two channels per thread (k_wino_in2, 1) or
+// one (k_wino_in, 0) -- mdx_conv_set_wino_in2; same values bit for bit
+static int g_wino_in2 = 0;
+extern "C" int mdx_conv_set_wino_in2(int on) {
+    const int old = g_wino_in2;
+    if (on >= 0) g_wino_in2 = on;
+    return old;
+}
 static int g_winograd = 6;
 extern "C" int mdx_conv_set_winograd(int mode) {
     const int old = g_winograd;
@@ -3189,6 +3150,10 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             hipLaunchKernelGGL(k_wino_in_x6<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
         else
             hipLaunchKernelGGL(k_wino_in_x6<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
+    } else if (g_wino_in2 && Cin % 2 == 0) {
+        unsigned bd;
+        const dim3 grid = tgrid(Cin / 2, bd);
+        mdx::launch_wino_in2(m, grid, bd, s, x, N, H, W, Cin, TH, TW, V);
     } else {
         unsigned bd;
         const dim3 grid = tgrid(Cin, bd);

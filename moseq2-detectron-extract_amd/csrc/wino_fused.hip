@@ -11,6 +11,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "wino_tables.h"
 
 namespace mdx {
 
@@ -391,6 +392,76 @@ __global__ __launch_bounds__(WF4_THREADS, 2) void k_wino_f4(WinoF4Args a) {
                 __syncthreads();  // quarter stored: red free
             }
     }
+}
+
+// k_wino_in (conv.hip) with two channels per thread (8-B loads and stores: half the
+// memory instructions per byte); the same sums per channel, in the same order.
+// B^T d is formed in place column by column, then each row of (B^T d) B is
+// stored as it is formed (d plus one 8-entry temporary stay live)
+template <int M>
+__global__ __launch_bounds__(256) void k_wino_in2(const float *__restrict__ x, int N, int H, int W, int C, int TH,
+                                                  int TW, float *__restrict__ V) {
+    constexpr int A = WinoT<M>::A;
+    const int t = blockIdx.x;
+    const int c = 2 * (blockIdx.y * blockDim.x + threadIdx.x);
+    if (c >= C) return;
+    const long long T = (long long)N * TH * TW;
+    const long long xs = T * C;
+    const int tx = t % TW, r = t / TW;
+    const int ty = r % TH, n = r / TH;
+    const int y0 = M * ty - 1, x0 = M * tx - 1;
+    const float *xb = x + (long long)n * H * W * C + c;
+    float2 d[A][A];
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            const int yy = y0 + i, xx = x0 + j;
+            d[i][j] = (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                          ? *reinterpret_cast<const float2 *>(xb + ((long long)yy * W + xx) * C)
+                          : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+    for (int j = 0; j < A; ++j) {  // B^T d, column j, in place
+        float2 col[A];
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+            float ax = 0.f, ay = 0.f;
+#pragma unroll
+            for (int k = 0; k < A; ++k)
+                if (WinoT<M>::BT(i, k) != 0.f) {
+                    ax = ax + WinoT<M>::BT(i, k) * d[k][j].x;
+                    ay = ay + WinoT<M>::BT(i, k) * d[k][j].y;
+                }
+            col[i] = make_float2(ax, ay);
+        }
+#pragma unroll
+        for (int i = 0; i < A; ++i) d[i][j] = col[i];
+    }
+    float *vo = V + (long long)t * C + c;
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+#pragma unroll
+        for (int j = 0; j < A; ++j) {  // (B^T d) B
+            float ax = 0.f, ay = 0.f;
+#pragma unroll
+            for (int k = 0; k < A; ++k)
+                if (WinoT<M>::BT(j, k) != 0.f) {
+                    ax = ax + d[i][k].x * WinoT<M>::BT(j, k);
+                    ay = ay + d[i][k].y * WinoT<M>::BT(j, k);
+                }
+            *reinterpret_cast<float2 *>(vo + (A * i + j) * xs) = make_float2(ax, ay);
+        }
+}
+
+void launch_wino_in2(int m, dim3 grid, unsigned bd, hipStream_t s, const float *x, int N, int H, int W, int C,
+                     int TH, int TW, float *V) {
+    if (m == 2)
+        hipLaunchKernelGGL(k_wino_in2<2>, grid, dim3(bd), 0, s, x, N, H, W, C, TH, TW, V);
+    else if (m == 4)
+        hipLaunchKernelGGL(k_wino_in2<4>, grid, dim3(bd), 0, s, x, N, H, W, C, TH, TW, V);
+    else
+        hipLaunchKernelGGL(k_wino_in2<6>, grid, dim3(bd), 0, s, x, N, H, W, C, TH, TW, V);
 }
 
 }  // namespace mdx
