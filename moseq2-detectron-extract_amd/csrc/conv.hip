@@ -299,7 +299,31 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
     constexpr unsigned OOB = 0xFFFFFFF0u;
+    // K a multiple of BK (every layer of the models): each issued piece lies
+    // inside K, so a pointwise load is base + k with the out-of-range rows
+    // based at 2^31 (past any buffer: sizes are < 2^31, and base + k does not
+    // wrap), no per-load compare or select
+    const bool kfull = PW && !DUAL && (a.K % BK) == 0;
+    constexpr unsigned FAR = 0x80000000u;
+    unsigned a_far[PW ? 4 : 1], b_far[BLOADS];
+#pragma unroll
+    for (int i = 0; i < (PW ? 4 : 1); ++i) a_far[i] = (unsigned)a_base[i] != OOB ? (unsigned)a_base[i] : FAR;
+#pragma unroll
+    for (int i = 0; i < BLOADS; ++i) {
+        const int gn = n0 + lrow + 32 * i;
+        b_far[i] = gn < a.Cout ? (unsigned)((long long)gn * a.K * (long long)sizeof(T)) : FAR;
+    }
     auto load_global = [&](uint4 (&A)[4], uint4 (&Bv)[BLOADS]) {
+        if (kfull) {
+            const unsigned kb = (unsigned)(kglob * (int)sizeof(T));
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                A[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, a_far[PW ? i : 0] + kb, 0, 0));
+#pragma unroll
+            for (int i = 0; i < BLOADS; ++i)
+                Bv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, b_far[i] + kb, 0, 0));
+            return;
+        }
         const bool kok = kglob < a.K;
         // (K1 is a multiple of BK: the whole K-step reads one source)
         if (DUAL && kglob >= a.K1) {
