@@ -417,9 +417,6 @@ int mdx_conv_set_narrow_kmax(int kmax);
 /* The fp32 Winograd input transform with two channels per thread (1) or one
  * (0, default).  Same values.  Returns the previous mode. */
 int mdx_conv_set_wino_in2(int on);
-/* The fp32 Winograd transforms with consecutive tiles on one XCD (1) or
- * round-robin over the XCDs (0, default).  Same values.  Returns the old mode. */
-int mdx_conv_set_wino_xcd(int on);
 
 /* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
  * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1

@@ -90,7 +90,6 @@ SIGNATURES = {
     "mdx_conv_set_direct_epilogue": (I32, [I32]),
     "mdx_conv_set_narrow_kmax": (I32, [I32]),
     "mdx_conv_set_wino_in2": (I32, [I32]),
-    "mdx_conv_set_wino_xcd": (I32, [I32]),
     "mdx_conv_set_split256": (I32, [I32, I32]),
     "mdx_conv_set_dma_after": (I32, [I32]),
     "mdx_conv2d_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32, I32, I32, I32]),

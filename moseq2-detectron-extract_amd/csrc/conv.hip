@@ -2135,20 +2135,11 @@ __global__ __launch_bounds__(X6_THREADS, 1) void k_gemm_x6(ConvArgs a) {
 // channel block of blockDim.x), so the tile coordinates are workgroup-uniform
 // scalars (the per-thread 64-bit div / mod of a flat index cost more than the
 // loads); sums over nonzero coefficients only
-// tile of workgroup column L of nwg: identity, or (xcd) XCD-contiguous --
-// consecutive tiles (which share halo columns and write adjacent rows of each
-// V / output plane) on one XCD's L2 instead of round-robin over the eight
-__device__ __forceinline__ int wino_tile(int L, int nwg, int xcd) {
-    if (!xcd) return L;
-    const int q = nwg / 8, r = nwg % 8, x = L % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
-}
-
 template <int M>
 __global__ __launch_bounds__(256) void k_wino_in(const float *__restrict__ x, int N, int H, int W, int C, int TH,
-                                                 int TW, float *__restrict__ V, int xcd) {
+                                                 int TW, float *__restrict__ V) {
     constexpr int A = WinoT<M>::A;
-    const int t = wino_tile(blockIdx.x, gridDim.x, xcd);
+    const int t = blockIdx.x;
     const int c = blockIdx.y * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const long long T = (long long)N * TH * TW;
@@ -2270,9 +2261,9 @@ __global__ __launch_bounds__(256) void k_wino_in_x6(const float *__restrict__ x,
 template <int M>
 __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, int N, int OH, int OW, int K, int TH,
                                                   int TW, const float *__restrict__ bias, int relu,
-                                                  float *__restrict__ out, int xcd) {
+                                                  float *__restrict__ out) {
     constexpr int A = WinoT<M>::A;
-    const int t = wino_tile(blockIdx.x, gridDim.x, xcd);
+    const int t = blockIdx.x;
     const int k = blockIdx.y * blockDim.x + threadIdx.x;
     if (k >= K) return;
     const long long T = (long long)N * TH * TW;
@@ -3018,14 +3009,6 @@ extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
 // ---------------------------------------------------------------------------
 // Winograd F(m x m, 3x3) host side
 // ---------------------------------------------------------------------------
-// Winograd transforms' tiles XCD-contiguous over the workgroup columns (1) or
-// round-robin (0, default) -- mdx_conv_set_wino_xcd; same values
-static int g_wino_xcd = 0;
-extern "C" int mdx_conv_set_wino_xcd(int on) {
-    const int old = g_wino_xcd;
-    if (on >= 0) g_wino_xcd = on;
-    return old;
-}
 // Winograd input transform with two channels per thread (k_wino_in2, 1) or
 // one (k_wino_in, 0) -- mdx_conv_set_wino_in2; same values bit for bit
 static int g_wino_in2 = 0;
@@ -3199,11 +3182,11 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         unsigned bd;
         const dim3 grid = tgrid(Cin, bd);
         if (m == 2)
-            hipLaunchKernelGGL(k_wino_in<2>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V, g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_in<2>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
         else if (m == 4)
-            hipLaunchKernelGGL(k_wino_in<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V, g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_in<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
         else
-            hipLaunchKernelGGL(k_wino_in<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V, g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_in<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, V);
     }
     mark(1);
     mark(2);
@@ -3301,14 +3284,11 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         unsigned bd;
         const dim3 grid2 = tgrid(Cout, bd);
         if (m == 2)
-            hipLaunchKernelGGL(k_wino_out<2>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out,
-                               g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_out<2>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
         else if (m == 4)
-            hipLaunchKernelGGL(k_wino_out<4>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out,
-                               g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_out<4>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
         else
-            hipLaunchKernelGGL(k_wino_out<6>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out,
-                               g_wino_xcd);
+            hipLaunchKernelGGL(k_wino_out<6>, grid2, dim3(bd), 0, s, Mx, N, H, W, Cout, TH, TW, bias, relu, out);
     }
     mark(5);
     if (probe) probe->gemm_kernel = gemm_kernel;

@@ -38,3 +38,6 @@ def test_fp32_symbols_exported_by_the_library():
     for kid in (18, 19, 20, 21, 22, 23):
         sym = b.KERNEL_SYMBOLS["fp32"][kid]
         assert any(n.startswith(sym) for n in names), sym
+    for kid in (12, 13):  # the Winograd transforms, both tile sizes: exact symbols (the PMC keys)
+        for sym in b.KERNEL_SYMBOLS["fp32"][kid]:
+            assert sym in names, sym

@@ -852,9 +852,8 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1, -2, -3, -4, -5],
-                         ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep", "f32-direct-epilogue", "f32-wino-in2",
-                              "f32-wino-xcd"])
+@pytest.mark.parametrize("split", [0, 6, -1, -2, -3, -4],
+                         ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep", "f32-direct-epilogue", "f32-wino-in2"])
 @pytest.mark.parametrize("m", [2, 4, 6])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True),
@@ -888,20 +887,17 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     old = call("mdx_conv_set_fp32_split", max(split, 0))
     # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it;
     # -2: on the half-step kernel (both tiles), -3: with the direct epilogue,
-    # -4: the two-channel input transform, -5: XCD-contiguous transform tiles,
-    # bit-equal to the default's
+    # -4: the two-channel input transform, bit-equal to the default's
     old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
     old_hb = call("mdx_conv_set_half_step", 2 if split == -2 else 0)
     old_de = call("mdx_conv_set_direct_epilogue", 1 if split == -3 else 0)
     old_in2 = call("mdx_conv_set_wino_in2", 1 if split == -4 else 0)
-    old_xcd = call("mdx_conv_set_wino_xcd", 1 if split == -5 else 0)
     try:
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
-        if split in (-2, -3, -4, -5):
+        if split in (-2, -3, -4):
             call("mdx_conv_set_half_step", 0)
             call("mdx_conv_set_direct_epilogue", 0)
             call("mdx_conv_set_wino_in2", 0)
-            call("mdx_conv_set_wino_xcd", 0)
             ref = torch.empty_like(out)
             call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(ref), P(ws), nb,
                  None)
@@ -912,7 +908,6 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
         call("mdx_conv_set_half_step", old_hb)
         call("mdx_conv_set_direct_epilogue", old_de)
         call("mdx_conv_set_wino_in2", old_in2)
-        call("mdx_conv_set_wino_xcd", old_xcd)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
