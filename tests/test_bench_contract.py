@@ -41,3 +41,25 @@ def test_fp32_symbols_exported_by_the_library():
     for kid in (12, 13):  # the Winograd transforms, both tile sizes: exact symbols (the PMC keys)
         for sym in b.KERNEL_SYMBOLS["fp32"][kid]:
             assert sym in names, sym
+
+
+def test_committed_roofline_agrees_with_rocprof():
+    """The committed bench line's dominant-kernel time (HIP events, serial
+    steps) and the committed rocprof serial summary's average launch of the
+    same kernel agree within 5 % (they come from the same tree; the boxes of
+    the pool differ by about 1.5 %)."""
+    import csv
+    import json
+    b = _bench()
+    prof = os.path.join(ROOT, "profiles")
+    line = json.load(open(os.path.join(prof, "r05_bench.json")))
+    roof = line["roofline"]
+    top = roof["kernels"][0]
+    per_launch_ms = top["ms_per_step"] / top["launches_per_step"]
+    demangled = b.KERNEL_DEMANGLED.get(top["symbol"], top["symbol"])
+    rows = {r["Name"]: r for r in csv.DictReader(open(os.path.join(prof, "r05_kernel_stats_fp32_serial.csv")))}
+    assert demangled in rows, demangled
+    avg_ms = float(rows[demangled]["AverageNs"]) / 1e6
+    assert abs(avg_ms / per_launch_ms - 1) < 0.05, (avg_ms, per_launch_ms)
+    assert roof["traffic"] and roof["traffic"] > 0
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
