@@ -176,3 +176,39 @@ def test_sessions_share_primed_streams(session):
     assert outs[0].keys() == outs[1].keys()
     for k in outs[0]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+def test_concurrent_sessions_one_predictor(session):
+    """Two sessions extracted at once from two threads through one predictor
+    borrow two stream sets (pipeline._checkout_streams hands a busy set to
+    nobody else; the model keeps a workspace per stream) and give the same
+    arrays as one session alone."""
+    import threading
+    from moseq2_detectron_extract_amd import pipeline as P
+    from moseq2_detectron_extract_amd.extract import extract_session
+    from moseq2_detectron_extract_amd.model import ModelConfig, Predictor
+    s, d = session
+    pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), weights="synthetic")
+    cfg = P.ExtractConfig(chunk_size=400, use_tracking=True)
+    path = str(d / "depth.dat")
+    kw = dict(true_depth=s.true_depth, frame_trim=(0, N - 800))
+    want = extract_session(path, s.bground_im, s.roi, pred, cfg, **kw)
+    got, errs = [None, None], []
+
+    def run(i):
+        try:
+            torch.cuda.set_device(0)
+            got[i] = extract_session(path, s.bground_im, s.roi, pred, cfg, **kw)
+        except BaseException as e:  # surfaced below
+            errs.append(e)
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert len(P._STREAM_POOLS[pred]) == 2
+    for g in got:
+        assert g.keys() == want.keys()
+        for k in want:
+            np.testing.assert_array_equal(g[k], want[k], err_msg=k)
