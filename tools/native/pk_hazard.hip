@@ -12,7 +12,7 @@
 // pure function of the inputs: any difference is an execution fault.
 //
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/native/pk_hazard.hip -o tools/native/pk_hazard
-// Run:   pk_hazard REPS BG   (BG: 0 none, 1 bf16 MFMA loop, 2 f16, 3 f32)
+// Run:   pk_hazard REPS BG [FIRST_FORM]   (BG: 0 none, 1 bf16 MFMA loop, 2 f16, 3 f32)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -41,8 +41,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // 9 v_pk_fma_f32 SGPR pair op_sel_hi:[1,0,1], 10 v_pk_mul_f32 SGPR pair,
 // 11 v_pk_mul_f32 constant op_sel_hi:[1,0], 12 v_pk_mul_f32 SGPR pair
 // op_sel_hi:[1,0], 13 v_pk_min_u16 / v_pk_max_u16 (plain, and an SGPR with
-// op_sel_hi:[1,0])
-constexpr int NFORMS = 14;
+// op_sel_hi:[1,0]); 14 v_pk_minimum3_f16 (three VGPRs, no modifiers) over
+// halves 0x6400 + v (v < 256: the normal f16 values 1024 + v), the form a
+// 3-input minimum in the clean_frames morphology would use
+constexpr int NFORMS = 15;
 
 template <int F>
 __global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *__restrict__ out, int iters,
@@ -94,6 +96,16 @@ __global__ __launch_bounds__(256) void k_victim(const f2 *__restrict__ in, f2 *_
             asm volatile("v_pk_min_u16 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(y) : "s"(su));
             asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(by));
             asm volatile("v_xor_b32 %0, %0, %1" : "+v"(y) : "v"(bx));
+            a = f2{__builtin_bit_cast(float, x), __builtin_bit_cast(float, y)};
+        } else if constexpr (F == 14) {
+            unsigned x = __builtin_bit_cast(unsigned, a.x), y = __builtin_bit_cast(unsigned, a.y);
+            const unsigned bx = __builtin_bit_cast(unsigned, b.x), by = __builtin_bit_cast(unsigned, b.y);
+            const unsigned p = (x & 0x00FF00FFu) | 0x64006400u, q = (by & 0x00FF00FFu) | 0x64006400u,
+                           r = ((bx >> 5) & 0x00FF00FFu) | 0x64006400u;
+            unsigned d;
+            asm volatile("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(p), "v"(q), "v"(r));
+            asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(d));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(y) : "v"(d));
             a = f2{__builtin_bit_cast(float, x), __builtin_bit_cast(float, y)};
         } else {
             float x = a.x, y = a.y;
@@ -161,13 +173,15 @@ static void launch_form(int f, const f2 *in, f2 *out, int blocks, int iters, hip
         case 10: launch<10>(in, out, blocks, iters, s); break;
         case 11: launch<11>(in, out, blocks, iters, s); break;
         case 12: launch<12>(in, out, blocks, iters, s); break;
-        default: launch<13>(in, out, blocks, iters, s); break;
+        case 13: launch<13>(in, out, blocks, iters, s); break;
+        default: launch<14>(in, out, blocks, iters, s); break;
     }
 }
 
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 200;
     const int bg = argc > 2 ? atoi(argv[2]) : 1;
+    const int f0 = argc > 3 ? atoi(argv[3]) : 0;  // first form to run
     const int blocks = 512, iters = 256, n = blocks * 256;
     std::vector<f2> hin(2 * n);
     unsigned s = 777u;
@@ -189,7 +203,7 @@ int main(int argc, char **argv) {
     CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
     std::vector<f2> ref(n), got(n);
     printf("{\"reps\": %d, \"background\": %d", reps, bg);
-    for (int f = 0; f < NFORMS; ++f) {
+    for (int f = f0; f < NFORMS; ++f) {
         int bad = 0, lanes_hi = 0, lanes_lo = 0;
         for (int r = 0; r <= reps; ++r) {
             if (r > 0 && bg == 1) hipLaunchKernelGGL(k_bg_mfma<1>, dim3(2048), dim3(256), 0, sb, bgout, 400 + 37 * (r % 5));
