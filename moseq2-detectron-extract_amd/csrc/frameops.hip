@@ -300,6 +300,14 @@ struct CleanStream {
 };
 
 __device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) { return pk_op<false>(a, b); }
+// 3-input minimum of u16 pairs held as 0x6400 + v (v <= 255): those halves
+// are the normal f16 values 1024 + v, ordered as their integers, so the f16
+// minimum is the integer minimum (one instruction for two pmin)
+__device__ __forceinline__ uint32_t pmin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 // one VALU instruction each (written out: the compiler shares min(a, b)
 // between a min3 and a med3 of the same operands and then emits neither)
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
@@ -332,7 +340,9 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
     const int tid = threadIdx.x, wave = tid >> 6;
     const bool med = wave >= C::MW;
     const int NSTEP = H + C::OUT(6) + 1;
-    constexpr uint32_t NEUT = 0x00FF00FFu;
+    // stage rows hold each pixel v as 0x6400 + v (pmin3); the neutral value
+    // is 255, dilation works on 255 - v = v ^ 0xFF
+    constexpr uint32_t FH = 0x64006400u, NEUT = 0x64FF64FFu, INVX = 0x00FF00FFu;
 
     // ---- per-lane role ----
     int stage = 0, q = -1, x0 = 0;
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
     bool cok[4];  // this lane's output columns inside the frame
 #pragma unroll
     for (int c = 0; c < 4; ++c) cok[c] = x0 + c >= 0 && x0 + c < W;
-    const uint32_t inv = stage == 3 || stage == 6 ? NEUT : 0u;  // dilation: work on 255 - v
+    const uint32_t inv = stage == 3 || stage == 6 ? INVX : 0u;  // dilation: work on 255 - v
     const int idx = x0 - BX;                                      // u16 / byte column of this lane's quad
     const int out_off = stage >= 1 ? C::OUT(stage) : 27;
 
@@ -444,7 +454,7 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
                         m4[p] = umed3(umax3(lo[p], lo[p + 1], lo[p + 2]), umed3(mi[p], mi[p + 1], mi[p + 2]),
                                       umin3(hi[p], hi[p + 1], hi[p + 2]));
                     const int row = t - out_off;
-                    uint32_t a = m4[0] | (m4[1] << 16), b = m4[2] | (m4[3] << 16);
+                    uint32_t a = m4[0] | (m4[1] << 16) | FH, b = m4[2] | (m4[3] << 16) | FH;
                     if (row < 0 || row >= H) {
                         a = b = NEUT;
                     } else {
@@ -465,16 +475,16 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
                 const uint32_t q1 = __builtin_amdgcn_alignbyte(q2, q0, 2);
                 const uint32_t q3 = __builtin_amdgcn_alignbyte(q4, q2, 2);
                 const uint32_t q5 = __builtin_amdgcn_alignbyte(q6, q4, 2);
-                const uint32_t u = pmin(pmin(pmin(qm1, q0), pmin(q1, q2)), q3);
-                const uint32_t s3a = pmin(u, pmin(qm3, qm2)), s3b = pmin(u, pmin(q4, q5));
+                const uint32_t u = pmin3(pmin3(qm1, q0, q1), q2, q3);
+                const uint32_t s3a = pmin3(u, qm3, qm2), s3b = pmin3(u, q4, q5);
                 // the ring keeps, per row r, the span-3 minimum of rows r-1 and r
                 // (the ellipse's half-width-3 rows come in adjacent pairs)
                 R3(k, 0) = pmin(s3a, s3p[0]);
                 R3(k, 1) = pmin(s3b, s3p[1]);
                 s3p[0] = s3a;
                 s3p[1] = s3b;
-                R4(k, 0) = pmin(s3a, pmin(qm4, q4));
-                R4(k, 1) = pmin(s3b, pmin(qm2, q6));
+                R4(k, 0) = pmin3(s3a, qm4, q4);
+                R4(k, 1) = pmin3(s3b, qm2, q6);
                 R0(k, 0) = q0;
                 R0(k, 1) = q2;
                 // ellipse rows 0..8 of the output row = ring slots k+1 .. k+9:
@@ -483,10 +493,9 @@ __global__ __launch_bounds__(CleanStream<SW>::THREADS) void k_clean_stream(const
                 uint32_t v[2];
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
-                    const uint32_t a = pmin(R0((k + 1) % 9, p), R0(k, p));
-                    const uint32_t b = pmin(R3((k + 3) % 9, p), R3((k + 8) % 9, p));
-                    const uint32_t c = pmin(pmin(R4((k + 4) % 9, p), R4((k + 5) % 9, p)), R4((k + 6) % 9, p));
-                    v[p] = pmin(pmin(a, b), c);
+                    v[p] = pmin3(pmin3(R0((k + 1) % 9, p), R0(k, p), R3((k + 3) % 9, p)),
+                                 pmin3(R3((k + 8) % 9, p), R4((k + 4) % 9, p), R4((k + 5) % 9, p)),
+                                 R4((k + 6) % 9, p));
                 }
                 const int row = t - out_off;
                 if (stage < 6) {
