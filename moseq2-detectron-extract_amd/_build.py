@@ -60,6 +60,26 @@ def sources(csrc: str = CSRC):
     return sorted(glob.glob(os.path.join(csrc, "*.hip")))
 
 
+def objects(csrc: str = CSRC, obj: str = OBJ):
+    """The objects the library is linked from: exactly one per csrc/*.hip
+    source.  Anything else left in the object directory (an experiment's
+    object) is never linked."""
+    return [os.path.join(obj, os.path.basename(s)[:-4] + ".o") for s in sources(csrc)]
+
+
+# libraries libmdx.so may depend on: the HIP runtime and the C/C++ runtime.
+# No vendor GEMM library (hipBLASLt / rocBLAS: the in-process copy is
+# PyTorch's ROCm 7.0 build, DESIGN.md section 3 "fp32 GEMM against the
+# library"), no MIOpen: every kernel of the hot path is this library's own.
+ALLOWED_NEEDED = ("libamdhip64.so", "libstdc++.so", "libm.so", "libgcc_s.so", "libc.so", "ld-linux-x86-64.so")
+
+
+def needed(lib: str = LIB):
+    """DT_NEEDED entries of `lib`."""
+    r = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True, check=True)
+    return [ln.split("[", 1)[1].rstrip("]").strip() for ln in r.stdout.splitlines() if "(NEEDED)" in ln]
+
+
 def _deps_newer(target: str, srcs, csrc: str = CSRC) -> bool:
     if not os.path.exists(target):
         return True
@@ -89,11 +109,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8, csrc: str =
     os.makedirs(obj, exist_ok=True)
     cc = hipcc()
     srcs = sources(csrc)
-    objs = []
+    objs = objects(csrc, obj)
     todo = []
-    for s in srcs:
-        o = os.path.join(obj, os.path.basename(s)[:-4] + ".o")
-        objs.append(o)
+    for s, o in zip(srcs, objs):
         if force or _deps_newer(o, [s], csrc) or _flags_changed(o, _cmd_flags(os.path.basename(s))):
             todo.append((s, o))
 
@@ -121,8 +139,20 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 8, csrc: str =
         if r.returncode != 0:
             raise RuntimeError(f"link of {os.path.basename(lib)} failed:\n{r.stderr[-6000:]}")
         check_symbols(lib)
+        check_needed(lib)
         check_isa(lib)
     return lib
+
+
+def check_needed(lib: str = LIB) -> None:
+    """Refuse (delete) a library that depends on anything but the HIP and
+    C/C++ runtimes."""
+    if not shutil.which("readelf"):
+        return
+    bad = [n for n in needed(lib) if not n.startswith(ALLOWED_NEEDED)]
+    if bad:
+        os.remove(lib)
+        raise RuntimeError(f"{os.path.basename(lib)} depends on {bad}: only {ALLOWED_NEEDED} are allowed")
 
 
 def check_symbols(lib: str = LIB) -> None:

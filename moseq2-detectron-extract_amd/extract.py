@@ -19,9 +19,11 @@ the session's single results_00 file and keypoints TSV -- the files one
 process writes, byte for byte (ResultWriterStep's single writer,
 M/pipeline/write_results_step.py:31-36).
 
-The h5 writer itself is not rebuilt (h5py is absent from this image); the
-results are returned as arrays keyed like the h5 datasets and can be saved as
-``.npz``.
+With `output_dir` the session's results file is written through
+results.open_results: a real ``results_00.h5`` when h5py is importable (its
+tree equals the reference writer's, tests/test_results_h5.py), else the same
+tree as ``results_00.npz``.  The results are also returned as arrays keyed
+like the h5 datasets.
 """
 from __future__ import annotations
 
@@ -240,6 +242,7 @@ class _ChunkWriter:
         # rank (= session) order at close
         self.tsv_parts = [KeypointsTSVWriter(output_dir, path=f"{self.tsv.path}.part{r}", header=False)
                           for r in range(parts)] if parts > 1 else None
+        self._remove_parts()  # an earlier failed run's parts (any world size) must not be joined
         self._cols = None
         self.timeline = None  # extract._Timeline when the extract loop is traced
         self._nwritten = 0
@@ -276,6 +279,14 @@ class _ChunkWriter:
             except BaseException as e:  # surfaced by write() / close()
                 self._err.append(e)
 
+    def _remove_parts(self) -> None:
+        """Delete every keypoints part file of this results index."""
+        if self.tsv_parts is None:
+            return
+        import glob
+        for p in glob.glob(glob.escape(self.tsv.path) + ".part*"):
+            os.remove(p)
+
     def write(self, d: dict, part: int = 0) -> None:
         if self._err:
             raise self._err[0]
@@ -291,7 +302,9 @@ class _ChunkWriter:
             raise self._err[0]
         t0 = self.timeline.now() if self.timeline else 0
         if self.tsv_parts is not None and self._cols is not None:
-            join_tsv_parts(self.tsv.path, self._cols, [w.path for w in self.tsv_parts])
+            # only the parts written in this run (a rank without chunks has none)
+            join_tsv_parts(self.tsv.path, self._cols, [w.path for w in self.tsv_parts if not w._fresh])
+        self._remove_parts()
         self.h5.close()
         if self.timeline:
             self.timeline.add("results file close", -1, t0)
@@ -306,6 +319,7 @@ class _ChunkWriter:
         self._err.append(RuntimeError("extraction failed"))  # the thread skips the queued chunks
         self._q.put(None)
         self._t.join()
+        self._remove_parts()
         if not isinstance(self.h5, MemoryH5):
             try:
                 self.h5.close()

@@ -312,7 +312,12 @@ def open_results(output_dir: str, bg_roi_index: int = 0):
 
 
 def dict_to_h5(h5_file, data: dict, root: str = "/", annotations: Optional[dict] = None) -> None:
-    """Nested dict -> datasets under `root` (None -> empty string dataset)."""
+    """Nested dict -> datasets under `root`.  None becomes an empty
+    variable-length string dataset (h5py.Empty; "" in a MemoryH5, which has
+    no empty datasets).  As in the reference, a value that cannot be stored
+    is logged and skipped, not raised: the parameters are metadata, and one
+    odd entry must not fail the results file."""
+    import logging
     if not root.endswith("/"):
         root = root + "/"
     annotations = annotations or {}
@@ -321,16 +326,25 @@ def dict_to_h5(h5_file, data: dict, root: str = "/", annotations: Optional[dict]
         if isinstance(item, dict):
             dict_to_h5(h5_file, item, dest)
             continue
-        if isinstance(item, (np.ndarray, np.int64, np.float64, str, bytes)):
-            h5_file[dest] = item
-        elif isinstance(item, (tuple, list)):
-            h5_file[dest] = np.asarray(item)
-        elif isinstance(item, (int, float)):
-            h5_file[dest] = np.asarray([item])[0]
-        elif item is None:
-            h5_file[dest] = ""
-        else:
-            raise ValueError(f"Cannot save {type(item)} type to key {dest}")
+        try:
+            if isinstance(item, (np.ndarray, np.int64, np.float64, str, bytes)):
+                h5_file[dest] = item
+            elif isinstance(item, (tuple, list)):
+                h5_file[dest] = np.asarray(item)
+            elif isinstance(item, (int, float)):
+                h5_file[dest] = np.asarray([item])[0]
+            elif item is None:
+                if isinstance(h5_file, MemoryH5):
+                    h5_file[dest] = ""
+                else:
+                    import h5py
+                    h5_file.create_dataset(dest, data=h5py.Empty(dtype=h5py.special_dtype(vlen=str)))
+            else:
+                raise ValueError(f"Cannot save {type(item)} type to key {dest}")
+        except Exception as exc:  # M/io/util.py:171-174
+            logging.error(exc, exc_info=True)
+            logging.error(f'h5py could not encode key: "{key}"')
+            continue
         if key in annotations:
             h5_file[dest].attrs["description"] = "" if annotations[key] is None else annotations[key]
 

@@ -79,3 +79,54 @@ def test_build_refuses_the_form(tmp_path):
     with pytest.raises(RuntimeError, match="outside the forms"):
         _build.build(csrc=str(csrc), obj=str(tmp_path / "obj"), lib=str(lib))
     assert not lib.exists()
+
+
+def test_library_depends_only_on_runtimes():
+    """libmdx.so's DT_NEEDED: the HIP runtime and the C/C++ runtime only --
+    no hipBLASLt / rocBLAS / MIOpen (round 5 routed fp32 GEMMs to hipBLASLt
+    from inside the library and faulted: PyTorch's bundled ROCm 7.0 copy
+    resolved against 7.2 headers; the route was removed
+    and this keeps it out)."""
+    import shutil
+    import _build
+    if not os.path.exists(LIB) or not shutil.which("readelf"):
+        pytest.skip("libmdx.so not built or readelf absent")
+    deps = _build.needed(LIB)
+    assert any(d.startswith("libamdhip64.so") for d in deps), deps
+    assert all(d.startswith(_build.ALLOWED_NEEDED) for d in deps), deps
+    for bad in ("blas", "miopen", "rccl", "torch"):
+        assert not any(bad in d.lower() for d in deps), deps
+
+
+def test_build_links_only_the_sources_objects(tmp_path):
+    """build() links exactly one object per csrc/*.hip: an experiment's
+    object left in the object directory (round 5's blas.o) is never linked."""
+    import _build
+    csrc = tmp_path / "csrc"
+    obj = tmp_path / "obj"
+    csrc.mkdir()
+    obj.mkdir()
+    for n in ("a", "b"):
+        (csrc / f"{n}.hip").write_text("")
+    (obj / "blas.o").write_text("")
+    assert _build.objects(str(csrc), str(obj)) == [str(obj / "a.o"), str(obj / "b.o")]
+    real = _build.objects()
+    assert sorted(os.path.basename(o) for o in real) == \
+        sorted(os.path.basename(s)[:-4] + ".o" for s in _build.sources())
+    assert not any("blas" in os.path.basename(o) for o in real)
+
+
+@needs_hipcc
+def test_build_refuses_a_vendor_blas_dependency(tmp_path):
+    """check_needed() deletes a library linked against a GEMM library."""
+    import _build
+    if not os.path.exists("/opt/rocm/lib/librocblas.so"):
+        pytest.skip("rocBLAS absent")
+    src = tmp_path / "k.cpp"
+    src.write_text("extern \"C\" int rocblas_create_handle(void **);\nint f(void **h) { return rocblas_create_handle(h); }\n")
+    lib = tmp_path / "libk.so"
+    subprocess.run(["g++", "-shared", "-fPIC", str(src), "-o", str(lib), "-L/opt/rocm/lib", "-lrocblas",
+                    "-Wl,--no-as-needed"], check=True, capture_output=True)
+    with pytest.raises(RuntimeError, match="depends on"):
+        _build.check_needed(str(lib))
+    assert not lib.exists()
