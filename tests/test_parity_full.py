@@ -33,14 +33,27 @@ Tolerances (written here, stated in DESIGN.md §4):
       has the oracle's centroid bit for bit and its angle to ANGLE_ULPS ulp
       (the moments are integer-exact; the orientation's atan2 is the GPU's
       libm, which may round the last bit differently from glibc), and the
-      pipeline's depth crop equals the oracle chain's byte for byte; at least
-      MIN_SEL_EXACT of the frames have the identical selected mask.
-    fp16 (BASELINE config 5's precision, vs the fp32 oracle): the detection
-      checks above hold on at least FP16_FRAMES of the frames and the pose
-      bounds on at least FP16_FRAMES; at least FP16_CROP_EXACT of the
-      non-NaN-pose frames give the oracle's depth crop byte for byte (the
-      rest differ because fp16 moves the small seeded-weight masks by a few
-      near-threshold pixels, and with them the pose); recorded per frame.
+      pipeline's depth crop equals the oracle chain's byte for byte.
+  conditioning (fp32): a frame is WELL-CONDITIONED when no pixel of the
+    oracle's pasted probability map of its selected detection lies within
+    NEAR_EPS of the 0.5 paste threshold (M/model/util.py:45-62,
+    detector_postprocess; M/proc/proc.py:657-685 takes that mask); there a
+    last-bit difference of the fp32 sums cannot flip the thresholded mask.
+    On the well-conditioned frames at least MIN_SEL_EXACT have the identical
+    selected mask.  On an ill-conditioned frame the pose bounds are excused
+    only when flipping its near-threshold pixels moves the ORACLE's own pose
+    past them (each pixel alone, and all of them on / off at once: the chain
+    clean -> moments -> angle re-run on the oracle side); every excluded or
+    excused frame is recorded with its reason.  The R50 fp32 cases run on
+    every weight seed of R50_SEEDS with these constants.
+    fp16 (BASELINE config 5's precision, vs the fp32 oracle), R50 over
+    R50_SEEDS: the detection checks above hold on at least FP16_FRAMES of the
+    frames of all seeds together and on at least FP16_FRAMES_MIN of each
+    seed's, the pose bounds likewise; at least FP16_CROP_EXACT of the
+    non-NaN-pose frames give the oracle's depth crop byte for byte (the rest
+    differ because fp16 moves the small seeded-weight masks by a few
+    near-threshold pixels, and with them the pose); which detection check
+    failed is recorded per frame (box, score, mask, keypoints).
   coverage: at least MIN_POSES frames per case (30 / 32 for R50, 60 / 64 for
     R101) carry a non-NaN pose on both sides (the chain is compared on real
     contours, not NaN against NaN).
@@ -65,34 +78,25 @@ TOL = {"fp32": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.03, kp=0.9, c
        "mixed": dict(feat=2e-4, box_iou=0.98, score=1e-3, mask_px=0.10, kp=0.75, cen=2.0, ang=5.0, margin=0.05)}
 MASK_PX_FLOOR = 4       # pixels: the seeded-weight masks can be a handful of pixels
 MIN_POSES = {50: 30, 101: 60}  # non-NaN poses (both sides) per case, by depth
-MIN_SEL_EXACT = 0.9     # fp32: fraction of frames whose selected mask is the oracle's, pixel for pixel
+MIN_SEL_EXACT = 0.9     # fp32: fraction of the WELL-CONDITIONED frames whose selected mask is the oracle's
+NEAR_EPS = 1e-4         # fp32: a pasted probability within this of 0.5 makes its frame ill-conditioned
 ANGLE_ULPS = 2          # fp32: angle agreement (deg) in units in the last place when the masks agree
-FP16_FRAMES = 0.8       # fp16: fraction of frames passing the detection checks / the pose bounds
+FP16_FRAMES = 0.85      # fp16: fraction of all seeds' frames passing the detection checks / the pose bounds
+FP16_FRAMES_MIN = 0.75  # fp16: the same per seed
 FP16_CROP_EXACT = 0.12  # fp16: fraction of non-NaN-pose frames whose crop equals the oracle chain's
                         # (round-4 records: R50 B=32 4 / 21, R101 B=64 8 / 63)
 MIXED_CROP_EXACT = 0.9  # config 5 as stated (fp32 trunk / box head, fp16 mask + keypoint heads): the same
                         # fraction (round-4 record: R101 B=64 62 / 64), and every frame passes the
                         # detection and pose checks
 SEED = 77               # synthetic session of the batch
-# seeded synthetic weights per depth, chosen so the downstream chain is
-# compared on (nearly) every frame: R101 with seed 0 selects detections off
-# the animal on 61 of 64 frames (NaN poses on both sides, nothing compared
-# downstream), seed 1 selects on-animal masks on every frame.  R50 with seed 0
-# gave 22 / 32 non-NaN oracle poses.  tools/pose_seed_scan.py 50 32 over
-# seeds 0-50 measures per seed the non-NaN oracle poses, the frames whose
-# selected mask has pixels within 1e-5 of the 0.5 paste threshold (where an
-# fp32 rounding difference flips a pixel) and the frames where flipping one
-# such pixel moves the oracle's own pose past the fp32 bounds.  Candidates
-# with >= 30 poses: 3 (31 poses, 22 near-threshold frames: 20-24 / 32
-# identical selected masks on the MI355X, below MIN_SEL_EXACT), 14 (30, 1,
-# but that frame's flip turns the angle 1.36 deg: failed the pose bound),
-# 11 (32, 5: 28-31 / 32 identical), 34 (31, 2), 35 (32, 0).  Seed 35 passed
-# every fp32 case but its fp16 case had 25 / 32 frames within the fp16
-# detection bounds (tools/parity_seed_check.py fp16 0: seeds 3, 11, 21, 34
-# pass, 33 and 35 fail); seed 34 passes all seven R50 cases: 31 / 32 poses,
-# 29-30 / 32 identical selected masks in fp32, 32 / 32 fp16 detections
-# (profiles/r05_parity_full_R50_*).
-WEIGHT_SEED = {50: 34, 101: 1}
+# seeded synthetic weights.  R50: the fp32 cases and the fp16 check run on
+# every seed of R50_SEEDS with one set of constants (the seeds whose oracle
+# chain carries >= MIN_POSES non-NaN poses, tools/pose_seed_scan.py 50 32).
+# R101 with seed 0 selects detections off the animal on 61 of 64 frames (NaN
+# poses on both sides, nothing compared downstream); seed 1 selects
+# on-animal masks on every frame.
+R50_SEEDS = (3, 11, 14, 34, 35)
+R101_SEED = 1
 ORACLE_CHUNK = 8        # frames per oracle forward (its intermediates of a whole batch would not fit)
 
 _ORACLE = {}
@@ -146,11 +150,12 @@ def _window(c, a):
     return [int(cx - 40) + 80, int(cx + 40) + 80, int(cy - 40) + 80, int(cy + 40) + 80]
 
 
-def _oracle(depth, B):
-    """The oracle chain over every frame of the batch (cached per (depth, B)):
-    prepped / scaled frames, per-frame Instances fields, p2..p6, the selected
-    d2 mask, cleaned frames, moments, angle and the crops at the oracle pose."""
-    key = (depth, B)
+def _oracle(depth, B, wseed):
+    """The oracle chain over every frame of the batch (cached per (depth, B,
+    weight seed)): prepped / scaled frames, per-frame Instances fields,
+    p2..p6, the selected d2 mask, cleaned frames, moments, angle, the crops at
+    the oracle pose, and per frame the conditioning of its selected mask."""
+    key = (depth, B, wseed)
     if key in _ORACLE:
         return _ORACLE[key]
     from moseq2_detectron_extract_amd import synth
@@ -160,7 +165,7 @@ def _oracle(depth, B):
     from oracle import model_ref as R
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     cfg = ModelConfig(depth=depth, score_thresh_test=0.0)
-    sd = synthetic_state_dict(cfg, WEIGHT_SEED[depth])
+    sd = synthetic_state_dict(cfg, wseed)
     s = synth.SyntheticSession(B, seed=SEED)
     raw = s.frames(0, B)
     prepped, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
@@ -182,40 +187,122 @@ def _oracle(depth, B):
     cl = O.clean_frames(prepped, iters_tail=3)
     fw = O.get_frame_features(cl, 3, mask=d2)
     ang = np.mod(-np.rad2deg(fw["orientation"]), 360)
-    res = dict(cfg=cfg, sd=sd, raw=raw, roi=(s.bground_im, s.roi), prepped=prepped, want=want, feats=feats,
-               keeps=keeps, d2=d2, cleaned=cl, centroid=fw["centroid"], angle=ang,
+    cond = [_conditioning(O, want[i], keeps[i], d2[i], cl[i], fw["centroid"][i], ang[i]) for i in range(B)]
+    res = dict(cfg=cfg, sd=sd, wseed=wseed, raw=raw, roi=(s.bground_im, s.roi), prepped=prepped, want=want,
+               feats=feats, keeps=keeps, d2=d2, cleaned=cl, centroid=fw["centroid"], angle=ang, cond=cond,
                crop=O.crop_and_rotate_frames(prepped, fw["centroid"], ang),
                crop_mask=O.crop_and_rotate_frames(d2, fw["centroid"], ang))
     _ORACLE[key] = res
     return res
 
 
-@pytest.mark.parametrize("depth,B,dtype,wino,split", [(50, 32, "fp32", 4, 0), (50, 32, "fp32", 6, 0),
-                                                      (50, 32, "fp32", 2, 0),
-                                                      (50, 32, "fp32", 0, 0), (50, 32, "fp32", 4, 6),
-                                                      (50, 32, "fp32", 6, 6),
-                                                      (50, 32, "fp16", 0, 0), (101, 64, "fp16", 0, 0),
-                                                      (101, 64, "mixed", 6, 0), (101, 64, "fp32", 6, 0)])
-def test_forward_full_frame(mdx, depth, B, dtype, wino, split):
+def _conditioning(O, w, keep, d2, cleaned, cen, ang, max_single=32):
+    """Conditioning of one frame's selected mask: the pixels of the oracle's
+    pasted probability within NEAR_EPS of 0.5 (also counted at other eps, for
+    the record), and how far flipping them moves the oracle's own pose --
+    each near pixel alone (up to max_single of them) and all of them on and
+    off at once -- as (max centroid shift px, max angle shift deg mod 180)."""
+    out = {"near_px": 0, "near_px_by_eps": {}, "pose_shift": [0.0, 0.0]}
+    if not keep:
+        return out
+    p = w["pred_mask_probs"][keep[0]].numpy()
+    dist = np.abs(p.astype(np.float64) - 0.5)
+    for e in (1e-6, 1e-5, 1e-4, 1e-3):
+        out["near_px_by_eps"][str(e)] = int((dist < e).sum())
+    near = np.argwhere(dist < NEAR_EPS)
+    out["near_px"] = int(len(near))
+    if not len(near) or np.isnan(cen).any():
+        return out
+    variants = []
+    for yx in near[:max_single]:
+        m = d2.copy()
+        m[yx[0], yx[1]] ^= 1
+        variants.append(m)
+    for v in (0, 1):
+        m = d2.copy()
+        m[near[:, 0], near[:, 1]] = v
+        variants.append(m)
+    g = O.get_frame_features(np.repeat(cleaned[None], len(variants), 0), 3, mask=np.stack(variants))
+    ga = np.mod(-np.rad2deg(g["orientation"]), 360)
+    dc = np.abs(g["centroid"] - cen[None]).max(1)
+    da = _ang_diff(ga, ang)
+    nan = np.isnan(dc) | np.isnan(da)
+    out["pose_shift"] = [float(np.inf) if nan.any() else float(dc.max()),
+                         float(np.inf) if nan.any() else float(da.max())]
+    return out
+
+
+FP32_VARIANTS = [("fp32", 4, 0), ("fp32", 6, 0), ("fp32", 2, 0), ("fp32", 0, 0), ("fp32", 4, 6), ("fp32", 6, 6)]
+
+
+@pytest.mark.parametrize("depth,B,dtype,wino,split,wseed",
+                         [(50, 32, d, w, x, ws) for ws in R50_SEEDS for d, w, x in FP32_VARIANTS] +
+                         [(101, 64, "fp16", 0, 0, R101_SEED), (101, 64, "mixed", 6, 0, R101_SEED),
+                          (101, 64, "fp32", 6, 0, R101_SEED)])
+def test_forward_full_frame(mdx, depth, B, dtype, wino, split, wseed):
     """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
     6 = F(6x6,3x3) on the large maps and F(4x4,3x3) elsewhere, 2 = F(2x2,3x3),
     0 = direct); split: the fp32 layers as exact bf16 plane
-    products (mdx_conv_set_fp32_split, 0 = the f32 MFMA kernels); the same
-    fp32 tolerances hold for all."""
-    from moseq2_detectron_extract_amd._lib import call
-    old = call("mdx_conv_set_winograd", wino)
-    old_s = call("mdx_conv_set_fp32_split", split)
-    try:
-        _forward_full_frame(depth, B, dtype, wino, split)
-    finally:
-        call("mdx_conv_set_winograd", old)
-        call("mdx_conv_set_fp32_split", old_s)
+    products (mdx_conv_set_fp32_split, 0 = the f32 MFMA kernels); wseed: the
+    synthetic weights; the same fp32 tolerances hold for all."""
+    with _policy(wino, split):
+        st = _forward_full_frame(depth, B, dtype, wino, split, wseed)["summary"]
+    if dtype == "fp16":
+        assert st["detections_ok"] >= FP16_FRAMES * B and st["pose_ok"] >= FP16_FRAMES * B, st
+        assert st["crop_bit_exact_vs_oracle_non_nan"][0] >= FP16_CROP_EXACT * st["crop_bit_exact_vs_oracle_non_nan"][1], st
 
 
-def _forward_full_frame(depth, B, dtype, wino, split=0):
+def test_forward_full_frame_fp16_seeds(mdx):
+    """R50 B=32 all-fp16 against the fp32 oracle on every seed of R50_SEEDS:
+    per seed and over all seeds, the fraction of frames passing the detection
+    and pose checks (FP16_FRAMES_MIN / FP16_FRAMES) and the crop exactness
+    (FP16_CROP_EXACT); the failing detection checks are recorded."""
+    tot = {"frames": 0, "detections_ok": 0, "pose_ok": 0, "crop_exact": 0, "non_nan": 0}
+    per = {}
+    for ws in R50_SEEDS:
+        with _policy(0, 0):
+            st = _forward_full_frame(50, 32, "fp16", 0, 0, ws)["summary"]
+        per[ws] = st
+        tot["frames"] += st["frames"]
+        tot["detections_ok"] += st["detections_ok"]
+        tot["pose_ok"] += st["pose_ok"]
+        tot["crop_exact"] += st["crop_bit_exact_vs_oracle_non_nan"][0]
+        tot["non_nan"] += st["crop_bit_exact_vs_oracle_non_nan"][1]
+    _record("parity_full_R50_B32_fp16_seeds", {"per_seed": per, "total": tot})
+    for ws, st in per.items():
+        assert st["detections_ok"] >= FP16_FRAMES_MIN * st["frames"], (ws, st)
+        assert st["pose_ok"] >= FP16_FRAMES_MIN * st["frames"], (ws, st)
+    assert tot["detections_ok"] >= FP16_FRAMES * tot["frames"], tot
+    assert tot["pose_ok"] >= FP16_FRAMES * tot["frames"], tot
+    assert tot["crop_exact"] >= FP16_CROP_EXACT * tot["non_nan"], tot
+
+
+class _policy:
+    def __init__(self, wino, split):
+        self.wino, self.split = wino, split
+
+    def __enter__(self):
+        from moseq2_detectron_extract_amd._lib import call
+        self.old = call("mdx_conv_set_winograd", self.wino), call("mdx_conv_set_fp32_split", self.split)
+
+    def __exit__(self, *exc):
+        from moseq2_detectron_extract_amd._lib import call
+        call("mdx_conv_set_winograd", self.old[0])
+        call("mdx_conv_set_fp32_split", self.old[1])
+
+
+def _record(name, obj):
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, name + ".json"), "w") as fh:
+            json.dump(obj, fh, indent=1, default=lambda o: o.item() if hasattr(o, "item") else str(o))
+
+
+def _forward_full_frame(depth, B, dtype, wino, split=0, wseed=None):
     from moseq2_detectron_extract_amd.model import Predictor
     from moseq2_detectron_extract_amd.pipeline import ExtractConfig, GPUExtractor
-    orc = _oracle(depth, B)
+    wseed = (R50_SEEDS[0] if depth == 50 else R101_SEED) if wseed is None else wseed
+    orc = _oracle(depth, B, wseed)
     tol = TOL[dtype]
     pred = Predictor.from_config(orc["cfg"], weights=orc["sd"], dtype=dtype)
     ex = GPUExtractor(*orc["roi"], pred, ExtractConfig(batch_size=B))
@@ -232,16 +319,15 @@ def _forward_full_frame(depth, B, dtype, wino, split=0):
     np.testing.assert_array_equal(prepped_d.cpu().numpy(), orc["prepped"])  # bit-exact frame ops feed both sides
     masks_all = torch.cat([m for m in inf["masks"]]).cpu().numpy()
     stats = {"case": f"R{depth} B={B} {dtype}" + (f" winograd F({wino}x{wino},3x3)" if wino else "") +
-             (f" bf16x{split} plane products" if split else ""), "frames": []}
+             (f" bf16x{split} plane products" if split else "") + f" weights seed {wseed}", "near_eps": NEAR_EPS,
+             "frames": []}
     try:
         _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail,
                  (oc.cpu().numpy(), ocm.cpu().numpy(), owin.cpu().numpy()), stats)
     finally:
-        out = os.path.join(ROOT, "gpurun_out")
-        if os.path.isdir(out):
-            name = f"parity_full_R{depth}_B{B}_{dtype}" + (f"_wino{wino}" if wino else "") + (f"_x{split}" if split else "")
-            with open(os.path.join(out, name + ".json"), "w") as fh:
-                json.dump(stats, fh, indent=1, default=lambda o: o.item() if hasattr(o, "item") else str(o))
+        _record(f"parity_full_R{depth}_B{B}_{dtype}" + (f"_wino{wino}" if wino else "") +
+                (f"_x{split}" if split else "") + f"_s{wseed}", stats)
+    return stats
 
 
 def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_oracle_pose, stats):
@@ -303,6 +389,14 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
         rec["crop_oracle_pose_bit_exact"] = bool(np.array_equal(oc[i], orc["crop"][i]))
         rec["crop_mask_oracle_pose_bit_exact"] = bool(np.array_equal(ocm[i], orc["crop_mask"][i]))
         rec["crop_bit_exact_vs_oracle"] = bool(np.array_equal(g_depth[i], orc["crop"][i]))
+        # conditioning of the oracle's selected mask (computed on the oracle side)
+        cnd = orc["cond"][i]
+        rec["near_px"], rec["near_px_by_eps"], rec["pose_shift"] = cnd["near_px"], cnd["near_px_by_eps"], cnd["pose_shift"]
+        rec["conditioned"] = cnd["near_px"] == 0
+        rec["pose_excusable"] = bool(cnd["pose_shift"][0] > tol["cen"] or cnd["pose_shift"][1] > tol["ang"])
+        # how close to the threshold the pixels the two sides disagree on are
+        diff = np.logical_xor(d2g, d2w)
+        rec["sel_diff_min_dist"] = float(np.abs(wp[keep[0]][diff] - 0.5).min()) if keep and diff.any() else None
     frames = stats["frames"]
     n_pose = sum(r["pose_non_nan"] for r in frames)
     n_sel = sum(r["sel_mask_identical"] for r in frames)
@@ -311,6 +405,8 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
                         "pose_bit_exact": sum(r["pose_bit_exact"] for r in frames),
                         "crop_bit_exact_vs_oracle_non_nan": [sum(exact_vs), len(exact_vs)]}
     det_ok = pose_ok = 0
+    excluded = []
+    fails = {"box": 0, "score": 0, "mask": 0, "kp": 0}
     for rec in frames:
         assert max(rec["feat_rel_err"].values()) <= tol["feat"], rec
         assert rec["ndet"][0] == rec["ndet"][1], rec
@@ -323,8 +419,13 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
         assert rec["crop_oracle_pose_bit_exact"], rec
         if rec["sel_mask_identical"]:
             assert rec["crop_mask_oracle_pose_bit_exact"], rec
-        det = (rec["box_iou_min"] >= tol["box_iou"] and rec["score_diff_max"] <= tol["score"] and
-               all(_mask_ok(x, tol["mask_px"]) for x in rec["mask_px"]) and rec["kp_within_1px"] >= tol["kp"])
+        checks = {"box": rec["box_iou_min"] >= tol["box_iou"], "score": rec["score_diff_max"] <= tol["score"],
+                  "mask": all(_mask_ok(x, tol["mask_px"]) for x in rec["mask_px"]),
+                  "kp": rec["kp_within_1px"] >= tol["kp"]}
+        rec["failed_checks"] = [k for k, v in checks.items() if not v]
+        for k in rec["failed_checks"]:
+            fails[k] += 1
+        det = all(checks.values())
         a, b = rec["angle"]
         pose = (_mask_ok(rec["sel_mask_px"], tol["mask_px"]) and
                 _close_nan(rec["centroid"][0], rec["centroid"][1], tol["cen"]) and
@@ -333,19 +434,31 @@ def _compare(orc, tol, dtype, B, inf, gfeat, masks_all, cleaned_d, tail, at_orac
         rec["detections_ok"], rec["pose_ok"] = bool(det), bool(pose)
         det_ok += int(det)
         pose_ok += int(pose)
+        if not rec["conditioned"]:
+            excluded.append({"frame": rec["frame"], "near_px": rec["near_px"], "pose_shift": rec["pose_shift"],
+                             "reason": f"{rec['near_px']} px of the oracle's selected mask within {NEAR_EPS} of the "
+                                       "0.5 paste threshold: excluded from MIN_SEL_EXACT" +
+                                       ("; flipping them moves the oracle pose past the bounds: pose bound excused"
+                                        if rec["pose_excusable"] else ""),
+                             "sel_mask_identical": rec["sel_mask_identical"], "pose_ok": bool(pose)})
         if dtype == "fp32":
-            assert det and pose, rec
+            assert det, rec
+            assert pose or (not rec["conditioned"] and rec["pose_excusable"]), rec
             if rec["sel_mask_identical"]:
                 # identical selected mask => the chain is integer-exact
                 assert rec["centroid_bit_exact"] and rec["angle_ulps"] <= ANGLE_ULPS, rec
                 assert rec["crop_bit_exact_vs_oracle"], rec
-    stats["summary"].update(detections_ok=det_ok, pose_ok=pose_ok)
+    n_cond = sum(r["conditioned"] for r in frames)
+    n_sel_cond = sum(r["sel_mask_identical"] for r in frames if r["conditioned"])
+    stats["excluded"] = excluded
+    stats["summary"].update(detections_ok=det_ok, pose_ok=pose_ok, failed_checks=fails, conditioned=n_cond,
+                            sel_mask_identical_conditioned=n_sel_cond,
+                            pose_outside_bounds=sum(1 for r in frames if not r["pose_ok"]))
     assert n_pose >= MIN_POSES[orc["cfg"].depth], stats["summary"]
     if dtype == "fp32":
-        assert n_sel >= MIN_SEL_EXACT * B, stats["summary"]
+        assert n_sel_cond >= MIN_SEL_EXACT * n_cond, stats["summary"]
     elif dtype == "mixed":
         assert det_ok == B and pose_ok == B, stats["summary"]
         assert sum(exact_vs) >= MIXED_CROP_EXACT * len(exact_vs), stats["summary"]
-    else:
-        assert det_ok >= FP16_FRAMES * B and pose_ok >= FP16_FRAMES * B, stats["summary"]
-        assert sum(exact_vs) >= FP16_CROP_EXACT * len(exact_vs), stats["summary"]
+    else:  # fp16: the per-case floor (the fractions over several cases: test_forward_full_frame_fp16_seeds)
+        assert det_ok >= FP16_FRAMES_MIN * B and pose_ok >= FP16_FRAMES_MIN * B, stats["summary"]

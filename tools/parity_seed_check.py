@@ -20,14 +20,14 @@ def main():
     old = call("mdx_conv_set_winograd", wino)
     try:
         for seed in (int(v) for v in sys.argv[3:]):
-            T.WEIGHT_SEED[50] = seed
             T._ORACLE.clear()
             try:
-                T._forward_full_frame(50, 32, dtype, wino)
+                T._forward_full_frame(50, 32, dtype, wino, 0, seed)
                 res = "pass"
             except AssertionError as e:
                 res = "fail: " + str(e)[:160]
-            out = os.path.join(ROOT, "gpurun_out", f"parity_full_R50_B32_{dtype}" + (f"_wino{wino}" if wino else "") + ".json")
+            out = os.path.join(ROOT, "gpurun_out", f"parity_full_R50_B32_{dtype}" + (f"_wino{wino}" if wino else "") +
+                               f"_s{seed}.json")
             summ = json.load(open(out))["summary"] if os.path.exists(out) else None
             print(json.dumps({"seed": seed, "dtype": dtype, "wino": wino, "result": res, "summary": summ}), flush=True)
     finally:
