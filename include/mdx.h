@@ -360,16 +360,6 @@ int64_t mdx_x6_plane_bytes(int64_t rows, int K);
 int mdx_split_x6(const float *x, int64_t rows, int K, int64_t ldx, void *out, mdx_stream_t stream);
 int mdx_gemm_x6(const void *a_planes, const void *b_planes, const float *bias, int M, int N, int K,
                 const float *residual, int relu, float *out, mdx_stream_t stream);
-/* fp32 GEMM on the ping-pong 256 x 256 MFMA kernel (the pointwise layers'
- * kernel: 1x1 convs, the box head FCs, the Winograd tile-point GEMMs; replaces
- * the torch/cuDNN conv2d + linear of Detectron2's heads, M/model/predict.py:92):
- * C[z] = act(A[z] . B[z]^T + bias (+ residual)) for z < batch, A [M][K],
- * B [N][K], C / residual [M][N] row-major fp32 at element strides stride_a /
- * stride_b / stride_c between batch entries; K % 32 == 0; a residual needs
- * batch == 1; relu 0/1; bias may be null. */
-int mdx_gemm_f32(const float *A, const float *B, const float *bias, const float *residual, int relu, float *C,
-                 int M, int N, int K, int batch, int64_t stride_a, int64_t stride_b, int64_t stride_c,
-                 mdx_stream_t stream);
 /* Kernel chosen by this thread's last mdx_conv2d / mdx_conv2d_splitk call
  * (host-only; for per-kernel timing): *kernel = MDX_CONV_KERNEL_*, *ksplit =
  * K slices launched (the split-K reduction is a second launch). */
@@ -399,7 +389,6 @@ enum {
     MDX_CONV_KERNEL_HB128 = 25, /* SB128 / SB64 on k_conv_hb: half K-steps, two LDS stages, four workgroups
                                    per CU (mdx_conv_set_half_step) */
     MDX_CONV_KERNEL_HB64 = 26,
-    MDX_CONV_KERNEL_PP256 = 27, /* the ping-pong 256x256 fp32 GEMM (mdx_gemm_f32; pointwise fp32 layers) */
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,

@@ -83,7 +83,6 @@ SIGNATURES = {
     "mdx_x6_plane_bytes": (I64, [I64, I32]),
     "mdx_split_x6": (I32, [P, I64, I32, I64, P, P]),
     "mdx_gemm_x6": (I32, [P, P, P, I32, I32, I32, P, I32, P, P]),
-    "mdx_gemm_f32": (I32, [P, P, P, P, I32, P, I32, I32, I32, I32, I64, I64, I64, P]),
     "mdx_conv2d_last_plan": (I32, [P, P]),
     "mdx_conv_set_stream1x1": (I32, [I32, I32]),
     "mdx_conv_set_stream1x1_f32": (I32, [I32]),

@@ -64,21 +64,4 @@ bool winograd_planes_enabled();  // the model runs Winograd GEMMs on k_gemm_x6 (
 // (mdx_split_x6 layout), or null; the model handle sets it around a layer
 void x3_weight_planes(const void *planes);
 
-// fp32 pointwise GEMM on the ping-pong 256 x 256 kernel (gemm_pp.hip):
-// out = act(A . w^T + bias (+ res)), A row m = NHWC pixel of output pixel m
-// (OH x OW outputs per image, stride over an H x W x K input; OH = 0: A is a
-// plain [M][K] matrix), w [N][K], out / res [M][N]; batch entries z at the
-// element strides bsx / bsw / bso (grid.z).  K % 32 == 0.
-struct GemmPP {
-    const float *x, *w, *bias, *res;
-    float *out;
-    int M, N, K;
-    int H, W, OH, OW, stride;
-    int relu;
-    int tiles_n, tiles_total;
-    long long bsx, bsw, bso;
-};
-bool gemm_pp_eligible(int M, int N, int K);
-int gemm_pp(GemmPP a, int batch, hipStream_t s);
-
 }  // namespace mdx
