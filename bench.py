@@ -23,7 +23,7 @@ scaling: weak (every rank processes its own 32-frame batches; frames shard
 secondary.fp16: the same loop with the fp16 MFMA forward (BASELINE config 5's
          precision), reported beside the fp32 headline, never as `value`.
 secondary.fp32_bf16x6: the same loop with the fp32 layers as exact bf16
-         plane products (mdx_conv_set_fp32_split(6)).
+         plane products (mdx_policy.fp32_split = 6).
 secondary.extract_loop: BASELINE config 3 -- extract.extract_session over a
          10k-frame synthetic session written as depth.dat (chunks of 1000,
          tracking on, fp32): frame source, device path, instance selection,
@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp16 secondary measurement")
     ap.add_argument("--no-x6", action="store_true",
-                    help="skip the secondary fp32 loop on the split-plane kernels (mdx_conv_set_fp32_split(6))")
+                    help="skip the secondary fp32 loop on the split-plane kernels (mdx_policy.fp32_split = 6)")
     ap.add_argument("--no-h2d", action="store_true", help="raw batches already resident in HBM (no H2D in the loop)")
     ap.add_argument("--cpu-sample-frames", type=int, default=64)
     ap.add_argument("--no-extract-loop", action="store_true", help="skip the config-3 extract-loop secondary")
@@ -92,12 +92,13 @@ def parse():
     ap.add_argument("--chunked", action="store_true",
                     help="the chunked loop (GPUExtractor.step_device over --chunk-batches batches) instead of the "
                          "pipeline")
-    ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_roi_align_set_mode)")
-    ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_conv_set_dma_f32)")
-    ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_conv_set_winograd)")
-    ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_conv_set_winograd_min_cin")
-    ap.add_argument("--set", action="append", default=[], metavar="FUNC=INT[,INT]",
-                    help="call a libmdx tuning knob before the run, e.g. --set mdx_rpn_set_sliced=0 (repeatable)")
+    ap.add_argument("--roi-mode", type=int, default=None, help="ROIAlign kernel (mdx_policy.roi_mode)")
+    ap.add_argument("--dma-f32", type=int, default=None, help="fp32 LDS-DMA conv policy (mdx_policy.dma_f32)")
+    ap.add_argument("--winograd", type=int, default=None, help="fp32 3x3 Winograd policy (mdx_policy.winograd)")
+    ap.add_argument("--winograd-min-cin", type=int, default=None, help="mdx_policy.winograd_min_cin")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=INT",
+                    help="set a field of the kernel-selection policy (include/mdx.h mdx_policy) before the model "
+                         "handles are created, e.g. --set rpn_sliced=0 (repeatable)")
     ap.add_argument("--model-streams", type=int, default=4,
                     help="forwards in flight at once (one HIP stream each)")
     ap.add_argument("--chunk-batches", type=int, default=8,
@@ -121,22 +122,22 @@ def _kconv(ti: str, to: str, bn: int, dual: bool, pw: bool):
 # kernel id -> (BN, DUAL, PW) of the k_conv instance (ids +10: fp16 in, fp32 out)
 _KCONV_IDS = {0: (128, False, False), 1: (64, False, False), 14: (128, False, True), 15: (64, False, True),
               16: (128, True, True), 17: (64, True, True)}
-KERNEL_SYMBOLS = {"fp16": {2: "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE",
-                           3: "_ZN3mdx7k_convgIDF16_DF16_Li4ELb1ELb0ELb0EEEvNS_8ConvArgsE",
+KERNEL_SYMBOLS = {"fp16": {2: "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0EEEvNS_8ConvArgsE",
+                           3: "_ZN3mdx7k_convgIDF16_DF16_Li4ELb1EEEvNS_8ConvArgsE",
                            4: "k_conv1x1_stream<KC> (three instances by K)",
                            5: "k_conv1x1_head<KC> (three instances by K)"},
-                  "fp32": {2: "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE"}}
+                  "fp32": {2: "_ZN3mdx7k_convgIffLi8ELb0EEEvNS_8ConvArgsE"}}
 # rocprofv3 reports some kernels demangled
 KERNEL_DEMANGLED = {
-    "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
-        "void mdx::k_convg<_Float16, _Float16, 8, false, false, false>(mdx::ConvArgs)",
-    "_ZN3mdx7k_convgIffLi8ELb0ELb0ELb0EEEvNS_8ConvArgsE":
-        "void mdx::k_convg<float, float, 8, false, false, false>(mdx::ConvArgs)",
+    "_ZN3mdx7k_convgIDF16_DF16_Li8ELb0EEEvNS_8ConvArgsE":
+        "void mdx::k_convg<_Float16, _Float16, 8, false>(mdx::ConvArgs)",
+    "_ZN3mdx7k_convgIffLi8ELb0EEEvNS_8ConvArgsE":
+        "void mdx::k_convg<float, float, 8, false>(mdx::ConvArgs)",
 }
-for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<float, float, BN, DUAL, AFP=false>
-    _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}ELb0EEEvNS_8ConvArgsE"
+for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<float, float, BN, DUAL>
+    _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
     KERNEL_SYMBOLS["fp32"][_k] = _m
-    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}, false>(mdx::ConvArgs)"
+    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
 for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<T, T, BN>: single stage, general layers
     for _dt, _mt, _dm in (("fp32", "ff", "float, float"), ("fp16", "DF16_DF16_", "_Float16, _Float16")):
         _m = f"_ZN3mdx10k_conv_sbgI{_mt}Li{_bn}EEEvNS_8ConvArgsE"
@@ -171,10 +172,8 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance"}
 # the transforms: one instance per Winograd tile size the default policy runs
 # (F(6,3) on the large maps, F(4,3) on the rest)
-KERNEL_SYMBOLS["fp32"].update({4: "_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE",
-                               12: tuple(f"_ZN3mdx9k_wino_inILi{m}EEEvPKfiiiiiiPf" for m in (4, 6)),
+KERNEL_SYMBOLS["fp32"].update({12: tuple(f"_ZN3mdx9k_wino_inILi{m}EEEvPKfiiiiiiPf" for m in (4, 6)),
                                13: tuple(f"_ZN3mdx10k_wino_outILi{m}EEEvPKfiiiiiiS2_iPf" for m in (4, 6))})
-KERNEL_DEMANGLED["_ZN3mdx20k_conv1x1_stream_f32ILi4EEEvNS_8ConvArgsE"] = "void mdx::k_conv1x1_stream_f32<4>(mdx::ConvArgs)"
 for _m in (4, 6):
     KERNEL_DEMANGLED[f"_ZN3mdx9k_wino_inILi{_m}EEEvPKfiiiiiiPf"] = \
         f"void mdx::k_wino_in<{_m}>(float const*, int, int, int, int, int, int, float*)"
@@ -257,7 +256,7 @@ def roofline_line(per, dtype, model_flop_per_step):
     time per serial step (a Winograd layer's batched GEMM counts under the
     kernel it ran on, at its executed FLOPs).  `kernels` lists the top
     kernels by time; the transforms are HBM-bound and listed in GB/s."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy
     peak = PEAK[dtype]
     kern = _pmc(dtype)
     mfma = [k for k in per if k not in TRANSFORMS and k < F16_KEY]
@@ -303,7 +302,7 @@ def roofline_line(per, dtype, model_flop_per_step):
                                  "MFMA kernels perform (the Winograd GEMMs do 1/4 of the direct 3x3 FLOPs); "
                                  "direct_equivalent = the model's algorithmic FLOPs (direct convolution, heads "
                                  "included) over the same time, which can exceed the peak"},
-            "winograd_tile": call("mdx_conv_winograd_enabled")}
+            "winograd_tile": policy()["winograd"]}
 
 
 def frame_ops_line(ex, raw, steps=5):
@@ -580,24 +579,16 @@ def main():
     from moseq2_detectron_extract_amd.model import ModelConfig
     from moseq2_detectron_extract_amd.model.runtime import flops_per_image
 
-    if args.dma_f32 is not None:
-        from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_dma_f32", args.dma_f32)
-    if args.winograd is not None:
-        from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_winograd", args.winograd)
-    if args.winograd_min_cin is not None:
-        from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_winograd_min_cin", args.winograd_min_cin)
-    if args.roi_mode is not None:
-        from moseq2_detectron_extract_amd._lib import call
-        call("mdx_roi_align_set_mode", args.roi_mode)
+    from moseq2_detectron_extract_amd._lib import POLICY_FIELDS, set_policy
+    upd = {k: v for k, v in (("dma_f32", args.dma_f32), ("winograd", args.winograd),
+                             ("winograd_min_cin", args.winograd_min_cin), ("roi_mode", args.roi_mode)) if v is not None}
     for kv in args.set:
-        from moseq2_detectron_extract_amd._lib import call
-        fn, val = kv.split("=")
-        if not (fn.startswith("mdx_") and "_set_" in fn):
-            raise SystemExit(f"--set: {fn} is not a libmdx tuning knob")
-        call(fn, *[int(v) for v in val.split(",")])
+        field, val = kv.split("=")
+        if field not in POLICY_FIELDS:
+            raise SystemExit(f"--set: {field} is not a field of mdx_policy ({', '.join(POLICY_FIELDS)})")
+        upd[field] = int(val)
+    if upd:
+        set_policy(**upd)
     B = args.batch
     sess = synth.SyntheticSession(2 * B, seed=1000 + rank)
     frames = sess.frames(0, 2 * B)
@@ -630,17 +621,14 @@ def main():
         del ex16
     if not args.no_secondary and args.dtype == "fp32" and not args.no_x6:
         torch.cuda.synchronize()
-        from moseq2_detectron_extract_amd._lib import call
-        old = call("mdx_conv_set_fp32_split", 6)
-        try:
+        from moseq2_detectron_extract_amd._lib import policy_scope
+        with policy_scope(fp32_split=6):  # the handle measure() creates captures it
             dtx, exx, _ = measure(args, "fp32", B, world, rank, raw_host, sess, dist, gather_bufs)
-        finally:
-            call("mdx_conv_set_fp32_split", old)
         secondary["fp32_bf16x6"] = {
             "value": round(frames_done / dtx, 2), "unit": "frames/s", "ms_per_step": round(dtx / args.steps * 1e3, 3),
             "dtype": "fp32 operands split exactly into 3 bf16 planes, 6 plane products on the bf16 matrix cores, "
                      "fp32 accumulation",
-            "note": "mdx_conv_set_fp32_split(6): conv layers and Winograd GEMMs on k_conv_x3 (weights split into "
+            "note": "mdx_policy.fp32_split = 6: conv layers and Winograd GEMMs on k_conv_x3 (weights split into "
                     "planes once when the handle is created, activations split in registers), box head FCs on "
                     "k_gemm_x6 (256x256 LDS-DMA over planes written by the box pooler / mdx_split_x6); per product the "
                     "dropped terms are below one fp32 rounding; "

@@ -227,6 +227,85 @@ int mdx_instance_tracker_select(void *handle, const int *nkeep, const double *ce
  * NHWC; dtype codes: 0 = float32, 1 = float16 (fp32 accumulation).
  * ------------------------------------------------------------------- */
 
+/* Kernel-selection policy of the model path (one struct instead of a setter
+ * per knob; replaces nothing in the reference: Detectron2 / cuDNN pick their
+ * algorithms internally).  The policy in force for a call is
+ *   - inside mdx_model_reserve / mdx_model_forward (and the handle's other
+ *     entry points): the model handle's own, captured from the creating
+ *     thread's policy at mdx_model_create (the weights are packed for it:
+ *     Winograd transforms, bf16 planes, folded stem, fused shortcuts);
+ *   - otherwise (direct mdx_conv2d / mdx_conv3x3_winograd / mdx_roi_align /
+ *     mdx_rpn_proposals calls): the calling thread's, set with
+ *     mdx_policy_set (initially the library defaults, mdx_policy_defaults).
+ * No process-global state: two handles with different policies run
+ * concurrently on different streams or threads.  Defaults in brackets. */
+typedef struct mdx_policy {
+    /* fp32 3x3 stride-1 layers with Cin >= winograd_min_cin [64]: 0 direct,
+     * 2 / 4 Winograd F(2x2,3x3) / F(4x4,3x3), 6 F(6x6,3x3) where
+     * mdx_winograd_tile picks it and F(4x4,3x3) elsewhere [6] */
+    int winograd, winograd_min_cin;
+    /* Winograd GEMMs (Cout % 256 == 0) on the 256x256 LDS-DMA kernel: 0 never
+     * [0: measured no faster], 1 from winograd_dma_min_wgs [384] workgroups,
+     * 2 whenever eligible */
+    int winograd_dma, winograd_dma_min_wgs;
+    /* model handles: Winograd layers in image slices of at most this many MB
+     * of transformed input, kept in the Infinity Cache between the three
+     * launches; 0 = one pass [0] */
+    int wino_slice_mb;
+    /* fp32 layers as exact bf16 plane products: 0 the f32 MFMA kernels [0],
+     * 6 the six largest of the nine plane products, 9 all nine */
+    int fp32_split;
+    /* split-plane launches: the 64-wide N tile everywhere [1]; the
+     * single-stage instance with pre-split weights [1] */
+    int x3_narrow, x3_single_stage;
+    /* fp16 layers (Cin % 64 == 0) on the 256x256 LDS-DMA kernel: 0 never,
+     * 1 when the layer fills the chip [1], 2 whenever eligible, 3 / 4 as 2 / 1
+     * on the 256x128 tile */
+    int large_tiles;
+    /* fp16 layers on the 128x128 LDS-DMA kernel: 0 never [0: slower in the
+     * full forward], 1 from dma128_min_tiles [1536] tiles, 2 whenever
+     * eligible; its DMA pieces issued between the MFMAs [1] */
+    int dma128, dma128_min_tiles, dma128_interleave;
+    /* fp32 layers (Cin % 32 == 0) on the LDS-DMA kernels: 0 never [0: the
+     * single-stage register-staged kernel is faster], 1 the 128x128 tile,
+     * 2 the 256x256 tile for >= 500 tiles and K >= 1024, 3 the 256x256 tile
+     * under the fp16 policy, 4 as 2 also in split-plane mode (diagnostic) */
+    int dma_f32;
+    /* pointwise layers on the instances with per-row load addresses [1] */
+    int pointwise;
+    /* single-LDS-stage instances: 1 fp32 pointwise, 2 + fp32 KxK, 3 + fp16
+     * pointwise, 4 + fp16 KxK [4]; 0 the two-stage instances */
+    int single_stage;
+    /* fp32-out GEMM epilogue straight from the accumulators [1] (0: through
+     * an LDS image; the same values) */
+    int direct_epilogue;
+    /* layers with K <= narrow_kmax [128] take the 64-wide N tile */
+    int narrow_kmax;
+    /* fp32 1x1 layers with Cout <= 16 (RPN / mask / box predictors) on
+     * k_head_f32 [1] */
+    int head_f32;
+    /* fp16 1x1 stride-1 layers (Cin in {64,128,256}, Cout % 64 == 0) on the
+     * streaming kernel: 0 never, 1 for M >= stream1x1_min_m [65536] (K = 256
+     * only when Cout == 64) [1], 2 every eligible layer */
+    int stream1x1, stream1x1_min_m;
+    /* model handles: fp32 stem with the pixel normalisation folded into its
+     * weights (2-channel s2d input) [1]; bottleneck conv3 + projection
+     * shortcut as one GEMM: 0 off, 1 fp32 handles [1], 2 all */
+    int stem_fold, fuse_shortcut;
+    /* RPN top-k: every (image, level) split over several workgroups [1] */
+    int rpn_sliced;
+    /* ROIAlign kernel: 0 the per-sample kernel, 1 / 2 / 3 one workgroup per
+     * ROI with 1 / 2 / 4 items per thread, 4 the separable form (per-bin row /
+     * column weight sums) [4], 5 its row-shared form, 6 the separable form
+     * with each ROI's sample window staged in LDS for >= 1024 ROIs (7: for
+     * any count); XCD-contiguous ROI ranges [1]; ROIs permuted by level and
+     * map band before pooling (mdx_roi_align_ex) [1] */
+    int roi_mode, roi_xcd_order, roi_sorted;
+} mdx_policy;
+int mdx_policy_defaults(mdx_policy *out);
+int mdx_policy_get(mdx_policy *out);
+int mdx_policy_set(const mdx_policy *policy);
+
 /* Implicit-GEMM convolution / linear layer on MFMA:
  * out = act(conv(x, w) + bias (+ residual)).  x (N,H,W,Cin); w packed
  * [Cout][KH][KW][Cin] (FrozenBN folded); bias float32 [Cout] or NULL;
@@ -240,39 +319,6 @@ int mdx_conv2d(const void *x, int N, int H, int W, int Cin, const void *w, const
  * (ksplit*M*Cout*4 bytes), a second launch sums them in fixed order and applies
  * bias/residual/ReLU.  ksplit 0 = choose from the grid size and workspace_bytes
  * (falls back to 1 slice when it does not pay or does not fit). */
-/* Policy for the 256x256 fp16 kernel (Cin % 64 == 0): 0 never, 1 auto (default:
- * when the layer fills the chip), 2 whenever eligible; 3 / 4 as 2 / 1 with
- * the fp16 layers on the 256x128 tile (two workgroups per CU) instead.
- * Returns the old mode. */
-int mdx_conv_set_large_tiles(int mode);
-/* Policy for the 128x128 LDS-DMA fp16 kernel (Cin % 64 == 0): 0 never, 1 when
- * the layer has >= min_tiles 128x128 tiles, 2 whenever eligible (default 0:
- * slower than the 256x256 / split-K kernels inside the full forward).
- * Returns the old mode. */
-int mdx_conv_set_dma128(int mode, int min_tiles);
-/* Issue the LDS-DMA pieces between the MFMAs of the LDS-DMA kernels (0/1). */
-int mdx_conv_set_mfma_prio(int on);
-/* s_setprio(1) around the MFMA bursts of the 256x256 LDS-DMA kernel (0/1). */
-int mdx_conv_set_mfma_prio256(int on);
-/* fp32 layers (Cin % 32 == 0, fp32 output) on the LDS-DMA kernels (16x16x4
- * f32 MFMAs): 0 never (default: the register-staged single-stage kernel is
- * faster on every fp32 layer, box fc1 included), 1 the 128x128 tile (>= 512
- * tiles), 2 the 256x256 tile for layers with >= 500 such tiles and K >= 1024, 3 the 256x256
- * tile under the fp16 policy, 4 as 2 also while mdx_conv_set_fp32_split
- * routes the other fp32 layers to the split-plane kernel (diagnostic).
- * Returns the old value. */
-int mdx_conv_set_dma_f32(int on);
-/* fp32 layers (fp32 in and out) as bf16 matrix-core products: every operand
- * is split exactly into three bf16 planes (hi + mid + lo) in the kernel and
- * the products accumulate in fp32.  9: all nine plane products (the exact
- * products, fp32 accumulation); 6: without the three smallest (each below one
- * fp32 rounding of the product); 0 (default): the f32 MFMA kernels.  Also
- * used for the Winograd GEMMs.  Returns the old value. */
-int mdx_conv_set_fp32_split(int mode);
-int mdx_conv_fp32_split(void);
-/* Tuning knob: 1 (default) runs every split-plane launch on the 64-wide N
- * tile (two workgroups per CU), 0 the 128-wide tile where Cout > 64. */
-int mdx_conv_set_x3_narrow(int on);
 /* Winograd F(m x m, 3x3), m = 2, 4 or 6, for fp32 3x3 / stride-1 / pad-1
  * convolutions (NHWC): the algorithm the model handle uses for such layers
  * with Cin >= 64 (cuDNN's WINOGRAD family, which PyTorch selects for fp32
@@ -280,72 +326,23 @@ int mdx_conv_set_x3_narrow(int on);
  * [(m+2)^2][Cout][Cin] (host function).  conv: x float32 (N,H,W,Cin), U as
  * above, bias [Cout] or NULL, optional ReLU -> out (N,H,W,Cout); workspace
  * (16-B aligned) >= mdx_winograd_workspace_bytes.  Cin % 4 == 0, Cout % 8 == 0.
- * set_winograd: the model handle's policy (0 off (direct), 2 F(2x2,3x3),
- * 4 F(4x4,3x3), 6 F(6x6,3x3) on the layers where winograd_tile picks it and
- * F(4x4,3x3) on the rest (default)); returns the old one.  winograd_tile: the m
- * a policy runs an H x W layer with (policy 6: 6 where the 8x8 tiles execute
- * under 0.9x the tile products of F(4,3)'s 6x6, else 4). */
+ * winograd_tile: the m a policy (mdx_policy.winograd) runs an H x W layer with
+ * (policy 6: 6 where the 8x8 tiles execute under 0.9x the tile products of
+ * F(4,3)'s 6x6, else 4). */
 int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U);
 int64_t mdx_winograd_workspace_bytes(int N, int H, int W, int Cin, int Cout, int m);
 int mdx_conv3x3_winograd(const float *x, int N, int H, int W, int Cin, const float *U, const float *bias, int Cout,
                          int relu, int m, float *out, void *workspace, int64_t workspace_bytes, mdx_stream_t stream);
-/* Split-plane mode (mdx_conv_set_fp32_split(6)): the same layer with U also
+/* Split-plane mode (mdx_policy.fp32_split = 6): the same layer with U also
  * split once into bf16 planes (mdx_split_x6 of U as NB*Cout rows of Cin):
  * the input transform writes V as planes and the NB GEMMs run on the 256x256
  * LDS-DMA plane kernel (k_gemm_x6); outside split mode, or with Cin % 16 != 0,
  * as mdx_conv3x3_winograd.  Model handles use it only with MDX_WINO_X6 set in
  * the environment (4 % slower end to end than k_conv_x3 on every layer). */
-/* Split-plane launches with pre-split weights (model handles in mode 6) on
- * the single-stage k_conv_x3 (one LDS stage, one accumulator set, three
- * workgroups per CU): 1 (default) or 0 (two LDS stages, separate hi*hi and
- * cross-product accumulators).  Returns the old value. */
-int mdx_conv_set_x3_single_stage(int on);
 int mdx_conv3x3_winograd_x6(const float *x, int N, int H, int W, int Cin, const float *U, const void *U_planes,
                             const float *bias, int Cout, int relu, int m, float *out, void *workspace,
                             int64_t workspace_bytes, mdx_stream_t stream);
-int mdx_conv_set_winograd(int mode);
-int mdx_conv_winograd_enabled(void);
 int mdx_winograd_tile(int H, int W, int mode);
-/* Minimum Cin of the layers the model handle runs on Winograd (default 64,
- * so res2's 64-channel 3x3 layers run F(6,3) too; handles pack the
- * transformed weights of the fp32 3x3 layers with Cin >= 64). */
-int mdx_conv_set_winograd_min_cin(int cin);
-int mdx_conv_winograd_min_cin(void);
-/* fp32 single-stage GEMM (k_conv_sb): 1 = the A fragments of the next row
- * tile are read from LDS while the current tile's MFMAs issue (two register
- * quads), 0 = one quad reloaded per tile.  Same MFMA order: bit-identical.
- * Returns the previous value. */
-int mdx_conv_set_sb_afp(int on);
-/* Model handle: run each fp32 Winograd layer in image slices whose transformed
- * input (or output) is at most `mb` MB, so the transforms' intermediate
- * tensors stay in the Infinity Cache between the three launches; 0 (default)
- * = one pass over the batch.  Returns the previous value. */
-int mdx_model_set_wino_slice(int mb);
-/* Winograd GEMMs with Cout % 256 == 0 and Cin % 32 == 0 on the 256x256
- * LDS-DMA fp32 kernel: mode 0 never (default: measured no faster), 1 when the
- * batched launch has at least min_wgs workgroups, 2 whenever eligible; returns
- * the old mode. */
-int mdx_conv_set_winograd_dma(int mode, int min_wgs);
-/* Fused Winograd F(4x4,3x3), fp32 (k_wino_f4): the input transform, the 36
- * tile-point GEMMs and the output transform + bias + ReLU in one launch, no
- * workspace.  Weights: U of mdx_winograd_weights(m = 4) repacked by the host
- * function mdx_winograd_pack_f4 (same size, 36 * Cout * Cin floats).
- * Cin % 8 == 0, Cout % 32 == 0, x / U under 2 GiB. */
-int mdx_winograd_pack_f4(const float *U, int Cout, int Cin, float *U_packed);
-int mdx_conv3x3_winograd_fused(const float *x, int N, int H, int W, int Cin, const float *U_packed,
-                               const float *bias, int Cout, int relu, float *out, mdx_stream_t stream);
-/* Policy for fused F(4,3): mode 0 never (default; measured slower than the
- * three-launch path except on 64-channel layers), 1 when the
- * launch has at least min_wgs workgroups (32 tiles x 32 channels each;
- * min_wgs <= 0 keeps the current threshold), 2 whenever the shape allows (not
- * in split-plane mode).  Returns the old mode.  mdx_winograd_fused_eligible:
- * 1 if the policy takes the fused kernel for this layer. */
-int mdx_conv_set_winograd_fused(int mode, int min_wgs);
-int mdx_winograd_fused_eligible(int N, int H, int W, int Cin, int Cout);
-/* fp32 1x1 layers with Cout <= 16 (the RPN / mask / box predictors) on the
- * narrow-output kernel k_head_f32 (1, default) or the general kernels (0);
- * returns the old value. */
-int mdx_conv_set_head_f32(int on);
 /* fp32 GEMM on the bf16 matrix cores over operands split once into bf16
  * planes (replaces the fp32 Linear layers of Detectron2's FastRCNNConvFCHead,
  * M/model/config.py:21-94 box head, when the model handle's x6 mode is on).
@@ -371,78 +368,25 @@ enum {
     MDX_CONV_KERNEL_STREAM1X1 = 4,
     MDX_CONV_KERNEL_HEAD1X1 = 5,
     MDX_CONV_KERNEL_WINOGRAD = 6,
-    MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_conv_set_fp32_split), 128-wide N tile */
+    MDX_CONV_KERNEL_X3_128 = 7, /* fp32 as bf16 plane products (mdx_policy.fp32_split), 128-wide N tile */
     MDX_CONV_KERNEL_X3_64 = 8,
     MDX_CONV_KERNEL_X6DMA = 9,  /* fp32 GEMM over pre-split bf16 planes, 256x256 LDS-DMA (mdx_gemm_x6) */
     MDX_CONV_KERNEL_PW128 = 14, /* REG128 / REG64 on a pointwise layer (1x1 unpadded, Winograd GEMMs): */
-    MDX_CONV_KERNEL_PW64 = 15,  /* per-row precomputed addresses (mdx_conv_set_pointwise) */
+    MDX_CONV_KERNEL_PW64 = 15,  /* per-row precomputed addresses (mdx_policy.pointwise) */
     MDX_CONV_KERNEL_DUAL128 = 16, /* mdx_conv2d_dual (conv3 + projection shortcut in one GEMM) */
     MDX_CONV_KERNEL_DUAL64 = 17,
-    MDX_CONV_KERNEL_SB128 = 18, /* PW128 / PW64 on the single-LDS-stage k_conv_sb (mdx_conv_set_single_stage) */
+    MDX_CONV_KERNEL_SB128 = 18, /* PW128 / PW64 on the single-LDS-stage k_conv_sb (mdx_policy.single_stage) */
     MDX_CONV_KERNEL_SB64 = 19,
     MDX_CONV_KERNEL_SBDUAL128 = 20, /* DUAL128 / DUAL64 on k_conv_sb */
     MDX_CONV_KERNEL_SBDUAL64 = 21,
-    MDX_CONV_KERNEL_SBG128 = 22, /* REG128 / REG64 on the single-stage k_conv_sbg (mdx_conv_set_single_stage(2)) */
+    MDX_CONV_KERNEL_SBG128 = 22, /* REG128 / REG64 on the single-stage k_conv_sbg (mdx_policy.single_stage 2) */
     MDX_CONV_KERNEL_SBG64 = 23,
-    MDX_CONV_KERNEL_WINO_FUSED = 24, /* fused Winograd F(4,3) (mdx_conv_set_winograd_fused): both transforms
-                                        and the 36 GEMMs in one launch */
-    MDX_CONV_KERNEL_HB128 = 25, /* SB128 / SB64 on k_conv_hb: half K-steps, two LDS stages, four workgroups
-                                   per CU (mdx_conv_set_half_step) */
-    MDX_CONV_KERNEL_HB64 = 26,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
     MDX_CONV_KERNEL_WINO_IN = 12,
     MDX_CONV_KERNEL_WINO_OUT = 13
 };
-/* Policy for the streaming 1x1 kernel (fp16, stride 1, Cin in {64,128,256},
- * Cout % 64 == 0): 0 never, 1 (default) for layers with M >= min_m (K = 256
- * only when Cout == 64), 2 for every eligible layer with M >= min_m. */
-int mdx_conv_set_stream1x1(int mode, int min_m);
-/* Its fp32 form (f32 MFMAs; fp32 in and out, not in split-plane mode), same
- * M threshold: 0 (default) never, 1 Cin == 64, 2 Cin in {64,128,256}.
- * Returns the previous mode. */
-int mdx_conv_set_stream1x1_f32(int mode);
-/* fp32 pointwise GEMMs (1x1 convs, FC layers, the Winograd GEMMs) on the
- * half-step kernel k_conv_hb instead of k_conv_sb: 0 (default) off, 1 the
- * 128-wide N tile, 2 also the 64-wide.  Same sums bit for bit.  Returns the
- * previous mode. */
-int mdx_conv_set_half_step(int mode);
-/* fp32-out GEMMs on k_conv / k_conv_sb: the epilogue (bias, residual, ReLU,
- * store) straight from each lane's accumulators (1, default) instead of
- * through a half-tile LDS image (0).  Same values.  Returns the previous mode. */
-int mdx_conv_set_direct_epilogue(int on);
-/* fp32 / fp16 GEMM layers with K <= kmax (default 128) take the 64-wide N
- * tile (more workgroups per CU for the short-K layers).  Returns the old value. */
-int mdx_conv_set_narrow_kmax(int kmax);
-/* The fp32 Winograd input transform with two channels per thread (1) or one
- * (0, default).  Same values.  Returns the previous mode. */
-int mdx_conv_set_wino_in2(int on);
-
-/* Split-K on the 256x256 LDS-DMA kernel for layers with few 256x256 tiles and
- * a deep K (Cout % 256 == 0, a split-K workspace given): 0 (default) off, 1
- * when the split reaches >= 192 workgroups with >= min_sub 32-deep substeps
- * per slice, 2 whenever possible (tests).  Measured slower than the 128-row
- * kernel on every such layer of the bench (short slices: pipeline fill/drain
- * and the fp32 partial round trip), hence off.  Slices are summed in fixed order by
- * the split-K reduction.  Returns the old mode. */
-int mdx_conv_set_split256(int mode, int min_sub);
-
-/* 256x256 LDS-DMA kernel schedule: 1 = issue each substep's DMA after its
- * MFMA burst (address arithmetic overlaps the burst), 0 (default) = before.
- * Returns the old setting. */
-int mdx_conv_set_dma_after(int on);
 int mdx_conv2d_last_plan(int *kernel, int *ksplit);
-/* Pointwise layers (1x1, unpadded, any stride) and the Winograd GEMMs on the
- * register-staged kernel's instance with per-row precomputed load addresses:
- * 1 on (default), 0 the general instance.  Returns the old value. */
-int mdx_conv_set_pointwise(int on);
-/* Pointwise layers / Winograd GEMMs / box FCs on the single-LDS-stage
- * instance k_conv_sb (three workgroups per CU, two barriers per K-step, the
- * same sums bit for bit as the two-stage instance): 1 fp32, 2 also the
- * fp32 KxK layers (k_conv_sbg), 3 also the fp16 register-staged pointwise
- * layers, 4 also the fp16 register-staged KxK layers (default), 0 the
- * two-stage instances.  Returns the old value. */
-int mdx_conv_set_single_stage(int on);
 int64_t mdx_conv2d_workspace_bytes(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad);
 int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, const void *w, const float *bias, int Cout,
                       int KH, int KW, int stride, int pad, const void *residual, int relu, int out_mode,
@@ -493,10 +437,6 @@ int mdx_groupnorm(const void *x, int N, int H, int W, int C, int G, float eps, c
                   const float *beta, const void *up, int fuse, int dtype, void *out, float *workspace,
                   mdx_stream_t stream);
 
-/* RPN top-k policy (testing / timing): 1 (default) splits every (image,
- * level) over several workgroups (per-slice top-k, then a merge), 0 one
- * workgroup per (image, level).  Returns the old value. */
-int mdx_rpn_set_sliced(int on);
 
 /* RPN find_top_rpn_proposals: per level head tensor float32 (B,H_l,W_l,A*5)
  * = [objectness(A), deltas(A*4)]; cell_anchors float32 [L][A][4].
@@ -522,7 +462,7 @@ int mdx_roi_align(const void *const *feats, const int *fh, const int *fw, const 
                   void *out, mdx_stream_t stream);
 
 /* Same, with an optional int32 scratch of R entries: when order_ws is not
- * NULL (and mdx_roi_align_set_sorted(1), the default) the ROIs of each image
+ * NULL (and mdx_policy.roi_sorted, the default) the ROIs of each image
  * are first permuted by pyramid level and map band (k_roi_order) so the
  * workgroups in flight share one band of one level map; outputs are
  * identical to the unordered call.  order_ws == NULL is mdx_roi_align. */
@@ -530,22 +470,6 @@ int mdx_roi_align_ex(const void *const *feats, const int *fh, const int *fw, con
                      int min_level, int C, const float *rois, const int *counts, int R, int per_image, int P,
                      int sampling, int aligned, float canonical_size, float canonical_level, int dtype,
                      int *order_ws, void *out, mdx_stream_t stream);
-/* Tuning knob for the permutation above (1 on, 0 off); returns the old value. */
-int mdx_roi_align_set_sorted(int on);
-/* Current ROIAlign kernel choice (mdx_roi_align_set_mode). */
-int mdx_roi_align_get_mode(void);
-
-/* ROIAlign kernel choice: 0 = one workgroup per (ROI, 128-B channel slice)
- * with the sample window staged in LDS; 1, 2, 3 = one workgroup per
- * ROI over all channels, taps gathered from the map, 1/2/4 items per thread
- * in lockstep; 4 (default) = one workgroup per ROI, separable form (per-bin row and
- * column weight sums, (gh+1)(gw+1) taps per output instead of 4 gh gw).
- * Returns the old mode. */
-/* Tuning knob: 1 (default) maps the ROIAlign workgroups to XCD-contiguous
- * ROI ranges; 0 keeps dispatch order (ROIs of the same images in flight on
- * every XCD).  Returns the previous value. */
-int mdx_roi_align_set_order(int xcd_remap);
-int mdx_roi_align_set_mode(int mode);
 
 /* fast_rcnn_inference_single_image + detector_postprocess for 1 class:
  * pred float32 (B*R, ld_pred) = [cls0, bg, dx, dy, dw, dh].  Outputs
@@ -673,14 +597,6 @@ typedef struct mdx_model_cfg {
 
 typedef void *mdx_model_t;
 
-/* fp32 handles created afterwards fold the per-channel pixel normalisation
- * into the stem weights (2-channel s2d input, K 256 -> 128): 1 on (default),
- * 0 the 3-channel normalised input.  Returns the old value. */
-int mdx_model_set_stem_fold(int on);
-/* Handles created afterwards run each bottleneck's projection shortcut and
- * conv3 as one GEMM (mdx_conv2d_dual): 0 off, 1 fp32 handles, 2 fp32 and fp16
- * handles.  Default 1.  Returns the old value. */
-int mdx_model_set_fuse_shortcut(int mode);
 
 /* Weights blob: Detectron2 state-dict layout (parameter / buffer names of
  * GeneralizedRCNN, e.g. "backbone.bottom_up.res2.0.conv1.weight"), serialised
@@ -693,6 +609,8 @@ int mdx_model_set_fuse_shortcut(int mode);
 int mdx_model_create(const void *weights_blob, int64_t blob_bytes, const mdx_model_cfg *cfg, int device,
                      mdx_model_t *out);
 int mdx_model_destroy(mdx_model_t model);
+/* The policy this handle runs with (captured at mdx_model_create). */
+int mdx_model_get_policy(mdx_model_t model, mdx_policy *out);
 
 /* Caller-owned device outputs of one forward over B frames of h x w
  * (D = detections_per_image, K = num_keypoints, S = 4 * keypoint pooler

@@ -51,58 +51,23 @@ SIGNATURES = {
     "mdx_flips_from_keypoints": (I32, [P, I64, I32, P, P, P, P, P]),
     "mdx_finalize_angles": (I32, [P, P, P, P, I64, I32, P, P]),
     "mdx_conv2d": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P]),
-    "mdx_conv_set_large_tiles": (I32, [I32]),
-    "mdx_conv_set_dma128": (I32, [I32, I32]),
-    "mdx_conv_set_mfma_prio": (I32, [I32]),
-    "mdx_conv_set_mfma_prio256": (I32, [I32]),
-    "mdx_conv_set_dma_f32": (I32, [I32]),
-    "mdx_conv_set_pointwise": (I32, [I32]),
-    "mdx_conv_set_single_stage": (I32, [I32]),
-    "mdx_conv_set_fp32_split": (I32, [I32]),
-    "mdx_conv_set_x3_single_stage": (I32, [I32]),
-    "mdx_conv_set_sb_afp": (I32, [I32]),
-    "mdx_conv_fp32_split": (I32, []),
-    "mdx_roi_align_get_mode": (I32, []),
-    "mdx_conv_set_x3_narrow": (I32, [I32]),
-    "mdx_rpn_set_sliced": (I32, [I32]),
     "mdx_winograd_weights": (I32, [P, I32, I32, I32, P]),
     "mdx_winograd_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32]),
     "mdx_conv3x3_winograd": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
     "mdx_conv3x3_winograd_x6": (I32, [P, I32, I32, I32, I32, P, P, P, I32, I32, I32, P, P, I64, P]),
-    "mdx_conv_set_winograd": (I32, [I32]),
-    "mdx_conv_winograd_enabled": (I32, []),
     "mdx_winograd_tile": (I32, [I32, I32, I32]),
-    "mdx_conv_set_winograd_min_cin": (I32, [I32]),
-    "mdx_conv_winograd_min_cin": (I32, []),
-    "mdx_conv_set_winograd_dma": (I32, [I32, I32]),
-    "mdx_conv_set_winograd_fused": (I32, [I32, I32]),
-    "mdx_winograd_fused_eligible": (I32, [I32, I32, I32, I32, I32]),
-    "mdx_winograd_pack_f4": (I32, [P, I32, I32, P]),
-    "mdx_conv3x3_winograd_fused": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, P, P]),
-    "mdx_conv_set_head_f32": (I32, [I32]),
     "mdx_x6_plane_bytes": (I64, [I64, I32]),
     "mdx_split_x6": (I32, [P, I64, I32, I64, P, P]),
     "mdx_gemm_x6": (I32, [P, P, P, I32, I32, I32, P, I32, P, P]),
     "mdx_conv2d_last_plan": (I32, [P, P]),
-    "mdx_conv_set_stream1x1": (I32, [I32, I32]),
-    "mdx_conv_set_stream1x1_f32": (I32, [I32]),
-    "mdx_conv_set_half_step": (I32, [I32]),
-    "mdx_conv_set_direct_epilogue": (I32, [I32]),
-    "mdx_conv_set_narrow_kmax": (I32, [I32]),
-    "mdx_conv_set_wino_in2": (I32, [I32]),
-    "mdx_conv_set_split256": (I32, [I32, I32]),
-    "mdx_conv_set_dma_after": (I32, [I32]),
     "mdx_conv2d_workspace_bytes": (I64, [I32, I32, I32, I32, I32, I32, I32, I32, I32]),
     "mdx_conv2d_splitk": (I32, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, I32, I32, I32, P, I32,
                                 P, I64, P]),
     "mdx_format_tsv_rows": (I64, [P, P, I32, I64, P, I64]),
     "mdx_conv2d_dual": (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, I64, P]),
-    "mdx_model_set_fuse_shortcut": (I32, [I32]),
-    "mdx_model_set_wino_slice": (I32, [I32]),
     "mdx_preprocess": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, I32, P, P]),
     "mdx_preprocess_s2d": (I32, [P, I32, I32, I32, P, P, P, I32, I32, I32, I32, P, P]),
     "mdx_preprocess_s2d_folded": (I32, [P, I32, I32, I32, P, I32, I32, I32, P, P]),
-    "mdx_model_set_stem_fold": (I32, [I32]),
     "mdx_maxpool2d": (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "mdx_convert": (I32, [P, I64, I32, P, I32, P]),
     "mdx_groupnorm_workspace_bytes": (I64, [I32, I32, I32, I32]),
@@ -112,9 +77,6 @@ SIGNATURES = {
                                 P, P, P, P, P, P]),
     "mdx_roi_align": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "mdx_roi_align_ex": (I32, [P, P, P, P, I32, I32, I32, P, P, I32, I32, I32, I32, I32, F32, F32, I32, P, P, P]),
-    "mdx_roi_align_set_sorted": (I32, [I32]),
-    "mdx_roi_align_set_mode": (I32, [I32]),
-    "mdx_roi_align_set_order": (I32, [I32]),
     "mdx_box_postprocess": (I32, [P, I32, P, P, I32, I32, I32, F32, F32, I32, I32, P, F32, P, P, P, P, P]),
     "mdx_paste_masks": (I32, [P, P, P, I32, I32, I32, I32, I32, I64, F32, P, P]),
     "mdx_deconv_col2im": (I32, [P, P, I32, I32, I32, I32, P, P]),
@@ -140,7 +102,80 @@ SIGNATURES = {
     "mdx_model_debug_fill": (I32, [P, I32, I32, I32, I32, P]),
     "mdx_model_debug_arena": (I32, [P, P, ctypes.c_char_p, P, P, P, I64]),
     "mdx_model_profile_read": (I32, [P, P, I32]),
+    "mdx_model_get_policy": (I32, [P, P]),
+    "mdx_policy_defaults": (I32, [P]),
+    "mdx_policy_get": (I32, [P]),
+    "mdx_policy_set": (I32, [P]),
 }
+
+# include/mdx.h mdx_policy, field for field (tests/test_abi.py checks the order
+# against the header)
+POLICY_FIELDS = ("winograd", "winograd_min_cin", "winograd_dma", "winograd_dma_min_wgs", "wino_slice_mb",
+                 "fp32_split", "x3_narrow", "x3_single_stage", "large_tiles", "dma128", "dma128_min_tiles",
+                 "dma128_interleave", "dma_f32", "pointwise", "single_stage", "direct_epilogue", "narrow_kmax",
+                 "head_f32", "stream1x1", "stream1x1_min_m", "stem_fold", "fuse_shortcut", "rpn_sliced", "roi_mode",
+                 "roi_xcd_order", "roi_sorted")
+
+
+class Policy(ctypes.Structure):
+    """mdx_policy (include/mdx.h): the kernel-selection policy."""
+    _fields_ = [(f, ctypes.c_int) for f in POLICY_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f in POLICY_FIELDS}
+
+
+def policy() -> dict:
+    """The calling thread's policy (mdx_policy_get)."""
+    p = Policy()
+    call("mdx_policy_get", ctypes.byref(p))
+    return p.as_dict()
+
+
+def policy_defaults() -> dict:
+    p = Policy()
+    call("mdx_policy_defaults", ctypes.byref(p))
+    return p.as_dict()
+
+
+def set_policy(**fields) -> dict:
+    """Change fields of the calling thread's policy (model handles created
+    afterwards on this thread capture it); returns the previous policy."""
+    old = policy()
+    bad = set(fields) - set(POLICY_FIELDS)
+    if bad:
+        raise KeyError(f"unknown policy field(s): {sorted(bad)}")
+    p = Policy(**{**old, **fields})
+    call("mdx_policy_set", ctypes.byref(p))
+    return old
+
+
+class policy_scope:
+    """with policy_scope(winograd=4): ... -- the thread's policy with these
+    fields changed, restored on exit."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+
+    def __enter__(self):
+        self.old = set_policy(**self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        p = Policy(**self.old)
+        call("mdx_policy_set", ctypes.byref(p))
+
+
+def knob(field: str, value: int, *more):
+    """Set one policy field (and, for the (mode, threshold) pairs, the
+    threshold field after it in POLICY_FIELDS) on the calling thread; returns
+    the field's previous value."""
+    old = policy()
+    upd = {field: value}
+    if more:
+        upd[POLICY_FIELDS[POLICY_FIELDS.index(field) + 1]] = more[0]
+    set_policy(**upd)
+    return old[field]
 
 
 def lib():

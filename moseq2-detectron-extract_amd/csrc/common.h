@@ -55,13 +55,21 @@ void wino_probe(WinoProbe *p);
 WinoProbe *wino_probe_current();
 // the kernel id / K slices mdx_conv2d_last_plan reports for this thread
 void set_last_plan(int kernel, int ksplit);
-// the fp32 Winograd input transform with two channels per thread (wino_fused.hip,
-// built without packed FP32): grid (tiles, channel pairs / bd), bd threads
-void launch_wino_in2(int m, dim3 grid, unsigned bd, hipStream_t s, const float *x, int N, int H, int W, int C,
-                     int TH, int TW, float *V);
 bool winograd_planes_enabled();  // the model runs Winograd GEMMs on k_gemm_x6 (MDX_WINO_X6 set)
 // weights of the next split-plane conv launch on this thread as bf16 planes
 // (mdx_split_x6 layout), or null; the model handle sets it around a layer
 void x3_weight_planes(const void *planes);
+
+// the kernel-selection policy in force on this thread (include/mdx.h,
+// mdx_policy): the running model handle's inside its entry points
+// (PolicyScope), else the thread's own (mdx_policy_set)
+const mdx_policy &pol();
+struct PolicyScope {
+    const mdx_policy *prev;
+    explicit PolicyScope(const mdx_policy *p);
+    ~PolicyScope();
+    PolicyScope(const PolicyScope &) = delete;
+    PolicyScope &operator=(const PolicyScope &) = delete;
+};
 
 }  // namespace mdx

@@ -219,7 +219,7 @@ __device__ __forceinline__ void finish_batch(const ConvArgs &a, F item) {
 // SB: one LDS stage instead of two (a second barrier per K-step before the
 // next stage overwrites it), so three workgroups fit a CU instead of two
 // (launched as k_conv_sb).
-template <typename T, typename TO, int BN_, bool DUAL, bool PW, bool SB, bool AFP = false>
+template <typename T, typename TO, int BN_, bool DUAL, bool PW, bool SB>
 __device__ __forceinline__ void conv_body(ConvArgs &a) {
     constexpr int BK = Prec<T>::BK, VEC = Prec<T>::VEC;
     constexpr int TI = BM / 32, TJ = BN_ / 32;
@@ -428,30 +428,6 @@ __device__ __forceinline__ void conv_body(ConvArgs &a) {
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-            } else if constexpr (AFP && TJ >= 4) {
-                // A fragments double-buffered: row tile i + 1's fragment is
-                // read while tile i's 4 TJ MFMAs issue (the plain form below
-                // compiles to one register quad reloaded per tile behind an
-                // lgkmcnt(0)); same MFMA order per accumulator: bit-identical
-                float4v bf[TJ];
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * PITCH + koff);
-                float4v a_cur = *reinterpret_cast<const float4v *>(Ab + koff);
-#pragma unroll
-                for (int i = 0; i < TI; ++i) {
-                    const float4v a_nxt =
-                        i + 1 < TI ? *reinterpret_cast<const float4v *>(Ab + (i + 1) * 16 * PITCH + koff) : a_cur;
-                    // keep the read above the MFMAs (the scheduler would sink it
-                    // below them to save the four registers)
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-#pragma unroll
-                        for (int j = 0; j < TJ; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[e], bf[j][e], acc[i][j], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    a_cur = a_nxt;
-                }
             } else {
                 // B fragments first and the row tile outermost: the MFMAs of
                 // tile i start once bf and af[i] have arrived (per accumulator
@@ -626,9 +602,9 @@ template <typename T, typename TO, int BN_, bool DUAL = false, bool PW = false>
 __global__ __launch_bounds__(CONV_THREADS, 2) void k_conv(ConvArgs a) {
     conv_body<T, TO, BN_, DUAL, PW, false>(a);
 }
-template <typename T, typename TO, int BN_, bool DUAL = false, bool AFP = false>
+template <typename T, typename TO, int BN_, bool DUAL = false>
 __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sb(ConvArgs a) {
-    conv_body<T, TO, BN_, DUAL, true, true, AFP>(a);
+    conv_body<T, TO, BN_, DUAL, true, true>(a);
 }
 // the single-stage schedule for general layers (padded / KxK: the stem, the
 // Cin < 128 3x3 layers)
@@ -637,179 +613,6 @@ __global__ __launch_bounds__(CONV_THREADS, BN_ == 64 ? 4 : 3) void k_conv_sbg(Co
     conv_body<T, TO, BN_, false, false, true>(a);
 }
 
-// fp32 pointwise GEMM (1x1 convs, FC layers, the batched Winograd GEMMs) in
-// half K-steps of 16 floats: 64-B LDS rows, two LDS stages and one barrier
-// per half-step, one register stage of 2 + BN_/64 16-B loads per thread.  The
-// half-step halves the fragment and staging registers of k_conv_sb, so four
-// workgroups (16 waves) fit a CU instead of three.  Per accumulator the
-// MFMAs take the same k's in the same order as k_conv_sb's substeps (half-
-// step h = K-step h / 2, substep h % 2): bit-identical sums.
-//   iteration h: [store half-step h + 1 (registers) into the other stage,
-//   load h + 2 into the registers, fragments + MFMAs of h] barrier
-// (the other stage was last read in iteration h - 1, before its barrier).
-__device__ __forceinline__ int hb_swz(int r) { return ((r >> 3) & 1) << 1; }
-
-template <typename TO, int BN_>
-__global__ __launch_bounds__(CONV_THREADS, 4) void k_conv_hb(ConvArgs a) {
-    constexpr int RB = 64;  // LDS row bytes: 16 floats
-    constexpr int TI = BM / 32, TJ = BN_ / 32;
-    constexpr int A_TILE = BM * RB, STAGE = A_TILE + BN_ * RB;
-    constexpr int ALD = BM * 4 / CONV_THREADS, BLD = BN_ * 4 / CONV_THREADS;  // 16-B loads per thread
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (gridDim.z > 1) {  // batch entry z of a batched GEMM
-        const long long z = blockIdx.z;
-        a.x = reinterpret_cast<const char *>(a.x) + z * a.bsx;
-        a.w = reinterpret_cast<const char *>(a.w) + z * a.bsw;
-        a.out = reinterpret_cast<char *>(a.out) + z * a.bso;
-    }
-    int tile;
-    {
-        const int L = blockIdx.x, nwg = a.tiles_total;
-        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
-        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-    }
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN_;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-
-    // loads: rows lrow + 64 i, 16-B piece kc of the half-step's 64 B
-    const int kc = tid & 3, lrow = tid >> 2;
-    constexpr unsigned OOB = 0xFFFFFFF0u;
-    unsigned a_off[ALD], b_off[BLD];
-    const int ohw = a.OH * a.OW;
-#pragma unroll
-    for (int i = 0; i < ALD; ++i) {
-        const int gm = m0 + lrow + 64 * i;
-        const int b = gm / ohw, rem = gm - b * ohw;
-        const int oy = rem / a.OW, ox = rem - oy * a.OW;
-        a_off[i] = gm < a.M ? (unsigned)((((long long)b * a.H + (long long)oy * a.stride) * a.W +
-                                          (long long)ox * a.stride) * a.Cin * 4)
-                            : OOB;
-    }
-#pragma unroll
-    for (int i = 0; i < BLD; ++i) {
-        const int gn = n0 + lrow + 64 * i;
-        b_off[i] = gn < a.Cout ? (unsigned)((long long)gn * a.K * 4) : OOB;
-    }
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void *)a.w, (short)0, a.wbytes, 0x00020000);
-    const int k0 = (int)blockIdx.y * a.ksteps * 32;
-    const int nh = min(2 * a.ksteps, (a.K - k0 + 15) / 16);
-    int kglob = k0 + kc * 4;
-    uint4 ra[ALD], rb[BLD];
-    auto load = [&]() {
-        const bool kok = kglob < a.K;
-        const unsigned kb = (unsigned)kglob * 4u;
-#pragma unroll
-        for (int i = 0; i < ALD; ++i)
-            ra[i] = __builtin_bit_cast(
-                uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, (kok && a_off[i] != OOB) ? a_off[i] + kb : OOB, 0, 0));
-#pragma unroll
-        for (int i = 0; i < BLD; ++i)
-            rb[i] = __builtin_bit_cast(
-                uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, (kok && b_off[i] != OOB) ? b_off[i] + kb : OOB, 0, 0));
-        kglob += 16;
-    };
-    // piece kc of row R at physical piece kc ^ g_swz(R) (k_convg's 64-B row
-    // layout: the fragment reads, rows l & 15 and pieces l >> 4, are
-    // conflict-free); (lrow + 64 i) has lrow's bit 3
-    const int wpiece = (kc ^ hb_swz(lrow)) * 16;
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < ALD; ++i)
-            *reinterpret_cast<uint4 *>(smem + buf * STAGE + (lrow + 64 * i) * RB + wpiece) = ra[i];
-#pragma unroll
-        for (int i = 0; i < BLD; ++i)
-            *reinterpret_cast<uint4 *>(smem + buf * STAGE + A_TILE + (lrow + 64 * i) * RB + wpiece) = rb[i];
-    };
-
-    float4v acc[TI][TJ];
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-    const int koff = ((lane >> 4) ^ hb_swz(lane & 15)) * 16;
-    const char *Ab0 = smem + (wm * (BM / 2) + (lane & 15)) * RB + koff;
-    const char *Bb0 = smem + A_TILE + (wn * (BN_ / 2) + (lane & 15)) * RB + koff;
-
-    load();
-    store(0);
-    if (nh > 1) load();
-    __syncthreads();
-    for (int h = 0; h < nh; ++h) {
-        const int cur = h & 1;
-        if (h + 1 < nh) store(cur ^ 1);
-        if (h + 2 < nh) load();
-        const char *Ab = Ab0 + cur * STAGE, *Bb = Bb0 + cur * STAGE;
-        float4v af[TI], bf[TJ];
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const float4v *>(Bb + j * 16 * RB);
-#pragma unroll
-        for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const float4v *>(Ab + i * 16 * RB);
-        constexpr int IG = TJ >= 4 ? 1 : 4 / TJ;
-#pragma unroll
-        for (int i0 = 0; i0 < TI; i0 += IG)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int i = i0; i < i0 + IG; ++i)
-#pragma unroll
-                    for (int j = 0; j < TJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-        __syncthreads();
-    }
-
-    // epilogue: as conv_body's (two halves of BM/2 rows through LDS)
-    constexpr int CP = BN_ + 4;
-    constexpr int HM = BM / 2;
-    float *Cs = reinterpret_cast<float *>(smem);
-    constexpr int CPR = BN_ / 8;
-    constexpr int NQ = HM * CPR / CONV_THREADS;
-    const int kz = blockIdx.y;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-        if (wm == hh) {
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-#pragma unroll
-                for (int j = 0; j < TJ; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = i * 16 + (lane >> 4) * 4 + r;
-                        const int col = wn * (BN_ / 2) + j * 16 + (lane & 15);
-                        Cs[row * CP + col] = acc[i][j][r];
-                    }
-        }
-        __syncthreads();
-        const int mh = m0 + hh * HM;
-        if (a.ksplit > 1) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int c = tid + q * CONV_THREADS;
-                const int row = c / CPR, ch = c - row * CPR;
-                const int gm = mh + row, gn0 = n0 + ch * 8;
-                if (gm >= a.M || gn0 >= a.Cout) continue;
-                const float *src = Cs + row * CP + ch * 8;
-                float *pp = a.part + ((long long)kz * a.M + gm) * a.Cout + gn0;
-                *reinterpret_cast<float4 *>(pp) = *reinterpret_cast<const float4 *>(src);
-                *reinterpret_cast<float4 *>(pp + 4) = *reinterpret_cast<const float4 *>(src + 4);
-            }
-        } else {
-            finish_batch<TO, NQ>(a, [&](int q, int &gm, int &gn0, const float *&src) {
-                const int c = tid + q * CONV_THREADS;
-                const int row = c / CPR, ch = c - row * CPR;
-                gm = mh + row;
-                gn0 = n0 + ch * 8;
-                src = Cs + row * CP + ch * 8;
-                if (gm >= a.M || gn0 >= a.Cout) gm = -1;
-            });
-        }
-        if (hh == 0) __syncthreads();
-    }
-}
-
-// split-K reduction: sum the slices (fixed order) and apply the epilogue
 template <typename TO>
 __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
     const int cpr = a.Cout / 8;
@@ -829,7 +632,7 @@ __global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a) {
 
 // ---------------------------------------------------------------------------
 // fp32 GEMM on the bf16 matrix cores (the fp32 model's layers when
-// mdx_conv_set_fp32_split(6 | 9)).  Every fp32 operand is split into three
+// mdx_policy.fp32_split = 6 | 9).  Every fp32 operand is split into three
 // bf16 values x = hi + mid + lo (hi = RN(x), mid = RN(x - hi), lo = x - hi -
 // mid): each subtraction is exact (Sterbenz) and the last residual has at most
 // 8 significant bits, so the three parts represent x EXACTLY (normal range).
@@ -1300,104 +1103,6 @@ __global__ __launch_bounds__(256) void k_conv1x1_stream(ConvArgs a) {
     }
 }
 
-// fp32 streaming 1x1 kernel (K = Cin = 16 KQ in {64, 128, 256}, Cout % 64 ==
-// 0): the fp16 kernel's tiling on 16x16x4 f32 MFMAs.  A lane's 16-B load of
-// an activation row holds 4 consecutive K values; MFMA e of a 16-K block takes
-// component e from every lane group, i.e. K values 16 kq + 4 (l >> 4) + e --
-// a fixed permutation of K, the same for both operands:
-//   W operand = W[n0 + 16 ns + (l & 15)][16 kq + 4 (l >> 4) + e]
-//   X operand = X[m0 + 16 ms + (l & 15)][16 kq + 4 (l >> 4) + e]
-//   D[ms][ns][r] = out[m0 + 16 ms + (l & 15)][n0 + 16 ns + 4 (l >> 4) + r]
-// Each lane ends with 4 consecutive fp32 channels of one pixel = one 16-B
-// residual load and one 16-B store (no exchange, no LDS epilogue).
-template <int KQ>
-__global__ __launch_bounds__(256) void k_conv1x1_stream_f32(ConvArgs a) {
-    constexpr int K = 16 * KQ, WPITCH = 4 * K + 16;  // +16 B: rows (l & 15) land 4 banks apart
-    __shared__ __attribute__((aligned(16))) char sw[64 * WPITCH];
-    int tile;
-    {
-        const int L = blockIdx.x, nwg = a.tiles_total;
-        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
-        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
-    }
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int n0 = tn * 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
-    const float *Wt = reinterpret_cast<const float *>(a.w);
-    const int m0 = tm * 128 + wid * 32;
-    // residual first (the longest stream, independent of everything else)
-    float4v rr[2][4];
-    if (a.res) {
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.res, (short)0, a.rbytes,
-                                                                            0x00020000);
-#pragma unroll
-        for (int ms = 0; ms < 2; ++ms) {
-            const int m = m0 + 16 * ms + (lane & 15);
-#pragma unroll
-            for (int ns = 0; ns < 4; ++ns) {
-                const unsigned off =
-                    m < a.M ? (unsigned)(((long long)m * a.Cout + n0 + 16 * ns + 4 * g) * 4) : 0xFFFFFFF0u;
-                rr[ms][ns] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
-            }
-        }
-    }
-    // stage the 64 x K weight slice
-    for (int i = tid; i < 64 * K / 4; i += 256) {
-        const int r = i / (K / 4), c = i - r * (K / 4);
-        *reinterpret_cast<uint4 *>(sw + r * WPITCH + c * 16) =
-            *reinterpret_cast<const uint4 *>(Wt + (long long)(n0 + r) * K + c * 4);
-    }
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)a.x, (short)0, a.xbytes, 0x00020000);
-    float4v xf[2][KQ];
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-        const int m = m0 + 16 * ms + (lane & 15);
-        const unsigned base = (unsigned)((long long)m * K * 4) + 16u * g;
-#pragma unroll
-        for (int kq = 0; kq < KQ; ++kq)
-            xf[ms][kq] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         rx, m < a.M ? base + 64u * kq : 0xFFFFFFF0u, 0, 0));
-    }
-    __syncthreads();
-    float4v acc[2][4];
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = float4v{0.f, 0.f, 0.f, 0.f};
-    const char *wl = sw + (lane & 15) * WPITCH + 16 * g;
-#pragma unroll
-    for (int kq = 0; kq < KQ; ++kq) {
-        float4v wf[4];
-#pragma unroll
-        for (int ns = 0; ns < 4; ++ns) wf[ns] = *reinterpret_cast<const float4v *>(wl + 16 * ns * WPITCH + 64 * kq);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-                for (int ns = 0; ns < 4; ++ns)
-                    acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[ns][e], xf[ms][kq][e], acc[ms][ns], 0, 0, 0);
-    }
-    float *O = reinterpret_cast<float *>(a.out);
-#pragma unroll
-    for (int ns = 0; ns < 4; ++ns) {
-        const int c = n0 + 16 * ns + 4 * g;
-        const float4v bv = a.bias ? *reinterpret_cast<const float4v *>(a.bias + c) : float4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ms = 0; ms < 2; ++ms) {
-            const int m = m0 + 16 * ms + (lane & 15);
-            if (m >= a.M) continue;
-            float4v v = acc[ms][ns] + bv;
-            if (a.res) v += rr[ms][ns];
-            if (a.relu) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-            }
-            *reinterpret_cast<float4v *>(O + (long long)m * a.Cout + c) = v;
-        }
-    }
-}
-
 // Narrow-output streaming 1x1 kernel (RPN head: 256 -> 15 logits/deltas,
 // fp32 out): one 16-row MFMA block of output channels (rows >= Cout read as
 // zero weights), no LDS and no barrier -- each wave loads its 16 x K weight
@@ -1514,33 +1219,6 @@ __global__ __launch_bounds__(256) void k_head_f32(ConvArgs a) {
     }
 }
 
-// fp32 narrow-output 1x1 kernel (k_head_f32) for Cout <= 16: 1 on (default), 0 off
-static int g_head_f32 = 1;
-extern "C" int mdx_conv_set_head_f32(int on) {
-    const int old = g_head_f32;
-    g_head_f32 = on;
-    return old;
-}
-// streaming 1x1 kernel policy: 0 never, 1 for eligible layers with M >= g_stream_min_m (default),
-// 2 also for K = 256 layers with Cout > 64
-static int g_stream1x1 = 1, g_stream_min_m = 65536;
-extern "C" int mdx_conv_set_stream1x1(int mode, int min_m) {
-    const int old = g_stream1x1;
-    g_stream1x1 = mode;
-    g_stream_min_m = min_m;
-    return old;
-}
-// fp32 streaming 1x1 kernel (k_conv1x1_stream_f32), layers with M >= g_stream_min_m: 0 never
-// (default since the GEMMs' direct epilogue: res2 conv3 on k_conv_sb<64> 307 vs 318 us, bench
-// loop 1477 vs 1473 fps over two interleaved pairs, profiles/r05_ab_stream1x1_f32.txt),
-// 1 Cin = 64 (3-9 % faster than k_conv<float, float, 64> on the res2 1x1 layers before
-// that; 8-27 % slower at Cin = 128 and 256), 2 Cin in {64, 128, 256}
-static int g_stream1x1_f32 = 0;
-extern "C" int mdx_conv_set_stream1x1_f32(int mode) {
-    const int old = g_stream1x1_f32;
-    g_stream1x1_f32 = mode;
-    return old;
-}
 
 // Tile codes: 8 = 256x256 (8 waves), 4 = 128x128 (4 waves), both 4 LDS
 // buffers; 6 = 256x128 (4 waves, 3 buffers: 72 KiB, so two workgroups share
@@ -1589,7 +1267,7 @@ __device__ __forceinline__ int g_swz(int r) { return ((r >> 3) & 1) << 1; }
 // same permutation on both operands, so the dot products are unchanged).
 // A K "chunk" is one 128-B run of input channels (64 halves / 32 floats),
 // split into two 64-B substeps.
-template <typename TIN, typename TO, int NW, bool ILV, bool PRIO = false, bool DMA_AFTER = false>
+template <typename TIN, typename TO, int NW, bool ILV>
 __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 8 ? 1 : 2) void k_convg(ConvArgs a) {
     using GT = GTile<NW>;
     constexpr int BM = GT::BM, SUB = GT::SUB, TI = GT::TI, TJ = GT::TJ;
@@ -1738,7 +1416,6 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 8 ? 1 : 2) void k_convg(C
         for (int i = 0; i < TI; ++i) fa[set][i] = *reinterpret_cast<const frag_t *>(Ab + i * 16 * 64);
     };
     auto mma = [&](int set) {
-        if (PRIO) __builtin_amdgcn_s_setprio(1);  // the wave in its MFMA burst keeps the issue slots
         if constexpr (F32) {
             // row tile outermost: the MFMAs of tile i need only fb and fa[i],
             // so they start while the later A fragments are still arriving
@@ -1758,7 +1435,6 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 8 ? 1 : 2) void k_convg(C
                 for (int j = 0; j < TJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[set][i], fb[set][j], acc[i][j], 0, 0, 0);
         }
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
     };
     // wait until substep u has landed (PIECES DMAs per thread per substep;
     // at most NBUF - 2 substeps in flight beyond it)
@@ -1855,20 +1531,11 @@ __global__ __launch_bounds__(GTile<NW>::THREADS, NW == 8 ? 1 : 2) void k_convg(C
                     issued = t + 3;
                     return;
                 }
-                if (!DMA_AFTER) {
-                    issue((t + 3) & 3);
-                    issued = t + 3;
-                }
+                issue((t + 3) & 3);
+                issued = t + 3;
             }
         }
         mma(cur);
-        if (DMA_AFTER && t + 3 < T) {
-            // MFMAs first: right after the barrier every wave has its
-            // operands, and the DMA address arithmetic then overlaps the tail
-            // of the SIMD's MFMA bursts
-            issue((t + 3) & 3);
-            issued = t + 3;
-        }
     };
     int t = 0;
     for (; t + 1 < T; t += 2) {
@@ -2315,99 +1982,9 @@ using namespace mdx;
 // kernel chosen by the calling thread's last mdx_conv2d* call (measurement)
 static thread_local int t_plan_kernel = -1, t_plan_ksplit = 0;
 
-// dtype codes: 0 = fp32, 1 = fp16
-// large-tile kernel policy (tests): 0 never, 1 auto (default), 2 whenever eligible
-static int g_large_tiles = 1;
-extern "C" int mdx_conv_set_large_tiles(int mode) {
-    const int old = g_large_tiles;
-    g_large_tiles = mode;
-    return old;
-}
-// 128x128 LDS-DMA kernel policy: 0 never, 1 when the layer has at least
-// g_dma128_min_tiles tiles (and no wider kernel was chosen), 2 whenever eligible
-static int g_dma128 = 0, g_dma128_min_tiles = 1536;
-// DMA pieces interleaved with the MFMAs in the 128x128 LDS-DMA kernel (0/1)
-static int g_prio = 1;
-// split-K on the 256x256 kernel for few-tile deep-K layers (0 off -- default, measured slower --, 1 auto,
-// 2 whenever Cout % 256 == 0 -- tests) and the minimum substeps (of 32) per slice
-static int g_split256 = 0, g_split256_min_sub = 18;
-extern "C" int mdx_conv_set_split256(int mode, int min_sub) {
-    const int old = g_split256;
-    g_split256 = mode;
-    g_split256_min_sub = min_sub;
-    return old;
-}
-// 256x256 kernel: issue the next DMA after the MFMA burst instead of before (0/1)
-static int g_dma_after = 0;
-extern "C" int mdx_conv_set_dma_after(int on) {
-    const int old = g_dma_after;
-    g_dma_after = on;
-    return old;
-}
-// fp32 layers on the LDS-DMA kernels: 0 never (default since round 3: box
-// fc1 on the single-stage k_conv_sb runs at 0.86 of the f32 peak, 6.10 ms,
-// against 0.83 on the 256x256 tile; bench loop 1324 -> 1338 fps), 1 the
-// 128x128 tile for layers with >= 512 tiles, 2 the 256x256 tile for the big
-// deep-K layers (the round-2 default), 3 the 256x256 tile under the fp16 policy
-static int g_dma_f32 = 0;
-extern "C" int mdx_conv_set_dma_f32(int on) {
-    const int old = g_dma_f32;
-    g_dma_f32 = on;
-    return old;
-}
-// pointwise layers (1x1, unpadded) and the Winograd GEMMs on k_conv's PW
-// instances (addresses precomputed per row): 1 (default), 0 the general instances
-static int g_pw = 1;
-extern "C" int mdx_conv_set_pointwise(int on) {
-    const int old = g_pw;
-    g_pw = on;
-    return old;
-}
-// PW layers on the instances with a single LDS stage and a single register
-// stage, three (128-wide) / four (64-wide) workgroups per CU (k_conv_sb, the
-// same sums bit for bit): 1 fp32 (GEMM microbench 14.35 -> 13.92 ms per
-// forward, bench loop 1281 -> 1306 fps), 2 also the general (padded / KxK)
-// fp32 layers (k_conv_sbg: res2 conv2 306 -> 284 us, loop unchanged), 3 also
-// the fp16 register-staged PW layers (default: fp16 loop 3924 -> 4009 fps,
-// config 5 3310 -> 3320), 0 the two-stage k_conv instances
-static int g_conv_sb = 4;
-// k_conv_sb's fp32 A fragments double-buffered in registers (1) or reloaded
-// per row tile (0, default) -- mdx_conv_set_sb_afp; bit-identical sums
-static int g_sb_afp = 0;
-extern "C" int mdx_conv_set_sb_afp(int on) {
-    const int old = g_sb_afp;
-    if (on >= 0) g_sb_afp = on ? 1 : 0;
-    return old;
-}
-extern "C" int mdx_conv_set_single_stage(int on) {
-    const int old = g_conv_sb;
-    g_conv_sb = on;
-    return old;
-}
-// fp32 PW GEMMs on k_conv_hb (half K-steps, two LDS stages, four workgroups
-// per CU) instead of k_conv_sb: 0 off, 1 the 128-wide tile, 2 also the
-// 64-wide -- mdx_conv_set_half_step; bit-identical sums
-static int g_conv_hb = 0;
-extern "C" int mdx_conv_set_half_step(int mode) {
-    const int old = g_conv_hb;
-    if (mode >= 0) g_conv_hb = mode;
-    return old;
-}
-static size_t hb_lds(int bn) {
-    const size_t main_ = 2 * ((size_t)BM * 64 + (size_t)bn * 64);
-    const size_t epi = (size_t)(BM / 2) * (bn + 4) * 4;
-    return main_ > epi ? main_ : epi;
-}
-// k_conv / k_conv_sb epilogue straight from the accumulators (1, default:
-// R50 B=32 GEMM layers 19.90 -> 19.62 ms per forward, no layer slower by more
-// than the spread) instead of through the half-tile LDS image (0) --
-// mdx_conv_set_direct_epilogue; fp32 out, no split-K; the same values bit for bit
-static int g_epi_direct = 1;
-extern "C" int mdx_conv_set_direct_epilogue(int on) {
-    const int old = g_epi_direct;
-    if (on >= 0) g_epi_direct = on;
-    return old;
-}
+// dtype codes: 0 = fp32, 1 = fp16.  Kernel choice follows the policy in
+// force on the calling thread (pol(): include/mdx.h, mdx_policy).
+//
 // LDS of a k_conv launch: stage buffers (one when the whole K is one step or
 // the single-stage instance, else two) or the half-tile fp32 epilogue image
 static size_t conv_lds(int bn, int ksteps, bool sb) {
@@ -2415,50 +1992,26 @@ static size_t conv_lds(int bn, int ksteps, bool sb) {
     const size_t epi = (size_t)(BM / 2) * (bn + 4) * 4;
     return main_ > epi ? main_ : epi;
 }
-// fp32 layers as bf16 plane products (k_conv_x3): 0 off, 6 or 9 products
-static int g_fp32_split = 0;
-extern "C" int mdx_conv_set_fp32_split(int mode) {
-    const int old = g_fp32_split;
-    if (mode == 0 || mode == 6 || mode == 9) g_fp32_split = mode;
-    return old;
-}
-extern "C" int mdx_conv_fp32_split(void) { return g_fp32_split; }
-// 64-wide N tile for every split-plane launch (72 KB of LDS and <= 256
-// registers: two workgroups per CU, measured 6-25 % faster per layer than the
-// 128-wide tile's one workgroup per CU, whose single wave per SIMD serialises
-// the split/LDS work with the MFMAs) -- default; 0: the 128-wide tile where Cout > 64
-static int g_x3_narrow = 1;
-extern "C" int mdx_conv_set_x3_narrow(int on) {
-    const int old = g_x3_narrow;
-    g_x3_narrow = on;
-    return old;
-}
 // weight planes for the next split-plane launch on this thread (set by the
 // model handle around a layer's conv call; see mdx::x3_weight_planes)
 static thread_local const void *t_x3_wplanes = nullptr;
 void mdx::x3_weight_planes(const void *planes) { t_x3_wplanes = planes; }
 
-// the single-stage split-plane instance (k_conv_x3<..., SB>) for the pre-split-weight launches
-static int g_x3_sb = 1;
-extern "C" int mdx_conv_set_x3_single_stage(int on) {
-    const int old = g_x3_sb;
-    g_x3_sb = on;
-    return old;
-}
 // launch of the split-plane fp32 kernel (LDS: double-buffered planes or the epilogue image)
 // (with weight planes pending and K % 32 == 0: the pre-split-B instance; a.w,
 // a.wbytes and a.bsw switch to the planes)
 static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
+    const mdx_policy &P = pol();
     const size_t stage = 3 * ((size_t)BM * X3_ROWB + (size_t)bn * X3_ROWB);
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * stage;
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     const bool pw = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && (long long)a.M * a.Cin * 4 < (1ll << 31);
-    if (t_x3_wplanes && g_fp32_split == 6 && a.K % 32 == 0 && (long long)a.Cout * a.K * 6 < (1ll << 31)) {
+    if (t_x3_wplanes && P.fp32_split == 6 && a.K % 32 == 0 && (long long)a.Cout * a.K * 6 < (1ll << 31)) {
         a.bsw = a.bsw / 4 * 6;
         a.w = t_x3_wplanes;
         a.wbytes = a.Cout * a.K * 6;
-        if (bn == 64 && g_x3_sb) {
+        if (bn == 64 && P.x3_single_stage) {
             // one LDS stage: the stage or the epilogue image
             const size_t lds1 = stage > lds_epi ? stage : lds_epi;
             if (pw)
@@ -2477,48 +2030,21 @@ static void launch_x3(ConvArgs a, int bn, dim3 grid, hipStream_t s) {
             hipLaunchKernelGGL((k_conv_x3<float, 128, 6, true>), grid, dim3(CONV_THREADS), lds, s, a);
         return;
     }
-    if (bn == 64 && pw && g_fp32_split == 6) {
+    if (bn == 64 && pw && P.fp32_split == 6) {
         hipLaunchKernelGGL((k_conv_x3<float, 64, 6, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
         return;
     }
     if (bn == 64) {
-        if (g_fp32_split == 9)
+        if (P.fp32_split == 9)
             hipLaunchKernelGGL((k_conv_x3<float, 64, 9>), grid, dim3(CONV_THREADS), lds, s, a);
         else
             hipLaunchKernelGGL((k_conv_x3<float, 64, 6>), grid, dim3(CONV_THREADS), lds, s, a);
     } else {
-        if (g_fp32_split == 9)
+        if (P.fp32_split == 9)
             hipLaunchKernelGGL((k_conv_x3<float, 128, 9>), grid, dim3(CONV_THREADS), lds, s, a);
         else
             hipLaunchKernelGGL((k_conv_x3<float, 128, 6>), grid, dim3(CONV_THREADS), lds, s, a);
     }
-}
-// s_setprio(1) around the MFMA bursts of the 256x256 kernel (0/1)
-static int g_prio8 = 0;
-extern "C" int mdx_conv_set_mfma_prio256(int on) {
-    const int old = g_prio8;
-    g_prio8 = on;
-    return old;
-}
-extern "C" int mdx_conv_set_mfma_prio(int on) {
-    const int old = g_prio;
-    g_prio = on;
-    return old;
-}
-extern "C" int mdx_conv_set_dma128(int mode, int min_tiles) {
-    const int old = g_dma128;
-    g_dma128 = mode;
-    g_dma128_min_tiles = min_tiles;
-    return old;
-}
-// layers with K <= g_narrow_kmax use the 64-wide N tile (4 workgroups per CU:
-// the HBM-bound small-K 1x1 convs need the memory parallelism more than the
-// wider tile's A-operand reuse)
-static int g_narrow_kmax = 128;
-extern "C" int mdx_conv_set_narrow_kmax(int kmax) {
-    const int old = g_narrow_kmax;
-    if (kmax >= 0) g_narrow_kmax = kmax;
-    return old;
 }
 
 // resident workgroups the split-K model assumes for the register-staged
@@ -2561,6 +2087,7 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
                                  int out_mode, int in_dtype, int out_dtype, void *out, int ksplit, void *workspace,
                                  int64_t workspace_bytes, mdx_stream_t stream) {
     MDX_REQUIRE(x && w && out, "mdx_conv2d: null pointer");
+    const mdx_policy &P = pol();
     MDX_REQUIRE(in_dtype == 0 || in_dtype == 1, "mdx_conv2d: in_dtype must be 0 (f32) or 1 (f16)");
     MDX_REQUIRE(out_dtype == 0 || out_dtype == 1, "mdx_conv2d: out_dtype must be 0 (f32) or 1 (f16)");
     const int VEC = in_dtype == 1 ? 8 : 4;
@@ -2593,7 +2120,7 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     a.out_mode = out_mode;
     hipStream_t s = as_stream(stream);
     // fp32 narrow-output 1x1 layers (RPN / mask / box predictors)
-    if (g_head_f32 && in_dtype == 0 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+    if (P.head_f32 && in_dtype == 0 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
         pad == 0 && !residual && Cout <= 16 && Cin % 16 == 0 && Cin <= 1024 && (ksplit == 1 || ksplit == 0)) {
         a.tiles_n = 1;
         a.tiles_total = 1;
@@ -2615,7 +2142,7 @@ extern "C" int mdx_conv2d_splitk(const void *x, int N, int H, int W, int Cin, co
     }
 general:
     // HBM-bound 1x1 layers: the streaming kernel
-    if (g_stream1x1 && in_dtype == 1 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+    if (P.stream1x1 && in_dtype == 1 && out_dtype == 0 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
         pad == 0 && !residual && (Cin == 64 || Cin == 128 || Cin == 256) && Cout <= 16 && (ksplit == 1 || ksplit == 0)) {
         a.tiles_n = 1;
         a.tiles_total = (int)ceil_div(M, 128);
@@ -2631,9 +2158,9 @@ general:
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
-    if (g_stream1x1 && in_dtype == 1 && out_dtype == 1 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
-        pad == 0 && (Cin == 64 || Cin == 128 || (Cin == 256 && (Cout == 64 || g_stream1x1 == 2))) && Cout % 64 == 0 &&
-        (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m) {
+    if (P.stream1x1 && in_dtype == 1 && out_dtype == 1 && out_mode == 0 && KH == 1 && KW == 1 && stride == 1 &&
+        pad == 0 && (Cin == 64 || Cin == 128 || (Cin == 256 && (Cout == 64 || P.stream1x1 == 2))) && Cout % 64 == 0 &&
+        (ksplit == 1 || ksplit == 0) && M >= P.stream1x1_min_m) {
         // (K = 256 with Cout > 64 stays on the 256x256 kernel: measured faster)
         a.tiles_n = Cout / 64;
         a.tiles_total = (int)(ceil_div(M, 128) * a.tiles_n);
@@ -2649,39 +2176,21 @@ general:
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
-    if (g_stream1x1_f32 && in_dtype == 0 && out_dtype == 0 && !g_fp32_split && out_mode == 0 && KH == 1 &&
-        KW == 1 && stride == 1 && pad == 0 &&
-        (Cin == 64 || (g_stream1x1_f32 == 2 && (Cin == 128 || Cin == 256))) && Cout % 64 == 0 &&
-        (ksplit == 1 || ksplit == 0) && M >= g_stream_min_m) {
-        a.tiles_n = Cout / 64;
-        a.tiles_total = (int)(ceil_div(M, 128) * a.tiles_n);
-        a.ksplit = 1;
-        if (Cin == 64)
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<4>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        else if (Cin == 128)
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<8>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_conv1x1_stream_f32<16>, dim3(a.tiles_total), dim3(256), 0, s, a);
-        t_plan_kernel = MDX_CONV_KERNEL_STREAM1X1;
-        t_plan_ksplit = 1;
-        MDX_CHECK_LAUNCH("mdx_conv2d");
-        return MDX_OK;
-    }
     // fp16 layers with Cin % 64 == 0: the LDS-DMA pipelined kernels -- the
     // 128x128 tile (DMA pieces interleaved with the MFMAs) for layers with
     // many tiles, the 256x256 tile by policy, else the register-staged kernel
     // (with split-K) below, which serves the small grids better
     // fp32 operands (Cin % 32 == 0, fp32 out): the 256x256 kernel on 16x16x4 f32
     // MFMAs, same LDS image (64-B rows of 16 floats)
-    const bool x3 = in_dtype == 0 && out_dtype == 0 && g_fp32_split;
+    const bool x3 = in_dtype == 0 && out_dtype == 0 && P.fp32_split;
     // (mode 4: as 2, also while the split-plane mode routes the other fp32
     // layers to k_conv_x3 -- a diagnostic for kernel-level A/B runs)
-    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && g_dma_f32 && (!x3 || g_dma_f32 == 4);
+    const bool dma_f32 = in_dtype == 0 && out_dtype == 0 && Cin % 32 == 0 && P.dma_f32 && (!x3 || P.dma_f32 == 4);
     if (((in_dtype == 1 && Cin % 64 == 0) || dma_f32) && (ksplit == 1 || ksplit == 0) &&
-        KH * KW * Cin > g_narrow_kmax) {
+        KH * KW * Cin > P.narrow_kmax) {
         const int subk = in_dtype == 1 ? 32 : 16;  // K elements per 64-B substep
         const long long t128 = ceil_div(M, 128) * ceil_div(Cout, 128);
-        if (in_dtype == 0 && g_dma_f32 == 1 && Cout > 64 && (g_large_tiles == 2 || t128 >= 512)) {
+        if (in_dtype == 0 && P.dma_f32 == 1 && Cout > 64 && (P.large_tiles == 2 || t128 >= 512)) {
             // fp32: the 128x128 LDS-DMA tile, two workgroups per CU (their
             // barriers interleave, so one wave's fragment reads overlap the
             // other's MFMA bursts)
@@ -2697,13 +2206,13 @@ general:
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
-        if (in_dtype == 1 && (g_dma128 == 2 || (g_dma128 == 1 && Cout > 64 && t128 >= g_dma128_min_tiles))) {
+        if (in_dtype == 1 && (P.dma128 == 2 || (P.dma128 == 1 && Cout > 64 && t128 >= P.dma128_min_tiles))) {
             using G4 = GTile<4>;
             a.tiles_n = (int)ceil_div(Cout, G4::BN);
             a.tiles_total = (int)t128;
             a.ksplit = 1;
             a.ksteps = a.K / 32;
-            if (out_dtype == 1 && g_prio)
+            if (out_dtype == 1 && P.dma128_interleave)
                 hipLaunchKernelGGL((k_convg<_Float16, _Float16, 4, true>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s, a);
             else if (out_dtype == 1)
                 hipLaunchKernelGGL((k_convg<_Float16, _Float16, 4, false>), dim3(a.tiles_total), dim3(G4::THREADS), G4::LDS, s,
@@ -2716,22 +2225,10 @@ general:
             return MDX_OK;
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && (in_dtype == 1 || g_dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 1024);
-        // split-K on the 256x256 kernel for layers with few tiles but a deep
-        // K (res4/res5 and head 3x3 convs): enough slices to fill the chip
-        int ks256 = 1;
-        if (!big && g_split256 && workspace && Cout % 256 == 0 && ksplit <= 1) {
-            const int nsub = a.K / subk;
-            for (int k = 2; k <= 8; ++k) {
-                if (nsub / k < g_split256_min_sub || (long long)k * M * Cout * 4 > workspace_bytes) break;
-                ks256 = k;
-                if (t256 * k >= 256) break;
-            }
-            if (g_split256 == 1 && t256 * ks256 < 192) ks256 = 1;  // still too few workgroups: the 128-row kernel
-        }
+        const bool big = Cout >= 192 && (in_dtype == 1 || P.dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 1024);
         // fp16: the 256x128 tile (two workgroups per CU) in place of 256x256
         // (large-tile modes 3: whenever eligible, 4: the layers mode 1 takes)
-        if (in_dtype == 1 && ks256 == 1 && (g_large_tiles == 3 || (g_large_tiles == 4 && big))) {
+        if (in_dtype == 1 && (P.large_tiles == 3 || (P.large_tiles == 4 && big))) {
             using G6 = GTile<6>;
             a.tiles_n = (int)ceil_div(Cout, G6::BN);
             a.tiles_total = (int)(ceil_div(M, G6::BM) * a.tiles_n);
@@ -2748,43 +2245,28 @@ general:
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
-        if (g_large_tiles == 2 || g_large_tiles == 3 || ((g_large_tiles == 1 || g_large_tiles == 4) && big) ||
-            ks256 > 1) {
+        if (P.large_tiles == 2 || P.large_tiles == 3 || ((P.large_tiles == 1 || P.large_tiles == 4) && big)) {
             a.tiles_n = (int)ceil_div(Cout, G_BN);
             a.tiles_total = (int)t256;
-            a.ksplit = ks256;
-            a.ksteps = (a.K / subk + ks256 - 1) / ks256;
-            a.ksplit = (a.K / subk + a.ksteps - 1) / a.ksteps;
-            a.part = reinterpret_cast<float *>(workspace);
-            const dim3 grid256((unsigned)a.tiles_total, (unsigned)a.ksplit);
+            a.ksplit = 1;
+            a.ksteps = a.K / subk;
+            const dim3 grid256((unsigned)a.tiles_total);
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
             if (in_dtype == 0)
                 hipLaunchKernelGGL((k_convg<float, float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
-            else if (out_dtype == 1 && g_dma_after)
-                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
-            else if (out_dtype == 1 && g_prio8)
-                hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false, true>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else if (out_dtype == 1)
                 hipLaunchKernelGGL((k_convg<_Float16, _Float16, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
             else
                 hipLaunchKernelGGL((k_convg<_Float16, float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);
-            if (a.ksplit > 1) {
-                if (out_dtype == 1)
-                    hipLaunchKernelGGL((k_conv_reduce<_Float16>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)),
-                                       dim3(256), 0, s, a);
-                else
-                    hipLaunchKernelGGL((k_conv_reduce<float>), dim3((unsigned)ceil_div(M * (Cout / 8), 256)),
-                                       dim3(256), 0, s, a);
-            }
             t_plan_kernel = MDX_CONV_KERNEL_DMA256;
-            t_plan_ksplit = a.ksplit;
+            t_plan_ksplit = 1;
             MDX_CHECK_LAUNCH("mdx_conv2d");
             return MDX_OK;
         }
     }
     // 64-wide N tile: no wasted MFMA columns for 64-channel layers; more
     // workgroups per CU for the small-K layers
-    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax || (x3 && g_x3_narrow);
+    const bool narrow = Cout <= 64 || a.K <= P.narrow_kmax || (x3 && P.x3_narrow);
     const int bn = narrow ? 64 : BN;
     const int tiles_m = (int)ceil_div(M, BM), tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_n = tiles_n;
@@ -2799,7 +2281,7 @@ general:
     a.ksteps = (nk + ksplit - 1) / ksplit;
     a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
     a.part = reinterpret_cast<float *>(workspace);
-    a.epi_direct = g_epi_direct && out_dtype == 0;
+    a.epi_direct = P.direct_epilogue && out_dtype == 0;
     // stage buffers: one when the whole K is one step, else two; epilogue
     // image: half the tile in fp32
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
@@ -2814,29 +2296,17 @@ general:
         MDX_CHECK_LAUNCH("mdx_conv2d");
         return MDX_OK;
     }
-    const bool pw = g_pw && KH == 1 && KW == 1 && pad == 0;
+    const bool pw = P.pointwise && KH == 1 && KW == 1 && pad == 0;
     // (mode 3: the fp16 register-staged PW layers too; the fp16 model's big
     // layers stay on the LDS-DMA kernels)
     // (mode 4: as 3, plus the fp16 KxK layers the LDS-DMA kernels do not take)
-    const bool sb = g_conv_sb && ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 3 && in_dtype == 1 && out_dtype == 1));
-    const bool sbg = g_conv_sb >= 2 && !pw &&
-                     ((in_dtype == 0 && out_dtype == 0) || (g_conv_sb >= 4 && in_dtype == 1 && out_dtype == 1));
-    // (k_conv_hb: fp32 in and out, PW; the 64-wide tile at mode 2)
-    const bool hb = g_conv_hb && pw && sb && in_dtype == 0 && out_dtype == 0 && (!narrow || g_conv_hb >= 2);
+    const bool sb = P.single_stage && ((in_dtype == 0 && out_dtype == 0) || (P.single_stage >= 3 && in_dtype == 1 && out_dtype == 1));
+    const bool sbg = P.single_stage >= 2 && !pw &&
+                     ((in_dtype == 0 && out_dtype == 0) || (P.single_stage >= 4 && in_dtype == 1 && out_dtype == 1));
 #define MDX_LAUNCH_CONV(TI_, TO_)                                                                           \
     do {                                                                                                    \
         const dim3 grid(a.tiles_total, a.ksplit);                                                           \
-        if (hb && narrow)                                                                                   \
-            hipLaunchKernelGGL((k_conv_hb<TO_, 64>), grid, dim3(CONV_THREADS), hb_lds(64), s, a);            \
-        else if (hb)                                                                                        \
-            hipLaunchKernelGGL((k_conv_hb<TO_, 128>), grid, dim3(CONV_THREADS), hb_lds(128), s, a);          \
-        else if (narrow && pw && sb && g_sb_afp)                                                            \
-            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64, false, true>), grid, dim3(CONV_THREADS),             \
-                               conv_lds(64, a.ksteps, true), s, a);                                         \
-        else if (!narrow && pw && sb && g_sb_afp)                                                           \
-            hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 128, false, true>), grid, dim3(CONV_THREADS),            \
-                               conv_lds(128, a.ksteps, true), s, a);                                        \
-        else if (narrow && pw && sb)                                                                        \
+        if (narrow && pw && sb)                                                                             \
             hipLaunchKernelGGL((k_conv_sb<TI_, TO_, 64>), grid, dim3(CONV_THREADS),          \
                                conv_lds(64, a.ksteps, true), s, a);                                         \
         else if (!narrow && pw && sb)                                                                       \
@@ -2869,8 +2339,7 @@ general:
     else
         MDX_LAUNCH_CONV(float, _Float16);
 #undef MDX_LAUNCH_CONV
-    t_plan_kernel = hb ? (narrow ? MDX_CONV_KERNEL_HB64 : MDX_CONV_KERNEL_HB128) :
-                    narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64)
+    t_plan_kernel = narrow ? (pw ? (sb ? MDX_CONV_KERNEL_SB64 : MDX_CONV_KERNEL_PW64)
                                  : (sbg ? MDX_CONV_KERNEL_SBG64 : MDX_CONV_KERNEL_REG64))
                            : (pw ? (sb ? MDX_CONV_KERNEL_SB128 : MDX_CONV_KERNEL_PW128)
                                  : (sbg ? MDX_CONV_KERNEL_SBG128 : MDX_CONV_KERNEL_REG128));
@@ -2930,6 +2399,7 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
                                int stride2, const void *w, const float *bias, int Cout, int relu, int dtype, void *out,
                                void *workspace, int64_t workspace_bytes, mdx_stream_t stream) {
     MDX_REQUIRE(x && x2 && w && out, "mdx_conv2d_dual: null pointer");
+    const mdx_policy &P = pol();
     MDX_REQUIRE(dtype == 0 || dtype == 1, "mdx_conv2d_dual: dtype must be 0 (f32) or 1 (f16)");
     const int BKd = dtype == 1 ? 64 : 32;
     MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0 && stride2 > 0 && Cin > 0 && Cin2 > 0,
@@ -2953,7 +2423,7 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
     a.relu = relu;
     a.out_mode = 0;
     a.x2 = x2; a.K1 = Cin; a.H2 = H2; a.W2 = W2; a.Cin2 = Cin2; a.stride2 = stride2; a.x2bytes = (int)x2b;
-    const bool narrow = Cout <= 64 || a.K <= g_narrow_kmax;
+    const bool narrow = Cout <= 64 || a.K <= P.narrow_kmax;
     const int bn = narrow ? 64 : BN;
     a.tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_total = (int)(ceil_div(M, BM) * a.tiles_n);
@@ -2963,13 +2433,13 @@ extern "C" int mdx_conv2d_dual(const void *x, int N, int H, int W, int Cin, cons
     a.ksteps = (nk + ksplit - 1) / ksplit;
     a.ksplit = (nk + a.ksteps - 1) / a.ksteps;
     a.part = reinterpret_cast<float *>(workspace);
-    a.epi_direct = g_epi_direct && dtype == 0;
+    a.epi_direct = P.direct_epilogue && dtype == 0;
     const size_t lds_main = (a.ksteps == 1 ? 1 : 2) * ((size_t)BM * PITCH + (size_t)bn * PITCH);
     const size_t lds_epi = (size_t)(BM / 2) * (bn + 4) * 4;
     const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
     hipStream_t s = as_stream(stream);
     const dim3 grid(a.tiles_total, a.ksplit);
-    const bool sb = dtype == 0 && g_conv_sb;
+    const bool sb = dtype == 0 && P.single_stage;
     if (dtype == 0) {
         if (narrow && sb)
             hipLaunchKernelGGL((k_conv_sb<float, float, 64, true>), grid, dim3(CONV_THREADS),
@@ -3009,41 +2479,6 @@ extern "C" int mdx_conv2d_last_plan(int *kernel, int *ksplit) {
 // ---------------------------------------------------------------------------
 // Winograd F(m x m, 3x3) host side
 // ---------------------------------------------------------------------------
-// Winograd input transform with two channels per thread (k_wino_in2, 1) or
-// one (k_wino_in, 0) -- mdx_conv_set_wino_in2; same values bit for bit
-static int g_wino_in2 = 0;
-extern "C" int mdx_conv_set_wino_in2(int on) {
-    const int old = g_wino_in2;
-    if (on >= 0) g_wino_in2 = on;
-    return old;
-}
-static int g_winograd = 6;
-extern "C" int mdx_conv_set_winograd(int mode) {
-    const int old = g_winograd;
-    g_winograd = mode;
-    return old;
-}
-extern "C" int mdx_conv_winograd_enabled(void) { return g_winograd; }
-// the model handle uses Winograd for layers with Cin >= this (64: with the
-// F(6,3) tiles res2's 64-channel 3x3 layers gain too, 288 -> 259 us each; the
-// transforms' traffic outweighs the saved multiplies on thinner layers)
-static int g_wino_min_cin = 64;
-extern "C" int mdx_conv_set_winograd_min_cin(int c) {
-    const int old = g_wino_min_cin;
-    g_wino_min_cin = c;
-    return old;
-}
-extern "C" int mdx_conv_winograd_min_cin(void) { return g_wino_min_cin; }
-// Winograd GEMMs on the 256x256 LDS-DMA fp32 kernel: 0 never, 1 when the
-// batched launch has at least min_wgs workgroups, 2 whenever eligible; off by
-// default (measured no faster than k_conv<128> on the p2 / p3 layers)
-static int g_wino_dma = 0, g_wino_dma_min_wgs = 384;
-extern "C" int mdx_conv_set_winograd_dma(int mode, int min_wgs) {
-    const int old = g_wino_dma;
-    g_wino_dma = mode;
-    g_wino_dma_min_wgs = min_wgs;
-    return old;
-}
 
 extern "C" int mdx_winograd_weights(const float *w, int Cout, int Cin, int m, float *U) {
     MDX_REQUIRE(w && U && Cout > 0 && Cin > 0 && (m == 2 || m == 4 || m == 6), "mdx_winograd_weights: bad args");
@@ -3134,6 +2569,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
                          const float *bias, int Cout, int relu, int m, float *out, void *workspace,
                          int64_t workspace_bytes, mdx_stream_t stream) {
     MDX_REQUIRE(x && U && out && workspace, "mdx_conv3x3_winograd: null pointer");
+    const mdx_policy &P = pol();
     MDX_REQUIRE(m == 2 || m == 4 || m == 6, "mdx_conv3x3_winograd: tile m must be 2, 4 or 6");
     MDX_REQUIRE(N > 0 && H > 0 && W > 0 && Cin % 4 == 0 && Cout % 8 == 0,
                 "mdx_conv3x3_winograd: Cin %% 4 == 0 and Cout %% 8 == 0 required");
@@ -3149,7 +2585,7 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     hipStream_t s = as_stream(stream);
     // split-plane mode with the U planes: V written as planes, the NB GEMMs on
     // the 256 x 256 LDS-DMA plane kernel
-    const bool planes = Up && g_fp32_split == 6 && Cin % 16 == 0 &&
+    const bool planes = Up && P.fp32_split == 6 && Cin % 16 == 0 &&
                         T * Cin * 6 < (1ll << 31) && (long long)Cout * Cin * 6 < (1ll << 31);
     WinoProbe *probe = t_wino_probe;
     float *V = reinterpret_cast<float *>(workspace);
@@ -3174,10 +2610,6 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             hipLaunchKernelGGL(k_wino_in_x6<4>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
         else
             hipLaunchKernelGGL(k_wino_in_x6<6>, grid, dim3(bd), 0, s, x, N, H, W, Cin, TH, TW, Vp);
-    } else if (g_wino_in2 && Cin % 2 == 0) {
-        unsigned bd;
-        const dim3 grid = tgrid(Cin / 2, bd);
-        mdx::launch_wino_in2(m, grid, bd, s, x, N, H, W, Cin, TH, TW, V);
     } else {
         unsigned bd;
         const dim3 grid = tgrid(Cin, bd);
@@ -3202,8 +2634,8 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     a.bsx = T * Cin * 4;
     a.bsw = (long long)Cout * Cin * 4;
     a.bso = T * Cout * 4;
-    a.epi_direct = g_epi_direct;
-    const int bn = Cout <= 64 || (g_fp32_split && g_x3_narrow) ? 64 : BN;
+    a.epi_direct = P.direct_epilogue;
+    const int bn = Cout <= 64 || (P.fp32_split && P.x3_narrow) ? 64 : BN;
     a.tiles_n = (int)ceil_div(Cout, bn);
     a.tiles_total = (int)(ceil_div(T, BM) * a.tiles_n);
     const int nk = (Cin + 31) / 32;
@@ -3216,8 +2648,8 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
     // the wide GEMMs (Cout a multiple of 256) on the 256x256 LDS-DMA kernel
     // when the NB batch entries give it enough workgroups
     const long long t256 = ceil_div(T, G_BM) * (Cout / G_BN);
-    const bool dma = !g_fp32_split && Cin % 32 == 0 && Cout % G_BN == 0 &&
-                     (g_wino_dma == 2 || (g_wino_dma == 1 && t256 * NB >= g_wino_dma_min_wgs));
+    const bool dma = !P.fp32_split && Cin % 32 == 0 && Cout % G_BN == 0 &&
+                     (P.winograd_dma == 2 || (P.winograd_dma == 1 && t256 * NB >= P.winograd_dma_min_wgs));
     if (planes) {
         a.x = workspace;
         a.w = Up;
@@ -3236,25 +2668,15 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
         hipLaunchKernelGGL((k_convg<float, float, 8, false>), dim3((unsigned)t256, 1, (unsigned)NB), dim3(G_THREADS),
                            G_LDS, s, a);
         gemm_kernel = MDX_CONV_KERNEL_DMA256;
-    } else if (g_fp32_split) {
+    } else if (P.fp32_split) {
         launch_x3(a, bn, grid, s);
         gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_X3_64 : MDX_CONV_KERNEL_X3_128;
-    } else if (g_pw && g_conv_sb && g_conv_hb && (bn == 128 || g_conv_hb >= 2)) {
-        if (bn == 64)
-            hipLaunchKernelGGL((k_conv_hb<float, 64>), grid, dim3(CONV_THREADS), hb_lds(64), s, a);
-        else
-            hipLaunchKernelGGL((k_conv_hb<float, 128>), grid, dim3(CONV_THREADS), hb_lds(128), s, a);
-        gemm_kernel = bn == 64 ? MDX_CONV_KERNEL_HB64 : MDX_CONV_KERNEL_HB128;
     } else if (bn == 64) {
-        if (g_pw && g_conv_sb && g_sb_afp) {
-            hipLaunchKernelGGL((k_conv_sb<float, float, 64, false, true>), grid, dim3(CONV_THREADS),
-                               conv_lds(64, a.ksteps, true), s, a);
-            gemm_kernel = MDX_CONV_KERNEL_SB64;
-        } else if (g_pw && g_conv_sb) {
+        if (P.pointwise && P.single_stage) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 64>), grid, dim3(CONV_THREADS),
                                conv_lds(64, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB64;
-        } else if (g_pw) {
+        } else if (P.pointwise) {
             hipLaunchKernelGGL((k_conv<float, float, 64, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
             gemm_kernel = MDX_CONV_KERNEL_PW64;
         } else {
@@ -3262,15 +2684,11 @@ static int winograd_impl(const float *x, int N, int H, int W, int Cin, const flo
             gemm_kernel = MDX_CONV_KERNEL_REG64;
         }
     } else {
-        if (g_pw && g_conv_sb && g_sb_afp) {
-            hipLaunchKernelGGL((k_conv_sb<float, float, 128, false, true>), grid, dim3(CONV_THREADS),
-                               conv_lds(128, a.ksteps, true), s, a);
-            gemm_kernel = MDX_CONV_KERNEL_SB128;
-        } else if (g_pw && g_conv_sb) {
+        if (P.pointwise && P.single_stage) {
             hipLaunchKernelGGL((k_conv_sb<float, float, 128>), grid, dim3(CONV_THREADS),
                                conv_lds(128, a.ksteps, true), s, a);
             gemm_kernel = MDX_CONV_KERNEL_SB128;
-        } else if (g_pw) {
+        } else if (P.pointwise) {
             hipLaunchKernelGGL((k_conv<float, float, 128, false, true>), grid, dim3(CONV_THREADS), lds, s, a);
             gemm_kernel = MDX_CONV_KERNEL_PW128;
         } else {

@@ -58,7 +58,7 @@ struct ConvW {
     // winox6[m / 2 - 1] for F(m x m, 3x3)
     void *winox6[3] = {nullptr, nullptr, nullptr};
     // fp32 Linear layers: the weights split once into bf16 planes for
-    // mdx_gemm_x6 (used while mdx_conv_fp32_split() != 0)
+    // mdx_gemm_x6 (used while mdx_policy.fp32_split != 0)
     void *x6 = nullptr;
     // fp32 conv layers of split-plane handles (KH*KW*Cin % 32 == 0): the OHWI
     // weights as bf16 planes, k_conv_x3's pre-split B operand
@@ -74,7 +74,7 @@ struct Block {
     bool has_sc;
     ConvW sc, c1, c2, c3;
     // conv3 and the projection shortcut as one GEMM over K = Cin3 + Cin_sc
-    // (mdx_conv2d_dual; packed when mdx_model_set_fuse_shortcut is on)
+    // (mdx_conv2d_dual; packed when mdx_policy.fuse_shortcut is on)
     ConvW c3sc;
 };
 
@@ -118,8 +118,10 @@ struct Model {
     // the Winograd policy and fp32 split mode the weights were prepared for
     // (Winograd U tiles, bf16 planes): a later switch runs the layers it did
     // not prepare on the fallback kernels, reported once
-    int create_wino = 0, create_split = 0;
-    std::atomic<bool> policy_warned{false};
+    // the kernel-selection policy of this handle (captured from the creating
+    // thread at mdx_model_create; installed on the calling thread by every
+    // entry point that packs or runs the forward, PolicyScope)
+    mdx_policy policy{};
     size_t es = 4;     // activation element size
     std::vector<void *> allocs;
     ConvW stem;
@@ -277,10 +279,10 @@ struct Packer {
     // size that was not packed runs those layers direct.
     int map_hw = 0;
     bool want_tile(int m_) const {
-        const int pol = mdx_conv_winograd_enabled();
-        if (pol == 0) return false;
-        if (map_hw > 0) return mdx_winograd_tile(map_hw, map_hw, pol) == m_;
-        return pol == 6 ? (m_ == 4 || m_ == 6) : pol == m_;
+        const int wp = pol().winograd;
+        if (wp == 0) return false;
+        if (map_hw > 0) return mdx_winograd_tile(map_hw, map_hw, wp) == m_;
+        return wp == 6 ? (m_ == 4 || m_ == 6) : wp == m_;
     }
     // OIHW (optionally scaled per output channel) -> [Cout][KH][KW][Cin]
     ConvW conv(const HostT *w, const float *scale, const std::vector<float> *bias, int stride, int pad) {
@@ -307,7 +309,7 @@ struct Packer {
         c.stride = stride;
         c.pad = pad;
         c.dt = cur_dt;
-        if (cur_dt == 0 && mdx_conv_fp32_split() == 6 && ((size_t)kh * kw * ci) % 32 == 0 && c.w && err.empty()) {
+        if (cur_dt == 0 && pol().fp32_split == 6 && ((size_t)kh * kw * ci) % 32 == 0 && c.w && err.empty()) {
             c.wp = split_planes((const float *)c.w, co, kh * kw * ci);
             if (!c.wp) return c;
         }
@@ -326,7 +328,7 @@ struct Packer {
                 (m_ == 2 ? c.wino2 : m_ == 4 ? c.wino4 : c.wino6) = ud;
                 // split-plane handles: U as bf16 planes too (the pre-split B
                 // operand of k_conv_x3, or k_gemm_x6's with MDX_WINO_X6)
-                if (mdx_conv_fp32_split() == 6 && ci % 16 == 0 && ud && err.empty()) {
+                if (pol().fp32_split == 6 && ci % 16 == 0 && ud && err.empty()) {
                     c.winox6[m_ / 2 - 1] = split_planes(ud, (int64_t)nb * co, ci);
                     if (!c.winox6[m_ / 2 - 1]) break;
                 }
@@ -612,22 +614,16 @@ bool pack(Model &m, std::unordered_map<std::string, HostT> &sd, std::string &err
 }
 
 // ------------------------------------------------------------ forward
-// Winograd layers in image slices (knob, MB of transformed input per slice;
+// Winograd layers in image slices (mdx_policy.wino_slice_mb: MB of transformed input per slice;
 // 0 = the whole batch in one pass): the input transform, batched GEMM and
 // output transform of a slice then move V and M through the 256 MB Infinity
 // Cache instead of HBM.  Profiled forwards keep one pass (the probe times
 // the three launches of one call).
-static int g_wino_slice_mb = 0;
-extern "C" int mdx_model_set_wino_slice(int mb) {
-    const int old = g_wino_slice_mb;
-    if (mb >= 0) g_wino_slice_mb = mb;
-    return old;
-}
 static int wino_slice_images(int N, int H, int W, int cin, int cout, int m, bool profile) {
-    if (g_wino_slice_mb <= 0 || profile) return N;
+    if (pol().wino_slice_mb <= 0 || profile) return N;
     const double tiles = (double)((H + m - 1) / m) * ((W + m - 1) / m);
     const double v = tiles * (m + 2) * (m + 2) * 4.0 * (cin > cout ? cin : cout);  // V or M bytes per image
-    const int per = (int)((double)g_wino_slice_mb * (1 << 20) / v);
+    const int per = (int)((double)pol().wino_slice_mb * (1 << 20) / v);
     return per < 1 ? 1 : (per >= N ? N : per);
 }
 
@@ -673,9 +669,9 @@ struct Fwd {
             return out;
         }
         if (!out) out = alloc((size_t)N * OH * OW * cw.cout * oes);
-        const int wm = mdx_winograd_tile(H, W, mdx_conv_winograd_enabled());
+        const int wm = mdx_winograd_tile(H, W, pol().winograd);
         const float *wu = wm == 2 ? cw.wino2 : wm == 4 ? cw.wino4 : wm == 6 ? cw.wino6 : nullptr;
-        const bool wino = wu && !residual && out_mode == 0 && cw.cin >= mdx_conv_winograd_min_cin();
+        const bool wino = wu && !residual && out_mode == 0 && cw.cin >= pol().winograd_min_cin;
         if (wino) {
             const size_t need = (size_t)mdx_winograd_workspace_bytes(N, H, W, cw.cin, cw.cout, wm);
             if (c.dry) c.wino_need = need > c.wino_need ? need : c.wino_need;
@@ -683,7 +679,7 @@ struct Fwd {
         // fp32 Linear layers in split-plane mode: activations split into bf16
         // planes, GEMM on the bf16 matrix cores (mdx_gemm_x6)
         const bool x6 = cw.x6 && cw.dt == 0 && !out_f32 && out_mode == 0 && cw.k == 1 && cw.stride == 1 &&
-                        mdx_conv_fp32_split() == 6;
+                        pol().fp32_split == 6;
         if (in_planes && !x6 && rc == MDX_OK) {
             set_error("model forward: plane input for a layer not in split-plane mode");
             rc = MDX_EINVAL;
@@ -708,14 +704,14 @@ struct Fwd {
             chk(mdx_gemm_x6(in_planes ? x : planes, cw.x6, cw.b, (int)rows, cw.cout, cw.cin, (const float *)residual, relu ? 1 : 0,
                             (float *)out, s));
         } else if (wino) {
-            const void *wx6 = mdx_conv_fp32_split() == 6 ? cw.winox6[wm / 2 - 1] : nullptr;
+            const void *wx6 = pol().fp32_split == 6 ? cw.winox6[wm / 2 - 1] : nullptr;
             if (wx6 && mdx::winograd_planes_enabled())
                 chk(mdx_conv3x3_winograd_x6((const float *)x, N, H, W, cw.cin, wu, wx6, cw.b, cw.cout, relu ? 1 : 0,
                                             wm, (float *)out, c.wino_base, (int64_t)c.wino_cap, s));
             else {
                 mdx::x3_weight_planes(wx6);  // the split-plane GEMMs take U's planes (K = Cin % 32 == 0)
                 // image slices whose transformed tensors stay in the Infinity
-                // Cache between the three launches (mdx_model_set_wino_slice)
+                // Cache between the three launches (mdx_policy.wino_slice_mb)
                 const int ns = wino_slice_images(N, H, W, cw.cin, cw.cout, wm, m.profile);
                 for (int i0 = 0; i0 < N; i0 += ns) {
                     const int n = std::min(ns, N - i0);
@@ -736,14 +732,7 @@ struct Fwd {
                      0, 0},
                     {MDX_CONV_KERNEL_WINO_OUT, 1, T, cw.cout, A * A, 4.0 * ((double)A * A * T + px) * cw.cout, 0.0, 0,
                      0}};
-                // the fused kernel (one launch, timed by ev[2] / ev[3]) is one record
-                const bool fused = probe.gemm_kernel == MDX_CONV_KERNEL_WINO_FUSED;
                 for (int q = 0; q < 3; ++q) {
-                    if (fused && q != 1) {
-                        (void)hipEventDestroy(probe.ev[2 * q]);
-                        (void)hipEventDestroy(probe.ev[2 * q + 1]);
-                        continue;
-                    }
                     c.prof.emplace_back();
                     ProfEv &p = c.prof.back();
                     p.e0 = probe.ev[2 * q];
@@ -860,7 +849,7 @@ struct Fwd {
             int h1, w1, h2, w2, h3, w3;
             const void *sc = cur;
             // (the split-plane mode runs every conv on its own kernels)
-            const bool fused = blk.c3sc.w && mdx_conv_fp32_split() == 0;
+            const bool fused = blk.c3sc.w && pol().fp32_split == 0;
             if (blk.has_sc && !fused) sc = conv(cur, B, H, W, blk.sc, false, h1, w1);
             void *t1 = conv(cur, B, H, W, blk.c1, true, h1, w1);
             void *t2 = conv(t1, B, h1, w1, blk.c2, true, h2, w2);
@@ -951,8 +940,8 @@ struct Fwd {
         // box head + fast_rcnn_inference
         const int R = cfg.box_pooler_resolution;
         // split-plane mode: the pooler writes fc1's A operand as bf16 planes
-        const bool pl = m.dt == 0 && !m.fc.empty() && m.fc[0].x6 && mdx_conv_fp32_split() == 6 &&
-                        (mdx_roi_align_get_mode() == 4 || mdx_roi_align_get_mode() == 5) && (R * R * C) % 16 == 0;
+        const bool pl = m.dt == 0 && !m.fc.empty() && m.fc[0].x6 && pol().fp32_split == 6 &&
+                        (pol().roi_mode == 4 || pol().roi_mode == 5) && (R * R * C) % 16 == 0;
         void *pooled = roi_align(feat, fh, fw, props, pcount, B * post, post, R, pl);
         if (pl)
             name("box_pooled", pooled, (int64_t)B * post, R * R * C / 16, 3, 16, 3);
@@ -1049,24 +1038,12 @@ int reserve(Model &m, Ctx &c, int B, int h, int w, hipStream_t s) {
 
 using namespace mdx;
 
-// fp32 handles: the stem folded to the 2-channel (value, inside) form (1,
-// default) or over the normalised 3-channel input (0); read at mdx_model_create
-// 0 off, 1 fp32 handles (default: fp32 loop +1.2 %), 2 fp32 and fp16 handles
-// (fp16 R50 B=32 +2.5 %, R101 B=64 +0.8 %, but the full-frame fp16 case then
-// passes the detection check on 25 of 32 frames, one under its 80 % bar)
-static int g_fuse_sc = 1;
-extern "C" int mdx_model_set_fuse_shortcut(int mode) {
-    const int old = g_fuse_sc;
-    g_fuse_sc = mode;
-    return old;
-}
-static int g_stem_fold = 1;
-extern "C" int mdx_model_set_stem_fold(int on) {
-    const int old = g_stem_fold;
-    g_stem_fold = on;
-    return old;
-}
-
+// mdx_policy.stem_fold: fp32 handles fold the stem to the 2-channel (value,
+// inside) form (1, default) or keep the normalised 3-channel input (0).
+// mdx_policy.fuse_shortcut: 0 off, 1 fp32 handles (default: fp32 loop
+// +1.2 %), 2 fp32 and fp16 handles (fp16 R50 B=32 +2.5 %, R101 B=64 +0.8 %,
+// but the full-frame fp16 case then passes the detection check on 25 of 32
+// frames, one under its 80 % bar).  Both are read at mdx_model_create.
 extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_model_cfg *cfg, int device,
                                 mdx_model_t *out) {
     MDX_REQUIRE(blob && cfg && out && blob_bytes >= 12, "mdx_model_create: null argument or blob shorter than its header");
@@ -1097,16 +1074,22 @@ extern "C" int mdx_model_create(const void *blob, int64_t blob_bytes, const mdx_
     m->dt = cfg->dtype;
     m->hdt = cfg->head_dtype == 1 ? 1 : cfg->dtype;
     m->es = cfg->dtype == 1 ? 2 : 4;
-    m->stem_fold = cfg->dtype == 0 && g_stem_fold;
-    m->fuse_sc = g_fuse_sc == 2 || (g_fuse_sc == 1 && cfg->dtype == 0);
-    m->create_wino = mdx_conv_winograd_enabled();
-    m->create_split = mdx_conv_fp32_split();
+    m->policy = pol();
+    PolicyScope ps(&m->policy);
+    m->stem_fold = cfg->dtype == 0 && m->policy.stem_fold;
+    m->fuse_sc = m->policy.fuse_shortcut == 2 || (m->policy.fuse_shortcut == 1 && cfg->dtype == 0);
     std::string err;
     if (!pack(*m, sd, err)) {
         set_error("mdx_model_create: %s", err.c_str());
         return MDX_EINVAL;
     }
     *out = m.release();
+    return MDX_OK;
+}
+
+extern "C" int mdx_model_get_policy(mdx_model_t model, mdx_policy *out) {
+    MDX_REQUIRE(model && out, "mdx_model_get_policy: null argument");
+    *out = ((Model *)model)->policy;
     return MDX_OK;
 }
 
@@ -1122,6 +1105,7 @@ extern "C" int mdx_model_destroy(mdx_model_t model) {
 extern "C" int mdx_model_reserve(mdx_model_t model, int B, int h, int w, mdx_stream_t stream) {
     MDX_REQUIRE(model && B > 0 && h > 0 && w > 0, "mdx_model_reserve: bad arguments");
     Model &m = *(Model *)model;
+    PolicyScope ps(&m.policy);
     hipStream_t s = as_stream(stream);
     return reserve(m, *get_ctx(m, s), B, h, w, s);
 }
@@ -1135,13 +1119,7 @@ extern "C" int mdx_model_forward(mdx_model_t model, const uint8_t *frames, int B
     MDX_REQUIRE(!out->masks || out->mask_plane_stride >= (int64_t)h * w,
                 "mdx_model_forward: mask_plane_stride < h*w");
     hipStream_t s = as_stream(stream);
-    if (m.dt == 0 && (mdx_conv_winograd_enabled() != m.create_wino || mdx_conv_fp32_split() != m.create_split) &&
-        !m.policy_warned.exchange(true))
-        fprintf(stderr,
-                "mdx_model_forward: this handle's weights were prepared for Winograd policy %d / fp32 split %d, "
-                "now %d / %d: layers without prepared weights run on the fallback kernels (create the handle "
-                "after setting the policy)\n",
-                m.create_wino, m.create_split, mdx_conv_winograd_enabled(), mdx_conv_fp32_split());
+    PolicyScope ps(&m.policy);
     Ctx &c = *get_ctx(m, s);
     const int r = reserve(m, c, B, h, w, s);
     if (r != MDX_OK) return r;
@@ -1189,13 +1167,7 @@ extern "C" int mdx_model_debug_fill(mdx_model_t model, int B, int h, int w, int 
     MDX_REQUIRE(model && byte >= 0 && byte <= 255, "mdx_model_debug_fill: bad arguments");
     Model &m = *(Model *)model;
     hipStream_t s = as_stream(stream);
-    if ((mdx_conv_winograd_enabled() != m.create_wino || mdx_conv_fp32_split() != m.create_split) &&
-        !m.policy_warned.exchange(true))
-        fprintf(stderr,
-                "mdx_model_forward: this handle's weights were prepared for Winograd policy %d / fp32 split %d, "
-                "now %d / %d: layers without prepared weights run on the fallback kernels (create the handle "
-                "after setting the policy)\n",
-                m.create_wino, m.create_split, mdx_conv_winograd_enabled(), mdx_conv_fp32_split());
+    PolicyScope ps(&m.policy);
     Ctx &c = *get_ctx(m, s);
     const int r = reserve(m, c, B, h, w, s);
     if (r != MDX_OK) return r;

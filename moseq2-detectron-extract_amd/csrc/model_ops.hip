@@ -510,7 +510,7 @@ constexpr int TOPK_THREADS = 1024, TOPK_MAX = 1024;
 // the head tensor (every pass re-reads it), the ties taken in index order,
 // bitonic sort, decode.  The default path splits the segment over RPN_SLICES
 // workgroups (k_rpn_part / k_rpn_merge_topk below); this one serves
-// mdx_rpn_set_sliced(0) and segments above RPN_SLICES * PART_KPT *
+// mdx_policy.rpn_sliced = 0 and segments above RPN_SLICES * PART_KPT *
 // TOPK_THREADS anchors.
 __global__ __launch_bounds__(TOPK_THREADS) void k_rpn_topk(RpnLevels rl, float *__restrict__ ws_boxes,
                                                            float *__restrict__ ws_scores, int *__restrict__ ws_valid,
@@ -1709,24 +1709,6 @@ __global__ __launch_bounds__(256) void k_roi_order(RoiLevels rl, const float *__
     }
 }
 
-static int g_roi_mode = 4, g_roi_xcd = 1, g_roi_sorted = 1;
-extern "C" int mdx_roi_align_get_mode(void) { return g_roi_mode; }
-extern "C" int mdx_roi_align_set_sorted(int on) {
-    const int old = g_roi_sorted;
-    g_roi_sorted = on;
-    return old;
-}
-extern "C" int mdx_roi_align_set_order(int xcd_remap) {
-    const int old = g_roi_xcd;
-    g_roi_xcd = xcd_remap;
-    return old;
-}
-extern "C" int mdx_roi_align_set_mode(int mode) {
-    const int old = g_roi_mode;
-    g_roi_mode = mode;
-    return old;
-}
-
 // ---------------------------------------------------------------------------
 // box head post-process (fast_rcnn_inference_single_image + detector_postprocess)
 // ---------------------------------------------------------------------------
@@ -2170,12 +2152,6 @@ extern "C" int64_t mdx_rpn_workspace_bytes(int B, int L, int pre_topk) {
 }
 
 // RPN top-k: several workgroups per (image, level) (1, default) or one (0)
-static int g_rpn_sliced = 1;
-extern "C" int mdx_rpn_set_sliced(int on) {
-    const int old = g_rpn_sliced;
-    g_rpn_sliced = on;
-    return old;
-}
 
 extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, const int *lvl_w, const int *strides,
                                  int L, int B, int A, const float *cell_anchors, float offset, int img_h, int img_w,
@@ -2218,7 +2194,7 @@ extern "C" int mdx_rpn_proposals(const float *const *head, const int *lvl_h, con
     hipStream_t s = as_stream(stream);
     int nmax = 0;
     for (int l = 0; l < L; ++l) nmax = std::max(nmax, lvl_h[l] * lvl_w[l] * A);
-    if (g_rpn_sliced && nmax <= RPN_SLICES * PART_KPT * TOPK_THREADS) {
+    if (pol().rpn_sliced && nmax <= RPN_SLICES * PART_KPT * TOPK_THREADS) {
         hipLaunchKernelGGL(k_rpn_part, dim3(RPN_SLICES, (unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount);
         hipLaunchKernelGGL(k_rpn_merge_topk, dim3((unsigned)segs), dim3(TOPK_THREADS), 0, s, rl, wcand, wccount, wb, wsc,
                            wv, wk);
@@ -2264,19 +2240,19 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
     }
     rl.L = L; rl.min_level = min_level; rl.C = C; rl.P = P; rl.sampling = sampling; rl.aligned = aligned;
     rl.per_image = per_image; rl.canonical_size = canonical_size; rl.canonical_level = canonical_level;
-    rl.xcd_remap = g_roi_xcd;
+    rl.xcd_remap = pol().roi_xcd_order;
     rl.order = nullptr;
     // dtype 2: fp32 features, output rows as bf16 planes (mdx_split_x6 layout,
     // the A operand of mdx_gemm_x6); separable kernels only
     rl.planes = dtype == 2;
-    MDX_REQUIRE(dtype != 2 || ((g_roi_mode >= 4 && g_roi_mode <= 7) && P <= ROI_PMAX && (P * P * C) % 16 == 0),
+    MDX_REQUIRE(dtype != 2 || ((pol().roi_mode >= 4 && pol().roi_mode <= 7) && P <= ROI_PMAX && (P * P * C) % 16 == 0),
                 "mdx_roi_align: plane output (dtype 2) needs the separable kernel and P*P*C %% 16 == 0");
-    if (order_ws && g_roi_sorted) {
+    if (order_ws && pol().roi_sorted) {
         hipLaunchKernelGGL(k_roi_order, dim3(R / per_image), dim3(256), 0, as_stream(stream), rl, rois, counts,
                            order_ws);
         rl.order = order_ws;
     }
-    if (((g_roi_mode == 6 && R >= 1024) || g_roi_mode == 7) && P <= ROI_PMAX) {
+    if (((pol().roi_mode == 6 && R >= 1024) || pol().roi_mode == 7) && P <= ROI_PMAX) {
         // the box pooler (mode 6; 7: any ROI count, tests): each ROI's sample
         // window staged in LDS per channel slice
         if (dtype == 1)
@@ -2285,14 +2261,14 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
         else
             hipLaunchKernelGGL((k_roi_align_sep<float, false, true>), dim3(R), dim3(256), 0, as_stream(stream), rl,
                                rois, counts, (float *)out);
-    } else if (g_roi_mode == 5 && P <= ROI_PMAX) {
+    } else if (pol().roi_mode == 5 && P <= ROI_PMAX) {
         if (dtype == 1)
             hipLaunchKernelGGL((k_roi_align_sep<_Float16, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (_Float16 *)out);
         else
             hipLaunchKernelGGL((k_roi_align_sep<float, true>), dim3(R), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (float *)out);
-    } else if ((g_roi_mode == 4 || g_roi_mode == 6) && P <= ROI_PMAX) {
+    } else if ((pol().roi_mode == 4 || pol().roi_mode == 6) && P <= ROI_PMAX) {
         // few ROIs (mask / keypoint heads: B x D): split each ROI's items over
         // up to 4 workgroups so the grid covers the CUs
         const int split = R >= 1024 ? 1 : (R >= 512 ? 2 : 4);
@@ -2302,7 +2278,7 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
         else
             hipLaunchKernelGGL(k_roi_align_sep<float>, dim3(R, split), dim3(256), 0, as_stream(stream), rl, rois,
                                counts, (float *)out);
-    } else if (g_roi_mode >= 1 && g_roi_mode <= 4) {
+    } else if (pol().roi_mode >= 1 && pol().roi_mode <= 4) {
 #define MDX_ROI_FULL(NI_)                                                                                     \
     do {                                                                                                      \
         if (dtype == 1)                                                                                       \
@@ -2312,9 +2288,9 @@ extern "C" int mdx_roi_align_ex(const void *const *feats, const int *fh, const i
             hipLaunchKernelGGL((k_roi_align_full<float, NI_>), dim3(R), dim3(256), 0, as_stream(stream), rl,    \
                                rois, counts, (float *)out);                                                   \
     } while (0)
-        if (g_roi_mode == 1)
+        if (pol().roi_mode == 1)
             MDX_ROI_FULL(1);
-        else if (g_roi_mode == 2)
+        else if (pol().roi_mode == 2)
             MDX_ROI_FULL(2);
         else
             MDX_ROI_FULL(4);

@@ -34,7 +34,8 @@ class Predictor:
 
     @classmethod
     def from_config(cls, cfg: Union[ModelConfig, str, dict], weights: Union[None, str, dict] = None,
-                    dtype: str = "fp32", device="cuda", seed: int = 0) -> "Predictor":
+                    dtype: str = "fp32", device="cuda", seed: int = 0,
+                    policy: Optional[dict] = None) -> "Predictor":
         """The reference constructor (M/model/predict.py:31-44): build the
         model of `cfg`, load ``cfg.MODEL.WEIGHTS`` and check the input format.
 
@@ -46,9 +47,10 @@ class Predictor:
         ``"synthetic"`` selects seeded synthetic weights of this architecture
         (benchmarks and tests: no trained checkpoint exists offline).  The
         state dict must carry every parameter of the configuration with its
-        shape (weights.check_state_dict)."""
+        shape (weights.check_state_dict).  policy: kernel-selection policy
+        fields for this predictor's model handle (MaskRCNN)."""
         cfg, sd = resolve_model(cfg, weights, seed)
-        return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype))
+        return cls(MaskRCNN(cfg, sd, device=device, dtype=dtype, policy=policy))
 
     @classmethod
     def from_model_dir(cls, model_dir: str, checkpoint: Union[str, int] = "last", instance_threshold: float = 0.5,

@@ -23,7 +23,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from .._lib import MdxError, call, lib
+from .._lib import MdxError, Policy, call, lib, policy_scope
 from .config import ModelConfig
 from .weights import pack_blob, resnet_stage_specs
 
@@ -123,9 +123,13 @@ def model_cfg_c(cfg: ModelConfig, dtype: str) -> ModelCfgC:
 
 class MaskRCNN:
     """The reference model on one GPU behind the libmdx model handle
-    (mdx_model_create / mdx_model_forward / mdx_model_destroy)."""
+    (mdx_model_create / mdx_model_forward / mdx_model_destroy).  `policy`:
+    fields of the kernel-selection policy (include/mdx.h mdx_policy) this
+    handle runs with, over the calling thread's; the handle captures it at
+    creation, so handles with different policies run side by side."""
 
-    def __init__(self, cfg: ModelConfig, state_dict: Dict[str, torch.Tensor], device="cuda", dtype: str = "fp32"):
+    def __init__(self, cfg: ModelConfig, state_dict: Dict[str, torch.Tensor], device="cuda", dtype: str = "fp32",
+                 policy: Optional[dict] = None):
         if not torch.cuda.is_available():
             raise MdxError("MaskRCNN needs an AMD GPU; there is no CPU fallback")
         if dtype not in _DT:
@@ -141,9 +145,16 @@ class MaskRCNN:
         self._ccfg = model_cfg_c(cfg, dtype)
         blob = pack_blob(state_dict)
         h = ctypes.c_void_p()
-        call("mdx_model_create", blob, len(blob), ctypes.byref(self._ccfg), self.device.index, ctypes.byref(h))
+        with policy_scope(**(policy or {})):
+            call("mdx_model_create", blob, len(blob), ctypes.byref(self._ccfg), self.device.index, ctypes.byref(h))
         self._h = h
         self._lib = lib()
+
+    def policy(self) -> dict:
+        """The kernel-selection policy this handle runs with."""
+        p = Policy()
+        call("mdx_model_get_policy", self._h, ctypes.byref(p))
+        return p.as_dict()
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -93,37 +93,37 @@ def test_winograd_weight_transform_host(mdx, m):
     assert call("mdx_winograd_tile", 112, 128, 4) == 4 and call("mdx_winograd_tile", 5, 5, 2) == 2
 
 
-def test_winograd_fused_pack_and_policy_host(mdx):
-    """mdx_winograd_pack_f4 (host): the consumer B-fragment layout of the fused
-    F(4,3) kernel -- piece (channel block, K-step, point) of 64 lanes x 4, lane
-    (n = l & 15, k-pair kp = l >> 4) holding U at (n, 2 kp), (n, 2 kp + 1),
-    (n + 16, 2 kp), (n + 16, 2 kp + 1); a permutation of U (same multiset of
-    values).  Policy: off by default, eligibility needs Cin % 8 == 0 and
-    Cout % 32 == 0, shape errors are refused."""
-    import ctypes
-    import numpy as np
-    from moseq2_detectron_extract_amd._lib import MdxError, call
-    Cout, Cin = 64, 16
-    U = np.random.default_rng(3).standard_normal((36, Cout, Cin)).astype(np.float32)
-    Up = np.empty_like(U)
-    call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), Cout, Cin, Up.ctypes.data_as(ctypes.c_void_p))
-    KS = Cin // 8
-    pieces = Up.reshape(Cout // 32, KS, 36, 64, 4)
-    for nb, ks, xi, lane in [(0, 0, 0, 0), (1, 1, 35, 63), (0, 1, 17, 21), (1, 0, 5, 40)]:
-        n, kp = lane & 15, lane >> 4
-        want = [U[xi, nb * 32 + n + 16 * (e >> 1), ks * 8 + 2 * kp + (e & 1)] for e in range(4)]
-        np.testing.assert_array_equal(pieces[nb, ks, xi, lane], want)
-    np.testing.assert_array_equal(np.sort(Up, axis=None), np.sort(U, axis=None))
-    with pytest.raises(MdxError):
-        call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), 48, Cin, Up.ctypes.data_as(ctypes.c_void_p))
-    assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 0  # default policy: off
-    old = call("mdx_conv_set_winograd_fused", 2, 0)
-    try:
-        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 1
-        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 260, 256) == 0  # Cin % 8
-        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 48) == 0   # Cout % 32
-        call("mdx_conv_set_winograd_fused", 1, 384)
-        assert call("mdx_winograd_fused_eligible", 32, 112, 128, 256, 256) == 1  # 896 blocks x 8
-        assert call("mdx_winograd_fused_eligible", 32, 7, 8, 256, 256) == 0      # 4 blocks x 8 < 384
-    finally:
-        call("mdx_conv_set_winograd_fused", old, 384)
+def test_policy_struct_matches_header():
+    """_lib.POLICY_FIELDS is include/mdx.h's mdx_policy, field for field."""
+    import re
+    from moseq2_detectron_extract_amd._lib import POLICY_FIELDS
+    hdr = open(os.path.join(ROOT, "include", "mdx.h")).read()
+    body = hdr[hdr.index("typedef struct mdx_policy {"):hdr.index("} mdx_policy;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = [f.strip() for decl in re.findall(r"\bint\s+([^;]+);", body) for f in decl.split(",")]
+    assert tuple(fields) == POLICY_FIELDS
+
+
+def test_policy_per_thread_and_validated(mdx):
+    """mdx_policy_set / get: the calling thread's policy (another thread keeps
+    the library defaults), validated fields, restored by policy_scope."""
+    import threading
+    from moseq2_detectron_extract_amd._lib import MdxError, knob, policy, policy_defaults, policy_scope, set_policy
+    d = policy_defaults()
+    assert d["winograd"] == 6 and d["fp32_split"] == 0 and d["single_stage"] == 4 and d["roi_mode"] == 4
+    assert policy() == d
+    seen = {}
+    with policy_scope(winograd=4, roi_mode=7):
+        assert policy()["winograd"] == 4 and policy()["roi_mode"] == 7
+        t = threading.Thread(target=lambda: seen.update(policy()))
+        t.start()
+        t.join()
+        assert knob("winograd", 2) == 4 and policy()["winograd"] == 2
+    assert seen == d          # the other thread: its own (default) policy
+    assert policy() == d      # restored
+    for bad in ({"winograd": 3}, {"fp32_split": 5}, {"roi_mode": 9}, {"narrow_kmax": -1}):
+        with pytest.raises(MdxError):
+            set_policy(**bad)
+    assert policy() == d
+    with pytest.raises(KeyError):
+        set_policy(no_such_field=1)

@@ -73,11 +73,11 @@ def test_conv_head_1x1_fp32_out(mdx, Cin, Cout, M, relu):
     assert err < 1e-3, err
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large", "large128", "dma128", "stream", "split256"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "large128", "dma128", "stream"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
     if dtype == "fp32" and Cin % 4:
@@ -99,47 +99,24 @@ def test_conv2d(mdx, dtype, case, ksplit):
     if ksplit == "stream":
         if k != 1 or s != 1 or Cin not in (64, 128, 256) or Cout % 64:
             pytest.skip("streaming 1x1 kernels: 1x1/s1, Cin in {64,128,256}, Cout % 64 == 0")
-        old = call("mdx_conv_set_stream1x1", 2, 0)
-        old_f = call("mdx_conv_set_stream1x1_f32", 2)
-        try:
+        if dtype == "fp32":
+            pytest.skip("the streaming 1x1 kernels are fp16 (the fp32 one lost to k_conv_sb<64> and was removed)")
+        with policy_scope(stream1x1=2, stream1x1_min_m=0):
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
             assert kid.value == 4
-        finally:
-            call("mdx_conv_set_stream1x1_f32", old_f)
-            call("mdx_conv_set_stream1x1", old, 65536)
-    elif ksplit == "split256":
-        if Cin % (64 if dtype == "fp16" else 32) or Cout % 256:
-            pytest.skip("256x256 split-K: Cin % 64 (fp16) / 32 (fp32) == 0, Cout % 256 == 0")
-        nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, k, k, s, p)
-        ws = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
-        if Cin * k * k <= 128:
-            pytest.skip("K <= 128 layers stay on the 64-wide register-staged tile (the policy's narrow-K rule)")
-        old = call("mdx_conv_set_split256", 2, 1)
-        old_f = call("mdx_conv_set_dma_f32", 2)
-        try:
-            call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu),
-                 0, dc, dc, P(out), 0, P(ws), nb, None)
-            kid, ks_ = ctypes.c_int(), ctypes.c_int()
-            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-            assert kid.value == 2 and (ks_.value > 1 or Cin * k * k <= 32)
-        finally:
-            call("mdx_conv_set_dma_f32", old_f)
-            call("mdx_conv_set_split256", old, 18)
     elif ksplit in ("large", "large128", "dma128"):
         if (dtype != "fp16" and ksplit in ("dma128", "large128")) or Cin % (64 if dtype == "fp16" else 32):
             pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 / 256x128 ones fp16 only")
         if Cin * k * k <= 128:
             pytest.skip("K <= 128 layers stay on the 64-wide register-staged tile (the policy's narrow-K rule)")
-        old = call("mdx_conv_set_large_tiles", {"large": 2, "large128": 3}.get(ksplit, 0))
-        old_d = call("mdx_conv_set_dma128", 2 if ksplit == "dma128" else 0, 0)
-        old_i = call("mdx_conv_set_mfma_prio", int(case[0] % 2 == 0))  # both DMA schedules across the cases
-        old_da = call("mdx_conv_set_dma_after", int(case[1] % 2 == 0))
         f32_mode = 1 + CONV_CASES.index(case) % 2  # fp32: the 128x128 (1) and 256x256 (2) variants across the cases
-        old_f = call("mdx_conv_set_dma_f32", f32_mode)
-        try:
+        with policy_scope(large_tiles={"large": 2, "large128": 3}.get(ksplit, 0), dma128=2 if ksplit == "dma128" else 0,
+                          dma128_min_tiles=0,
+                          dma128_interleave=int(case[0] % 2 == 0),  # both DMA schedules across the cases
+                          dma_f32=f32_mode):
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
                  dc, P(out), None)
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
@@ -148,12 +125,6 @@ def test_conv2d(mdx, dtype, case, ksplit):
                 assert kid.value == (3 if f32_mode == 1 else 2)
             elif dtype == "fp16":
                 assert kid.value == (2 if ksplit in ("large", "large128") else 3)
-        finally:
-            call("mdx_conv_set_dma_f32", old_f)
-            call("mdx_conv_set_large_tiles", old)
-            call("mdx_conv_set_dma128", old_d, 1536)
-            call("mdx_conv_set_mfma_prio", old_i)
-            call("mdx_conv_set_dma_after", old_da)
     elif ksplit == 1:
         call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc, dc,
              P(out), None)
@@ -181,7 +152,7 @@ def test_conv2d_fp32_split(mdx, case, split, ksplit, narrow):
     rounding (x6), so the error against fp64 stays at the f32-MFMA kernel's:
     measured side by side here, bounded at 4x it (and 1e-5 of the output
     scale, the fp32 tolerance being 1e-4)."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
     if Cin % 4 or (ksplit > 1 and Cout % 8):
@@ -202,18 +173,11 @@ def test_conv2d_fp32_split(mdx, case, split, ksplit, narrow):
     errs = {}
     for mode in (0, split):
         out = torch.empty(N, OH, OW, Cout, device="cuda")
-        old = call("mdx_conv_set_fp32_split", mode)
-        old_f = call("mdx_conv_set_dma_f32", 0)
-        old_n = call("mdx_conv_set_x3_narrow", narrow)
-        try:
+        with policy_scope(fp32_split=mode, dma_f32=0, x3_narrow=narrow):
             call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 0, 0,
                  P(out), ksplit, P(ws), nb, None)
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-        finally:
-            call("mdx_conv_set_fp32_split", old)
-            call("mdx_conv_set_dma_f32", old_f)
-            call("mdx_conv_set_x3_narrow", old_n)
         assert (kid.value in (7, 8)) == (mode != 0)
         if mode and narrow:
             assert kid.value == 8
@@ -327,14 +291,15 @@ def test_rpn_proposals_from_identical_heads(mdx, sliced, anchors):
     ptrs = (ctypes.c_void_p * 5)(*[h.data_ptr() for h in heads])
     ia = lambda v: (ctypes.c_int * len(v))(*v)  # noqa: E731
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    old = call("mdx_rpn_set_sliced", sliced)
+    from moseq2_detectron_extract_amd._lib import knob
+    old = knob("rpn_sliced", sliced)
     try:
         call("mdx_rpn_proposals", ptrs, ia([s[0] for s in sizes]), ia([s[1] for s in sizes]), ia([4, 8, 16, 32, 64]),
              5, B, A, cells.ctypes.data_as(ctypes.c_void_p), cfg.anchor_offset, 423, 511, 1000, post, 0.7, 0.0,
              cfg.bbox_reg_clamp, (ctypes.c_float * 4)(*cfg.rpn_bbox_reg_weights), P(boxes), P(scores), P(cnt),
              P(ws), None)
     finally:
-        call("mdx_rpn_set_sliced", old)
+        knob("rpn_sliced", old)
     for b in range(B):
         wb, wsc = want[b]
         n = int(cnt[b])
@@ -391,7 +356,8 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
     bd, cd = boxes.contiguous().cuda(), counts.cuda()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     order = torch.full((B * per,), -1, dtype=torch.int32, device="cuda")
-    old = call("mdx_roi_align_set_mode", mode)
+    from moseq2_detectron_extract_amd._lib import knob
+    old = knob("roi_mode", mode)
     try:
         # the level/band permutation (k_roi_order) changes which workgroup pools
         # which ROI, never the pooled values
@@ -408,10 +374,10 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
         if mode == 7:
             # the LDS-window form sums the same taps in mode 4's order
             ref4 = torch.empty_like(out)
-            call("mdx_roi_align_set_mode", 4)
+            knob("roi_mode", 4)
             call("mdx_roi_align", ptrs, ia([s[0] for s in sizes.values()]), ia([s[1] for s in sizes.values()]), sc, 4,
                  2, C, P(bd), P(cd), B * per, per, 7, 0, 1, 224.0, 4.0, int(half), P(ref4), None)
-            call("mdx_roi_align_set_mode", mode)
+            knob("roi_mode", mode)
             assert torch.equal(out, ref4)
         if not half and mode in (4, 5, 7) and (49 * C) % 16 == 0:
             # dtype 2: the same rows written as bf16 planes (fc1's split-plane
@@ -423,7 +389,7 @@ def test_roi_align_matches_oracle(mdx, rt, C, half, mode, ordered):
             rec = pl.double().sum(2).float().reshape(out.shape)
             assert torch.equal(rec, out)
     finally:
-        call("mdx_roi_align_set_mode", old)
+        knob("roi_mode", old)
     got = out.cpu().float().permute(0, 3, 1, 2)
     got = torch.cat([got[:per], got[per:2 * per - 7]])
     tol = 2e-3 if half else 1e-5
@@ -852,8 +818,7 @@ def test_extract_session_from_dat(mdx, tmp_path):
         np.testing.assert_array_equal(out_xn[k], out[k], err_msg=k)
 
 
-@pytest.mark.parametrize("split", [0, 6, -1, -2, -3, -4],
-                         ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-halfstep", "f32-direct-epilogue", "f32-wino-in2"])
+@pytest.mark.parametrize("split", [0, 6, -1, -3], ids=["f32-mfma", "bf16x6", "f32-dma256", "f32-direct-epilogue"])
 @pytest.mark.parametrize("m", [2, 4, 6])
 @pytest.mark.parametrize("N,H,W,Cin,Cout,relu", [(2, 13, 17, 256, 256, True), (3, 7, 7, 512, 512, True),
                                                  (1, 14, 16, 256, 64, False), (4, 6, 5, 260, 136, True),
@@ -884,74 +849,22 @@ def test_conv3x3_winograd(mdx, N, H, W, Cin, Cout, relu, m, split):
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
     if split == -1 and (Cout % 256 or Cin % 32):
         pytest.skip("the 256x256 LDS-DMA GEMM needs Cout % 256 == 0 and Cin % 32 == 0")
-    old = call("mdx_conv_set_fp32_split", max(split, 0))
     # -1: the GEMMs forced onto the 256x256 LDS-DMA kernel; else kept off it;
-    # -2: on the half-step kernel (both tiles), -3: with the direct epilogue,
-    # -4: the two-channel input transform, bit-equal to the default's
-    old_dma = call("mdx_conv_set_winograd_dma", 2 if split == -1 else 0, 384)
-    old_hb = call("mdx_conv_set_half_step", 2 if split == -2 else 0)
-    old_de = call("mdx_conv_set_direct_epilogue", 1 if split == -3 else 0)
-    old_in2 = call("mdx_conv_set_wino_in2", 1 if split == -4 else 0)
-    try:
+    # -3: the direct epilogue, bit-equal to the LDS-image epilogue
+    from moseq2_detectron_extract_amd._lib import policy_scope
+    with policy_scope(fp32_split=max(split, 0), winograd_dma=2 if split == -1 else 0, winograd_dma_min_wgs=384,
+                      direct_epilogue=1 if split == -3 else 0):
         call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(out), P(ws), nb, None)
-        if split in (-2, -3, -4):
-            call("mdx_conv_set_half_step", 0)
-            call("mdx_conv_set_direct_epilogue", 0)
-            call("mdx_conv_set_wino_in2", 0)
+        if split == -3:
             ref = torch.empty_like(out)
-            call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(ref), P(ws), nb,
-                 None)
+            with policy_scope(direct_epilogue=0):
+                call("mdx_conv3x3_winograd", P(xd), N, H, W, Cin, P(Ud), P(bd), Cout, int(relu), m, P(ref), P(ws), nb,
+                     None)
             assert torch.equal(out, ref)
-    finally:
-        call("mdx_conv_set_fp32_split", old)
-        call("mdx_conv_set_winograd_dma", old_dma, 384)
-        call("mdx_conv_set_half_step", old_hb)
-        call("mdx_conv_set_direct_epilogue", old_de)
-        call("mdx_conv_set_wino_in2", old_in2)
     kid, ks_ = ctypes.c_int(), ctypes.c_int()
     call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
     assert kid.value == 6
     got = out.cpu().double()
-    err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
-    assert err < 1e-4, err
-
-
-@pytest.mark.parametrize("N,H,W,Cin,Cout,relu,bias", [(2, 13, 17, 256, 256, True, True), (3, 7, 7, 512, 512, True, True),
-                                                      (1, 14, 16, 256, 64, False, True), (4, 6, 5, 264, 96, True, False),
-                                                      (2, 56, 64, 256, 256, True, True), (2, 112, 128, 64, 64, True, True),
-                                                      (1, 3, 3, 8, 32, False, True), (5, 29, 31, 128, 160, True, True)])
-def test_conv3x3_winograd_fused(mdx, N, H, W, Cin, Cout, relu, bias):
-    """Fused Winograd F(4x4,3x3) (k_wino_f4: input transform, 36 tile-point
-    GEMMs and output transform + bias + ReLU in one launch, no workspace
-    traffic) against the fp64 direct convolution, within the unfused
-    kernels' tolerance (1e-4 of the output scale); ragged maps exercise
-    partial tiles, padding rows / columns and a partial last tile block,
-    Cin % 16 == 8 a half K-step pair, bias=False the null-bias path."""
-    from moseq2_detectron_extract_amd._lib import call
-    import ctypes
-    g = torch.Generator().manual_seed(N * 1000 + H + Cin)
-    x = torch.randn(N, H, W, Cin, generator=g).clamp_min(0)
-    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
-    b = torch.randn(Cout, generator=g) if bias else torch.zeros(Cout)
-    want = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1)
-    if relu:
-        want = want.clamp_min(0)
-    want = want.permute(0, 2, 3, 1)
-    U = np.empty((36, Cout, Cin), np.float32)
-    wn = np.ascontiguousarray(w.numpy())
-    call("mdx_winograd_weights", wn.ctypes.data_as(ctypes.c_void_p), Cout, Cin, 4, U.ctypes.data_as(ctypes.c_void_p))
-    Up = np.empty_like(U)
-    call("mdx_winograd_pack_f4", U.ctypes.data_as(ctypes.c_void_p), Cout, Cin, Up.ctypes.data_as(ctypes.c_void_p))
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    xd, Ud, bd = x.cuda(), torch.from_numpy(Up).cuda(), b.cuda()  # (bd kept alive for the call)
-    bp = P(bd) if bias else None
-    out = torch.full((N, H, W, Cout), float("nan"), device="cuda")
-    call("mdx_conv3x3_winograd_fused", P(xd), N, H, W, Cin, P(Ud), bp, Cout, int(relu), P(out), None)
-    kid, ks_ = ctypes.c_int(), ctypes.c_int()
-    call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-    assert kid.value == 24  # MDX_CONV_KERNEL_WINO_FUSED
-    got = out.cpu().double()
-    assert torch.isfinite(got).all()  # every output pixel written
     err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
     assert err < 1e-4, err
 
@@ -985,13 +898,11 @@ def test_conv3x3_winograd_planes(mdx, N, H, W, Cin, Cout, m):
     ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
     T = N * -(-H // m) * -(-W // m)
     wgs = -(-T // 256) * -(-Cout // 256) * NB
-    old = call("mdx_conv_set_fp32_split", 6)
-    try:
+    from moseq2_detectron_extract_amd._lib import policy_scope
+    with policy_scope(fp32_split=6):
         call("mdx_conv3x3_winograd_x6", P(xd), N, H, W, Cin, P(Ud), P(Up), P(bd), Cout, 1, m, P(out), P(ws), nb,
              None)
         torch.cuda.synchronize()
-    finally:
-        call("mdx_conv_set_fp32_split", old)
     got = out.cpu().double()
     err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-9)
     assert err < 1e-4, (err, wgs)
@@ -1049,7 +960,7 @@ def test_conv1x1_narrow_fp32(mdx, M, K, N, relu, head):
     """fp32 1x1 layers with Cout <= 16 (RPN head, mask / box predictors) on
     the narrow-output MFMA kernel vs fp64 (and the general kernel): 1e-5 of
     the output scale; ragged M covers partial 16-pixel groups."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     g = torch.Generator().manual_seed(M + K + N)
     x = torch.randn(M, K, generator=g)
@@ -1061,13 +972,10 @@ def test_conv1x1_narrow_fp32(mdx, M, K, N, relu, head):
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     xd, wd, bd = x.cuda(), w.cuda(), b.cuda()
     out = torch.full((M, N), float("nan"), device="cuda")
-    old = call("mdx_conv_set_head_f32", head)
-    try:
+    with policy_scope(head_f32=head):
         call("mdx_conv2d", P(xd), M, 1, 1, K, P(wd), P(bd), N, 1, 1, 1, 0, None, int(relu), 0, 0, 0, P(out), None)
         kid, ks_ = ctypes.c_int(), ctypes.c_int()
         call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-    finally:
-        call("mdx_conv_set_head_f32", old)
     assert (kid.value == 5) == bool(head)
     err = (out.cpu().double() - want).abs().max().item() / want.abs().max().item()
     assert err < 1e-5, err
@@ -1112,19 +1020,17 @@ def test_conv2d_dual_conv3_shortcut(mdx, dtype, N, H, W, Cin, Cout, H2, W2, Cin2
 
 def test_forward_fused_shortcut_matches_unfused(small_case):
     """A handle with the projection shortcuts fused into conv3
-    (mdx_model_set_fuse_shortcut) gives the unfused handle's features to
+    (mdx_policy.fuse_shortcut) gives the unfused handle's features to
     fp32 rounding, and the oracle's within the backbone tolerance."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import policy_scope
     from moseq2_detectron_extract_amd.model import MaskRCNN
     from oracle import model_ref as R
     cfg, sd, _, imgs = small_case
-    old = call("mdx_model_set_fuse_shortcut", 0)
-    try:
+    with policy_scope(fuse_shortcut=0):
         m0 = MaskRCNN(cfg, sd, dtype="fp32")
-        call("mdx_model_set_fuse_shortcut", 1)
+    with policy_scope(fuse_shortcut=1):
         m1 = MaskRCNN(cfg, sd, dtype="fp32")
-    finally:
-        call("mdx_model_set_fuse_shortcut", old)
+    assert m0.policy()["fuse_shortcut"] == 0 and m1.policy()["fuse_shortcut"] == 1
     x = torch.from_numpy(imgs[..., 0]).cuda()
     a = m0.forward(x, intermediates=True)["intermediates"]
     b = m1.forward(x, intermediates=True)["intermediates"]
@@ -1137,50 +1043,40 @@ def test_forward_fused_shortcut_matches_unfused(small_case):
         assert err < 2e-4, f"{k}: rel err {err:.2e}"
 
 
-def test_split_plane_preplit_weights_bit_equal(small_case):
-    """Split-plane mode (mdx_conv_set_fp32_split(6)): a handle created in that
-    mode carries its conv weights and Winograd U as bf16 planes (split once,
-    mdx_split_x6) and k_conv_x3 copies them instead of splitting the weights
-    per tile; a handle created outside it splits them in the kernel.  The
-    split is the same (RNE hi, mid of the exact remainder, lo) and the MFMA
-    order is the same, so the backbone and FPN features agree bit for bit --
-    with the pointwise (PW) instance on the 1x1 layers and Winograd GEMMs.
-    The single-stage instance those launches take by default
-    (mdx_conv_set_x3_single_stage) sums all six products in one accumulator
-    set: within fp32 rounding of the two-stage kernel."""
-    from moseq2_detectron_extract_amd._lib import call
+def test_split_plane_handles(small_case):
+    """Split-plane mode (mdx_policy.fp32_split = 6): handles created in it
+    carry their conv weights and Winograd U as bf16 planes (split once,
+    mdx_split_x6) for k_conv_x3.  The single-stage instance
+    (mdx_policy.x3_single_stage, the default) sums all six products in one
+    accumulator set: within fp32 rounding of the two-stage kernel's handle,
+    and both within the fp32 backbone tolerance of the f32-MFMA handle."""
+    from moseq2_detectron_extract_amd._lib import policy_scope
     from moseq2_detectron_extract_amd.model import MaskRCNN
     cfg, sd, _, imgs = small_case
-    old = call("mdx_conv_set_fp32_split", 0)
-    old_sb = call("mdx_conv_set_x3_single_stage", 0)
-    try:
-        m_kernel_split = MaskRCNN(cfg, sd, dtype="fp32")
-        call("mdx_conv_set_fp32_split", 6)
-        m_planes = MaskRCNN(cfg, sd, dtype="fp32")
-        x = torch.from_numpy(imgs[..., 0]).cuda()
-        a = m_kernel_split.forward(x, intermediates=True)["intermediates"]
-        b = m_planes.forward(x, intermediates=True)["intermediates"]
-        b = {k: v.clone() for k, v in b.items()}
-        call("mdx_conv_set_x3_single_stage", 1)
-        c = m_planes.forward(x, intermediates=True)["intermediates"]
-        torch.cuda.synchronize()
-    finally:
-        call("mdx_conv_set_fp32_split", old)
-        call("mdx_conv_set_x3_single_stage", old_sb)
+    with policy_scope(fp32_split=6, x3_single_stage=0):
+        m_two = MaskRCNN(cfg, sd, dtype="fp32")
+    with policy_scope(fp32_split=6, x3_single_stage=1):
+        m_one = MaskRCNN(cfg, sd, dtype="fp32")
+    m_f32 = MaskRCNN(cfg, sd, dtype="fp32")
+    x = torch.from_numpy(imgs[..., 0]).cuda()
+    b = {k: v.clone() for k, v in m_two.forward(x, intermediates=True)["intermediates"].items()}
+    c = {k: v.clone() for k, v in m_one.forward(x, intermediates=True)["intermediates"].items()}
+    f = m_f32.forward(x, intermediates=True)["intermediates"]
+    torch.cuda.synchronize()
     for k in ("res2", "res3", "res4", "res5", "p2", "p3", "p4", "p5", "p6"):
-        assert torch.equal(a[k], b[k]), k
-        gb, gc = b[k].double(), c[k].double()
+        gb, gc, gf = b[k].double(), c[k].double(), f[k].double()
         assert (gb - gc).abs().max().item() <= 2e-5 * gb.abs().max().item(), k
+        assert (gb - gf).abs().max().item() <= 2e-4 * gf.abs().max().item(), k
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 1 and c[7] == 0])
 def test_conv2d_fp32_pointwise_instances(mdx, case):
     """fp32 pointwise layers (1x1, unpadded, stride 1 or 2) on k_conv's PW
     instances, with two LDS stages and with one (k_conv_sb,
-    mdx_conv_set_single_stage), split-K 1 and 3 (Cout % 8 == 0), against the
+    mdx_policy.single_stage), split-K 1 and 3 (Cout % 8 == 0), against the
     fp64 convolution (rel. 1e-4 of the output scale) and against each other
     bit for bit (same MFMA order per accumulator)."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
     g = torch.Generator().manual_seed(Cin * 7 + Cout)
@@ -1195,40 +1091,24 @@ def test_conv2d_fp32_pointwise_instances(mdx, case):
     rd = res.cuda() if res is not None else None
     nb = call("mdx_conv2d_workspace_bytes", N, H, W, Cin, Cout, 1, 1, s, 0)
     ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
-    olds = [call("mdx_conv_set_single_stage", 0), call("mdx_conv_set_dma_f32", 0),
-            call("mdx_conv_set_head_f32", 0), call("mdx_conv_set_stream1x1_f32", 0)]
-    try:
+    with policy_scope(dma_f32=0, head_f32=0):
         for ks in ((1, 3) if Cout % 8 == 0 else (1,)):
             outs = []
-            # single-stage with the A-fragment prefetch (mdx_conv_set_sb_afp)
-            # too, and the half-step kernel (mdx_conv_set_half_step 2: both tiles)
-            # and the direct epilogue (mdx_conv_set_direct_epilogue)
-            for single, afp, hb, de in ((0, 0, 0, 0), (1, 0, 0, 0), (1, 1, 0, 0), (1, 0, 2, 0), (1, 0, 0, 1),
-                                        (0, 0, 0, 1)):
-                call("mdx_conv_set_single_stage", single)
-                old_afp = call("mdx_conv_set_sb_afp", afp)
-                old_hb = call("mdx_conv_set_half_step", hb)
-                old_de = call("mdx_conv_set_direct_epilogue", de)
-                try:
+            # two-stage / single-stage, each with the LDS-image and the direct
+            # epilogue (mdx_policy.direct_epilogue)
+            for single, de in ((0, 0), (1, 0), (1, 1), (0, 1)):
+                with policy_scope(single_stage=single, direct_epilogue=de):
                     out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
                     call("mdx_conv2d_splitk", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, 1, 1, s, 0, P(rd), int(relu), 0,
                          0, 0, P(out), ks, P(ws), nb, None)
-                finally:
-                    call("mdx_conv_set_sb_afp", old_afp)
-                    call("mdx_conv_set_half_step", old_hb)
-                    call("mdx_conv_set_direct_epilogue", old_de)
                 kid, ks_ = ctypes.c_int(), ctypes.c_int()
                 call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-                assert kid.value in ((25, 26) if hb else (18, 19) if single else (14, 15)), kid.value
+                assert kid.value in ((18, 19) if single else (14, 15)), kid.value
                 err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
-                assert err < 1e-4, (ks, single, hb, err)
+                assert err < 1e-4, (ks, single, de, err)
                 outs.append(out)
             for o in outs[1:]:
                 assert torch.equal(outs[0], o), ks
-    finally:
-        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_head_f32",
-                         "mdx_conv_set_stream1x1_f32"), olds):
-            call(f, o)
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if not (c[5] == 1 and c[7] == 0) and c[3] % 8 == 0])
@@ -1237,7 +1117,7 @@ def test_conv2d_fp16_single_stage_general(mdx, case):
     tiles off): the single-stage schedule (k_conv_sbg, single_stage mode 4,
     the default) against the two-stage kernel (mode 3) bit for bit, and
     against the fp64 convolution within fp16 output rounding."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
     g = torch.Generator().manual_seed(Cin * 13 + Cout + k)
@@ -1251,33 +1131,28 @@ def test_conv2d_fp16_single_stage_general(mdx, case):
     xd, bd = x.cuda(), b.cuda()
     wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
     rd = res.cuda() if res is not None else None
-    olds = [call("mdx_conv_set_single_stage", 3), call("mdx_conv_set_large_tiles", 0)]
-    try:
-        outs = []
-        for mode in (3, 4):
-            call("mdx_conv_set_single_stage", mode)
+    outs = []
+    for mode in (3, 4):
+        with policy_scope(single_stage=mode, large_tiles=0):
             out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda", dtype=torch.float16)
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 1, 1, P(out),
                  None)
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-            assert kid.value in ((22, 23) if mode == 4 else (0, 1)), kid.value
-            err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
-            assert err < 5e-3, (mode, err)
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1])
-    finally:
-        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_large_tiles"), olds):
-            call(f, o)
+        assert kid.value in ((22, 23) if mode == 4 else (0, 1)), kid.value
+        err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+        assert err < 5e-3, (mode, err)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if not (c[5] == 1 and c[7] == 0) and c[3] % 4 == 0])
 def test_conv2d_fp32_single_stage_general(mdx, case):
     """General fp32 layers (KxK / padded: the stem's shape, 3x3 / 7x7 with
     stride) on the single-stage schedule (k_conv_sbg,
-    mdx_conv_set_single_stage(2)) against the fp64 convolution (rel. 1e-4 of
+    mdx_policy.single_stage = 2) against the fp64 convolution (rel. 1e-4 of
     the output scale) and against the two-stage kernel bit for bit."""
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, policy_scope
     import ctypes
     N, H, W, Cin, Cout, k, s, p, use_res, relu = case
     g = torch.Generator().manual_seed(Cin * 11 + Cout + k)
@@ -1291,21 +1166,16 @@ def test_conv2d_fp32_single_stage_general(mdx, case):
     xd, bd = x.cuda(), b.cuda()
     wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().cuda()
     rd = res.cuda() if res is not None else None
-    olds = [call("mdx_conv_set_single_stage", 1), call("mdx_conv_set_dma_f32", 0), call("mdx_conv_set_winograd", 0)]
-    try:
-        outs = []
-        for mode in (1, 2):
-            call("mdx_conv_set_single_stage", mode)
+    outs = []
+    for mode in (1, 2):
+        with policy_scope(single_stage=mode, dma_f32=0, winograd=0):
             out = torch.full((N, OH, OW, Cout), float("nan"), device="cuda")
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(bd), Cout, k, k, s, p, P(rd), int(relu), 0, 0, 0, P(out),
                  None)
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
-            assert kid.value in ((22, 23) if mode == 2 else (0, 1)), kid.value
-            err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
-            assert err < 1e-4, (mode, err)
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1])
-    finally:
-        for f, o in zip(("mdx_conv_set_single_stage", "mdx_conv_set_dma_f32", "mdx_conv_set_winograd"), olds):
-            call(f, o)
+        assert kid.value in ((22, 23) if mode == 2 else (0, 1)), kid.value
+        err = (out.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-9)
+        assert err < 1e-4, (mode, err)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])

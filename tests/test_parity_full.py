@@ -240,10 +240,10 @@ FP32_VARIANTS = [("fp32", 4, 0), ("fp32", 6, 0), ("fp32", 2, 0), ("fp32", 0, 0),
                          [(101, 64, "fp16", 0, 0, R101_SEED), (101, 64, "mixed", 6, 0, R101_SEED),
                           (101, 64, "fp32", 6, 0, R101_SEED)])
 def test_forward_full_frame(mdx, depth, B, dtype, wino, split, wseed):
-    """wino: the fp32 3x3 algorithm (mdx_conv_set_winograd: 4 = F(4x4,3x3),
+    """wino: the fp32 3x3 algorithm (mdx_policy.winograd: 4 = F(4x4,3x3),
     6 = F(6x6,3x3) on the large maps and F(4x4,3x3) elsewhere, 2 = F(2x2,3x3),
     0 = direct); split: the fp32 layers as exact bf16 plane
-    products (mdx_conv_set_fp32_split, 0 = the f32 MFMA kernels); wseed: the
+    products (mdx_policy.fp32_split, 0 = the f32 MFMA kernels); wseed: the
     synthetic weights; the same fp32 tolerances hold for all."""
     with _policy(wino, split):
         st = _forward_full_frame(depth, B, dtype, wino, split, wseed)["summary"]
@@ -277,18 +277,11 @@ def test_forward_full_frame_fp16_seeds(mdx):
     assert tot["crop_exact"] >= FP16_CROP_EXACT * tot["non_nan"], tot
 
 
-class _policy:
-    def __init__(self, wino, split):
-        self.wino, self.split = wino, split
-
-    def __enter__(self):
-        from moseq2_detectron_extract_amd._lib import call
-        self.old = call("mdx_conv_set_winograd", self.wino), call("mdx_conv_set_fp32_split", self.split)
-
-    def __exit__(self, *exc):
-        from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_winograd", self.old[0])
-        call("mdx_conv_set_fp32_split", self.old[1])
+def _policy(wino, split):
+    """The thread's policy for the case: the Predictor's handle, created
+    inside, captures it."""
+    from moseq2_detectron_extract_amd._lib import policy_scope
+    return policy_scope(winograd=wino, fp32_split=split)
 
 
 def _record(name, obj):

@@ -138,6 +138,52 @@ def test_predictor_from_model_dir_matches_oracle(case):
     assert torch.equal(a[0]["instances"].pred_boxes.tensor, b[0]["instances"].pred_boxes.tensor)
 
 
+def test_two_policies_concurrently_on_two_streams(case):
+    """Per-handle kernel selection (include/mdx.h, mdx_policy): a predictor
+    built with direct 3x3 convolutions (winograd 0) and one built with F(6,3)
+    Winograd and another ROI-align mode, created side by side on one thread,
+    their forwards enqueued on two streams with no synchronisation between
+    them, three times over.  Each handle keeps the policy it was created
+    with, each concurrent result equals that handle's serial result bit for
+    bit, each matches the oracle, and the thread's own policy is untouched."""
+    from moseq2_detectron_extract_amd._lib import policy
+    from moseq2_detectron_extract_amd.model import Predictor
+    cfg, sd, img, want, _, _ = case
+    before = policy()
+    pa = Predictor.from_config(cfg, weights=sd, policy={"winograd": 0})
+    pb = Predictor.from_config(cfg, weights=sd, policy={"winograd": 6, "roi_mode": 7})
+    assert policy() == before
+    assert pa.model.policy()["winograd"] == 0 and pa.model.policy()["roi_mode"] == before["roi_mode"]
+    assert pb.model.policy()["winograd"] == 6 and pb.model.policy()["roi_mode"] == 7
+    _check(pa(img), want, img.shape[1:3])
+    _check(pb(img), want, img.shape[1:3])
+    x = torch.from_numpy(img[..., 0]).cuda()
+    keys = ("boxes", "scores", "classes", "ndet", "keypoints", "keypoint_heatmaps")
+
+    def snap(o):
+        return {k: o[k].clone() for k in keys} | {"masks": o["masks"].clone()}
+    serial_a, serial_b = snap(pa.model.forward(x)), snap(pb.model.forward(x))
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    sa.wait_stream(torch.cuda.current_stream())
+    sb.wait_stream(torch.cuda.current_stream())
+    runs = []
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            ra = snap(pa.model.forward(x))
+        with torch.cuda.stream(sb):
+            rb = snap(pb.model.forward(x))
+        runs.append((ra, rb))
+    torch.cuda.synchronize()
+    for ra, rb in runs:
+        for k in serial_a:
+            assert torch.equal(ra[k], serial_a[k]), ("winograd 0", k)
+            assert torch.equal(rb[k], serial_b[k]), ("winograd 6", k)
+    # the two policies run different 3x3 kernels: close, not identical
+    assert not torch.equal(serial_a["keypoint_heatmaps"], serial_b["keypoint_heatmaps"])
+    assert policy() == before
+
+
 def test_predictor_non_default_anchors_match_oracle(mdx, tmp_path):
     """A model directory whose config differs from the zoo defaults in the
     anchor generator (the reference notebook's five aspect ratios, other

@@ -29,9 +29,10 @@ def main():
     import mdx_pkg
     mdx_pkg.load()
     from moseq2_detectron_extract_amd._lib import call
-    for kv in sys.argv[2:]:  # knob=value, e.g. dma_after=1 -> mdx_conv_set_dma_after(1)
+    from moseq2_detectron_extract_amd._lib import knob
+    for kv in sys.argv[2:]:  # field=value of the kernel-selection policy, e.g. dma_f32=2
         name, val = kv.split("=")
-        call(f"mdx_conv_set_{name}", int(val))
+        knob(name, int(val))
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     ws = torch.empty(64 << 18, dtype=torch.float32, device="cuda")
     copy_src = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
@@ -60,7 +61,7 @@ def main():
         byts = 2.0 * (x.numel() + w.numel() + out.numel() + (r.numel() if res else 0))
         line = f"M={M:7d} N={Cout:5d} K={k * k * Cin:6d} res={int(res)}:"
         for mode, nk in ((0, 0), (2, 0)):
-            old = call("mdx_conv_set_large_tiles", mode)
+            old = knob("large_tiles", mode)
 
             def go():
                 call("mdx_conv2d_splitk", P(x), N, H, W, Cin, P(w), P(b), Cout, k, k, s, p, P(r), 1, 0, 1, 1,
@@ -72,7 +73,7 @@ def main():
                 go()
             e1.record()
             torch.cuda.synchronize()
-            call("mdx_conv_set_large_tiles", old)
+            knob("large_tiles", old)
             t = e0.elapsed_time(e1) / 10 * 1e-3
             line += f"  [{'64' if nk else ('128' if mode == 0 else '256')}] {t * 1e6:7.1f}us {flops / t / 1e12:6.1f}TF {byts / t / 1e12:5.2f}TB/s"
         print(line, flush=True)

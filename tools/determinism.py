@@ -30,7 +30,8 @@ def main():
     batches = [raw[i * B:(i + 1) * B] for i in range(nb)]
     if os.environ.get("DET_SPLIT"):
         from moseq2_detectron_extract_amd._lib import call
-        call("mdx_conv_set_fp32_split", int(os.environ["DET_SPLIT"]))
+        from moseq2_detectron_extract_amd._lib import knob
+        knob("fp32_split", int(os.environ["DET_SPLIT"]))
     pred = Predictor.from_config(ModelConfig(score_thresh_test=0.0), dtype=dtype, weights="synthetic")
     ex = GPUExtractor(s.bground_im, s.roi, pred, ExtractConfig(batch_size=B))
     keys = ("depth_frames", "mask_frames", "centroid", "angle", "keypoints", "ndet")

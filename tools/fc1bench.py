@@ -2,7 +2,7 @@
 (32000 pooled ROIs x 12544 -> 1024, + bias + ReLU) through mdx_conv2d_splitk,
 HIP events over REPS launches.  Run under rocprofv3 --pmc FETCH_SIZE (or
 WRITE_SIZE) to read its HBM bytes per launch apart from every other launch of
-the same kernel symbol.  Knobs: name=value calls mdx_conv_set_<name>(value).
+the same kernel symbol.  Knobs: field=value[,threshold] sets that field of the thread's kernel-selection policy.
 Usage: python tools/fc1bench.py [reps] [knob=value ...]"""
 import ctypes
 import json
@@ -17,11 +17,11 @@ def main():
     import torch
     import mdx_pkg
     mdx_pkg.load()
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, knob
     reps = int(sys.argv[1]) if len(sys.argv) > 1 and "=" not in sys.argv[1] else 10
     for kv in [a for a in sys.argv[1:] if "=" in a]:
         name, val = kv.split("=")
-        call(f"mdx_conv_set_{name}", *[int(v) for v in val.split(",")])
+        knob(name, *[int(v) for v in val.split(",")])
     M, N, K = int(os.environ.get("FC1_M", 32000)), 1024, 12544
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     g = torch.Generator(device="cuda").manual_seed(0)

@@ -4,7 +4,7 @@ mdx_conv2d_splitk and the 3x3 layers through mdx_conv3x3_winograd (the tile
 the library's Winograd policy picks per layer, mdx_winograd_tile; the
 GEMM timed apart from the transforms by the model's profiling hook is not
 available here, so the whole layer is timed).  Knobs: name=value calls
-mdx_conv_set_<name>(value) first.
+sets that field of the thread's kernel-selection policy (mdx_policy) first.
 Usage: python tools/gemm32bench.py [knob=value ...]"""
 import ctypes
 import json
@@ -46,12 +46,12 @@ def main():
     import torch
     import mdx_pkg
     mdx_pkg.load()
-    from moseq2_detectron_extract_amd._lib import call
+    from moseq2_detectron_extract_amd._lib import call, knob, policy as current_policy
     for kv in sys.argv[1:]:
         name, val = kv.split("=")
-        call(f"mdx_conv_set_{name}", *[int(v) for v in val.split(",")])
+        knob(name, *[int(v) for v in val.split(",")])
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-    policy = call("mdx_conv_winograd_enabled") or 4
+    policy = current_policy()["winograd"] or 4
     need = max([call("mdx_winograd_workspace_bytes", N, H, W, Ci, Co, call("mdx_winograd_tile", H, W, policy))
                 for N, H, W, Ci, Co, _ in WINO] + [1 << 28])
     ws = torch.empty(need, dtype=torch.uint8, device="cuda")

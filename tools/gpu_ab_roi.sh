@@ -1,4 +1,4 @@
-# ROIAlign kernel mode A/B in the bench loop (mdx_roi_align_set_mode 4 / 5 / 6),
+# ROIAlign kernel mode A/B in the bench loop (mdx_policy.roi_mode 4 / 5 / 6),
 # interleaved twice, without secondaries.  Usage: bash tools/gpu_ab_roi.sh
 O=gpurun_out
 mkdir -p $O

@@ -17,7 +17,8 @@ def main():
     import test_parity_full as T
     from moseq2_detectron_extract_amd._lib import call
     dtype, wino = sys.argv[1], int(sys.argv[2])
-    old = call("mdx_conv_set_winograd", wino)
+    from moseq2_detectron_extract_amd._lib import knob
+    old = knob("winograd", wino)
     try:
         for seed in (int(v) for v in sys.argv[3:]):
             T._ORACLE.clear()
@@ -31,7 +32,7 @@ def main():
             summ = json.load(open(out))["summary"] if os.path.exists(out) else None
             print(json.dumps({"seed": seed, "dtype": dtype, "wino": wino, "result": res, "summary": summ}), flush=True)
     finally:
-        call("mdx_conv_set_winograd", old)
+        knob("winograd", old)
 
 
 if __name__ == "__main__":

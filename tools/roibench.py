@@ -1,5 +1,5 @@
 """Box-head ROIAlign kernels on the bench workload (R50-FPN B=32, synthetic
-session frames): serial forwards per mdx_roi_align_set_mode, HIP events
+session frames): serial forwards per mdx_policy.roi_mode, HIP events
 around each forward (the ROIAlign difference is the forward-time difference;
 the whole model is enqueued from C, so the pooler has no Python hook), and
 the box_pooled tensor compared bit for bit against mode 4.
@@ -29,7 +29,8 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ref = None
     for mode in (4, 6, 4, 6):
-        old = call("mdx_roi_align_set_mode", mode)
+        from moseq2_detectron_extract_amd._lib import knob
+        old = knob("roi_mode", mode)
         try:
             for _ in range(2):
                 m.forward(prepped, lut)
@@ -41,7 +42,7 @@ def main():
             pooled = m.forward(prepped, lut, intermediates=True)["intermediates"]["box_pooled"].clone()
             torch.cuda.synchronize()
         finally:
-            call("mdx_roi_align_set_mode", old)
+            knob("roi_mode", old)
         if ref is None:
             ref = pooled
         print(json.dumps({"roi_mode": mode, "forward_ms": round(e0.elapsed_time(e1) / 6, 3),
