@@ -57,8 +57,18 @@ int mdx_prep_frames(const int16_t *raw, int64_t n, int H, int W, const double *b
 
 /* fill_invalid_pixels -> cv2.inpaint(frame, invalid, 3, cv2.INPAINT_NS) per
  * frame, in place on `frames`.  M/proc/proc.py:189-210.  workspace: device
- * buffer of at least mdx_inpaint_workspace_bytes(n, H, W) bytes. */
+ * buffer of at least mdx_inpaint_workspace_bytes(n, H, W) bytes, set up once
+ * by mdx_inpaint_workspace_init for frames of H x W (and again before it is
+ * used for another frame shape); every call leaves it ready for the next.
+ * Per frame it holds mdx_inpaint_sparse_capacity(H, W) unknown pixels (about
+ * 4 % of the frame; < 1 MB per 512 x 424 frame); frames with more unknown
+ * pixels are done one after another in one shared full-size slot.  A call on a
+ * workspace not set up for H x W leaves the frames un-inpainted, counts each
+ * of them in mdx_inpaint_errors / `errors`, and the workspace must be set up
+ * again before its next use. */
 int64_t mdx_inpaint_workspace_bytes(int64_t n, int H, int W);
+int mdx_inpaint_workspace_init(void *workspace, int64_t bytes, int H, int W, mdx_stream_t stream);
+int mdx_inpaint_sparse_capacity(int H, int W);
 int mdx_inpaint_ns(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W,
                    int radius, void *workspace, mdx_stream_t stream);
 /* Frames whose inpaint cluster labelling failed its convergence check (every
@@ -72,6 +82,14 @@ int mdx_inpaint_errors(int reset);
  * process-wide counter only. */
 int mdx_inpaint_ns_counted(uint8_t *frames, const uint8_t *invalid, int64_t n, int H, int W, int radius,
                            void *workspace, unsigned int *errors, mdx_stream_t stream);
+/* prep_raw_frames with fix_invalid_pixels=True in one call: mdx_prep_frames
+ * (invalid may be NULL: the invalid pixels then go to the workspace only, as
+ * a bit image) followed by the inpaint of `out` with `radius`.  workspace: as
+ * for mdx_inpaint_ns, for frames of (y1 - y0) x (x1 - x0).
+ * M/proc/proc.py:129-172 + 189-210. */
+int mdx_prep_inpaint(const int16_t *raw, int64_t n, int H, int W, const double *bg, const uint8_t *roi,
+                     int y0, int y1, int x0, int x1, int flags, double vmin, double vmax, uint8_t *out,
+                     uint8_t *invalid, int radius, void *workspace, unsigned int *errors, mdx_stream_t stream);
 
 /* scale_raw_frames(frames, vmin, vmax, 'uint8') as a 256-entry LUT built on
  * the host in float64 (M/proc/proc.py:214-234).  int_vmin != 0 reproduces

@@ -33,6 +33,9 @@ SIGNATURES = {
     "mdx_version": (ctypes.c_char_p, []),
     "mdx_prep_frames": (I32, [P, I64, I32, I32, P, P, I32, I32, I32, I32, I32, F64, F64, P, P, P]),
     "mdx_inpaint_workspace_bytes": (I64, [I64, I32, I32]),
+    "mdx_inpaint_workspace_init": (I32, [P, I64, I32, I32, P]),
+    "mdx_inpaint_sparse_capacity": (I32, [I32, I32]),
+    "mdx_prep_inpaint": (I32, [P, I64, I32, I32, P, P, I32, I32, I32, I32, I32, F64, F64, P, P, I32, P, P, P]),
     "mdx_inpaint_ns": (I32, [P, P, I64, I32, I32, I32, P, P]),
     "mdx_inpaint_errors": (I32, [I32]),
     "mdx_inpaint_ns_counted": (I32, [P, P, I64, I32, I32, I32, P, P, P]),

@@ -60,6 +60,13 @@ bool winograd_planes_enabled();  // the model runs Winograd GEMMs on k_gemm_x6 (
 // (mdx_split_x6 layout), or null; the model handle sets it around a layer
 void x3_weight_planes(const void *planes);
 
+// prep_raw_frames' kernel (frameops.hip); bits (or null): the invalid pixels
+// ORed into the inpaint workspace's bit images (zero at rest; padded rows of
+// wpr words, frame stride bits_fstride words)
+int launch_prep(const int16_t *raw, int64_t n, int H, int W, const double *bg, const uint8_t *roi, int y0, int y1,
+                int x0, int x1, int flags, double vmin, double vmax, uint8_t *out, uint8_t *invalid, uint32_t *bits,
+                int64_t bits_fstride, int wpr, hipStream_t s);
+
 // the kernel-selection policy in force on this thread (include/mdx.h,
 // mdx_policy): the running model handle's inside its entry points
 // (PolicyScope), else the thread's own (mdx_policy_set)

@@ -25,12 +25,18 @@ namespace mdx {
 // ---------------------------------------------------------------------------
 // prep
 // ---------------------------------------------------------------------------
-constexpr int PREP_FRAMES_PER_BLOCK = 8;
+constexpr int PREP_FRAMES_PER_BLOCK = 16;
 
+// One thread per cropped pixel (256 consecutive pixels per workgroup) and up
+// to 16 frames, loaded 8 at a time (the background and ROI read once per 16
+// frames); grid (ceil(oh * ow / 256), ceil(n / 16)).  bits (or null): the
+// inpaint workspace's bit images, zero at rest: each invalid pixel ORs its bit
+// (padded row y + 1, bit x + 1 of the row's wpr words).
 __global__ __launch_bounds__(256) void k_prep(const int16_t *__restrict__ raw, int64_t n, int H, int W,
                                               const double *__restrict__ bg, const uint8_t *__restrict__ roi,
                                               int y0, int x0, int oh, int ow, int flags, double vmin,
-                                              double vmax, uint8_t *__restrict__ out, uint8_t *__restrict__ inv) {
+                                              double vmax, uint8_t *__restrict__ out, uint8_t *__restrict__ inv,
+                                              uint32_t *__restrict__ bits, int64_t bits_fstride, int wpr) {
     const int64_t npix = (int64_t)oh * ow;
     const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= npix) return;
@@ -39,17 +45,40 @@ __global__ __launch_bounds__(256) void k_prep(const int16_t *__restrict__ raw, i
     const double b = bg ? bg[si] : 0.0;
     const uint8_t r8 = roi ? roi[si] : (uint8_t)1;
     const int64_t f0 = (int64_t)blockIdx.y * PREP_FRAMES_PER_BLOCK;
-    const int64_t f1 = f0 + PREP_FRAMES_PER_BLOCK < n ? f0 + PREP_FRAMES_PER_BLOCK : n;
+    const int nf = (int)(n - f0 < PREP_FRAMES_PER_BLOCK ? n - f0 : PREP_FRAMES_PER_BLOCK);
     const int64_t fstride = (int64_t)H * W;
-    for (int64_t f = f0; f < f1; ++f) {
-        const int16_t r = raw[f * fstride + si];
-        double v = bg ? b - (double)r : (double)r;       // bground_im - frames (float64)
-        if (roi) v = v * (double)r8;                      // frames * roi
-        if ((flags & 1) && v < vmin) v = 0.0;             // frames[frames < vmin] = 0
-        if ((flags & 2) && v > vmax) v = vmax;            // frames[frames > vmax] = vmax
-        out[f * npix + p] = (uint8_t)(int32_t)v;          // astype(uint8) (truncation)
-        if (inv) inv[f * npix + p] = (uint8_t)((r == 0) * r8);
+    const int16_t *rp = raw + f0 * fstride + si;
+    uint32_t *bp = bits ? bits + f0 * bits_fstride + (int64_t)(y + 1) * wpr + ((x + 1) >> 5) : nullptr;
+    const uint32_t bit = 1u << ((x + 1) & 31);
+    for (int u0 = 0; u0 < nf; u0 += 8) {
+        int16_t r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = u0 + u < nf ? rp[(int64_t)(u0 + u) * fstride] : (int16_t)1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (u0 + u >= nf) break;
+            const int64_t f = f0 + u0 + u;
+            double v = bg ? b - (double)r[u] : (double)r[u];  // bground_im - frames (float64)
+            if (roi) v = v * (double)r8;                      // frames * roi
+            if ((flags & 1) && v < vmin) v = 0.0;             // frames[frames < vmin] = 0
+            if ((flags & 2) && v > vmax) v = vmax;            // frames[frames > vmax] = vmax
+            out[f * npix + p] = (uint8_t)(int32_t)v;          // astype(uint8) (truncation)
+            const bool invalid = r[u] == 0 && r8;
+            if (inv) inv[f * npix + p] = (uint8_t)invalid;
+            if (bp && invalid) atomicOr(bp + (int64_t)(u0 + u) * bits_fstride, bit);
+        }
     }
+}
+
+int launch_prep(const int16_t *raw, int64_t n, int H, int W, const double *bg, const uint8_t *roi, int y0, int y1,
+                int x0, int x1, int flags, double vmin, double vmax, uint8_t *out, uint8_t *invalid, uint32_t *bits,
+                int64_t bits_fstride, int wpr, hipStream_t s) {
+    const int oh = y1 - y0, ow = x1 - x0;
+    dim3 grid((unsigned)ceil_div((int64_t)oh * ow, 256), (unsigned)ceil_div(n, PREP_FRAMES_PER_BLOCK));
+    hipLaunchKernelGGL(k_prep, grid, dim3(256), 0, s, raw, n, H, W, bg, roi, y0, x0, oh, ow, flags, vmin, vmax, out,
+                       invalid, bits, bits_fstride, wpr);
+    MDX_CHECK_LAUNCH("mdx_prep_frames");
+    return MDX_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1041,11 +1070,9 @@ extern "C" int mdx_prep_frames(const int16_t *raw, int64_t n, int H, int W, cons
                 "mdx_prep_frames: bad crop [%d,%d)x[%d,%d) for %dx%d", y0, y1, x0, x1, H, W);
     const int oh = y1 - y0, ow = x1 - x0;
     if (n == 0 || oh == 0 || ow == 0) return MDX_OK;
-    dim3 grid((unsigned)ceil_div((int64_t)oh * ow, 256), (unsigned)ceil_div(n, PREP_FRAMES_PER_BLOCK));
-    hipLaunchKernelGGL(k_prep, grid, dim3(256), 0, as_stream(stream), raw, n, H, W, bg, roi, y0, x0, oh, ow, flags,
-                       vmin, vmax, out, invalid);
-    MDX_CHECK_LAUNCH("mdx_prep_frames");
-    return MDX_OK;
+    MDX_REQUIRE(ceil_div(n, PREP_FRAMES_PER_BLOCK) <= 65535, "mdx_prep_frames: too many frames");
+    return launch_prep(raw, n, H, W, bg, roi, y0, y1, x0, x1, flags, vmin, vmax, out, invalid, nullptr, 0, 0,
+                       as_stream(stream));
 }
 
 extern "C" int mdx_build_scale_lut(double vmin, double vmax, int int_vmin, uint8_t lut[256]) {

@@ -149,15 +149,19 @@ class FramePrep:
         oh, ow = y1 - y0, x1 - x0
         if out is None:
             out = torch.empty((n, oh, ow), dtype=torch.uint8, device=raw.device)
-        need_inv = self.fix_invalid_pixels or return_invalid
         inv = None
-        if need_inv:
+        if return_invalid:
             inv = invalid_out if invalid_out is not None else torch.empty_like(out)
         flags = (1 if self.vmin is not None else 0) | (2 if self.vmax is not None else 0)
-        call("mdx_prep_frames", _ptr(raw), n, H, W, _ptr(self.bg), _ptr(self.roi), y0, y1, x0, x1, flags,
-             float(self.vmin or 0.0), float(self.vmax or 0.0), _ptr(out), _ptr(inv), _stream())
-        if self.fix_invalid_pixels:
-            fill_invalid_pixels(out, inv, _workspace_owner=self)
+        args = (_ptr(raw), n, H, W, _ptr(self.bg), _ptr(self.roi), y0, y1, x0, x1, flags, float(self.vmin or 0.0),
+                float(self.vmax or 0.0), _ptr(out), _ptr(inv))
+        if self.fix_invalid_pixels and n > 0 and oh > 0 and ow > 0:
+            # one call: the invalid pixels go straight to the inpaint
+            # workspace as bit images (mdx_prep_inpaint)
+            ws = _inpaint_workspace(self, n, oh, ow, raw.device)
+            call("mdx_prep_inpaint", *args, 3, _ptr(ws), _ptr(_error_counter(self, raw.device)), _stream())
+        else:
+            call("mdx_prep_frames", *args, _stream())
         if return_invalid:
             return _ret(out, as_np), _ret(inv, as_np)
         return _ret(out, as_np)
@@ -179,6 +183,29 @@ def find_invalid_pixels(frames):
     return inv
 
 
+def _inpaint_workspace(owner, n, H, W, device):
+    """The owner's inpaint workspace for n frames of H x W (a fresh one if no
+    owner): sparse per-frame slots, set up once per frame shape; each call
+    leaves it ready for the next (mdx_inpaint_workspace_init)."""
+    torch = _torch()
+    nbytes = call("mdx_inpaint_workspace_bytes", n, H, W)
+    ws = getattr(owner, "_ws", None) if owner is not None else None
+    if ws is None or ws.numel() < nbytes or getattr(owner, "_ws_shape", None) != (H, W):
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        call("mdx_inpaint_workspace_init", _ptr(ws), ws.numel(), H, W, _stream())
+        if owner is not None:
+            owner._ws, owner._ws_shape = ws, (H, W)
+    return ws
+
+
+def _error_counter(owner, device):
+    """The owner's own device count of unconverged inpaint frames."""
+    if getattr(owner, "_errors", None) is None:
+        owner._errors = _torch().zeros((1,), dtype=_torch().int32, device=device)
+    return owner._errors
+
+
 def fill_invalid_pixels(frames, invalid_mask, _workspace_owner=None):
     """In-place NS inpaint of every frame (cv2.inpaint(f, m, 3, INPAINT_NS)),
     M/proc/proc.py:189-210.  Device tensors are filled in place; numpy input
@@ -192,18 +219,10 @@ def fill_invalid_pixels(frames, invalid_mask, _workspace_owner=None):
     if tuple(m.shape) != tuple(f.shape):
         raise AssertionError("frames and invalid_mask shapes differ")
     n, H, W = f.shape
-    nbytes = call("mdx_inpaint_workspace_bytes", n, H, W)
-    owner = _workspace_owner
-    ws = getattr(owner, "_ws", None) if owner is not None else None
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=f.device)
-        if owner is not None:
-            owner._ws = ws
-    err = None
-    if owner is not None:  # the owner's own non-convergence counter (FramePrep.inpaint_errors)
-        if getattr(owner, "_errors", None) is None:
-            owner._errors = torch.zeros((1,), dtype=torch.int32, device=f.device)
-        err = owner._errors
+    if n == 0:
+        return _ret(f, as_np)
+    ws = _inpaint_workspace(_workspace_owner, n, H, W, f.device)
+    err = _error_counter(_workspace_owner, f.device) if _workspace_owner is not None else None
     call("mdx_inpaint_ns_counted", _ptr(f), _ptr(m), n, H, W, 3, _ptr(ws), _ptr(err), _stream())
     return _ret(f, as_np)
 

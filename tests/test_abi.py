@@ -44,6 +44,23 @@ def test_host_only_entry_points(mdx):
     assert mdx.lib().mdx_version().decode().startswith("mdx")
 
 
+def test_inpaint_workspace_is_sparse(mdx):
+    """The inpaint workspace of a 423 x 511 extract frame (512 x 424 ROI crop)
+    stays under 1 MB per frame at batch 32 and 1024 (sparse per-frame slots
+    plus one shared full-size slot), with room for about 4 % of the frame's
+    pixels per frame in the sparse slot."""
+    from moseq2_detectron_extract_amd._lib import call
+    H, W = 423, 511
+    for n in (32, 1024):
+        per_frame = call("mdx_inpaint_workspace_bytes", n, H, W) / n
+        assert per_frame < (1 << 20) * (1.5 if n == 32 else 1.0), (n, per_frame)
+    slope = (call("mdx_inpaint_workspace_bytes", 1024, H, W) - call("mdx_inpaint_workspace_bytes", 32, H, W)) / 992
+    assert slope < 1e6
+    cap = call("mdx_inpaint_sparse_capacity", H, W)
+    assert 0.04 * H * W <= cap <= 0.05 * H * W
+    assert call("mdx_inpaint_workspace_bytes", 0, H, W) == 0
+
+
 def test_no_gpu_means_loud_failure(mdx):
     import numpy as np
     import torch

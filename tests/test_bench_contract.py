@@ -52,12 +52,12 @@ def test_committed_roofline_agrees_with_rocprof():
     import json
     b = _bench()
     prof = os.path.join(ROOT, "profiles")
-    line = json.load(open(os.path.join(prof, "r05_bench.json")))
+    line = json.load(open(os.path.join(prof, "r06_bench.json")))
     roof = line["roofline"]
     top = roof["kernels"][0]
     per_launch_ms = top["ms_per_step"] / top["launches_per_step"]
     demangled = b.KERNEL_DEMANGLED.get(top["symbol"], top["symbol"])
-    rows = {r["Name"]: r for r in csv.DictReader(open(os.path.join(prof, "r05_kernel_stats_fp32_serial.csv")))}
+    rows = {r["Name"]: r for r in csv.DictReader(open(os.path.join(prof, "r06_kernel_stats_fp32_serial.csv")))}
     assert demangled in rows, demangled
     avg_ms = float(rows[demangled]["AverageNs"]) / 1e6
     assert abs(avg_ms / per_launch_ms - 1) < 0.05, (avg_ms, per_launch_ms)

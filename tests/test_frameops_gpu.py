@@ -58,6 +58,15 @@ def test_prep_with_inpaint(mdx, roi_kind):
     out = proc.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100)
     ref, _ = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100, fix_invalid_pixels=True)
     np.testing.assert_array_equal(out, ref)
+    # the fused call (mdx_prep_inpaint) with the byte mask requested too, on
+    # a prep whose workspace is reused for another batch size
+    _, rinv = O.prep_raw_frames(raw, s.bground_im, s.roi, 0, 100, fix_invalid_pixels=False)
+    prep = proc.FramePrep(s.bground_im, s.roi, 0, 100, fix_invalid_pixels=True)
+    for sl in (slice(0, 6), slice(1, 4), slice(0, 6)):
+        got, inv = prep(raw[sl], return_invalid=True)
+        np.testing.assert_array_equal(got, ref[sl])
+        np.testing.assert_array_equal(inv, rinv[sl])
+    assert prep.inpaint_errors() == 0
 
 
 def test_clean_frames(mdx, session, raw):
@@ -191,6 +200,106 @@ def test_inpaint_dense_holes(mdx, p, seed):
     want = O.inpaint_ns(f, m)
     np.testing.assert_array_equal(got, want)
     assert call("mdx_inpaint_errors", 1) == 0
+
+
+def test_inpaint_sparse_and_dense_slots(mdx):
+    """One call holding frames within the sparse slots' capacity (scattered
+    pixels, one-pixel clusters, a small hole, invalid pixels on the first row
+    and column) and frames over it (done in the shared dense slot: dense noise,
+    a big blob, a fully invalid frame, one just over the capacity), then more
+    calls on the same workspace with other masks and frame counts: each equals
+    the serial oracle, so every call left the workspace at rest."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    from moseq2_detectron_extract_amd._lib import call
+    H, W = 90, 120
+    cap = call("mdx_inpaint_sparse_capacity", H, W)
+    assert 256 <= cap < H * W // 10
+    rng = np.random.default_rng(31)
+
+    def masks(n):
+        m = np.zeros((n, H, W), np.uint8)
+        kinds = rng.permutation(n)
+        for f in range(n):
+            k = kinds[f] % 8
+            if k == 0:
+                m[f] = rng.random((H, W)) < 0.01
+            elif k == 1:
+                m[f] = rng.random((H, W)) < 0.2
+            elif k == 2:
+                m[f, 20:40, 30:80] = 1
+            elif k == 3:
+                m[f] = 1
+            elif k == 4:  # exactly one over the capacity, scattered
+                m[f].flat[rng.choice(H * W, cap + 1, replace=False)] = 1
+            elif k == 5:  # exactly the capacity
+                m[f].flat[rng.choice(H * W, cap, replace=False)] = 1
+            elif k == 6:
+                m[f, 0, ::7] = 1
+                m[f, ::5, 0] = 1
+                m[f, 50:53, 60:62] = 1
+            # k == 7: nothing to fill
+        return m
+
+    class Owner:
+        _ws = None
+        _errors = None
+
+    owner = Owner()
+    call("mdx_inpaint_errors", 1)
+    for n in (8, 8, 3, 16):
+        f = rng.integers(0, 100, size=(n, H, W), dtype=np.uint8)
+        m = masks(n)
+        got = proc.fill_invalid_pixels(f.copy(), m, _workspace_owner=owner)
+        np.testing.assert_array_equal(got, O.inpaint_ns(f, m), err_msg=f"n={n}")
+    assert call("mdx_inpaint_errors", 1) == 0
+    assert int(owner._errors.item()) == 0
+
+
+@pytest.mark.parametrize("shape", [(2, 1030, 1030), (3, 7, 1000), (2, 600, 9), (4, 1, 1), (2, 3, 3)])
+def test_inpaint_frame_shapes(mdx, shape):
+    """Frames whose bit image does not fit the setup workgroup's LDS (all done
+    in the dense slot), long thin and tiny frames: equal to the serial
+    oracle."""
+    from oracle import frameops as O
+    from moseq2_detectron_extract_amd import proc
+    from moseq2_detectron_extract_amd._lib import call
+    rng = np.random.default_rng(sum(shape))
+    f = rng.integers(0, 200, size=shape, dtype=np.uint8)
+    m = (rng.random(shape) < 0.01).astype(np.uint8)
+    if shape[1] * shape[2] < 100000:
+        m[0].flat[::3] = 1
+    call("mdx_inpaint_errors", 1)
+    got = proc.fill_invalid_pixels(f.copy(), m)
+    np.testing.assert_array_equal(got, O.inpaint_ns(f, m))
+    assert call("mdx_inpaint_errors", 1) == 0
+
+
+def test_inpaint_workspace_not_set_up_is_counted(mdx):
+    """A workspace that was not set up for the frame shape: the frames are
+    left as they are and each one is counted (device and caller counters)."""
+    import ctypes
+    import torch
+    from moseq2_detectron_extract_amd._lib import call
+    H, W, n = 40, 50, 3
+    f = torch.randint(0, 100, (n, H, W), dtype=torch.uint8, device="cuda")
+    m = (torch.rand((n, H, W), device="cuda") < 0.05).to(torch.uint8)
+    ws = torch.zeros(call("mdx_inpaint_workspace_bytes", n, H, W), dtype=torch.uint8, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    before = f.clone()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    call("mdx_inpaint_errors", 1)
+    call("mdx_inpaint_ns_counted", p(f), p(m), n, H, W, 3, p(ws), p(err), s)
+    torch.cuda.synchronize()
+    assert torch.equal(f, before)
+    assert int(err.item()) == n and call("mdx_inpaint_errors", 1) == n
+    # set up for another shape: the same
+    call("mdx_inpaint_workspace_init", p(ws), ws.numel(), H + 1, W, s)
+    call("mdx_inpaint_ns_counted", p(f), p(m), n, H, W, 3, p(ws), p(err), s)
+    torch.cuda.synchronize()
+    assert torch.equal(f, before) and int(err.item()) == 2 * n
+    call("mdx_inpaint_errors", 1)
 
 
 def test_inpaint_long_chain_converges(mdx):

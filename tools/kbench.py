@@ -63,7 +63,7 @@ def main():
         "moments_in_kernel_pack": moments_nows,
         "prep_noinpaint": lambda: prep_noinp(raw),
         "prep_inpaint": lambda: prep(raw),
-        "inpaint_only": lambda: proc.fill_invalid_pixels(p0.clone(), inv),
+        "inpaint_only": lambda: proc.fill_invalid_pixels(p0.clone(), inv, _workspace_owner=prep_noinp),
         "clean": lambda: proc.clean_frames(prepped, iters_tail=3),
         "median_only": lambda: proc.clean_frames(prepped, iters_tail=0),
         "moments": lambda: proc.frame_moments(cleaned, mask, 3.0),
