@@ -46,14 +46,15 @@ HOST_FLAGS = {"host_tracking.hip": ["-Xarch_host", "-mavx2", "-Xarch_host", "-mf
 # bf16 MFMA loop, never alone or beside f32 MFMAs; the plain, broadcast,
 # multiply and FMA packed forms never fault).  With the forms, the fp16
 # pipelined loop differed from the serial step in 133 of 150 steps.
-# conv.hip and inpaint.hip keep the packed forms: every packed instruction
-# they compile to is one of the forms tools/native/pk_hazard.hip cleared
+# inpaint.hip (its serial tap sums would pack with SGPR operands) is also
+# compiled without them.  conv.hip keeps the packed forms: every packed
+# instruction it compiles to is one of the forms tools/native/pk_hazard.hip cleared
 # beside 16-bit MFMAs, which build() checks on every library it links
 # (_isa_lint.py, a whitelist; the build fails on anything else).  The
 # target-feature switch reaches the host compile too, where clang ignores it
 # with a warning.
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
-DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32, "wino_fused.hip": NO_PACKED_FP32}
+DEVICE_FLAGS = {"model_ops.hip": NO_PACKED_FP32, "inpaint.hip": NO_PACKED_FP32}
 
 
 def sources(csrc: str = CSRC):

@@ -25,11 +25,11 @@ namespace mdx {
 // ---------------------------------------------------------------------------
 // prep
 // ---------------------------------------------------------------------------
-constexpr int PREP_FRAMES_PER_BLOCK = 16;
+constexpr int PREP_FRAMES_PER_BLOCK = 32;
 
 // One thread per cropped pixel (256 consecutive pixels per workgroup) and up
-// to 16 frames, loaded 8 at a time (the background and ROI read once per 16
-// frames); grid (ceil(oh * ow / 256), ceil(n / 16)).  bits (or null): the
+// to 32 frames, loaded 8 at a time (the background and ROI read once per 32
+// frames); grid (ceil(oh * ow / 256), ceil(n / 32)).  bits (or null): the
 // inpaint workspace's bit images, zero at rest: each invalid pixel ORs its bit
 // (padded row y + 1, bit x + 1 of the row's wpr words).
 __global__ __launch_bounds__(256) void k_prep(const int16_t *__restrict__ raw, int64_t n, int H, int W,

@@ -48,7 +48,14 @@ namespace mdx {
 
 constexpr int INP_SETUP_THREADS = 512, INP_DENSE_THREADS = 1024;
 constexpr int INP_LDS_MAX = 150 * 1024;  // bit image + word ranks + labels of one frame
-constexpr int INP_MARCH_BLOCKS = 16, MARCH_WAVES = 4, DENSE_WAVES = INP_DENSE_THREADS / 64, MAX_TAPS = 15 * 15;
+#ifndef MDX_INP_MARCH_BLOCKS
+#define MDX_INP_MARCH_BLOCKS 64
+#endif
+#ifndef MDX_INP_MARCH_WAVES
+#define MDX_INP_MARCH_WAVES 1
+#endif
+constexpr int INP_MARCH_BLOCKS = MDX_INP_MARCH_BLOCKS, MARCH_WAVES = MDX_INP_MARCH_WAVES;
+constexpr int DENSE_WAVES = INP_DENSE_THREADS / 64, MAX_TAPS = 15 * 15;
 constexpr int INP_HDR = 16;        // ints of a slot header
 constexpr int INP_GLOBAL = 256;    // bytes of the workspace header
 constexpr int INP_MAGIC = 0x4d445049;
@@ -279,26 +286,34 @@ __device__ __forceinline__ void rest_pixel(const Slot<Idx> &S, int j, int PW) {
 // frames whose label propagation ended unconverged (see setup_body)
 __device__ unsigned int g_inp_errors = 0;
 
-// "is (k, l) an unknown pixel not yet filled": the global plane, or the bit
-// image in LDS (one-pixel clusters: nothing in their window changes)
+// A march's view of the frame: "is (k, l) an unknown pixel not yet filled"
+// (padded coordinates) and the current value of unpadded pixel (r, c).  The
+// global plane and frame; the bit image in LDS (one-pixel clusters: nothing in
+// their window changes); a cluster's window staged in LDS (WinState).
 template <typename Idx>
 struct PlaneState {
     const Idx *plane;
     int PW;
+    const uint8_t *out;
+    int W;
     __device__ __forceinline__ bool unknown(int k, int l) const { return plane[k * PW + l] > 0; }
+    __device__ __forceinline__ int px(int r, int c) const { return out[r * W + c]; }
 };
 struct BitState {
     const uint32_t *bits;
     int wpr;
+    const uint8_t *out;
+    int W;
     __device__ __forceinline__ bool unknown(int k, int l) const { return (bits[k * wpr + (l >> 5)] >> (l & 31)) & 1u; }
+    __device__ __forceinline__ int px(int r, int c) const { return out[r * W + c]; }
 };
 
 // One NS window tap (k, l) around the pixel (i, j) being filled: returns the
 // weight w and the product w * I exactly as the serial loop forms them (0, 0
 // for a tap the loop skips, an exact no-op in its running sums).
 template <typename U>
-__device__ __forceinline__ void ns_tap(int k, int l, int i, int j, int range, int PH, int PW, int W, const U &u,
-                                       const uint8_t *out, float &w_out, float &wi_out) {
+__device__ __forceinline__ void ns_tap(int k, int l, int i, int j, int range, int PH, int PW, const U &u,
+                                       float &w_out, float &wi_out) {
     w_out = 0.f;
     wi_out = 0.f;
     const int km = k - 1 + (k == 1), kp = k - 1 - (k == PH - 2);
@@ -314,23 +329,23 @@ __device__ __forceinline__ void ns_tap(int k, int l, int i, int j, int range, in
     float gx, gy;
     if (dn_ok) {
         if (up_ok)
-            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm]) + abs(out[kp * W + lm] - out[(km - 1) * W + lm]));
+            gx = (float)(abs(u.px(kp + 1, lm) - u.px(kp, lm)) + abs(u.px(kp, lm) - u.px(km - 1, lm)));
         else
-            gx = (float)(abs(out[(kp + 1) * W + lm] - out[kp * W + lm])) * 2.0f;
+            gx = (float)(abs(u.px(kp + 1, lm) - u.px(kp, lm))) * 2.0f;
     } else {
         if (up_ok)
-            gx = (float)(abs(out[kp * W + lm] - out[(km - 1) * W + lm])) * 2.0f;
+            gx = (float)(abs(u.px(kp, lm) - u.px(km - 1, lm))) * 2.0f;
         else
             gx = 0;
     }
     if (rt_ok) {
         if (lf_ok)
-            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm]) + abs(out[km * W + lm] - out[km * W + lm - 1]));
+            gy = -(float)(abs(u.px(km, lp + 1) - u.px(km, lm)) + abs(u.px(km, lm) - u.px(km, lm - 1)));
         else
-            gy = -(float)(abs(out[km * W + lp + 1] - out[km * W + lm])) * 2.0f;
+            gy = -(float)(abs(u.px(km, lp + 1) - u.px(km, lm))) * 2.0f;
     } else {
         if (lf_ok)
-            gy = -(float)(abs(out[km * W + lm] - out[km * W + lm - 1])) * 2.0f;
+            gy = -(float)(abs(u.px(km, lm) - u.px(km, lm - 1))) * 2.0f;
         else
             gy = 0;
     }
@@ -340,13 +355,34 @@ __device__ __forceinline__ void ns_tap(int k, int l, int i, int j, int range, in
     if (!(dir > 0.01f)) dir = 0.000001f;
     const float w = dst * dir;
     w_out = w;
-    wi_out = w * (float)out[km * W + lm];
+    wi_out = w * (float)u.px(km, lm);
 }
 
 __device__ __forceinline__ uint8_t ns_value(float Ia, float sw) {
     const double v = (double)Ia / sw;
     const int r = __double2int_rn(v);
     return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+}
+
+// The window of the pixel (i, j) being filled, one tap per lane (up to 4 taps
+// a lane for range 7) into the wave's LDS rows tw / twi, summed by lane 0 in
+// the serial loop's (k, l) order: the serial loop's float sums (valid in lane
+// 0 only).
+template <typename U>
+__device__ __forceinline__ void wave_tap_sum(const U &u, int i, int j, int range, int PH, int PW, float *tw,
+                                             float *twi, float &Ia, float &sw) {
+    const int lane = threadIdx.x & 63;
+    const int wside = 2 * range + 1, ntaps = wside * wside;
+    for (int tp = lane; tp < ntaps; tp += 64)
+        ns_tap(i - range + tp / wside, j - range + tp % wside, i, j, range, PH, PW, u, tw[tp], twi[tp]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    Ia = 0.0f;
+    sw = 1.0e-20f;
+    if (lane == 0)
+        for (int tp = 0; tp < ntaps; ++tp) {
+            Ia += twi[tp];
+            sw += tw[tp];
+        }
 }
 
 // a one-pixel cluster at padded (i, j), by one thread: the taps summed in the
@@ -359,7 +395,7 @@ __device__ void fill_single(const U &u, int i, int j, uint8_t *out, int H, int W
         float Ia = 0.0f, sw = 1.0e-20f;
         for (int tp = 0; tp < ntaps; ++tp) {
             float w, wi;
-            ns_tap(i - range + tp / wside, j - range + tp % wside, i, j, range, PH, PW, W, u, out, w, wi);
+            ns_tap(i - range + tp / wside, j - range + tp % wside, i, j, range, PH, PW, u, w, wi);
             Ia += wi;
             sw += w;
         }
@@ -496,7 +532,7 @@ __device__ int setup_body(const Slot<Idx> &S, int nin, uint8_t *out, int H, int 
     for (int c = tid; c < ncl; c += NT) {
         if (S.start[c + 1] - S.start[c] == 1) {
             const int j = S.ins[S.ord[S.start[c]]];
-            fill_single(PlaneState<Idx>{S.plane, PW}, j / PW, j - j / PW * PW, out, H, W, range);
+            fill_single(PlaneState<Idx>{S.plane, PW, out, W}, j / PW, j - j / PW * PW, out, H, W, range);
             rest_pixel(S, j, PW);
         } else
             S.fill[atomicAdd(&s_multi, 1)] = c;
@@ -537,6 +573,95 @@ __device__ __forceinline__ bool has_other(const uint32_t *bits, int wpr, int y, 
         if (sp) return true;
     }
     return false;
+}
+
+// fill_single for a compile-time radius on the bit image: the (2R+3)^2 pixel
+// box and the (2R+3)^2 state bits around the pixel loaded once into registers
+// (every load issued up front), the taps unrolled with the serial loop's
+// arithmetic (weights of taps the serial loop skips are 0: exact no-ops in
+// its running sums; the distance factors fold to the same constants).
+// box[r][c] = out[i - R - 2 + r][j - R - 2 + c] (unpadded, clamped: the
+// clamped entries are the ones no tap reads); bit (r, c) of sb = padded
+// (i - R - 1 + r, j - R - 1 + c) unknown.
+template <int R>
+__device__ void fill_single_box(const uint32_t *bits, int wpr, int i, int j, uint8_t *out, int H, int W) {
+    const int PH = H + 2, PW = W + 2;
+    if (!(i > 1 && j > 1)) return;  // the serial loop never fills the first row / column
+    constexpr int WS = 2 * R + 1, BS = WS + 2;
+    int box[BS][BS];
+    const int r0 = i - R - 2, c0 = j - R - 2;
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+        const int rr = min(max(r0 + r, 0), H - 1);
+#pragma unroll
+        for (int c = 0; c < BS; ++c) box[r][c] = out[rr * W + min(max(c0 + c, 0), W - 1)];
+    }
+    uint32_t sb[BS];  // padded rows i - R - 1 .. i + R + 1, columns j - R - 1 .. j + R + 1
+    {
+        const int xa = j - R - 1, xb = j + R + 1;
+        const int ca = xa > 0 ? xa : 0, cb = xb < PW - 1 ? xb : PW - 1;
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+            const int y = i - R - 1 + r;
+            sb[r] = (y >= 0 && y < PH) ? row_span(bits, wpr, y, ca, cb) << (ca - xa) : 0u;
+        }
+    }
+    float Ia = 0.0f, sw = 1.0e-20f;
+#pragma unroll
+    for (int a = 0; a < WS; ++a) {
+#pragma unroll
+        for (int b = 0; b < WS; ++b) {
+            if ((a - R) * (a - R) + (b - R) * (b - R) > R * R) continue;  // outside the radius: (0, 0)
+            const int k = i - R + a, l = j - R + b;
+            if (!(k > 0 && l > 0 && k < PH - 1 && l < PW - 1)) continue;
+            if ((sb[a + 1] >> (b + 1)) & 1u) continue;  // unknown
+            const bool e0 = k == 1, e1 = k == PH - 2, f0 = l == 1, f1 = l == PW - 2;
+#define BOX(rr, cc) box[rr][cc]
+            const int pA = e1 ? (f0 ? BOX(a + 1, b + 2) : BOX(a + 1, b + 1)) : (f0 ? BOX(a + 2, b + 2) : BOX(a + 2, b + 1));
+            const int pB = e1 ? (f0 ? BOX(a, b + 2) : BOX(a, b + 1)) : (f0 ? BOX(a + 1, b + 2) : BOX(a + 1, b + 1));
+            const int pC = e0 ? (f0 ? BOX(a + 1, b + 2) : BOX(a + 1, b + 1)) : (f0 ? BOX(a, b + 2) : BOX(a, b + 1));
+            const int pD = e0 ? (f1 ? BOX(a + 2, b + 1) : BOX(a + 2, b + 2)) : (f1 ? BOX(a + 1, b + 1) : BOX(a + 1, b + 2));
+            const int pE = e0 ? (f0 ? BOX(a + 2, b + 2) : BOX(a + 2, b + 1)) : (f0 ? BOX(a + 1, b + 2) : BOX(a + 1, b + 1));
+            const int pF = e0 ? (f0 ? BOX(a + 2, b + 1) : BOX(a + 2, b)) : (f0 ? BOX(a + 1, b + 1) : BOX(a + 1, b));
+#undef BOX
+            const float ry = (float)(a - R), rx = (float)(b - R);
+            const float lr = rx * rx + ry * ry;
+            const float dst = (float)(1. / (lr * sqrt((double)lr)));
+            const bool up_ok = !((sb[a] >> (b + 1)) & 1u), dn_ok = !((sb[a + 2] >> (b + 1)) & 1u);
+            const bool lf_ok = !((sb[a + 1] >> b) & 1u), rt_ok = !((sb[a + 1] >> (b + 2)) & 1u);
+            float gx, gy;
+            if (dn_ok) {
+                if (up_ok)
+                    gx = (float)(abs(pA - pB) + abs(pB - pC));
+                else
+                    gx = (float)(abs(pA - pB)) * 2.0f;
+            } else {
+                if (up_ok)
+                    gx = (float)(abs(pB - pC)) * 2.0f;
+                else
+                    gx = 0;
+            }
+            if (rt_ok) {
+                if (lf_ok)
+                    gy = -(float)(abs(pD - pE) + abs(pE - pF));
+                else
+                    gy = -(float)(abs(pD - pE)) * 2.0f;
+            } else {
+                if (lf_ok)
+                    gy = -(float)(abs(pE - pF)) * 2.0f;
+                else
+                    gy = 0;
+            }
+            const float dot = rx * gx + ry * gy;
+            const float lg = gx * gx + gy * gy;
+            float dir = fabsf(dot / sqrtf(lr * lg));
+            if (!(dir > 0.01f)) dir = 0.000001f;
+            const float w = dst * dir;
+            Ia += w * (float)pE;
+            sw += w;
+        }
+    }
+    out[(i - 1) * W + (j - 1)] = ns_value(Ia, sw);
 }
 
 // Per-frame setup, one workgroup per frame, on the frame's bit image in LDS.
@@ -712,29 +837,25 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(uint8_t *__rest
         __syncthreads();
         for (int cl = tid; cl < ncl; cl += NT) S.cnt[cl] = 0;
         __syncthreads();
-        const BitState bs{bits, wpr};
+        // member lists: list index (S.ord) and padded pixel (S.fill); the
+        // march marks the plane itself for the clusters it cannot window
         for (int k = tid; k < nin; k += NT) {
             if (lab[k] < 0) continue;
             const int cl = S.lab[k];
             const int slot = atomicAdd(&S.cnt[cl], 1);
             S.ord[S.start[cl] + slot] = k;
-            const int p = S.ins[k];
-            S.plane[p] = (int16_t)(k + 1);
-            S.t[k] = 1.0e6f;
-            const int y = p / PW, x = p - y * PW;
-            const int nb[4][2] = {{y - 1, x}, {y, x - 1}, {y + 1, x}, {y, x + 1}};
-            for (int q = 0; q < 4; ++q) {
-                const int yy = nb[q][0], xx = nb[q][1];
-                if (yy >= 1 && yy <= H && xx >= 1 && xx <= W && !bs.unknown(yy, xx)) S.plane[yy * PW + xx] = -1;
-            }
+            S.fill[S.start[cl] + slot] = S.ins[k];
         }
     }
     // one-pixel clusters, in place
-    const BitState bs{bits, wpr};
+    const BitState bs{bits, wpr, out, W};
     for (int k = tid; k < nin; k += NT)
         if (lab[k] < 0) {
             const int j = S.ins[k];
-            fill_single(bs, j / PW, j - j / PW * PW, out, H, W, range);
+            if (range == 3)  // the extract path's radius
+                fill_single_box<3>(bits, wpr, j / PW, j - j / PW * PW, out, H, W);
+            else
+                fill_single(bs, j / PW, j - j / PW * PW, out, H, W, range);
         }
     if (tid == 0) {
         S.hdr[1] = ncl;
@@ -742,17 +863,17 @@ __global__ __launch_bounds__(INP_SETUP_THREADS) void k_inp_setup(uint8_t *__rest
     }
 }
 
-// One cluster of m > 1 pixels on one wave.  Lane 0 owns the cluster's serial
-// state (member sort, narrow band FIFO, (T, seq) heap); the window of every
-// pixel being filled is evaluated one tap per lane and summed by lane 0 in the
-// serial loop's (k, l) order, so the float sums are the serial ones bit for
-// bit.  The cluster's plane entries are put back to rest at the end.
+// One cluster of m > 1 pixels on one wave, on the global plane and frame.
+// Lane 0 owns the cluster's serial state (member sort, narrow band FIFO, (T,
+// seq) heap); the window of every pixel being filled is evaluated one tap per
+// lane and summed in the serial loop's (k, l) order (wave_tap_sum), so the
+// float sums are the serial ones bit for bit.  The cluster's plane entries are
+// put back to rest at the end.
 template <typename Idx>
 __device__ void march_cluster(const Slot<Idx> &S, int c, uint8_t *out, int H, int W, int range, float *tw,
                               float *twi) {
     const int lane = threadIdx.x & 63;
     const int PH = H + 2, PW = W + 2;
-    const int wside = 2 * range + 1, ntaps = wside * wside;
     const int s0 = S.start[c], m = S.start[c + 1] - s0;
     int *mem = S.ord + s0;
     int *band = S.scr + 7LL * s0;
@@ -814,19 +935,11 @@ __device__ void march_cluster(const Slot<Idx> &S, int c, uint8_t *out, int H, in
             if (i <= 1 || j <= 1 || i > PH - 1 || j > PW - 1) continue;
             const int v = code[i * PW + j];
             if (v <= 0) continue;
-            for (int tp = lane; tp < ntaps; tp += 64) {
-                const int k = i - range + tp / wside, l = j - range + tp % wside;
-                ns_tap(k, l, i, j, range, PH, PW, W, PlaneState<Idx>{code, PW}, out, tw[tp], twi[tp]);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            float Ia, sw;
+            wave_tap_sum(PlaneState<Idx>{code, PW, out, W}, i, j, range, PH, PW, tw, twi, Ia, sw);
             if (lane == 0) {
                 const float dist = min4f(fm_solve(i - 1, j, i, j - 1, S, PW), fm_solve(i + 1, j, i, j - 1, S, PW),
                                          fm_solve(i - 1, j, i, j + 1, S, PW), fm_solve(i + 1, j, i, j + 1, S, PW));
-                float Ia = 0.0f, sw = 1.0e-20f;
-                for (int tp = 0; tp < ntaps; ++tp) {
-                    Ia += twi[tp];
-                    sw += tw[tp];
-                }
                 out[(i - 1) * W + (j - 1)] = ns_value(Ia, sw);
                 S.t[v - 1] = dist;
                 code[i * PW + j] = (Idx)(-v - 1);  // filled: -(k + 2)
@@ -838,17 +951,227 @@ __device__ void march_cluster(const Slot<Idx> &S, int c, uint8_t *out, int H, in
     for (int a = lane; a < m; a += 64) rest_pixel(S, S.ins[mem[a]], PW);
 }
 
+// A small cluster's march in LDS: the window of padded pixels within range + 1
+// of the cluster's bounding box (every state and pixel value the march reads)
+// staged per wave, marched with the global march's exact arithmetic and
+// order, the filled values written back.  Window states: 0 KNOWN, -1 band,
+// a + 1 member a (sorted list) not yet filled, -(a + 2) filled.
+constexpr int WIN_MAX = 1024, WIN_MMAX = 64;
+struct WinLds {
+    int16_t code[WIN_MAX];
+    uint8_t px[WIN_MAX];
+    float tm[WIN_MMAX];
+    int mem[WIN_MMAX], mloc[WIN_MMAX];
+    int band[4 * WIN_MMAX];
+    HEnt heap[WIN_MMAX];
+    float tw[MAX_TAPS], twi[MAX_TAPS];
+};
+
+struct WinState {
+    const int16_t *code;
+    const uint8_t *pxv;
+    int wy0, wx0, ww;
+    __device__ __forceinline__ bool unknown(int k, int l) const { return code[(k - wy0) * ww + (l - wx0)] > 0; }
+    __device__ __forceinline__ int px(int r, int c) const { return pxv[(r + 1 - wy0) * ww + (c + 1 - wx0)]; }
+};
+
+__device__ __forceinline__ float win_t(const WinLds &w, int li) {
+    const int v = w.code[li];
+    return v == 0 ? 1.0e6f : (v == -1 ? 0.0f : w.tm[v > 0 ? v - 1 : -v - 2]);
+}
+
+__device__ __forceinline__ float win_fm_solve(const WinLds &w, int l1, int l2) {
+    double sol;
+    const double a11 = win_t(w, l1), a22 = win_t(w, l2);
+    const double m12 = a11 < a22 ? a11 : a22;
+    const bool in1 = w.code[l1] > 0, in2 = w.code[l2] > 0;
+    if (!in1) {
+        if (!in2) {
+            if (fabs(a11 - a22) >= 1.0)
+                sol = 1 + m12;
+            else
+                sol = (a11 + a22 + sqrt((double)(2 - (a11 - a22) * (a11 - a22)))) * 0.5;
+        } else
+            sol = 1 + a11;
+    } else if (!in2)
+        sol = 1 + a22;
+    else
+        sol = 1 + m12;
+    return (float)sol;
+}
+
+// false (nothing done) when the cluster or its window is too large.  The
+// window's states come from the member pixels alone (S.fill[s0, s0 + m),
+// written by k_inp_setup): members, then their interior 4-neighbours as the
+// band; no other unknown pixel lies within reach of the march.
+template <typename Idx>
+__device__ bool march_window(const Slot<Idx> &S, int s0, int m, uint8_t *out, int H, int W, int range, WinLds &w) {
+    const int lane = threadIdx.x & 63;
+    const int PH = H + 2, PW = W + 2;
+    if (m > WIN_MMAX) return false;
+    int ymin = 1 << 30, ymax = -1, xmin = 1 << 30, xmax = -1;
+    for (int a = lane; a < m; a += 64) {
+        const int j = S.fill[s0 + a], y = j / PW, x = j - y * PW;
+        w.mem[a] = j;
+        ymin = y < ymin ? y : ymin;
+        ymax = y > ymax ? y : ymax;
+        xmin = x < xmin ? x : xmin;
+        xmax = x > xmax ? x : xmax;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ymin = min(ymin, __shfl_xor(ymin, o));
+        ymax = max(ymax, __shfl_xor(ymax, o));
+        xmin = min(xmin, __shfl_xor(xmin, o));
+        xmax = max(xmax, __shfl_xor(xmax, o));
+    }
+    const int E = range + 1;
+    const int wy0 = ymin - E > 0 ? ymin - E : 0, wy1 = ymax + E < PH - 1 ? ymax + E : PH - 1;
+    const int wx0 = xmin - E > 0 ? xmin - E : 0, wx1 = xmax + E < PW - 1 ? xmax + E : PW - 1;
+    const int ww = wx1 - wx0 + 1, area = (wy1 - wy0 + 1) * ww;
+    if (area > WIN_MAX) return false;
+    for (int li = lane; li < area; li += 64) {
+        const int ly = li / ww, y = wy0 + ly, x = wx0 + li - ly * ww;
+        w.code[li] = 0;
+        w.px[li] = (y >= 1 && y <= H && x >= 1 && x <= W) ? out[(y - 1) * W + (x - 1)] : (uint8_t)0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (lane == 0) {  // members in raster order (pixel index order == list order)
+        for (int a = 1; a < m; ++a) {
+            const int v = w.mem[a];
+            int b = a - 1;
+            while (b >= 0 && w.mem[b] > v) {
+                w.mem[b + 1] = w.mem[b];
+                --b;
+            }
+            w.mem[b + 1] = v;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int a = lane; a < m; a += 64) {
+        const int j = w.mem[a], y = j / PW, x = j - y * PW;
+        const int li = (y - wy0) * ww + (x - wx0);
+        w.mloc[a] = li;
+        w.code[li] = (int16_t)(a + 1);
+        w.tm[a] = 1.0e6f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int a = lane; a < m; a += 64) {  // the band: interior 4-neighbours that are not members
+        const int li = w.mloc[a], ly = li / ww, y = wy0 + ly, x = wx0 + li - ly * ww;
+        const int nb[4] = {li - ww, li - 1, li + 1, li + ww};
+        const int ny[4] = {y - 1, y, y, y + 1}, nx[4] = {x, x - 1, x + 1, x};
+        for (int q = 0; q < 4; ++q)
+            if (ny[q] >= 1 && ny[q] <= H && nx[q] >= 1 && nx[q] <= W && w.code[nb[q]] <= 0) w.code[nb[q]] = -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    int nb = 0;
+    if (lane == 0) {  // this cluster's narrow band, raster order, unique
+        for (int a = 0; a < m; ++a) {
+            const int i = w.mloc[a];
+            const int cand[4] = {i - ww, i - 1, i + 1, i + ww};
+            for (int q = 0; q < 4; ++q) {
+                const int p = cand[q];
+                if (w.code[p] != -1) continue;
+                int b = nb - 1;
+                bool dup = false;
+                while (b >= 0 && w.band[b] >= p) {
+                    if (w.band[b] == p) {
+                        dup = true;
+                        break;
+                    }
+                    --b;
+                }
+                if (dup) continue;
+                for (int z = nb; z > b + 1; --z) w.band[z] = w.band[z - 1];
+                w.band[b + 1] = p;
+                ++nb;
+            }
+        }
+    }
+    const WinState st{w.code, w.px, wy0, wx0, ww};
+    int head = 0, hn = 0, seq = __shfl(nb, 0);
+    for (;;) {
+        int idx = -1;
+        if (lane == 0) {
+            if (head < nb)
+                idx = w.band[head++];
+            else if (hn > 0)
+                idx = heap_pop(w.heap, hn).idx;
+        }
+        idx = __shfl(idx, 0);
+        if (idx < 0) break;
+        const int iy = idx / ww, ii = wy0 + iy, jj = wx0 + idx - iy * ww;
+        for (int q = 0; q < 4; ++q) {
+            int i, j;
+            if (q == 0) { i = ii - 1; j = jj; }
+            else if (q == 1) { i = ii; j = jj - 1; }
+            else if (q == 2) { i = ii + 1; j = jj; }
+            else { i = ii; j = jj + 1; }
+            if (i <= 1 || j <= 1 || i > PH - 1 || j > PW - 1) continue;
+            const int li = (i - wy0) * ww + (j - wx0);
+            const int v = w.code[li];
+            if (v <= 0) continue;
+            float Ia, sw;
+            wave_tap_sum(st, i, j, range, PH, PW, w.tw, w.twi, Ia, sw);
+            if (lane == 0) {
+                const float dist = min4f(win_fm_solve(w, li - ww, li - 1), win_fm_solve(w, li + ww, li - 1),
+                                         win_fm_solve(w, li - ww, li + 1), win_fm_solve(w, li + ww, li + 1));
+                w.px[li] = ns_value(Ia, sw);
+                w.tm[v - 1] = dist;
+                w.code[li] = (int16_t)(-v - 1);  // filled: -(a + 2)
+                heap_push(w.heap, hn, HEnt{dist, seq++, li});
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+    }
+    for (int a = lane; a < m; a += 64) {
+        const int li = w.mloc[a];
+        const int ly = li / ww, y = wy0 + ly, x = wx0 + li - ly * ww;
+        out[(y - 1) * W + (x - 1)] = w.px[li];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    return true;
+}
+
+// a cluster the window does not hold: its plane entries (members k + 1, T
+// 1e6; their band -1), then the march on the global plane (which puts them
+// back to rest)
+template <typename Idx>
+__device__ void march_global(const Slot<Idx> &S, int c, uint8_t *out, int H, int W, int range, float *tw,
+                             float *twi) {
+    const int lane = threadIdx.x & 63;
+    const int PW = W + 2;
+    const int s0 = S.start[c], m = S.start[c + 1] - s0;
+    for (int a = lane; a < m; a += 64) {
+        const int k = S.ord[s0 + a];
+        S.plane[S.fill[s0 + a]] = (Idx)(k + 1);
+        S.t[k] = 1.0e6f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int a = lane; a < m; a += 64) {
+        const int p = S.fill[s0 + a], y = p / PW, x = p - y * PW;
+        const int nb[4] = {p - PW, p - 1, p + 1, p + PW};
+        const int ny[4] = {y - 1, y, y, y + 1}, nx[4] = {x, x - 1, x + 1, x};
+        for (int q = 0; q < 4; ++q)
+            if (ny[q] >= 1 && ny[q] <= H && nx[q] >= 1 && nx[q] <= W && S.plane[nb[q]] <= 0) S.plane[nb[q]] = (Idx)-1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    march_cluster(S, c, out, H, W, range, tw, twi);
+}
+
 __global__ __launch_bounds__(64 * MARCH_WAVES) void k_inp_march(uint8_t *__restrict__ frames, int range, char *ws,
                                                                  InpLayout L) {
-    __shared__ float s_w[MARCH_WAVES][MAX_TAPS], s_wi[MARCH_WAVES][MAX_TAPS];
+    __shared__ WinLds s_win[MARCH_WAVES];
     if (!ws_ok(ws, L)) return;
     const long long f = blockIdx.y;
     const int wid = threadIdx.x >> 6;
     const Slot<int16_t> S = slot_view<int16_t>(frame_slot(ws, L, f), L.s);
     const int nmulti = S.hdr[2];
     uint8_t *out = frames + f * (long long)L.hw;
-    for (int q = blockIdx.x * MARCH_WAVES + wid; q < nmulti; q += gridDim.x * MARCH_WAVES)
-        march_cluster(S, q, out, L.H, L.W, range, s_w[wid], s_wi[wid]);
+    WinLds &w = s_win[wid];
+    for (int q = blockIdx.x * MARCH_WAVES + wid; q < nmulti; q += gridDim.x * MARCH_WAVES) {
+        const int s0 = S.start[q], m = S.start[q + 1] - s0;
+        if (!march_window(S, s0, m, out, L.H, L.W, range, w)) march_global(S, q, out, L.H, L.W, range, w.tw, w.twi);
+    }
 }
 
 // The frames over the sparse capacity, one after another on one workgroup in

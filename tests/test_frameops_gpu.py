@@ -221,7 +221,7 @@ def test_inpaint_sparse_and_dense_slots(mdx):
         m = np.zeros((n, H, W), np.uint8)
         kinds = rng.permutation(n)
         for f in range(n):
-            k = kinds[f] % 8
+            k = kinds[f] % 10
             if k == 0:
                 m[f] = rng.random((H, W)) < 0.01
             elif k == 1:
@@ -234,10 +234,23 @@ def test_inpaint_sparse_and_dense_slots(mdx):
                 m[f].flat[rng.choice(H * W, cap + 1, replace=False)] = 1
             elif k == 5:  # exactly the capacity
                 m[f].flat[rng.choice(H * W, cap, replace=False)] = 1
-            elif k == 6:
+            elif k == 6:  # pixels on and next to every edge (the taps' border clamps)
                 m[f, 0, ::7] = 1
                 m[f, ::5, 0] = 1
+                m[f, 1, 3::9] = 1
+                m[f, 4::11, 1] = 1
+                m[f, H - 1, 2::8] = 1
+                m[f, 3::7, W - 1] = 1
+                m[f, H - 2, 5::13] = 1
+                m[f, 6::9, W - 2] = 1
                 m[f, 50:53, 60:62] = 1
+            elif k == 8:  # a sparse frame's cluster too large for the march window (100 pixels)
+                m[f, 30:40, 50:60] = 1
+                m[f].flat[rng.choice(H * W, 50, replace=False)] = 1
+            elif k == 9:  # few pixels, window too large: a dotted diagonal (every 2 px) and a ring
+                for t in range(0, 70, 2):
+                    m[f, 5 + t, 10 + t] = 1
+                m[f, 60, 20:100:3] = 1
             # k == 7: nothing to fill
         return m
 
@@ -247,7 +260,7 @@ def test_inpaint_sparse_and_dense_slots(mdx):
 
     owner = Owner()
     call("mdx_inpaint_errors", 1)
-    for n in (8, 8, 3, 16):
+    for n in (10, 10, 3, 20):
         f = rng.integers(0, 100, size=(n, H, W), dtype=np.uint8)
         m = masks(n)
         got = proc.fill_invalid_pixels(f.copy(), m, _workspace_owner=owner)
