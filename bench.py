@@ -613,11 +613,16 @@ def main():
 
     secondary = None
     if not args.no_secondary and args.dtype == "fp32":
-        dt16, ex16, _ = measure(args, "fp16", B, world, rank, raw_host, sess, dist, gather_bufs)
+        dt16, ex16, cfg16 = measure(args, "fp16", B, world, rank, raw_host, sess, dist, gather_bufs)
         secondary = {"fp16": {"value": round(frames_done / dt16, 2), "unit": "frames/s",
                               "ms_per_step": round(dt16 / args.steps * 1e3, 3), "dtype": "fp16",
                               "note": "fp16 MFMA forward (fp32 accumulation), same loop; tolerance vs the fp32 "
                                       "oracle: tests/test_parity_full.py::test_forward_full_frame[50-32-fp16-0-0]"}}
+        if not args.no_roofline:  # its own roofline: the dominant fp16 kernel at the dense fp16 peak
+            per16 = conv_roofline(ex16, raw_host[0].cuda())
+            r16 = roofline_line(per16, "fp16", flops_per_image(cfg16) * B)
+            secondary["fp16"]["roofline"] = {k: r16[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                                 "kernel", "kernels", "all_conv")}
         del ex16
     if not args.no_secondary and args.dtype == "fp32" and not args.no_x6:
         torch.cuda.synchronize()

@@ -103,7 +103,7 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
     parts = []
     if exchange is None:  # two passes around the exchange step (needs torch.distributed initialised)
         exchange = world > 1 and (config.use_tracking or config.select_instances)
-    ok = False
+    err = None
     try:
         if exchange:
             parts = _run_two_pass(src, batches, ex, config, true_depth, finished)
@@ -112,17 +112,26 @@ def extract_session(path: str, bground_im: np.ndarray, roi: np.ndarray, predicto
         else:
             for idx, raw in src.iterate(device=True, batches=batches):
                 parts.append(finished(ex.process_chunk(raw, np.asarray(idx), 0, true_depth)))
-        ok = True
-    finally:
-        t0 = tl.now()
-        src.close()
-        ex.close()
-        if writer is not None:
-            if ok:
+    except BaseException as e:  # propagated below, after the writer and the other ranks know
+        err = e
+    t0 = tl.now()
+    src.close()
+    ex.close()
+    if writer is not None:
+        if err is None:
+            try:
                 writer.close()
-            else:  # the extraction's own exception propagates; the results file is left unfinished
-                writer.abort()
-        tl.add("writer close", -1, t0)
+            except BaseException as e:
+                err = e
+        else:  # the extraction's own exception propagates; the results file is left unfinished
+            writer.abort()
+    tl.add("writer close", -1, t0)
+    if output_dir and world > 1 and not _all_ranks(err is None) and err is None:
+        # every rank completes or fails together: a rank whose writes all went
+        # through still fails when another rank did (its status stays incomplete)
+        err = RuntimeError("extract_session: another rank of the sharded session failed")
+    if err is not None:
+        raise err
     if output_dir:
         if rank == 0:
             status["complete"] = True  # M/extract.py:129-131
@@ -364,12 +373,18 @@ class _GatherWriter:
     round's chunks (one per rank, rank order; rows land at their frame
     indices, TSV rows in per-rank part files joined at close).  `nrounds`
     is the most chunks any rank owns: close() runs the rounds this rank has
-    no chunk for."""
+    no chunk for.  Each round starts with an error flag (a MIN all-reduce):
+    a rank that fails says so in the round it would have sent next
+    (abort()), and every other rank raises in that same round instead of
+    waiting in the gather."""
 
     def __init__(self, local, nrounds: int):
-        self.local, self.nrounds, self.done = local, nrounds, 0
+        self.local, self.nrounds, self.done, self.failed = local, nrounds, 0, False
 
     def _round(self, d) -> None:
+        if not _all_ranks(True):
+            self.failed = True
+            raise RuntimeError(f"sharded session: another rank failed (result round {self.done + 1})")
         got = gather_chunk_results(d)
         self.done += 1
         if self.local is not None:
@@ -387,6 +402,9 @@ class _GatherWriter:
             self.local.close()
 
     def abort(self) -> None:
+        if not self.failed and self.done < self.nrounds:
+            self.failed = True  # this rank's failure, told to the others in its next round
+            _all_ranks(False)
         if self.local is not None:
             self.local.abort()
 

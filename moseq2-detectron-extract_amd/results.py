@@ -21,6 +21,7 @@ every chunk: O(n^2) in the session length); the file bytes are the same.
 """
 from __future__ import annotations
 
+import functools
 import io
 import os
 import struct
@@ -61,9 +62,8 @@ class MemoryH5:
 
     The datasets named in `stream` (the crop stacks: 12.8 KB per frame, the
     bulk of the file) are deflated while the session runs: rows_written(rows)
-    compresses each newly completed prefix of rows (chunks arrive in frame
-    order), so close() only finishes their streams and compresses the small
-    datasets."""
+    compresses each piece of their streams that the rows complete, so close()
+    only finishes their streams and compresses the small datasets."""
 
     def __init__(self, path: Optional[str] = None, stream=("frames", "frames_mask"), level: int = 4):
         self.path = path
@@ -103,22 +103,20 @@ class MemoryH5:
 
     def rows_written(self, rows) -> None:
         """Rows `rows` of the streamed datasets hold their final values:
-        deflate the prefix of rows now complete."""
+        deflate every piece of their streams now complete (wherever it lies:
+        a sharded session's rounds fill the frame range in several places)."""
         keys = [k for k in self._stream_keys if k in self.datasets and self.datasets[k].data.ndim >= 1]
         if not keys:
             return
         n = self.datasets[keys[0]].data.shape[0]
         if self._filled is None:
             self._filled = np.zeros(n, bool)
-        self._filled[np.asarray(rows)] = True
-        done = min(self._streams[k].rows for k in keys) if self._streams else 0
-        upto = done
-        while upto < n and self._filled[upto]:
-            upto += 1
-        if upto == done:
+        rows = np.asarray(rows)
+        if rows.size == 0:
             return
+        self._filled[rows] = True
         for k in keys:
-            self._stream(k).feed(upto)
+            self._stream(k).feed_rows(self._filled, int(rows.min()), int(rows.max()) + 1)
 
     def _stream(self, key):
         if key not in self._streams:
@@ -175,6 +173,34 @@ def _npy_header(a: np.ndarray) -> bytes:
     return hdr.getvalue()
 
 
+def _gf2_times(mat, vec: int) -> int:
+    s, i = 0, 0
+    while vec:
+        if vec & 1:
+            s ^= mat[i]
+        vec >>= 1
+        i += 1
+    return s
+
+
+@functools.lru_cache(maxsize=8)
+def _crc_zeros_op(nbytes: int) -> tuple:
+    """The GF(2) operator (32 columns) that advances a CRC-32 over `nbytes`
+    zero bytes: crc(A || B) = op(len B)(crc(A)) ^ crc(B) (zlib's
+    crc32_combine, restated)."""
+    op = [1 << n for n in range(32)]  # identity
+    sq = [0xEDB88320] + [1 << n for n in range(31)]  # one zero bit
+    for _ in range(3):  # -> one zero byte
+        sq = [_gf2_times(sq, sq[n]) for n in range(32)]
+    while nbytes:
+        if nbytes & 1:
+            op = [_gf2_times(sq, op[n]) for n in range(32)]
+        nbytes >>= 1
+        if nbytes:
+            sq = [_gf2_times(sq, sq[n]) for n in range(32)]
+    return tuple(op)
+
+
 class _DeflateStream:
     """The ``<key>.npy`` member of a C-contiguous array as one raw deflate
     stream built as rows complete: the header, then the body in
@@ -182,45 +208,68 @@ class _DeflateStream:
     (each ends on a sync flush, the last one finishes the stream -- pigz's
     layout), so the compressed bytes do not depend on the order or the
     grouping in which rows arrive (one process or the ranks of a sharded
-    session write the same file); CRC-32 and size run along."""
+    session write the same file).  A piece is deflated as soon as all its
+    rows are in, wherever it lies; the CRC-32 is the pieces' CRCs combined in
+    order at finish."""
 
     def __init__(self, arr: np.ndarray, level: int, pool):
         self.arr, self.level, self.pool = arr, level, pool
         head = _npy_header(arr)
         c = zlib.compressobj(level, zlib.DEFLATED, -15)
-        self.pieces = [c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)]
-        self.crc = zlib.crc32(head)
-        self.size = len(head)
+        self.head = c.compress(head) + c.flush(zlib.Z_SYNC_FLUSH)
+        self.head_crc, self.head_size = zlib.crc32(head), len(head)
         self.rowbytes = arr[0].nbytes if arr.ndim and arr.shape[0] else 0
-        self.off = 0   # body bytes deflated so far (a multiple of _PIECE until finish)
-        self.rows = 0  # rows whose bytes are complete
+        self.nbytes = arr.nbytes if arr.ndim else 0
+        self.npieces = self.nbytes // _PIECE  # whole pieces (the tail is deflated at finish)
+        self.done: Dict[int, tuple] = {}      # piece -> (deflated bytes, crc)
 
     def _body(self) -> memoryview:
         return memoryview(self.arr.reshape(-1).view(np.uint8))
 
-    def feed(self, upto: int) -> None:
-        """Rows [0, upto) are final: deflate the whole pieces they complete."""
-        if upto <= self.rows:
+    def _rows_of(self, i: int):
+        return (i * _PIECE) // self.rowbytes, ((i + 1) * _PIECE - 1) // self.rowbytes + 1
+
+    def feed_rows(self, filled: np.ndarray, r0: int, r1: int) -> None:
+        """Rows [r0, r1) were just written (`filled`: every final row): deflate
+        the whole pieces they touch that are now complete."""
+        if not self.rowbytes:
             return
-        self.rows = upto
-        end = (upto * self.rowbytes) // _PIECE * _PIECE
-        if end > self.off:
-            body = self._body()[self.off:end]
-            self.pieces += _deflate_pieces(body, self.level, self.pool, final=False)
-            self.crc = zlib.crc32(body, self.crc)
-            self.size += len(body)
-            self.off = end
+        i0, i1 = (r0 * self.rowbytes) // _PIECE, min(self.npieces, (r1 * self.rowbytes - 1) // _PIECE + 1)
+        todo = [i for i in range(i0, i1) if i not in self.done and filled[slice(*self._rows_of(i))].all()]
+        if not todo:
+            return
+        body = self._body()
+        res = self.pool.map(lambda i: (_deflate_one(body[i * _PIECE:(i + 1) * _PIECE], self.level, False),
+                                       zlib.crc32(body[i * _PIECE:(i + 1) * _PIECE])), todo)
+        for i, r in zip(todo, res):
+            self.done[i] = r
+
+    def feed(self, upto: int) -> None:
+        """Rows [0, upto) are final."""
+        if self.rowbytes and upto:
+            self.feed_rows(np.arange(self.arr.shape[0]) < upto, 0, upto)
 
     def finish(self):
-        body = self._body()[self.off:] if self.arr.ndim else memoryview(b"")
-        if len(body):
-            self.pieces += _deflate_pieces(body, self.level, self.pool, final=True)
-            self.crc = zlib.crc32(body, self.crc)
-            self.size += len(body)
+        body = self._body() if self.arr.ndim else memoryview(b"")
+        missing = [i for i in range(self.npieces) if i not in self.done]
+        if missing:
+            res = self.pool.map(lambda i: (_deflate_one(body[i * _PIECE:(i + 1) * _PIECE], self.level, False),
+                                           zlib.crc32(body[i * _PIECE:(i + 1) * _PIECE])), missing)
+            for i, r in zip(missing, res):
+                self.done[i] = r
+        pieces, crc = [self.head], self.head_crc
+        op = _crc_zeros_op(_PIECE) if self.npieces else None
+        for i in range(self.npieces):
+            z, c = self.done[i]
+            pieces.append(z)
+            crc = _gf2_times(op, crc) ^ c
+        tail = body[self.npieces * _PIECE:]
+        if len(tail):
+            pieces.append(_deflate_one(tail, self.level, True))
+            crc = _gf2_times(_crc_zeros_op(len(tail)), crc) ^ zlib.crc32(tail)
         else:
-            self.pieces.append(zlib.compressobj(self.level, zlib.DEFLATED, -15).flush(zlib.Z_FINISH))
-        self.off += len(body)
-        return self.pieces, self.crc, self.size
+            pieces.append(zlib.compressobj(self.level, zlib.DEFLATED, -15).flush(zlib.Z_FINISH))
+        return pieces, crc & 0xFFFFFFFF, self.head_size + self.nbytes
 
 
 def save_npz(path: str, arrays: Dict[str, np.ndarray], level: int = 4, workers: int = 0,

@@ -132,10 +132,10 @@ def test_save_npz_parallel_pieces_round_trip(tmp_path, monkeypatch):
 @pytest.mark.parametrize("order", ["in-order", "reversed", "partial"])
 def test_streamed_npz_members(RS, tmp_path, monkeypatch, order):
     """The crop stacks deflated chunk by chunk while the session runs
-    (MemoryH5.rows_written) load back equal to the arrays, with chunks
-    arriving in frame order, in reverse (nothing completes until the first
-    chunk: all compressed at close) and with rows never written (zeros);
-    small pieces so every member spans several."""
+    (MemoryH5.rows_written: every piece as soon as its rows are in, wherever
+    it lies) load back equal to the arrays, with chunks arriving in frame
+    order, in reverse and with rows never written (zeros, compressed at
+    close); small pieces so every member spans several."""
     monkeypatch.setattr(RS, "_PIECE", 4096)
     n, c = 50, 7
     rng = np.random.default_rng(3)
@@ -155,8 +155,11 @@ def test_streamed_npz_members(RS, tmp_path, monkeypatch, order):
         h["frames_mask"][rows] = rng.random((len(rows), 80, 80)) > 0.5
         h["scalars/x"][rows] = rng.random(len(rows))
         h.rows_written(rows)
-    if order == "in-order":
-        assert h._streams["frames"].rows == n  # compressed before close
+    st = h._streams["frames"]
+    if order in ("in-order", "reversed"):  # every whole piece compressed before close
+        assert st.npieces > 3 and len(st.done) == st.npieces
+    else:
+        assert 0 < len(st.done) < st.npieces
     want = {k: v.data.copy() for k, v in h.datasets.items()}
     h.close()
     got = np.load(path)

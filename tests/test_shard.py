@@ -376,6 +376,67 @@ def test_sharded_writer_one_file_equals_one_process(mdx, tmp_path, world, n, chu
     assert z["frames"].shape == (n, 80, 80) and z["frames"].any()
 
 
+def _gather_writer_failing_worker(rank, world, port, q, out_dir, n, chunk, fail_rank, fail_at):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import time
+    from datetime import timedelta
+    import mdx_pkg
+    mdx_pkg.load()
+    from moseq2_detectron_extract_amd.extract import _ChunkWriter, _GatherWriter, shard_chunk_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=120))
+    chunks = _fake_chunks(n, chunk)
+    c0, c1 = shard_chunk_range(len(chunks), world, rank)
+    nrounds = len(range(*shard_chunk_range(len(chunks), world, 0)))
+    local = _ChunkWriter(out_dir, *_writer_args(out_dir, n), parts=world) if rank == 0 else None
+    w = _GatherWriter(local, nrounds)
+    t0 = time.time()
+    res = "ok"
+    try:
+        for i, d in enumerate(chunks[c0:c1]):
+            if rank == fail_rank and i == fail_at:
+                raise ValueError("chunk failed")  # as extract_session: abort() on the way out
+            w.write(d)
+        w.close()
+    except ValueError:
+        w.abort()
+        res = "failed"
+    except RuntimeError as e:
+        assert "another rank failed" in str(e), e
+        w.abort()
+        res = f"raised in round {w.done + 1}"
+    q.put((rank, res, round(time.time() - t0, 1)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,fail_at", [(2, 1, 1), (2, 0, 2), (3, 2, 0)])
+def test_sharded_writer_rank_failure_ends_every_rank(mdx, tmp_path, world, fail_rank, fail_at):
+    """A rank that fails in the middle of a sharded session's result rounds
+    (as extract_session does on a chunk's exception: writer.abort()) makes
+    every other rank raise in that same round, within seconds, instead of
+    waiting in the gather for the process group's timeout; no part file is
+    left behind."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n, chunk = 300, 50
+    procs = [ctx.Process(target=_gather_writer_failing_worker,
+                         args=(r, world, port, q, str(tmp_path), n, chunk, fail_rank, fail_at)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (res, t) for r, res, t in (q.get(timeout=90) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[fail_rank][0] == "failed"
+    others = {got[r][0] for r in range(world) if r != fail_rank}
+    assert others == {f"raised in round {fail_at + 1}"}, got
+    assert max(t for _, t in got.values()) < 60, got
+    assert not [f for f in os.listdir(tmp_path) if ".part" in f]
+
+
 def test_deflate_stream_independent_of_arrival(mdx, tmp_path, monkeypatch):
     """The streamed crop member's bytes are the same whatever groups of rows
     arrive in which order (pieces cut at absolute _PIECE offsets), and equal
