@@ -134,10 +134,11 @@ KERNEL_DEMANGLED = {
     "_ZN3mdx7k_convgIffLi8ELb0EEEvNS_8ConvArgsE":
         "void mdx::k_convg<float, float, 8, false>(mdx::ConvArgs)",
 }
-for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<float, float, BN, DUAL>
-    _m = f"_ZN3mdx9k_conv_sbIffLi{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
-    KERNEL_SYMBOLS["fp32"][_k] = _m
-    KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<float, float, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
+for _k, _bn, _dual in ((18, 128, 0), (19, 64, 0), (20, 128, 1), (21, 64, 1)):  # k_conv_sb<T, T, BN, DUAL>
+    for _dt, _mt, _dm in (("fp32", "ff", "float, float"), ("fp16", "DF16_DF16_", "_Float16, _Float16")):
+        _m = f"_ZN3mdx9k_conv_sbI{_mt}Li{_bn}ELb{_dual}EEEvNS_8ConvArgsE"
+        KERNEL_SYMBOLS[_dt][_k] = _m
+        KERNEL_DEMANGLED[_m] = f"void mdx::k_conv_sb<{_dm}, {_bn}, {'true' if _dual else 'false'}>(mdx::ConvArgs)"
 for _k, _bn in ((22, 128), (23, 64)):  # k_conv_sbg<T, T, BN>: single stage, general layers
     for _dt, _mt, _dm in (("fp32", "ff", "float, float"), ("fp16", "DF16_DF16_", "_Float16, _Float16")):
         _m = f"_ZN3mdx10k_conv_sbgI{_mt}Li{_bn}EEEvNS_8ConvArgsE"
@@ -182,7 +183,7 @@ for _m in (4, 6):
 TRANSFORMS = (12, 13)  # records whose "flop" field holds algorithmic HBM bytes
 PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
-PMC_FILE = {"fp16": "r04_pmc_kernels_fp16.json", "fp32": "r06_pmc_kernels_fp32.json"}
+PMC_FILE = {"fp16": "r06_pmc_kernels_fp16.json", "fp32": "r06_pmc_kernels_fp32.json"}
 # frame kernels per stage (rocprofv3 symbol substrings) for the PMC bytes
 FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k_morph", "k_clean_stream"),
                  "moments": ("k_moments",), "crop": ("k_crop",)}
