@@ -185,7 +185,8 @@ PEAK = {"fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md
 HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
 PMC_FILE = {"fp16": "r06_pmc_kernels_fp16.json", "fp32": "r06_pmc_kernels_fp32.json"}
 # frame kernels per stage (rocprofv3 symbol substrings) for the PMC bytes
-FRAME_KERNELS = {"prep_inpaint": ("k_prep", "k_inp_"), "clean": ("k_median3", "k_morph", "k_clean_stream"),
+FRAME_KERNELS = {"prep_inpaint": ("mdx::k_prep(", "k_inp_"),  # (not the model's k_preprocess_s2d)
+                 "clean": ("k_median3", "k_morph", "k_clean_stream"),
                  "moments": ("k_moments",), "crop": ("k_crop",)}
 
 
