@@ -170,7 +170,11 @@ KERNEL_NAMES = {0: "k_conv<128> register-staged implicit GEMM", 1: "k_conv<64> r
                 21: "k_conv_sb<64, DUAL> conv3 + projection shortcut GEMM, single LDS stage",
                 22: "k_conv_sbg<128> register-staged implicit GEMM, single LDS stage",
                 23: "k_conv_sbg<64> register-staged implicit GEMM, single LDS stage",
-                24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance"}
+                24: "k_conv<128, PW> fp32-output instance", 25: "k_conv<64, PW> fp32-output instance",
+                26: "k_conv16_pp 256x256 fp16 ping-pong implicit GEMM (two wave groups one barrier apart)"}
+KERNEL_SYMBOLS["fp16"][26] = "_ZN3mdx11k_conv16_ppIDF16_EEvNS_8ConvArgsE"
+KERNEL_DEMANGLED["_ZN3mdx11k_conv16_ppIDF16_EEvNS_8ConvArgsE"] = "void mdx::k_conv16_pp<_Float16>(mdx::ConvArgs)"
+KERNEL_DEMANGLED["_ZN3mdx11k_conv16_ppIfEEvNS_8ConvArgsE"] = "void mdx::k_conv16_pp<float>(mdx::ConvArgs)"
 # the transforms: one instance per Winograd tile size the default policy runs
 # (F(6,3) on the large maps, F(4,3) on the rest)
 KERNEL_SYMBOLS["fp32"].update({12: tuple(f"_ZN3mdx9k_wino_inILi{m}EEEvPKfiiiiiiPf" for m in (4, 6)),

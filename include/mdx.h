@@ -319,6 +319,9 @@ typedef struct mdx_policy {
      * any count); XCD-contiguous ROI ranges [1]; ROIs permuted by level and
      * map band before pooling (mdx_roi_align_ex) [1] */
     int roi_mode, roi_xcd_order, roi_sorted;
+    /* fp16 layers the 256x256 tile takes (large_tiles): 1 on the ping-pong
+     * kernel (two wave groups one barrier apart) [1], 0 on k_convg */
+    int f16_pingpong;
 } mdx_policy;
 int mdx_policy_defaults(mdx_policy *out);
 int mdx_policy_get(mdx_policy *out);
@@ -401,6 +404,7 @@ enum {
     MDX_CONV_KERNEL_SBG64 = 23,
     /* profile records only (mdx_model_profile_read): the Winograd layers'
      * transforms; their GEMM is recorded under the kernel it ran on */
+    MDX_CONV_KERNEL_PP16 = 26, /* fp16 256x256 ping-pong (mdx_policy.f16_pingpong) */
     MDX_CONV_KERNEL_WINO_IN = 12,
     MDX_CONV_KERNEL_WINO_OUT = 13
 };

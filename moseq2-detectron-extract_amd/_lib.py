@@ -117,7 +117,7 @@ POLICY_FIELDS = ("winograd", "winograd_min_cin", "winograd_dma", "winograd_dma_m
                  "fp32_split", "x3_narrow", "x3_single_stage", "large_tiles", "dma128", "dma128_min_tiles",
                  "dma128_interleave", "dma_f32", "pointwise", "single_stage", "direct_epilogue", "narrow_kmax",
                  "head_f32", "stream1x1", "stream1x1_min_m", "stem_fold", "fuse_shortcut", "rpn_sliced", "roi_mode",
-                 "roi_xcd_order", "roi_sorted")
+                 "roi_xcd_order", "roi_sorted", "f16_pingpong")
 
 
 class Policy(ctypes.Structure):

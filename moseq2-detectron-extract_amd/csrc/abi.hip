@@ -40,6 +40,7 @@ static mdx_policy library_defaults() {
     p.roi_mode = 4;
     p.roi_xcd_order = 1;
     p.roi_sorted = 1;
+    p.f16_pingpong = 1;
     return p;
 }
 // the calling thread's policy, and the model handle's while one of its entry

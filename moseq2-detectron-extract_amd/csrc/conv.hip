@@ -1975,6 +1975,183 @@ __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp16 implicit-GEMM convolution on the ping-pong schedule (the fp16 layers
+// the 256x256 tile takes: box head FCs, the FPN 3x3 outputs, the mask /
+// keypoint head convs):  out[m][n] = act(sum_k A[m][k] W[n][k] + bias[n]
+// (+ res)), A row m = the input pixels under output pixel m's taps (NHWC, K
+// order tap outer, channel inner, Cin % 64 == 0), W = weights
+// [Cout][KH][KW][Cin].
+//
+// Tile 256 x 256 per 512-thread workgroup (one per CU), 8 waves: group g =
+// wid >> 2 owns output rows 128 g .. +127, wave (g, wn) a 128 x 64 block =
+// 8 x 4 tiles of v_mfma_f32_16x16x32_f16 (128 fp32 accumulators per lane).
+// K in tiles of 64 halves (128-B LDS rows, pieces XOR-swizzled by row), A and
+// B of a K-tile staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction, 8 per wave and K-tile; padding taps read a zero piece), two
+// K-tile buffers (128 KiB).  (Measured against 32-deep K-tiles in four
+// buffers with the DMA three K-tiles ahead: the deeper pipeline's extra
+// barriers cost more than its lookahead gains, 3-7 % slower.)
+//
+// A K-tile is two phases (32-deep halves).  Every phase is, per wave,
+//   R: 12 ds_read_b128 fragments (8 A + 4 B) [+ DMA issue / wait] lgkmcnt(0)
+//      barrier
+//   M: 32 MFMAs barrier
+// and group 1 runs one barrier behind group 0, so between any two barriers
+// one wave of every SIMD multiplies while the other reads.  Global barrier b
+// opens interval b; group 0 runs R(p) in interval 2p and M(p) in 2p + 1,
+// group 1 R(p) in 2p + 1 and M(p) in 2p + 2.  K-tile t is phases 2t, 2t + 1
+// in buffer t & 1:
+//   * its last reads (phase 2t + 1) retire (lgkmcnt(0)) before barriers
+//     4t + 3 (group 0) and 4t + 4 (group 1);
+//   * the DMA of K-tile t + 2 into the same buffer is issued in R(2t + 2),
+//     intervals 4t + 4 / 4t + 5: after both (WAR);
+//   * each wave waits for its own DMA of K-tile t + 1 (vmcnt(0): the only
+//     vector-memory operations in the loop) in R(2t + 1), before barrier
+//     4t + 3 / 4t + 4, and the first read of K-tile t + 1 is group 0's
+//     R(2t + 2) in interval 4t + 4: after both (RAW; LDS-DMA data is
+//     ordered for ds_read only by the issuer's vmcnt and a barrier).
+// Rows past M / Cout are clamped to the last row (their products only reach
+// outputs that are never stored).  The epilogue stages each wave's block
+// through LDS (32 rows at a time) into finish_batch: bias, residual, ReLU,
+// 16-B stores, the deconv pixel shuffle.
+constexpr int P16_THREADS = 512, P16_BM = 256, P16_BN = 256, P16_BK = 64;
+constexpr int P16_ROWB = 128, P16_OPND = P16_BM * P16_ROWB, P16_BUF = 2 * P16_OPND, P16_LDS = 2 * P16_BUF;
+constexpr int P16_EPI_PITCH = 68;  // floats per staged epilogue row (bank-conflict-free writes)
+
+__device__ __forceinline__ void p16_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <typename TO>
+__global__ __launch_bounds__(P16_THREADS, 1) void k_conv16_pp(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int tile;
+    {
+        const int L = blockIdx.x, nwg = a.tiles_total;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+    }
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int m0 = tm * P16_BM, n0 = tn * P16_BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wn = wid & 3;
+
+    // ---- LDS-DMA sources: instruction j of wave w fills tile rows
+    // 32 w + 8 j .. + 7 of A (and of B); lane l writes row + (l >> 3), 16-B
+    // slot l & 7, which holds the row's logical piece (l & 7) ^ ((row >> 1) & 7)
+    const _Float16 *X = reinterpret_cast<const _Float16 *>(a.x);
+    const _Float16 *Wt = reinterpret_cast<const _Float16 *>(a.w);
+    const int ohw = a.OH * a.OW;
+    int a_iy0[4], a_ix0[4];
+    long long a_base[4];
+    const _Float16 *b_src[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = 32 * wid + 8 * j + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int gm = min(m0 + r, a.M - 1), gn = min(n0 + r, a.Cout - 1);
+        const int b = gm / ohw, rem = gm - b * ohw, oy = rem / a.OW, ox = rem - oy * a.OW;
+        a_iy0[j] = oy * a.stride - a.pad;
+        a_ix0[j] = ox * a.stride - a.pad;
+        a_base[j] = (long long)b * a.H * a.W * a.Cin + 8 * c;
+        b_src[j] = Wt + (long long)gn * a.K + 8 * c;
+    }
+    char *const adst = smem + (32 * wid) * P16_ROWB;  // wave-uniform DMA bases (+ buffer, + j KiB)
+    auto dma = [&](int t) {
+        char *d = adst + (t & 1) * P16_BUF;
+        const int k = t * P16_BK;
+        const int tap = k / a.Cin, ci0 = k - tap * a.Cin;
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
+            const bool ok = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const void *src = ok ? (const void *)(X + a_base[j] + ((long long)iy * a.W + ix) * a.Cin + ci0)
+                                 : (const void *)g_zero16;
+            glds16(src, d + j * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glds16(b_src[j] + k, d + P16_OPND + j * 1024);
+    };
+
+    // ---- fragments: lane l reads row (l & 15) of each 16-row tile, logical
+    // piece 4 s + (l >> 4) of the phase's half s (K elements 8 (l >> 4) ..
+    // of the MFMA's 32)
+    const int fr = lane & 15, fsw = (fr >> 1) & 7, fh = lane >> 4;
+    const char *abase = smem + (grp * 128 + fr) * P16_ROWB;
+    const char *bbase = smem + P16_OPND + (wn * 64 + fr) * P16_ROWB;
+    half8 fa[8], fb[4];
+    auto read_frags = [&](int buf, int s) {
+        const int off = buf * P16_BUF + (((4 * s + fh) ^ fsw) << 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const half8 *>(bbase + off + j * 16 * P16_ROWB);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const half8 *>(abase + off + i * 16 * P16_ROWB);
+    };
+
+    float4v acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+    const int KT = a.K / P16_BK;
+    dma(0);
+    MDX_WAIT_VM(0);
+    p16_barrier();               // K-tile 0 in LDS
+    if (grp == 1) p16_barrier();  // group 1 one barrier behind
+    for (int t = 0; t < KT; ++t) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            read_frags(t & 1, s);  // R
+            if (t + 1 < KT) {
+                if (s == 0)
+                    dma(t + 1);
+                else
+                    MDX_WAIT_VM(0);
+            }
+            MDX_WAIT_LGKM0();
+            p16_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i)  // M
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            p16_barrier();
+        }
+    }
+    if (grp == 0) p16_barrier();  // every wave crosses the same number of barriers
+    __syncthreads();              // the K-tile buffers become the epilogue staging
+
+    // ---- epilogue: 32 rows of the wave's block at a time through its own
+    // LDS rows (acc[i][j][r] = row 16 i + 4 (l >> 4) + r, column 16 j + (l & 15))
+    float *ep = reinterpret_cast<float *>(smem) + wid * (32 * P16_EPI_PITCH);
+    const int rowb = m0 + grp * 128, colb = n0 + wn * 64;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ep[(16 * ii + 4 * fh + r) * P16_EPI_PITCH + 16 * j + fr] = acc[2 * p + ii][j][r];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        finish_batch<TO, 4>(a, [&](int q, int &gm, int &gn0, const float *&src) {
+            const int c = lane + 64 * q, rr = c >> 3, cc = (c & 7) * 8;
+            gm = rowb + 32 * p + rr;
+            gn0 = colb + cc;
+            if (gm >= a.M || gn0 >= a.Cout) gm = -1;
+            src = ep + rr * P16_EPI_PITCH + cc;
+        });
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
 }  // namespace mdx
 
 using namespace mdx;
@@ -2225,7 +2402,8 @@ general:
             return MDX_OK;
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && (in_dtype == 1 || P.dma_f32 == 3 ? t256 >= 384 : t256 >= 500 && a.K >= 1024);
+        const bool big = Cout >= 192 && (in_dtype == 1 || P.dma_f32 == 3 ? t256 >= (P.f16_pingpong ? 160 : 384)
+                                                                            : t256 >= 500 && a.K >= 1024);
         // fp16: the 256x128 tile (two workgroups per CU) in place of 256x256
         // (large-tile modes 3: whenever eligible, 4: the layers mode 1 takes)
         if (in_dtype == 1 && (P.large_tiles == 3 || (P.large_tiles == 4 && big))) {
@@ -2251,6 +2429,16 @@ general:
             a.ksplit = 1;
             a.ksteps = a.K / subk;
             const dim3 grid256((unsigned)a.tiles_total);
+            if (in_dtype == 1 && P.f16_pingpong) {  // fp16: the ping-pong kernel
+                if (out_dtype == 1)
+                    hipLaunchKernelGGL((k_conv16_pp<_Float16>), grid256, dim3(P16_THREADS), P16_LDS, s, a);
+                else
+                    hipLaunchKernelGGL((k_conv16_pp<float>), grid256, dim3(P16_THREADS), P16_LDS, s, a);
+                t_plan_kernel = MDX_CONV_KERNEL_PP16;
+                t_plan_ksplit = 1;
+                MDX_CHECK_LAUNCH("mdx_conv2d");
+                return MDX_OK;
+            }
             // (the interleaved schedule spills at the 8-wave tile's 256-VGPR budget)
             if (in_dtype == 0)
                 hipLaunchKernelGGL((k_convg<float, float, 8, false>), grid256, dim3(G_THREADS), G_LDS, s, a);

@@ -73,7 +73,7 @@ def test_conv_head_1x1_fp32_out(mdx, Cin, Cout, M, relu):
     assert err < 1e-3, err
 
 
-@pytest.mark.parametrize("ksplit", [1, 3, "large", "large128", "dma128", "stream"])
+@pytest.mark.parametrize("ksplit", [1, 3, "large", "large128", "dma128", "stream", "pp16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d(mdx, dtype, case, ksplit):
@@ -107,6 +107,22 @@ def test_conv2d(mdx, dtype, case, ksplit):
             kid, ks_ = ctypes.c_int(), ctypes.c_int()
             call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
             assert kid.value == 4
+    elif ksplit == "pp16":
+        if dtype != "fp16" or Cin % 64 or Cin * k * k <= 128:
+            pytest.skip("the fp16 ping-pong kernel: fp16, Cin % 64 == 0, K > 128")
+        with policy_scope(large_tiles=2, f16_pingpong=1):
+            call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, 1, 1,
+                 P(out), None)
+            kid, ks_ = ctypes.c_int(), ctypes.c_int()
+            call("mdx_conv2d_last_plan", ctypes.byref(kid), ctypes.byref(ks_))
+            assert kid.value == 26
+            if res is None:  # fp16 in, fp32 out (the mixed model's head outputs): the same sums
+                out32 = torch.empty(N, OH, OW, Cout, dtype=torch.float32, device="cuda")
+                call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, None, int(relu), 0, 1,
+                     0, P(out32), None)
+                e32 = (out32.cpu().double() - want).abs().max().item() / (want.abs().max().item() + 1e-6)
+                assert e32 < 2e-3, e32
+                assert torch.equal(out32.half(), out)
     elif ksplit in ("large", "large128", "dma128"):
         if (dtype != "fp16" and ksplit in ("dma128", "large128")) or Cin % (64 if dtype == "fp16" else 32):
             pytest.skip("LDS-DMA kernels: Cin % 64 (fp16) / 32 (fp32) == 0; the 128x128 / 256x128 ones fp16 only")
@@ -114,7 +130,7 @@ def test_conv2d(mdx, dtype, case, ksplit):
             pytest.skip("K <= 128 layers stay on the 64-wide register-staged tile (the policy's narrow-K rule)")
         f32_mode = 1 + CONV_CASES.index(case) % 2  # fp32: the 128x128 (1) and 256x256 (2) variants across the cases
         with policy_scope(large_tiles={"large": 2, "large128": 3}.get(ksplit, 0), dma128=2 if ksplit == "dma128" else 0,
-                          dma128_min_tiles=0,
+                          dma128_min_tiles=0, f16_pingpong=0,
                           dma128_interleave=int(case[0] % 2 == 0),  # both DMA schedules across the cases
                           dma_f32=f32_mode):
             call("mdx_conv2d", P(xd), N, H, W, Cin, P(wd), P(b.cuda()), Cout, k, k, s, p, P(rd), int(relu), 0, dc,
