@@ -1338,6 +1338,9 @@ constexpr int ROI_RMAX = 8, ROI_PMAX = 16, ROI_SPAN_FLOATS = 8192;
 // order (same sums, bit for bit).  Windows above ROI_SWIN_BYTES per slice take
 // mode 4's loop.
 constexpr int ROI_SWIN_SG = 8, ROI_SWIN_BYTES = 32768;
+#ifndef MDX_ROI_TAPS9  // (A/B builds: 0 = every bin through the padded two-round loop)
+#define MDX_ROI_TAPS9 1
+#endif
 
 // x / c for the bin average with the ROI's reciprocal r = RN(1/c): q = RN(x r)
 // refined by one FMA residual step (Markstein), 3 VALU instead of the ~10 of
@@ -1628,6 +1631,35 @@ __global__ __launch_bounds__(256) void k_roi_align_sep(RoiLevels rl, const float
         float acc[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        // bins of at most 3 x 3 taps (3 / 4 of the box pooler's): the nine
+        // taps loaded in one round (the loop below loads 16 in two rounds for a
+        // 3 x 3 bin), then the loop's FMA sequence (rows in pairs, columns in
+        // order, rows within a pair); an absent tap re-reads the bin's last
+        // valid pixel with weight 0 and adds exactly nothing, as the loop's
+        // padding taps do -- the same sums, bit for bit.  When G is a multiple
+        // of 64 a wave's lanes share one bin, so the bounds are wave-uniform.
+        if (MDX_ROI_TAPS9 && nr <= 3 && nc <= 3 && nr > 0 && nc > 0) {
+            uint4 raw[9];
+            float wq[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const int jr = q < 6 ? (q & 1) : 2, k = q < 6 ? (q >> 1) : q - 6;
+                const bool ok = jr < nr && k < nc;
+                const int jc = ok ? jr : nr - 1, kk = ok ? k : nc - 1;
+                raw[q] = *reinterpret_cast<const uint4 *>(fc + ((long long)jc * g.W + kk) * C);
+                wq[q] = ok ? s_A[ph][jr] * s_B[pw][k] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const T *e = reinterpret_cast<const T *>(&raw[q]);
+#pragma unroll
+                for (int i = 0; i < V; ++i) acc[i] = __builtin_fmaf(wq[q], (float)e[i], acc[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[i] = div_count(acc[i], g.count, inv_count);
+            put((long long)t * V, acc);
+            continue;
+        }
         // two rows x four columns of taps per round, all eight loads issued
         // before any is consumed (the kernel is bound by load latency):
         // out-of-range taps re-read the last valid pixel with weight 0

@@ -24,7 +24,7 @@ def main():
         o = os.path.join(_build.OBJ, base[:-4] + ".o")
         if base in files:
             o = os.path.join(_build.OBJ, f"{base[:-4]}_{name}.o")
-            cmd = [cc, *_build._flags(), *_build.HOST_FLAGS.get(base, []), *defines, "-c", src, "-o", o]
+            cmd = [cc, *_build._cmd_flags(base), *defines, "-c", src, "-o", o]
             subprocess.check_call(cmd)
         objs.append(o)
     out = os.path.join(_build.HERE, f"libmdx_{name}.so")

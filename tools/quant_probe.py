@@ -3,7 +3,7 @@ R50 / box-head GEMM shape at its real M and at nearby M whose 128x128 tile
 count is a whole number of per-CU rounds (256 CUs), one launch at a time, HIP
 events over 10 launches.  If TFLOP/s at the real M is well below the
 whole-round M, the loss is balance, not the inner loop.
-Usage: python tools/quant_probe.py [ksplit]"""
+Usage: python tools/quant_probe.py [ksplit [name,...]]"""
 import ctypes
 import json
 import os
@@ -44,13 +44,16 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps * 1e-3
 
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     for name, M0, N, K in SHAPES:
+        if only and name not in only:
+            continue
         tn = (N + 127) // 128
         tiles0 = (M0 + 127) // 128 * tn
         cands = {M0}
         for rounds in (1, 2, 3, 4, 6, 8, 9, 12):
             t = 256 * rounds
-            if t % tn == 0 and 0.4 * tiles0 <= t <= 1.6 * tiles0:
+            if t % tn == 0 and 0.4 * tiles0 <= t <= 1.6 * tiles0 and t // tn * 128 * K * 4 < (1 << 31):
                 cands.add(t // tn * 128)
         w = torch.randn(N, K, device="cuda") / K ** 0.5
         b = torch.randn(N, device="cuda")
