@@ -48,16 +48,18 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP hardware queues: at least 8 (HIP's default is 4), set before the runtime
-# initialises, so that the loop's streams -- H2D, front, four model forwards,
+# HIP hardware queues: at least 12 (HIP's default is 4), set before the runtime
+# initialises, so that the loop's streams -- H2D, front, eight model forwards,
 # tail, the gather -- each get a queue of their own: with 4 queues a third
 # model stream shared a queue with another stage and lost 2 %, with 8 it gained
-# 2.5 % over two streams (1348 -> 1382 fps, profiles/r03_experiments.json), and
-# a fourth 0.7-1.0 % over three (profiles/r04_experiments.json).
+# 2.5 % over two streams (1348 -> 1382 fps, profiles/r03_experiments.json), a
+# fourth 0.7-1.0 % over three (profiles/r04_experiments.json), and at 12 queues
+# eight forwards 2.3 % over four (1491 -> 1525-1528; 12 or 16 forwards no more,
+# profiles/r06_model_streams/).
 # Recorded in the line.  (The illegal-address faults once seen with 8 queues
 # and three model streams were the inpaint set-up race, fixed: DESIGN.md §3.)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 
 
 def parse():
@@ -99,7 +101,7 @@ def parse():
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=INT",
                     help="set a field of the kernel-selection policy (include/mdx.h mdx_policy) before the model "
                          "handles are created, e.g. --set rpn_sliced=0 (repeatable)")
-    ap.add_argument("--model-streams", type=int, default=4,
+    ap.add_argument("--model-streams", type=int, default=8,
                     help="forwards in flight at once (one HIP stream each)")
     ap.add_argument("--chunk-batches", type=int, default=8,
                     help="batches per chunk in the default loop (the chunk's forwards alternate over the streams)")

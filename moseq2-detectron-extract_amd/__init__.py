@@ -5,12 +5,12 @@ proc/ per-frame ops and the Mask/Keypoint R-CNN forward, as hand-written
 gfx950 HIP kernels behind a C ABI (include/mdx.h), with the reference's
 Python-level signatures on top (``proc``, ``model``, ``pipeline``).
 
-Hardware queues.  The extract loop keeps up to four model forwards in flight
-beside its frame stages (pipeline.OverlappedExtractor), each on its own HIP
-stream; HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues
-(default 4).  Importing this package before the HIP runtime starts sets the
-variable to 8 when the caller has not set it; a caller may set any value up
-to 8 itself before HIP initialises.  ``HW_QUEUES`` is the count this process
+Hardware queues.  The extract loop keeps up to eight model forwards in
+flight beside its frame stages (pipeline.OverlappedExtractor), each on its
+own HIP stream; HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware
+queues (default 4).  Importing this package before the HIP runtime starts
+sets the variable to 12 when the caller has not set it; a caller may set its
+own value before HIP initialises.  ``HW_QUEUES`` is the count this process
 runs with, and pipeline.ExtractConfig derives its default number of model
 streams from it (default_model_streams).
 """
@@ -30,8 +30,8 @@ def _setup_hw_queues() -> int:
         started = False
     if started:  # too late to change it: HIP's default
         return 4
-    _os.environ["GPU_MAX_HW_QUEUES"] = "8"
-    return 8
+    _os.environ["GPU_MAX_HW_QUEUES"] = "12"
+    return 12
 
 
 HW_QUEUES = _setup_hw_queues()

@@ -45,13 +45,16 @@ def _stream():
 
 def default_model_streams(hw_queues: Optional[int] = None) -> int:
     """Model streams for the hardware queues this process has (package
-    HW_QUEUES, from GPU_MAX_HW_QUEUES): the front, tail and copy streams share
-    two queues and every forward keeps one of its own, up to 4 forwards (the
-    measured optimum at 8 queues; at HIP's default of 4 queues a third
-    forward lost 2 %)."""
+    HW_QUEUES, from GPU_MAX_HW_QUEUES).  Up to 8 queues: the front, tail and
+    copy streams share two queues and every forward keeps one of its own, up
+    to 4 forwards (at HIP's default of 4 queues a third forward lost 2 %).
+    From 12 queues: 8 forwards (queues - 4), the measured plateau of the hot
+    loop (4 / 6 / 8 / 12 / 16 forwards: 1491 / 1505 / 1525-1528 / 1528-1532 /
+    1528 frames/s)."""
     if hw_queues is None:
         from . import HW_QUEUES as hw_queues
-    return max(1, min(4, int(hw_queues) - 2))
+    q = int(hw_queues)
+    return max(1, min(8, max(q - 4, min(4, q - 2))))
 
 
 @dataclass
@@ -68,11 +71,12 @@ class ExtractConfig:
     mask_iou_threshold: float = 0.5
     fix_invalid_pixels: bool = True
     use_tracking: bool = True        # --use-tracking/--no-use-tracking (M/cli.py:366), default on
-    # forwards of consecutive batches in flight within a chunk: 4 at 8
-    # hardware queues, as in the hot loop (config-3 loop, 6000 frames,
-    # tracking off / on: 2 streams 1266 / 1293 frames/s, 3 streams 1293 / 1313
-    # and 1294 / 1314, 4 streams 1315 / 1332; profiles/r04_experiments.json),
-    # 2 at HIP's default of 4 queues (default_model_streams)
+    # forwards of consecutive batches in flight within a chunk: 8 at 12
+    # hardware queues (the package default), as in the hot loop; 4 at 8 queues
+    # (config-3 loop, 6000 frames, tracking off / on: 2 streams 1266 / 1293
+    # frames/s, 3 streams 1293 / 1313 and 1294 / 1314, 4 streams 1315 / 1332;
+    # profiles/r04_experiments.json), 2 at HIP's default of 4 queues
+    # (default_model_streams)
     model_streams: int = field(default_factory=default_model_streams)
     overlap_host: bool = True        # extract loop: host angle/tracking step in a worker thread
     select_instances: bool = True    # norfair instance selection (process_features_step.py:133-160)

@@ -648,13 +648,13 @@ def test_overlapped_extractor_matches_serial(mdx):
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 def test_overlapped_extractor_benched_config(mdx, dtype):
     """The benched configuration of the pipelined loop (bench.py): B = 32,
-    four model streams, GPU_MAX_HW_QUEUES = 8 -- set before the runtime
+    eight model streams, GPU_MAX_HW_QUEUES = 12 -- set before the runtime
     initialises, so in a fresh process (tools/determinism.py) -- every output
     of every pipelined step bit-equal to the serial step on the same batch."""
     import subprocess
     import sys
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "determinism.py"), dtype, "60", "32", "4"],
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="12")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "determinism.py"), dtype, "60", "32", "8"],
                        env=env, capture_output=True, text=True, timeout=600)
     print(r.stdout[-2000:], r.stderr[-2000:])
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

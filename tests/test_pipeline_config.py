@@ -14,7 +14,9 @@ def test_default_model_streams_by_queue_count(mdx):
     assert default_model_streams(4) == 2
     assert default_model_streams(3) == 1
     assert default_model_streams(1) == 1
-    assert default_model_streams(32) == 4
+    assert default_model_streams(10) == 6
+    assert default_model_streams(12) == 8
+    assert default_model_streams(32) == 8
 
 
 def _probe(env):
@@ -27,8 +29,9 @@ def _probe(env):
 
 
 def test_package_sets_queues_before_hip_starts():
-    """Unset: the package sets 8 queues before HIP initialises and the
-    extractor runs 4 forwards; a caller's own setting is kept."""
+    """Unset: the package sets 12 queues before HIP initialises and the
+    extractor runs 8 forwards; a caller's own setting is kept."""
     env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
-    assert _probe(env) == ["8", "8", "4"]
+    assert _probe(env) == ["12", "12", "8"]
+    assert _probe(dict(env, GPU_MAX_HW_QUEUES="8")) == ["8", "8", "4"]
     assert _probe(dict(env, GPU_MAX_HW_QUEUES="4")) == ["4", "4", "2"]
