@@ -2016,6 +2016,18 @@ __global__ __launch_bounds__(256) void k_wino_out(const float *__restrict__ Mx, 
 // outputs that are never stored).  The epilogue stages each wave's block
 // through LDS (32 rows at a time) into finish_batch: bias, residual, ReLU,
 // 16-B stores, the deconv pixel shuffle.
+// fp16 layers (Cout >= 192, Cin % 64 == 0) from this many 256x256 tiles take
+// the ping-pong kernel.  With eight forwards in flight every eligible layer
+// on it ran the fp16 loop 2.8 % faster (thresholds 160 / 80 / 32 / 8 / 1:
+// 4465-4491 / 4487-4497 / 4572-4584, then 4606-4615 / 4622-4650 / 4628-4648
+// frames/s on a second box; profiles/r06_f16_pp_threshold/), but the small
+// layers it takes over from the split-K register-staged kernel round
+// differently, and the all-fp16 parity case of weight seed 35 then passes
+// the detection checks on 23 of 32 frames, under its floor of 24 (150 -> 146
+// of 160 over the five seeds): kept at 160
+#ifndef MDX_F16_PP_MIN_TILES
+#define MDX_F16_PP_MIN_TILES 160
+#endif
 constexpr int P16_THREADS = 512, P16_BM = 256, P16_BN = 256, P16_BK = 64;
 constexpr int P16_ROWB = 128, P16_OPND = P16_BM * P16_ROWB, P16_BUF = 2 * P16_OPND, P16_LDS = 2 * P16_BUF;
 constexpr int P16_EPI_PITCH = 68;  // floats per staged epilogue row (bank-conflict-free writes)
@@ -2402,7 +2414,7 @@ general:
             return MDX_OK;
         }
         const long long t256 = ceil_div(M, G_BM) * ceil_div(Cout, G_BN);
-        const bool big = Cout >= 192 && (in_dtype == 1 || P.dma_f32 == 3 ? t256 >= (P.f16_pingpong ? 160 : 384)
+        const bool big = Cout >= 192 && (in_dtype == 1 || P.dma_f32 == 3 ? t256 >= (P.f16_pingpong ? MDX_F16_PP_MIN_TILES : 384)
                                                                             : t256 >= 500 && a.K >= 1024);
         // fp16: the 256x128 tile (two workgroups per CU) in place of 256x256
         // (large-tile modes 3: whenever eligible, 4: the layers mode 1 takes)
